@@ -1,0 +1,145 @@
+/*
+ * rifraf_hip.h -- C-ABI of the MI355X-native RIFRAF hot-path engine
+ * (librifraf_hip.so, built from rifraf.jl_amd/csrc/).
+ *
+ * The reference (Rifraf.jl) has no FFI layer: the hot path is a set of
+ * internal Julia functions.  Each entry point below replaces one of them and
+ * is what a Julia `ccall` or Python `ctypes` binds:
+ *
+ *   rf_set_sequences  <- RifrafSequence tables      src/rifrafsequences.jl:19-82
+ *   rf_set_templates  <- state.consensus            src/model.jl:169
+ *   rf_realign        <- forward_moves!/forward!/backward! over a batch
+ *                        src/align.jl:114-141,155-179,196-202;
+ *                        realign! src/model.jl:679-714
+ *   rf_backtrace      <- backtrace + count_errors   src/align.jl:229-245
+ *   rf_score          <- score_proposal(m, state, newcols, use_ref) summed
+ *                        over the batch, as called by get_candidates and
+ *                        estimate_probs  src/model.jl:385-399,499-526,737-791
+ *                        (per-sequence: score_nocodon :242-285 / codon
+ *                        score_proposal :302-383 / seq_score_deletion :227-236)
+ *   rf_download_band  <- BandedArray data (tests)   src/bandedarrays.jl:5-42
+ *
+ * Conventions
+ *  - Every call returns 0 on success and a negative code on failure; the
+ *    message is rf_last_error(ctx), using the reference's error text
+ *    ("new score is invalid", "failed to compute a valid score", ...).
+ *  - Bases are 2-bit codes A=0, C=1, G=2, T=3 (BioSequences DNAAlphabet{2}).
+ *  - Sequence tables are FP64 and uploaded bit-exact from the host (the
+ *    host computes them exactly as RifrafSequence() does).
+ *  - Proposal positions use the reference's 1-based Proposal.pos
+ *    (Insertion(0, b) inserts before the first base). kind: 0 = Substitution,
+ *    1 = Insertion, 2 = Deletion.
+ *  - Bands stay device resident between calls.  A "slot" is one alignment
+ *    (sequence x template) owning an A band and a B band, each H x (m+1)
+ *    FP64, column-major, H = 2*bw + |n-m| + 1 -- the reference layout
+ *    data[(i-j)+h_off+bw+1, j] (src/bandedarrays.jl:101-114).
+ *  - One context per host thread; calls are synchronous on the context's
+ *    HIP stream.  No torch types cross this boundary.
+ */
+#ifndef RIFRAF_HIP_H
+#define RIFRAF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RF_ABI_VERSION 1
+
+/* rf_realign flags */
+#define RF_FWD  1   /* A band: forward_moves!/forward!             align.jl:114,155 */
+#define RF_BWD  2   /* B band: backward! (reverse forward + flip!) align.jl:196    */
+#define RF_SKEW 4   /* skew_matches: mismatch score *= 0.99        align.jl:70-72  */
+#define RF_TRIM 8   /* trim: free insertions in first/last column  align.jl:74-76  */
+
+/* rf_download_band `which` */
+#define RF_BAND_A 0
+#define RF_BAND_B 1
+
+/* error codes */
+#define RF_ERR_ARG        (-1)
+#define RF_ERR_HIP        (-2)
+#define RF_ERR_NUMERIC    (-3)   /* a reference error() on the numeric path */
+#define RF_ERR_STATE      (-4)   /* stale / mismatched bands */
+
+typedef struct rf_ctx rf_ctx;
+
+int rf_abi_version(void);
+
+/* Create a context on HIP device `device`. */
+int rf_create(int device, rf_ctx **out);
+int rf_destroy(rf_ctx *ctx);
+const char *rf_last_error(const rf_ctx *ctx);
+
+/* Pre-size the device band arena (bytes); optional. */
+int rf_reserve(rf_ctx *ctx, int64_t band_bytes);
+/* Bytes currently allocated on the device by this context. */
+int64_t rf_device_bytes(const rf_ctx *ctx);
+
+/* Sequences (reads or a reference): ids [first, first+nseq).  Replaces any
+ * previous content of those ids.  Per sequence k (n_k = off[k+1]-off[k]):
+ *   bases    off[k]..off[k+1]                    (n_k codes)
+ *   match, mismatch, ins at off[k]..off[k+1]     (rifrafsequences.jl:45-47)
+ *   del      at off[k]+k .. off[k+1]+k+1         (n_k+1, :49-53)
+ *   cins     cins_off[k]..cins_off[k+1]           (n_k-2 or 0, :57-64)
+ *   cdel     cdel_off[k]..cdel_off[k+1]           (n_k+1 or 0, :65-72)
+ * cins/cdel/cins_off/cdel_off may be NULL (no codon moves). */
+int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq,
+                     const uint8_t *bases, const int64_t *off,
+                     const double *match, const double *mismatch,
+                     const double *ins, const double *del,
+                     const double *cins, const int64_t *cins_off,
+                     const double *cdel, const int64_t *cdel_off);
+
+/* Templates (consensus sequences, one per cluster): ids [first, first+n). */
+int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl,
+                     const uint8_t *bases, const int64_t *off);
+
+/* Batched DP fill.  Job k aligns sequence seq[k] (rows) against template
+ * tpl[k] (columns) with bandwidth bw[k] into slot slot[k].  flags: RF_FWD
+ * and/or RF_BWD, optionally RF_SKEW / RF_TRIM (forward only).
+ * out_score[k] (may be NULL) = A[end,end] if RF_FWD else B[1,1]. */
+int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot,
+               const int32_t *seq, const int32_t *tpl, const int32_t *bw,
+               int32_t flags, double *out_score);
+
+/* Backtrace of the A band of each slot (align.jl:229-238), moves in
+ * alignment order written at moves[moves_off[k] ...] (capacity n+m each);
+ * nmoves[k] = count; nerrors[k] = count_errors (align.jl:240-245).
+ * Any of moves/moves_off/nmoves/nerrors may be NULL. */
+int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot,
+                 int8_t *moves, const int64_t *moves_off,
+                 int32_t *nmoves, int32_t *nerrors);
+
+/* Proposal scoring.  Group g (one cluster) = batch slots
+ * slots[slot_off[g] .. slot_off[g+1]) in batch order, an optional
+ * reference slot ref_slot[g] (-1: none; scored with codon moves when its
+ * sequence has codon tables), and proposals prop_off[g] .. prop_off[g+1].
+ * out_total[k] = 0.0 + s_1 + ... + s_R (+ s_ref), the left fold of
+ * model.jl:389-397.  out_per_seq (may be NULL) receives s_r for every
+ * (proposal, batch slot) pair, row-major [k][r] with r in batch order,
+ * followed by s_ref in an extra last column when the group has a
+ * reference (row width R_g or R_g + 1). */
+int rf_score(rf_ctx *ctx, int32_t ngroups,
+             const int32_t *slot_off, const int32_t *slots,
+             const int32_t *ref_slot, const int64_t *prop_off,
+             const uint8_t *kind, const int32_t *pos, const uint8_t *base,
+             double *out_total, double *out_per_seq);
+
+/* Geometry of a slot's band: nrows = n+1, ncols = m+1, bandwidth, H. */
+int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,
+                     int32_t *nrows, int32_t *ncols, int32_t *bw, int32_t *H);
+
+/* Copy a slot's band (H x ncols doubles, column-major) to the host. */
+int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out);
+
+/* Kernel timing of the last rf_realign / rf_score call (HIP events on the
+ * context stream), milliseconds; used by bench.py's roofline. */
+int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms,
+                   double *gather_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

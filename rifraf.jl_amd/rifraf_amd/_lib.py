@@ -1,0 +1,85 @@
+"""ctypes binding of librifraf_hip.so (the C-ABI in include/rifraf_hip.h).
+
+This is the only way the host reaches the hot path: there is no CPU fallback.
+If the shared library is missing, cannot be loaded, or no HIP device is
+present, every engine entry point raises instead of computing anything.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int8, c_int32, c_int64, c_uint8, c_void_p
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RIFRAF_HIP_LIB", os.path.join(PKG_DIR, "librifraf_hip.so"))
+
+RF_FWD, RF_BWD, RF_SKEW, RF_TRIM = 1, 2, 4, 8
+RF_BAND_A, RF_BAND_B = 0, 1
+RF_ABI_VERSION = 1
+
+# every symbol include/rifraf_hip.h declares, with its ctypes signature
+_SIGNATURES = {
+    "rf_abi_version": (c_int, []),
+    "rf_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rf_destroy": (c_int, [c_void_p]),
+    "rf_last_error": (c_char_p, [c_void_p]),
+    "rf_reserve": (c_int, [c_void_p, c_int64]),
+    "rf_device_bytes": (c_int64, [c_void_p]),
+    "rf_set_sequences": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rf_set_templates": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "rf_realign": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "rf_backtrace": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rf_score": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p]),
+    "rf_slot_geometry": (c_int, [c_void_p, c_int32, c_int32, POINTER(c_int32), POINTER(c_int32),
+                                 POINTER(c_int32), POINTER(c_int32)]),
+    "rf_download_band": (c_int, [c_void_p, c_int32, c_int32, c_void_p]),
+    "rf_last_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
+}
+
+_lib = None
+_load_error = None
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP engine cannot run here (library missing or no GPU)."""
+
+
+def load(path: str | None = None):
+    """Load librifraf_hip.so and bind every C-ABI symbol (raises if absent)."""
+    global _lib, _load_error
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineUnavailable(
+            f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError as e:  # pragma: no cover - environment dependent
+        _load_error = e
+        raise EngineUnavailable(f"cannot load {p}: {e}") from e
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = missing export: loud
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rf_abi_version() != RF_ABI_VERSION:
+        raise EngineUnavailable("librifraf_hip.so ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def ptr(a: np.ndarray | None):
+    """Pointer to a contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(c_void_p)
+
+
+__all__ = ["load", "ptr", "EngineUnavailable", "RF_FWD", "RF_BWD", "RF_SKEW", "RF_TRIM",
+           "RF_BAND_A", "RF_BAND_B", "_SIGNATURES", "c_int8", "c_uint8"]

@@ -1,0 +1,199 @@
+"""Device engine: one HIP context (rf_ctx) of librifraf_hip.so.
+
+Thin, typed wrapper over the C-ABI of include/rifraf_hip.h.  All numeric
+work (DP fills, backtraces, proposal scoring) runs in the HIP kernels; this
+module only marshals arrays.  There is no CPU fallback: a missing library or
+GPU raises EngineUnavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_double, c_int32, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import RF_BAND_A, RF_BAND_B, RF_BWD, RF_FWD, RF_SKEW, RF_TRIM, ptr
+from .bandedarrays import BandedArray
+from .proposals import to_arrays
+
+
+class RifrafError(Exception):
+    """A reference `error(...)` raised on the engine path (same message text)."""
+
+
+class Engine:
+    """One device context.  Sequence ids, template ids and slot ids are small
+    integers chosen by the caller (see model.py for the RIFRAF mapping)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = c_void_p()
+        rc = self.lib.rf_create(int(device), byref(h))
+        if rc != 0:
+            raise _lib.EngineUnavailable(f"rf_create(device={device}) failed with {rc}: no HIP device?")
+        self.ctx = h
+        self.device = device
+
+    # ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.rf_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != 0:
+            msg = self.lib.rf_last_error(self.ctx).decode()
+            raise RifrafError(msg)
+
+    # ------------------------------------------------------------------
+    def reserve(self, nbytes: int):
+        self._check(self.lib.rf_reserve(self.ctx, int(nbytes)))
+
+    def device_bytes(self) -> int:
+        return int(self.lib.rf_device_bytes(self.ctx))
+
+    def set_sequences(self, first: int, seqs):
+        """Upload RifrafSequence tables for ids [first, first+len(seqs))."""
+        if not seqs:
+            return
+        lens = np.array([len(s) for s in seqs], np.int64)
+        if (lens < 1).any():
+            raise ValueError("empty sequence")
+        off = np.zeros(len(seqs) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        bases = np.ascontiguousarray(np.concatenate([s.seq for s in seqs]), np.uint8)
+        match = np.ascontiguousarray(np.concatenate([s.match_scores for s in seqs]))
+        mism = np.ascontiguousarray(np.concatenate([s.mismatch_scores for s in seqs]))
+        ins = np.ascontiguousarray(np.concatenate([s.ins_scores for s in seqs]))
+        dele = np.ascontiguousarray(np.concatenate([s.del_scores for s in seqs]))
+        any_codon = any(s.do_codon_moves() for s in seqs)
+        cins = cdel = cins_off = cdel_off = None
+        if any_codon:
+            ci = [np.asarray(s.codon_ins_scores, np.float64) for s in seqs]
+            cd = [np.asarray(s.codon_del_scores, np.float64) for s in seqs]
+            cins_off = np.zeros(len(seqs) + 1, np.int64)
+            np.cumsum([len(x) for x in ci], out=cins_off[1:])
+            cdel_off = np.zeros(len(seqs) + 1, np.int64)
+            np.cumsum([len(x) for x in cd], out=cdel_off[1:])
+            cins = np.ascontiguousarray(np.concatenate(ci + [np.zeros(1)]))
+            cdel = np.ascontiguousarray(np.concatenate(cd + [np.zeros(1)]))
+        self._check(self.lib.rf_set_sequences(
+            self.ctx, int(first), len(seqs), ptr(bases), ptr(off), ptr(match), ptr(mism), ptr(ins),
+            ptr(dele), ptr(cins), ptr(cins_off), ptr(cdel), ptr(cdel_off)))
+
+    def set_templates(self, first: int, tpls):
+        if not tpls:
+            return
+        lens = np.array([len(t) for t in tpls], np.int64)
+        off = np.zeros(len(tpls) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        bases = np.ascontiguousarray(np.concatenate([np.asarray(t, np.uint8) for t in tpls]), np.uint8)
+        self._check(self.lib.rf_set_templates(self.ctx, int(first), len(tpls), ptr(bases), ptr(off)))
+
+    def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
+        """Batched forward_moves!/backward! fill; returns A[end,end] (RF_FWD)
+        or B[1,1] per job."""
+        slots = np.ascontiguousarray(slots, np.int32)
+        n = slots.shape[0]
+        seqs = np.ascontiguousarray(np.broadcast_to(seqs, (n,)), np.int32)
+        tpls = np.ascontiguousarray(np.broadcast_to(tpls, (n,)), np.int32)
+        bws = np.ascontiguousarray(np.broadcast_to(bws, (n,)), np.int32)
+        out = np.empty(max(n, 1))
+        self._check(self.lib.rf_realign(self.ctx, n, ptr(slots), ptr(seqs), ptr(tpls), ptr(bws),
+                                        int(flags), ptr(out)))
+        return out[:n]
+
+    def backtrace(self, slots, want_moves: bool = True):
+        """backtrace + count_errors of each slot's A band.
+        Returns (list of int8 move arrays in alignment order, nerrors)."""
+        slots = np.ascontiguousarray(slots, np.int32)
+        n = slots.shape[0]
+        nmoves = np.empty(max(n, 1), np.int32)
+        nerr = np.empty(max(n, 1), np.int32)
+        if want_moves:
+            caps = np.empty(n, np.int64)
+            for k, s in enumerate(slots):
+                nrows, ncols, _, _ = self.geometry(int(s), RF_BAND_A)
+                caps[k] = nrows + ncols - 2
+            moves_off = np.zeros(n + 1, np.int64)
+            np.cumsum(caps, out=moves_off[1:])
+            moves = np.empty(max(int(moves_off[-1]), 1), np.int8)
+            self._check(self.lib.rf_backtrace(self.ctx, n, ptr(slots), ptr(moves), ptr(moves_off),
+                                              ptr(nmoves), ptr(nerr)))
+            out = [moves[moves_off[k]:moves_off[k] + nmoves[k]].copy() for k in range(n)]
+            return out, nerr[:n].copy()
+        self._check(self.lib.rf_backtrace(self.ctx, n, ptr(slots), None, None, ptr(nmoves), ptr(nerr)))
+        return None, nerr[:n].copy()
+
+    def score(self, groups, per_seq: bool = False):
+        """Score proposals.  groups: list of (batch_slots, ref_slot, proposals)
+        with ref_slot = -1 for none.  Returns a list of total arrays (and of
+        per-sequence matrices if per_seq)."""
+        G = len(groups)
+        slot_off = np.zeros(G + 1, np.int32)
+        prop_off = np.zeros(G + 1, np.int64)
+        all_slots, refs, ks, ps, bs = [], np.empty(G, np.int32), [], [], []
+        widths = []
+        for g, (bslots, ref, props) in enumerate(groups):
+            bslots = np.asarray(bslots, np.int32)
+            all_slots.append(bslots)
+            slot_off[g + 1] = slot_off[g] + len(bslots)
+            refs[g] = ref
+            if isinstance(props, tuple):
+                k, p, b = props
+            else:
+                k, p, b = to_arrays(props)
+            ks.append(k)
+            ps.append(p)
+            bs.append(b)
+            prop_off[g + 1] = prop_off[g] + len(k)
+            widths.append(len(bslots) + (1 if ref >= 0 else 0))
+        slots = np.ascontiguousarray(np.concatenate(all_slots) if all_slots else np.zeros(1, np.int32), np.int32)
+        kind = np.ascontiguousarray(np.concatenate(ks) if ks else np.zeros(0), np.uint8)
+        pos = np.ascontiguousarray(np.concatenate(ps) if ps else np.zeros(0), np.int32)
+        base = np.ascontiguousarray(np.concatenate(bs) if bs else np.zeros(0), np.uint8)
+        nprops = int(prop_off[-1])
+        total = np.empty(max(nprops, 1))
+        per = None
+        if per_seq:
+            per = np.empty(max(int(sum(w * (prop_off[g + 1] - prop_off[g]) for g, w in enumerate(widths))), 1))
+        self._check(self.lib.rf_score(self.ctx, G, ptr(slot_off), ptr(slots), ptr(refs), ptr(prop_off),
+                                      ptr(kind) if nprops else None, ptr(pos) if nprops else None,
+                                      ptr(base) if nprops else None, ptr(total), ptr(per)))
+        totals = [total[prop_off[g]:prop_off[g + 1]].copy() for g in range(G)]
+        if not per_seq:
+            return totals
+        mats, at = [], 0
+        for g, w in enumerate(widths):
+            cnt = int(prop_off[g + 1] - prop_off[g])
+            mats.append(per[at:at + cnt * w].reshape(cnt, w).copy())
+            at += cnt * w
+        return totals, mats
+
+    def geometry(self, slot: int, which: int = RF_BAND_A):
+        nr, nc, bw, H = c_int32(), c_int32(), c_int32(), c_int32()
+        self._check(self.lib.rf_slot_geometry(self.ctx, int(slot), int(which), byref(nr), byref(nc),
+                                              byref(bw), byref(H)))
+        return nr.value, nc.value, bw.value, H.value
+
+    def download_band(self, slot: int, which: int = RF_BAND_A, default=-np.inf) -> BandedArray:
+        nrows, ncols, bw, H = self.geometry(slot, which)
+        buf = np.empty(H * ncols)
+        self._check(self.lib.rf_download_band(self.ctx, int(slot), int(which), ptr(buf)))
+        data = np.asfortranarray(buf.reshape(ncols, H).T)
+        return BandedArray((nrows, ncols), bw, default=default, data=data)
+
+    def last_timing(self):
+        a, b, c = c_double(), c_double(), c_double()
+        self._check(self.lib.rf_last_timing(self.ctx, byref(a), byref(b), byref(c)))
+        return a.value, b.value, c.value
+
+
+__all__ = ["Engine", "RifrafError", "RF_FWD", "RF_BWD", "RF_SKEW", "RF_TRIM", "RF_BAND_A", "RF_BAND_B"]

@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "rifraf.jl_amd"), os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from rifraf_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()

@@ -1,0 +1,237 @@
+"""HIP engine parity against the CPU oracle (bit-exact).
+
+Every test calls the engine through the C-ABI (librifraf_hip.so via ctypes)
+and the oracle (oracle/rifraf_oracle.c) on the same seeded inputs.  The
+oracle is pinned to the reference by tests/test_oracle_kats.py.
+Tolerance: bit-exact for bands, moves, error counts and scores (the engine
+evaluates the same FP64 sums in the same order as the reference).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from _util import (REF_SCORES, SEQ_SCORES, all_proposals_arrays, dense_slot, inband_mask, make_read,
+                   random_seq)
+from rifraf_amd import ErrorModel, RifrafSequence, Scores
+from rifraf_amd.engine import RF_BAND_A, RF_BAND_B, RF_BWD, RF_FWD, RF_SKEW, RF_TRIM, RifrafError
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_band_equal(got, exp_data, nrows, ncols, bw):
+    mask = inband_mask(nrows, ncols, bw)
+    g = got.data[mask]
+    e = np.asarray(exp_data)[mask]
+    bad = ~((g == e) | (np.isnan(g) & np.isnan(e)))
+    assert not bad.any(), f"{bad.sum()} of {mask.sum()} in-band cells differ"
+
+
+DP_CASES = [
+    # (template length, error rate, bandwidth, length jitter, codon)
+    (5, 0.05, 1, 0, False),
+    (30, 0.05, 3, 0, False),
+    (60, 0.05, 9, 4, False),
+    (120, 0.03, 9, 12, False),      # H up to 32 -> W=16 class
+    (200, 0.03, 20, 10, False),     # W=32 class
+    (300, 0.05, 40, 30, False),     # W=64 class
+    (90, 0.05, 9, 0, True),         # codon moves (reference-style tables)
+    (150, 0.10, 15, 6, True),
+]
+
+
+@pytest.mark.parametrize("L,err,bw,jit,codon", DP_CASES)
+def test_dp_bands_bitexact(engine, L, err, bw, jit, codon):
+    rng = np.random.default_rng(L * 7 + bw)
+    t = random_seq(L, rng)
+    seqs = []
+    for k in range(6):
+        if codon:
+            s = random_seq(max(3, L + int(rng.integers(-jit, jit + 1))), rng)
+            lp = np.log10(rng.uniform(0.01, 0.2, len(s)))
+            seqs.append(RifrafSequence(s, lp, bw, REF_SCORES))
+        else:
+            r = make_read(t, rng, err, bw)
+            if jit:
+                extra = random_seq(int(rng.integers(0, jit + 1)), rng)
+                s = np.concatenate([r.seq, extra])
+                lp = np.concatenate([r.error_log_p, np.full(len(extra), -1.0)])
+                r = RifrafSequence(s, lp, bw, SEQ_SCORES)
+            seqs.append(r)
+    n = len(seqs)
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    scores = engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
+    for k, s in enumerate(seqs):
+        A_exp, mv = oracle.forward(t, s, moves=True)
+        B_exp = oracle.backward(t, s)
+        A = engine.download_band(k, RF_BAND_A)
+        B = engine.download_band(k, RF_BAND_B)
+        assert_band_equal(A, A_exp, len(s) + 1, L + 1, bw)
+        assert_band_equal(B, B_exp, len(s) + 1, L + 1, bw)
+        H = A_exp.shape[0]
+        d_end = len(s) - L + max(L - len(s), 0) + bw
+        assert scores[k] == A_exp[d_end, L]
+        # backtrace recomputed from A == reference backtrace of the trace band
+        ref_moves = oracle.backtrace(mv, len(s) + 1, L + 1, bw)
+        got_moves, nerr = engine.backtrace([k])
+        np.testing.assert_array_equal(got_moves[0], ref_moves)
+        assert nerr[0] == oracle.count_errors(ref_moves, t, s.seq)
+
+
+@pytest.mark.parametrize("flags", [RF_SKEW, RF_TRIM, RF_SKEW | RF_TRIM])
+def test_dp_skew_trim(engine, flags):
+    rng = np.random.default_rng(flags)
+    t = random_seq(80, rng)
+    seqs = [make_read(t, rng, 0.08, 5) for _ in range(4)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(4), np.arange(4), 0, [5] * 4, RF_FWD | flags)
+    for k, s in enumerate(seqs):
+        A_exp, mv = oracle.forward(t, s, moves=True, skew=bool(flags & RF_SKEW), trim=bool(flags & RF_TRIM))
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(s) + 1, 81, 5)
+        moves, nerr = engine.backtrace([k])
+        ref = oracle.backtrace(mv, len(s) + 1, 81, 5)
+        np.testing.assert_array_equal(moves[0], ref)
+
+
+def test_dp_huge_band_global_ring(engine):
+    """H > 2040 takes the global-memory ring path (edit_distance-sized bands)."""
+    rng = np.random.default_rng(5)
+    t = random_seq(2300, rng)
+    s = make_read(t, rng, 0.02, 1100)
+    engine.set_sequences(0, [s])
+    engine.set_templates(0, [t])
+    engine.realign([0], [0], 0, [1100], RF_FWD | RF_BWD)
+    A_exp, _ = oracle.forward(t, s, moves=True)
+    assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, 2301, 1100)
+    B_exp = oracle.backward(t, s)
+    assert_band_equal(engine.download_band(0, RF_BAND_B), B_exp, len(s) + 1, 2301, 1100)
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("L,nreads,bw", [(40, 3, 9), (150, 7, 9), (260, 5, 25)])
+def test_score_all_proposals_bitexact(engine, monkeypatch, mode, L, nreads, bw):
+    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    rng = np.random.default_rng(L + nreads)
+    t = random_seq(L, rng)
+    seqs = [make_read(t, rng, 0.03, bw) for _ in range(nreads)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(nreads), np.arange(nreads), 0, [bw] * nreads, RF_FWD | RF_BWD)
+    props = all_proposals_arrays(t)
+    got = engine.score([(np.arange(nreads), -1, props)])[0]
+    ref_tot, _ = oracle.cpu_pass(t, seqs, nthreads=4)
+    exp = ref_tot[props[1], dense_slot(props[0], props[2])]
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_score_per_read_bitexact(engine):
+    rng = np.random.default_rng(3)
+    t = random_seq(70, rng)
+    seqs = [make_read(t, rng, 0.04, 9) for _ in range(4)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(4), np.arange(4), 0, [9] * 4, RF_FWD | RF_BWD)
+    props = all_proposals_arrays(t)
+    tot, per = engine.score([(np.arange(4), -1, props)], per_seq=True)
+    As = [oracle.forward(t, s)[0] for s in seqs]
+    Bs = [oracle.backward(t, s) for s in seqs]
+    for k in range(0, len(props[0]), 7):
+        for r, s in enumerate(seqs):
+            exp = oracle.score_proposal(props[0][k], props[1][k], props[2][k], As[r], Bs[r], t, s)
+            assert per[0][k, r] == exp
+        fold = 0.0
+        for r in range(4):
+            fold += per[0][k, r]
+        assert tot[0][k] == fold
+
+
+def test_score_many_clusters(engine, monkeypatch):
+    """Batched clusters: one group per consensus, fused ordered fold."""
+    monkeypatch.setenv("RIFRAF_SCORE_MODE", "fused")
+    rng = np.random.default_rng(99)
+    templates, seqs, groups = [], [], []
+    for c in range(6):
+        t = random_seq(int(rng.integers(50, 90)), rng)
+        templates.append(t)
+        rs = [make_read(t, rng, 0.03, 9) for _ in range(int(rng.integers(2, 5)))]
+        seqs.append(rs)
+    flat = [r for rs in seqs for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    ids, tpl, at = [], [], 0
+    for c, rs in enumerate(seqs):
+        ids.append(np.arange(at, at + len(rs)))
+        tpl += [c] * len(rs)
+        at += len(rs)
+    engine.realign(np.arange(at), np.arange(at), np.array(tpl), [9] * at, RF_FWD | RF_BWD)
+    groups = [(ids[c], -1, all_proposals_arrays(templates[c])) for c in range(6)]
+    got = engine.score(groups)
+    for c in range(6):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        k, p, b = groups[c][2]
+        np.testing.assert_array_equal(got[c], ref_tot[p, dense_slot(k, b)])
+
+
+def test_score_reference_codon(engine):
+    """Reference (codon-move) scoring, model.jl:302-383, alone and after reads."""
+    rng = np.random.default_rng(21)
+    t = random_seq(99, rng)
+    ref_s = random_seq(96, rng)
+    ref = RifrafSequence(ref_s, np.full(96, math.log10(0.05)), 9, REF_SCORES)
+    reads = [make_read(t, rng, 0.03, 9) for _ in range(3)]
+    engine.set_sequences(0, reads + [ref])
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(4), np.arange(4), 0, [9] * 4, RF_FWD | RF_BWD)
+    props = all_proposals_arrays(t)
+    tot_ref_only, per = engine.score([(np.arange(0), 3, props)], per_seq=True)
+    tot_all = engine.score([(np.arange(3), 3, props)])[0]
+    Ar, _ = oracle.forward(t, ref)
+    Br = oracle.backward(t, ref)
+    As = [oracle.forward(t, s)[0] for s in reads]
+    Bs = [oracle.backward(t, s) for s in reads]
+    for k in range(len(props[0])):
+        prop = (int(props[0][k]), int(props[1][k]), int(props[2][k]))
+        exp_ref = oracle.score_proposal(*prop, Ar, Br, t, ref)
+        assert tot_ref_only[0][k] == 0.0 + exp_ref
+        assert per[0][k, 0] == exp_ref
+        exp = oracle.score_total(prop, As, Bs, reads, t, Ar, Br, ref)
+        assert tot_all[k] == exp, prop
+
+
+def test_single_sequence_nocodon_group(engine):
+    """A group with only a non-codon 'reference' slot runs the per-proposal
+    score_nocodon path (model.jl:242-285)."""
+    rng = np.random.default_rng(8)
+    t = random_seq(45, rng)
+    r = make_read(t, rng, 0.05, 9)
+    engine.set_sequences(0, [r])
+    engine.set_templates(0, [t])
+    engine.realign([0], [0], 0, [9], RF_FWD | RF_BWD)
+    props = all_proposals_arrays(t)
+    got = engine.score([([], 0, props)])[0]
+    A, _ = oracle.forward(t, r)
+    B = oracle.backward(t, r)
+    for k in range(len(props[0])):
+        assert got[k] == oracle.score_proposal(props[0][k], props[1][k], props[2][k], A, B, t, r)
+
+
+def test_errors_are_loud(engine):
+    rng = np.random.default_rng(2)
+    t = random_seq(20, rng)
+    r = make_read(t, rng, 0.05, 3)
+    engine.set_sequences(0, [r])
+    engine.set_templates(0, [t])
+    with pytest.raises(RifrafError, match="bandwidth must be positive"):
+        engine.realign([0], [0], 0, [0], RF_FWD)
+    engine.realign([0], [0], 0, [3], RF_FWD)
+    with pytest.raises(RifrafError):
+        engine.score([([0], -1, all_proposals_arrays(t))])  # no B band yet
+    codon = RifrafSequence(r.seq, r.error_log_p, 3, REF_SCORES)
+    engine.set_sequences(1, [codon])
+    engine.realign([1], [1], 0, [3], RF_FWD | RF_BWD)
+    with pytest.raises(RifrafError, match="codon"):
+        engine.score([([1], -1, all_proposals_arrays(t))])
