@@ -1,0 +1,259 @@
+#!/usr/bin/env python
+"""bench.py -- RIFRAF hot path on MI355X.
+
+One step = one pass of the hot path over this rank's batch of clusters:
+  1. realign: forward (A) + backward (B) banded DP of every read against its
+     cluster consensus (forward_moves!/backward!, realign! model.jl:679-714);
+  2. score: every STAGE_SCORE proposal of every cluster (all_proposals,
+     model.jl:401-456: 8m+4 per cluster) summed over the cluster's reads in
+     batch order (score_proposal(state) model.jl:385-399, as estimate_probs
+     does, model.jl:737-791).  Totals stay in HBM.
+
+Workload (default "c4"): BASELINE.json configs[3] -- clusters of 50 reads x
+1.5 kb (sample_sequences(50, 1500), error_rate 0.01, seq_errors
+ErrorModel(1,5,5), default RifrafParams scores, bandwidth 9), sharded by
+cluster across ranks with a fixed per-rank share (weak scaling): 1,250
+clusters per GPU, so 8 GPUs = the config's 10,000 clusters.  No collective
+on the data path (clusters are independent); the only cross-rank traffic is
+the timing barrier / max.  "c2" / "c3" select configs[1] / configs[2]
+(single cluster; replicas under --gpus N).
+
+Prints ONE JSON line on rank 0 (contract in the task statement); metric
+value = GCUPS = in-band DP cells (forward + backward) per second over the
+whole step; proposals/s and (proposal x read) pairs/s are reported beside it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rifraf.jl_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VEC_TFLOPS = 78.6         # half the 157.3 TF FP32 vector spec
+
+CONFIGS = {
+    # name: (clusters per rank, reads per cluster, template length, error rate, bandwidth, label)
+    "c4": (1250, 50, 1500, 0.01, 9, "configs[3]: clusters x 50 reads x 1.5 kb, per-GPU share of 10k"),
+    "c2": (1, 100, 1000, 0.01, 9, "configs[1]: 1 kb template, 100 reads, ~1% error"),
+    "c3": (1, 1000, 2601, 0.01, 9, "configs[2]: 2.6 kb amplicon, 1000 reads (read DP + scoring)"),
+}
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def band_cells(n: int, m: int, bw: int) -> int:
+    """Number of in-band cells: sum_j |row_range(j)| (bandedarrays.jl:133-137)."""
+    nrows, ncols = n + 1, m + 1
+    h_off, v_off = max(ncols - nrows, 0), max(nrows - ncols, 0)
+    j = np.arange(1, ncols + 1)
+    start = np.maximum(1, j - h_off - bw)
+    stop = np.minimum(j + v_off + bw, nrows)
+    return int(np.sum(stop - start + 1))
+
+
+def make_workload(nclusters, nreads, length, error_rate, bw, seed):
+    """Synthetic clusters from the restated sample module (sample.jl)."""
+    from rifraf_amd import ErrorModel, RifrafSequence, Scores
+    from rifraf_amd.sample import MAX_PROB, MIN_PROB, random_seq, sample_from_template
+    rng = np.random.default_rng(seed)
+    scores = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0, 0.0, 0.0))   # RifrafParams default
+    seq_errors = ErrorModel(1, 5, 5)
+    alpha = 0.1
+    beta = alpha * (error_rate - MAX_PROB) / (MIN_PROB - error_rate)
+    clusters = []
+    for _ in range(nclusters):
+        t = random_seq(length, rng)
+        t_p = rng.beta(alpha, beta, size=length) * (MAX_PROB - MIN_PROB) + MIN_PROB
+        reads = []
+        for _ in range(nreads):
+            s, _, ph, _, _ = sample_from_template(t, t_p, seq_errors, 1.5, 3.0, 1.0, rng)
+            reads.append(RifrafSequence(s, ph, bw, scores))
+        clusters.append((t, reads))
+    return clusters
+
+
+def cpu_baseline(clusters, budget_s=12.0, max_threads=16):
+    """The oracle (C restatement of the reference) on the host cores, over a
+    bounded sample of the same workload (whole clusters until the budget)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+    threads = max(1, min(max_threads, os.cpu_count() or 1))
+    cells = props = done = 0
+    t0 = time.perf_counter()
+    for t, reads in clusters:
+        _, c = oracle.cpu_pass(t, reads, nthreads=threads)
+        cells += c
+        props += 8 * len(t) + 4
+        done += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": cells / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
+            "proposals_per_s": props / dt,
+            "sample": f"{done} cluster(s) x {len(clusters[0][1])} reads x {len(clusters[0][0])} bp, "
+                      f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--clusters", type=int, default=None, help="clusters per rank (override)")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+
+    nclu, nreads, length, err, bw, label = CONFIGS[args.config]
+    if args.clusters is not None:
+        nclu = args.clusters
+    t_gen = time.perf_counter()
+    clusters = make_workload(nclu, nreads, length, err, bw, seed=args.seed * 1000003 + rank)
+    gen_s = time.perf_counter() - t_gen
+
+    from rifraf_amd.engine import RF_BWD, RF_FWD, Engine
+    eng = Engine(local)
+    reads = [r for _, rs in clusters for r in rs]
+    tpl_of = np.concatenate([[c] * len(rs) for c, (_, rs) in enumerate(clusters)]).astype(np.int32)
+    nr = len(reads)
+    cells = 0
+    band_bytes = 0
+    for c, (t, rs) in enumerate(clusters):
+        for r in rs:
+            cells += 2 * band_cells(len(r), len(t), r.bandwidth)
+            band_bytes += 2 * 8 * (2 * r.bandwidth + abs(len(r) - len(t)) + 1) * (len(t) + 1)
+    eng.reserve(int(band_bytes * 1.05) + (64 << 20))
+    for a in range(0, nr, 4096):
+        eng.set_sequences(a, reads[a:a + 4096])
+    eng.set_templates(0, [t for t, _ in clusters])
+    slots = np.arange(nr, dtype=np.int32)
+    bws = np.array([r.bandwidth for r in reads], np.int32)
+    groups, at = [], 0
+    for _, rs in clusters:
+        groups.append(np.arange(at, at + len(rs), dtype=np.int32))
+        at += len(rs)
+    nprops = sum(8 * len(t) + 4 for t, _ in clusters)
+    npairs = sum((8 * len(t) + 4) * len(rs) for t, rs in clusters)
+    # algorithmic bytes: DP = 8 B stored per in-band cell;
+    # scoring = A + B in-band cells read once + 33 B of tables per read row +
+    # 72 B of totals per consensus position
+    dp_bytes = 8 * cells
+    score_bytes = 8 * cells + sum(33 * (len(r) + 1) for r in reads) + sum(72 * (len(t) + 1) for t, _ in clusters)
+
+    def step():
+        eng.realign(slots, slots, tpl_of, bws, RF_FWD | RF_BWD)
+        dp_ms, _, _ = eng.last_timing()
+        eng.score_dense(groups, to_host=False)
+        _, sc_ms, _ = eng.last_timing()
+        return dp_ms, sc_ms
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dps, scs = [], []
+    for _ in range(args.steps):
+        a, b = step()
+        dps.append(a)
+        scs.append(b)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot_cells, tot_props, tot_pairs = cells, nprops, npairs
+    if dist is not None:
+        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([cells, nprops, npairs], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        tot_cells, tot_props, tot_pairs = (float(x) for x in c.tolist())
+
+    ms_step = elapsed / args.steps * 1e3
+    dp_ms = float(np.mean(dps))
+    sc_ms = float(np.mean(scs))
+    dp_gbs = dp_bytes / (dp_ms * 1e-3) / 1e9
+    sc_gbs = score_bytes / (sc_ms * 1e-3) / 1e9
+    dominant = "k_score" if sc_ms >= dp_ms else "k_dp"
+    ach, byt, ms = (sc_gbs, score_bytes, sc_ms) if dominant == "k_score" else (dp_gbs, dp_bytes, dp_ms)
+    traffic = None
+    pmc_file = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(pmc_file):
+        try:
+            pm = json.load(open(pmc_file))
+            if pm.get("clusters") == nclu and dominant in pm.get("kernels", {}):
+                traffic = pm["kernels"][dominant]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+    result = {
+        "metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
+        "value": tot_cells / elapsed / 1e9,
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (restated sample.jl simulator, seeded)",
+        "config": {"workload": args.config, "description": label, "clusters_per_gpu": nclu,
+                   "reads_per_cluster": nreads, "template_len": length, "error_rate": err,
+                   "bandwidth": bw, "parallelism": f"clusters sharded over {world} rank(s)"},
+        "proposals_per_s": tot_props / elapsed,
+        "pairs_per_s": tot_pairs / elapsed,
+        "dp_ms": dp_ms,
+        "score_ms": sc_ms,
+        "dp_gcups_kernel": cells / (dp_ms * 1e-3) / 1e9,
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes": byt, "launch_ms": ms},
+        "roofline_other": {"k_dp": {"achieved": dp_gbs, "frac": dp_gbs / HBM_PEAK_GBS,
+                                    "bytes": dp_bytes, "ms": dp_ms},
+                           "k_score": {"achieved": sc_gbs, "frac": sc_gbs / HBM_PEAK_GBS,
+                                       "bytes": score_bytes, "ms": sc_ms}},
+        "setup_s": gen_s,
+    }
+    if rank == 0:
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(clusters, budget_s=args.cpu_budget)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

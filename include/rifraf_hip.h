@@ -127,6 +127,19 @@ int rf_score(rf_ctx *ctx, int32_t ngroups,
              const uint8_t *kind, const int32_t *pos, const uint8_t *base,
              double *out_total, double *out_per_seq);
 
+/* Dense scoring of every proposal anchored at every consensus position --
+ * the STAGE_SCORE all_proposals set (model.jl:401-456) that estimate_probs
+ * scores (model.jl:737-791) -- for batch reads only (no reference):
+ * out[(row_g + p) * 9 + k] = 0.0 + s_1 + ... + s_R for p = 0..m_g, with
+ * k = 0..3 Substitution(p, A/C/G/T) (the consensus base's own slot is not a
+ * proposal), k = 4 Deletion(p), k = 5..8 Insertion(p, A/C/G/T);
+ * row_g = sum over h < g of (m_h + 1).  Sub/Del slots of p = 0 are NaN.
+ * A failed update or a -Inf sum is reported as NaN in that slot (the
+ * reference raises on such a proposal when it scores it).
+ * out may be NULL: totals then stay on the device. */
+int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
+                   const int32_t *slots, double *out);
+
 /* Geometry of a slot's band: nrows = n+1, ncols = m+1, bandwidth, H. */
 int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,
                      int32_t *nrows, int32_t *ncols, int32_t *bw, int32_t *H);

@@ -177,6 +177,28 @@ class Engine:
             at += cnt * w
         return totals, mats
 
+    def score_dense(self, groups, to_host: bool = True, rows=None):
+        """Dense all-proposals scoring (rf_score_dense).  groups: list of
+        batch-slot arrays (one per cluster).  Returns a list of (m_g+1, 9)
+        arrays (or None when to_host is False: totals stay in HBM)."""
+        G = len(groups)
+        slot_off = np.zeros(G + 1, np.int32)
+        for g, sl in enumerate(groups):
+            slot_off[g + 1] = slot_off[g] + len(sl)
+        slots = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in groups]), np.int32)
+        if not to_host:
+            self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), None))
+            return None
+        if rows is None:
+            rows = [self.geometry(int(sl[0]), RF_BAND_A)[1] for sl in groups]
+        out = np.empty((int(sum(rows)), 9))
+        self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), ptr(out)))
+        res, at = [], 0
+        for r in rows:
+            res.append(out[at:at + r])
+            at += r
+        return res
+
     def geometry(self, slot: int, which: int = RF_BAND_A):
         nr, nc, bw, H = c_int32(), c_int32(), c_int32(), c_int32()
         self._check(self.lib.rf_slot_geometry(self.ctx, int(slot), int(which), byref(nr), byref(nc),

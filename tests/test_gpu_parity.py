@@ -235,3 +235,62 @@ def test_errors_are_loud(engine):
     engine.realign([1], [1], 0, [3], RF_FWD | RF_BWD)
     with pytest.raises(RifrafError, match="codon"):
         engine.score([([1], -1, all_proposals_arrays(t))])
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_score_dense_clusters(engine, monkeypatch, mode):
+    """rf_score_dense over several clusters == oracle all-proposals pass."""
+    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    rng = np.random.default_rng(123)
+    templates, seqs = [], []
+    for c in range(5):
+        t = random_seq(int(rng.integers(60, 140)), rng)
+        templates.append(t)
+        seqs.append([make_read(t, rng, 0.03, 9) for _ in range(int(rng.integers(1, 6)))])
+    flat = [r for rs in seqs for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), tpl, [9] * n, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in seqs:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    got = engine.score_dense(groups)
+    for c in range(5):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        t = templates[c]
+        mask = np.ones_like(ref_tot, bool)
+        mask[0, :5] = False                       # p = 0 has no sub/del
+        for j in range(1, len(t) + 1):
+            mask[j, t[j - 1]] = False             # not a proposal
+        np.testing.assert_array_equal(got[c][mask], ref_tot[mask])
+
+
+def test_plan_cache_follows_template_content(engine):
+    """A repeated realign/score with identical arguments reuses the uploaded
+    plan; a same-length consensus change must still be picked up."""
+    rng = np.random.default_rng(77)
+    t1 = random_seq(90, rng)
+    t2 = t1.copy()
+    t2[40:45] = (t2[40:45] + 1) % 4
+    seqs = [make_read(t1, rng, 0.03, 9) for _ in range(4)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t1])
+    sl = np.arange(4)
+    s1 = engine.realign(sl, sl, 0, [9] * 4, RF_FWD | RF_BWD)
+    d1 = engine.score_dense([sl])[0]
+    engine.set_templates(0, [t2])
+    s2 = engine.realign(sl, sl, 0, [9] * 4, RF_FWD | RF_BWD)
+    d2 = engine.score_dense([sl])[0]
+    ref2, _ = oracle.cpu_pass(t2, seqs, nthreads=2)
+    for k, s in enumerate(seqs):
+        A_exp, _ = oracle.forward(t2, s)
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(s) + 1, 91, 9)
+    assert not np.array_equal(s1, s2)
+    np.testing.assert_array_equal(d2[1:, 5:], ref2[1:, 5:])
+    engine.set_templates(0, [t1])
+    s3 = engine.realign(sl, sl, 0, [9] * 4, RF_FWD | RF_BWD)
+    np.testing.assert_array_equal(s3, s1)
+    np.testing.assert_array_equal(engine.score_dense([sl])[0][1:, 5:], d1[1:, 5:])
