@@ -35,6 +35,29 @@
 #define RF_INF (__builtin_inf())
 
 // ---------------------------------------------------------------------
+// Band storage on the device: anti-diagonal-major ("kappa-major")
+//
+//   d     = ii - jj + c    0-based data row of the reference layout
+//                          (bandedarrays.jl:109-114), c = h_off + bw
+//   kappa = d + 2*jj       anti-diagonal of cell (ii, jj)
+//   element (d, jj) lives at band[kappa * P + (d >> 1)],
+//   P = ceil(H/2) | 1 (odd row stride), kappa in [0, K), K = H + 2m.
+//
+// A kappa row holds one anti-diagonal (all band rows d of one parity), so the
+// DP fill stores every step as one contiguous run, and a window of columns
+// is one contiguous block of rows for the scorer.  The reference's
+// column-major `data` is produced on download (rf_download_band).
+// ---------------------------------------------------------------------
+
+__host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
+__host__ __device__ inline int64_t band_K(int H, int m) { return (int64_t)H + 2 * (int64_t)m; }
+
+__device__ __forceinline__ size_t bidx(int d, int jj, int P)
+{
+    return (size_t)(d + 2 * jj) * (size_t)P + (size_t)(d >> 1);
+}
+
+// ---------------------------------------------------------------------
 // device-side descriptors
 // ---------------------------------------------------------------------
 
@@ -49,8 +72,9 @@ struct alignas(16) DPTask {
     int32_t ncins, ncdel;
     int32_t flags;  // 1 = reverse, 2 = skew, 4 = trim
     int32_t out_idx;
-    int32_t klen;   // number of anti-diagonals = H + 2m
-    int32_t pad[2];
+    int32_t klen;   // number of anti-diagonals K = H + 2m
+    int32_t P;      // kappa row stride
+    int32_t pad;
 };
 
 // One batch read of a scoring group.
@@ -59,7 +83,8 @@ struct alignas(16) ScoreRead {
     int64_t sb, tab;  // sequence bases / tables
     int32_t n, bw, H, c;
     int32_t vb;       // v_off + bw
-    int32_t pad[3];
+    int32_t P, K;
+    int32_t pad;
 };
 
 struct alignas(16) ScoreGroup {
@@ -81,13 +106,14 @@ struct alignas(16) CodonTask {
     int32_t ncins, ncdel;
     int32_t kind, pos, base;
     int32_t out_idx;
-    int32_t pad[2];
+    int32_t P, pad;
 };
 
 struct alignas(16) BTTask {
     int64_t A, sb, tab, tb, out;
     int32_t n, m, bw, H;
     int32_t ncins, ncdel, flags, idx;
+    int32_t P, pad[3];
 };
 
 // error word: first error code wins (atomicCAS)
@@ -96,52 +122,60 @@ __device__ __forceinline__ void set_err(int *err, int code)
     atomicCAS(err, 0, code);
 }
 
+// Order LDS traffic between the lanes of one wave: LDS instructions of a
+// wave execute in issue order, so only the compiler has to be fenced.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------------
 // k_dp: anti-diagonal wavefront DP fill
 //
-// Band coordinates: d = ii - jj + c (0-based data row), jj = 0-based column,
-// kappa = d + 2*jj (anti-diagonal).  Cell (ii, jj) depends on kappa-1
-// (insert: d-1, delete: d+1), kappa-2 (match: d) and kappa-3 (codon insert
-// d-3, codon delete d+3).  Lane q of a W-lane segment owns the pair of band
-// rows {2q, 2q+1}; at anti-diagonal kappa it computes d = 2q + (kappa & 1),
-// so every lane produces one cell per step.  The last four anti-diagonals
-// live in an LDS ring padded with -Inf sentinels; out-of-band predecessors
-// read -Inf, which never wins the strict '>' (align.jl:43) -- identical to the
-// reference's inband() skip.  Evaluation order of the five candidates is
-// the reference's; every cell is the same FP64 additions, so A/B are
-// bit-identical to the scalar reference.
+// Cell (ii, jj) depends on kappa-1 (insert: d-1, delete: d+1), kappa-2
+// (match: d) and kappa-3 (codon insert d-3, codon delete d+3).  Lane q of a
+// W-lane segment owns the pair of band rows {2q, 2q+1}; at anti-diagonal
+// kappa it computes d = 2q + (kappa & 1), so every lane produces one cell per
+// step (lanes loop over further pairs when H > 2W).  One task per segment,
+// 64/W tasks per single-wave workgroup; the last four anti-diagonals live in
+// an LDS ring padded with -Inf sentinels.  Out-of-band predecessors read
+// -Inf, which never wins the strict '>' (align.jl:43) -- identical to the
+// reference's inband() skip.  The candidates are evaluated in the
+// reference's order with the same FP64 additions, so A/B are bit-identical
+// to the scalar reference.  Each step's cells are one contiguous run of the
+// kappa-major band; the reverse pass stores in flip!'ed position
+// (bandedarrays.jl:176-198): kappa' = K-1-kappa, d' = H-1-d.
 // ---------------------------------------------------------------------
 
 template <int W, bool GRING>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64)
 k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
      const double *__restrict__ tabs, double *__restrict__ bands,
      double *__restrict__ out_score, int *__restrict__ err, int ring_ld,
      double *__restrict__ gring)
 {
-    constexpr int SEGS = (W == 64) ? 1 : 256 / W;
-    // all LDS in the dynamic region: word 0 = block max kappa, ring from +16 B
+    constexpr int SEGS = 64 / W;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    int &kmax_s = *reinterpret_cast<int *>(smem);
     const int seg = threadIdx.x / W;
     const int q = threadIdx.x % W;
     const int tid = blockIdx.x * SEGS + seg;
-    const bool active = tid < ntasks;
 
     DPTask T = {};
-    if (active)
+    if (tid < ntasks)
         T = tasks[tid];
     double *ring = GRING ? gring + (size_t)blockIdx.x * 4 * ring_ld
-                         : smem + 2 + (size_t)seg * 4 * ring_ld;
-    if (threadIdx.x == 0)
-        kmax_s = 0;
+                         : smem + (size_t)seg * 4 * ring_ld;
     for (int e = q; e < 4 * ring_ld; e += W)
         ring[e] = -RF_INF;
-    __syncthreads();
-    if (q == 0 && active)
-        atomicMax(&kmax_s, T.klen);
-    __syncthreads();
-    const int kmax = kmax_s;
+    int kmax = T.klen;
+    for (int off = 32; off >= 1; off >>= 1)
+        kmax = max(kmax, __shfl_xor(kmax, off));
+    if (GRING)
+        __syncthreads();
+    else
+        wave_sync();
 
     const bool rev = T.flags & 1;
     const bool skew = T.flags & 2;
@@ -164,6 +198,7 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
             const double *r1 = ring + ((k - 1) & 3) * ring_ld + 3;
             const double *r2 = ring + ((k - 2) & 3) * ring_ld + 3;
             const double *r3 = ring + ((k - 3) & 3) * ring_ld + 3;
+            double *row = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
             for (int pp = q;; pp += W) {
                 const int d = 2 * pp + par;
                 if (d >= T.H || d > k)
@@ -212,16 +247,15 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
                         if (ii == T.n && jj == T.m && out_score)
                             out_score[T.out_idx] = v;
                     }
-                    // store in the reference layout; the reverse pass lands
-                    // directly in flip!'ed position (bandedarrays.jl:176-198)
-                    const size_t idx = rev ? (size_t)(T.m - jj) * T.H + (T.H - 1 - d)
-                                           : (size_t)jj * T.H + d;
-                    band[idx] = v;
                 }
+                row[(rev ? T.H - 1 - d : d) >> 1] = v;
                 r0[d] = v;
             }
         }
-        __syncthreads();
+        if (GRING)
+            __syncthreads();
+        else
+            wave_sync();
     }
 }
 
@@ -233,25 +267,33 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
 // to the consensus base is never requested), Deletion(p), Insertion(p, b) --
 // from A columns p-1 and p and B column p (0-based), exactly as
 // score_nocodon (model.jl:242-285) and seq_score_deletion (:227-236) do,
-// with new columns built by the reference's update order.  The per-read
+// with new columns built in the reference's update order.  The per-read
 // results are left-folded over the group's reads in batch order
 // (model.jl:389-393).  Output slots: 0-3 sub A,C,G,T; 4 del; 5-8 ins A,C,G,T.
 // A failed update ("new score is invalid") or a -Inf sum ("failed to compute
 // a valid score") is reported as NaN in that slot.
+//
+// The A/B kappa rows covering the 64 positions of a work item are one
+// contiguous block; it is staged through LDS with coalesced loads when it
+// fits (the common narrow band), otherwise read in place.
 // ---------------------------------------------------------------------
 
-__device__ __forceinline__ double band_at(const double *col, int d, int ii, int H, int n)
-{
-    return (d >= 0 && d < H && ii >= 0 && ii <= n) ? col[d] : -RF_INF;
-}
+constexpr int SCORE_C = 64;    // positions per work item
+
+// Accessor of a band window: rows [k0, ...) of a kappa-major band.
+struct BandWin {
+    const double *base;
+    int k0, P;
+    __device__ __forceinline__ double at(int d, int jj) const
+    {
+        return base[(size_t)(d + 2 * jj - k0) * P + (d >> 1)];
+    }
+};
 
 __device__ __forceinline__ void score_position(int p, int m, const ScoreRead &R,
                                                const uint8_t *__restrict__ s,
                                                const double *__restrict__ tb,
-                                               const double *__restrict__ Acol_m1,
-                                               const double *__restrict__ Acol0,
-                                               const double *__restrict__ Bcol0,
-                                               double out[9])
+                                               const BandWin A, const BandWin B, double out[9])
 {
     const int n = R.n, H = R.H, c = R.c, vb = R.vb;
     const double *t_match = tb;
@@ -260,9 +302,8 @@ __device__ __forceinline__ void score_position(int p, int m, const ScoreRead &R,
     const double *t_del = tb + 3 * (size_t)n;
 
     // row ranges (bandedarrays.jl:133-137), 0-based rows
-    const int pS = p;                       // Sub new column / B column
     const int pI = min(p + 1, m);           // Ins new column's row range
-    const int s0 = max(0, pS - c), s1 = min(pS + vb, n);           // rows(p)
+    const int s0 = max(0, p - c), s1 = min(p + vb, n);             // rows(p)
     const int i0 = max(0, pI - c), i1 = min(pI + vb, n);           // rows(pI)
     const int d0 = max(0, p - 1 - c), d1 = min(p - 1 + vb, n);     // rows(p-1)
     const bool has_sd = p >= 1;
@@ -280,23 +321,23 @@ __device__ __forceinline__ void score_position(int p, int m, const ScoreRead &R,
     }
     double del_acc = -RF_INF;
 
+    // A(p-1, ii) in band iff ii in rows(p-1); A(p, ii), B(p, ii) iff ii in rows(p)
+    auto Am1 = [&](int ii) { return (has_sd && ii >= d0 && ii <= d1) ? A.at(ii - (p - 1) + c, p - 1) : -RF_INF; };
+    auto A0 = [&](int ii) { return (ii >= s0 && ii <= s1) ? A.at(ii - p + c, p) : -RF_INF; };
+
     const int lo = has_sd ? d0 : s0;
     const int hi = i1;
-    // rolling A values: A(p-1, ii-1), A(p, ii-1)
-    double am1_prev = -RF_INF, a0_prev = -RF_INF;
-    if (lo >= 1) {
-        am1_prev = has_sd ? band_at(Acol_m1, lo - 1 - (p - 1) + c, lo - 1, H, n) : -RF_INF;
-        a0_prev = band_at(Acol0, lo - 1 - p + c, lo - 1, H, n);
-    }
+    double am1_prev = lo >= 1 ? Am1(lo - 1) : -RF_INF;
+    double a0_prev = lo >= 1 ? A0(lo - 1) : -RF_INF;
     for (int ii = lo; ii <= hi; ++ii) {
-        const double am1 = has_sd ? band_at(Acol_m1, ii - (p - 1) + c, ii, H, n) : -RF_INF;
-        const double a0 = band_at(Acol0, ii - p + c, ii, H, n);
-        const double b0 = band_at(Bcol0, ii - p + c, ii, H, n);
+        const double am1 = Am1(ii);
+        const double a0 = A0(ii);
+        const bool in_s = ii >= s0 && ii <= s1;
+        const double b0 = in_s ? B.at(ii - p + c, p) : -RF_INF;
         const int sb = ii >= 1 ? s[ii - 1] : 4;
         const int ks = max(ii - 1, 0);
         const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
         const double ds = t_del[ii];
-        const bool in_s = ii >= s0 && ii <= s1;
         if (has_sd && in_s) {
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -344,19 +385,20 @@ __device__ __forceinline__ void score_position(int p, int m, const ScoreRead &R,
     out[4] = has_sd ? del_acc : qnan;
 }
 
-// grid.x = work items (group, chunk of 64 positions); grid.y = read index in
-// split mode.  Fused mode folds all reads of the group in batch order.
+// grid.x = work items (group, chunk of SCORE_C positions); grid.y = read
+// index in split mode.  Fused mode folds all reads of the group in batch
+// order.  lds_rows: kappa rows the dynamic LDS holds per band (0 = never
+// stage).
 __global__ void __launch_bounds__(64)
 k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
         const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
         const double *__restrict__ tabs, const double *__restrict__ bands,
-        double *__restrict__ dense, double *__restrict__ split, int split_mode)
+        double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
 {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
     const WorkItem w = items[blockIdx.x];
     const ScoreGroup G = groups[w.group];
     const int p = w.p0 + threadIdx.x;
-    if (p > G.m)
-        return;
     int r0 = G.r0, r1 = G.r1;
     if (split_mode) {
         r0 = G.r0 + blockIdx.y;
@@ -368,19 +410,44 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
 #pragma unroll
     for (int k = 0; k < 9; ++k)
         tot[k] = 0.0;
+    double *sA = smem;
+    double *sB = smem + lds_elems;
+    const int k0 = 2 * (w.p0 - 1);                    // window's first kappa row
     for (int r = r0; r < r1; ++r) {
         const ScoreRead R = reads[r];
         const double *A = bands + R.A;
         const double *B = bands + R.B;
-        const double *Acol_m1 = p >= 1 ? A + (size_t)(p - 1) * R.H : A;
-        const double *Acol0 = A + (size_t)p * R.H;
-        const double *Bcol0 = B + (size_t)p * R.H;
+        const int kend = min(k0 + 2 * SCORE_C + R.H, R.K);
+        const int kbeg = max(k0, 0);
+        const int nel = (kend - kbeg) * R.P;
+        const bool stage = (k0 + 2 * SCORE_C + R.H - k0) * R.P <= lds_elems;
         double s[9];
-        score_position(p, G.m, R, bases + R.sb, tabs + R.tab, Acol_m1, Acol0, Bcol0, s);
+        if (stage) {
+            // contiguous kappa rows -> LDS, coalesced
+            const int off = (kbeg - k0) * R.P;
+            const double *ga = A + (size_t)kbeg * R.P;
+            const double *gb = B + (size_t)kbeg * R.P;
+            for (int e = threadIdx.x; e < nel; e += 64) {
+                sA[off + e] = ga[e];
+                sB[off + e] = gb[e];
+            }
+            wave_sync();
+            if (p <= G.m)
+                score_position(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{sA, k0, R.P},
+                               BandWin{sB, k0, R.P}, s);
+            wave_sync();
+        } else if (p <= G.m) {
+            score_position(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{A, 0, R.P},
+                           BandWin{B, 0, R.P}, s);
+        }
+        if (p <= G.m) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k)
-            tot[k] += s[k];
+            for (int k = 0; k < 9; ++k)
+                tot[k] += s[k];
+        }
     }
+    if (p > G.m)
+        return;
     double *dst = split_mode ? split + G.split_off + ((size_t)blockIdx.y * (G.m + 1) + p) * 9
                              : dense + G.dense_off + (size_t)p * 9;
 #pragma unroll
@@ -396,7 +463,7 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total)
         return;
-    // find group (gstart: prefix of (m+1)*9 per group)
+    // find group (gstart: prefix of (m+1)*9 per group; empty groups skipped)
     int lo = 0, hi = ngroups - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -418,35 +485,33 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
 // k_codon: codon-move scoring, one lane per proposal (model.jl:302-383)
 // ---------------------------------------------------------------------
 
-__device__ __forceinline__ bool inband0(int ii, int jj, int n, int m, int bw, int H)
-{
-    // 0-based cell (ii, jj) of an (n+1) x (m+1) band
-    if (ii < 0 || jj < 0 || ii > n || jj > m)
-        return false;
-    const int c = max(m - n, 0) + bw;
-    const int d = ii - jj + c;
-    return d >= 0 && d < H;
-}
-
-__device__ __forceinline__ double aget(const double *A, int ii, int jj, int n, int m, int bw, int H)
-{
-    const int c = max(m - n, 0) + bw;
-    return A[(size_t)jj * H + (ii - jj + c)];
-}
-
-__device__ __forceinline__ void rows0(int jj, int n, int m, int bw, int &a, int &b)
-{
-    const int h_off = max(m - n, 0), v_off = max(n - m, 0);
-    a = max(0, jj - h_off - bw);
-    b = min(jj + v_off + bw, n);
-}
+struct Geo {
+    int n, m, bw, H, P, c;
+    __device__ __forceinline__ bool inband(int ii, int jj) const
+    {
+        // 0-based cell (ii, jj) of an (n+1) x (m+1) band (bandedarrays.jl:151-157)
+        if (ii < 0 || jj < 0 || ii > n || jj > m)
+            return false;
+        const int d = ii - jj + c;
+        return d >= 0 && d < H;
+    }
+    __device__ __forceinline__ double get(const double *band, int ii, int jj) const
+    {
+        return band[bidx(ii - jj + c, jj, P)];
+    }
+    __device__ __forceinline__ void rows(int jj, int &a, int &b) const
+    {
+        a = max(0, jj - max(m - n, 0) - bw);
+        b = min(jj + max(n - m, 0) + bw, n);
+    }
+};
 
 // align.jl:50-112 with newcols / acol (1-based i, j like the reference)
-__device__ bool update_nc(const double *A, const double *nc, int ncld, int acol, int i, int j,
-                          int s_base, int t_base, const double *tb, int n, int m, int bw, int H,
-                          int ncins, int ncdel, double &out)
+__device__ bool update_nc(const Geo &g, const double *A, const double *nc, int ncld, int acol,
+                          int i, int j, int s_base, int t_base, const double *tb, int ncins,
+                          int ncdel, double &out)
 {
-    const int ncols = m + 1;
+    const int n = g.n, ncols = g.m + 1;
     const int seq_i = max(i - 1, 1);
     const int del_i = i;
     const double ms = (s_base == t_base) ? tb[seq_i - 1] : tb[n + seq_i - 1];
@@ -459,8 +524,8 @@ __device__ bool update_nc(const double *A, const double *nc, int ncld, int acol,
     auto helper = [&](double msc, int move, int a, int b) {
         const int pi = i - a, pj = j - b;
         const int rc = min(pj, ncols);
-        if (inband0(pi - 1, rc - 1, n, m, bw, H)) {
-            const double v = (acol < 1 || pj <= acol) ? aget(A, pi - 1, pj - 1, n, m, bw, H)
+        if (g.inband(pi - 1, rc - 1)) {
+            const double v = (acol < 1 || pj <= acol) ? g.get(A, pi - 1, pj - 1)
                                                       : nc[(size_t)(pi - 1) + (size_t)ncld * (pj - acol - 1)];
             const double sc = v + msc;
             if (sc > best) {
@@ -482,18 +547,19 @@ __device__ bool update_nc(const double *A, const double *nc, int ncld, int acol,
     return best != -RF_INF && mv != 0;
 }
 
-__device__ double summax_nc(const double *acolvals, int imn, int imx, const double *B, int bj,
-                            int n, int m, int bw, int H)
+// equal_ranges((imn,imx), row_range(B, bj)) then summax (1-based rows);
+// acolvals indexed by absolute 1-based row
+__device__ double summax_nc(const Geo &g, const double *acolvals, int imn, int imx,
+                            const double *B, int bj)
 {
-    // equal_ranges((imn,imx), row_range(B, bj)) then summax (1-based rows)
     int bs, be;
-    rows0(bj - 1, n, m, bw, bs, be);
+    g.rows(bj - 1, bs, be);
     bs += 1;
     be += 1;
     const int lo = max(imn, bs), hi = min(imx, be);
     double r = -RF_INF;
     for (int i = lo; i <= hi; ++i) {
-        const double x = acolvals[i - 1] + aget(B, i - 1, bj - 1, n, m, bw, H);
+        const double x = acolvals[i - 1] + g.get(B, i - 1, bj - 1);
         r = (i == lo) ? x : fmax(r, x);
     }
     return r;
@@ -515,25 +581,29 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
     const uint8_t *cons = bases + T.tb;
     const double *tb = tabs + T.tab;
     double *nc = scratch + T.scratch;
-    const int n = T.n, m = T.m, bw = T.bw, H = T.H;
+    Geo g;
+    g.n = T.n;
+    g.m = T.m;
+    g.bw = T.bw;
+    g.H = T.H;
+    g.P = T.P;
+    g.c = max(T.m - T.n, 0) + T.bw;
+    const int n = T.n, m = T.m;
     const int nrows = n + 1, ncols = m + 1;
     const int kind = T.kind, pos = T.pos;
-    double result = qnan;
 
     if (T.ncins == 0 && T.ncdel == 0) {
         // score_nocodon on a single sequence (model.jl:242-285)
+        double result = qnan;
         if (kind == 2) {
-            int as, ae;
-            rows0(pos - 1, n, m, bw, as, ae);
-            double colv[1];
-            (void)colv;
-            // seq_score_deletion: summax(A col pos, B col pos+1)
-            int bs, be;
-            rows0(pos, n, m, bw, bs, be);
+            // seq_score_deletion: summax(A col pos, B col pos+1) (model.jl:227-236)
+            int as, ae, bs, be;
+            g.rows(pos - 1, as, ae);
+            g.rows(pos, bs, be);
             const int lo = max(as, bs), hi = min(ae, be);
             double r = -RF_INF;
             for (int i = lo; i <= hi; ++i) {
-                const double x = aget(A, i, pos - 1, n, m, bw, H) + aget(B, i, pos, n, m, bw, H);
+                const double x = g.get(A, i, pos - 1) + g.get(B, i, pos);
                 r = (i == lo) ? x : fmax(r, x);
             }
             result = r;
@@ -541,19 +611,18 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
             const int acol = pos + (kind == 0 ? 0 : 1);
             const int new_acol = acol + 1;
             int amin, amax;
-            rows0(min(new_acol, ncols) - 1, n, m, bw, amin, amax);
+            g.rows(min(new_acol, ncols) - 1, amin, amax);
             amin += 1;
             amax += 1;
             bool ok = true;
             for (int i = amin; i <= amax && ok; ++i) {
                 const int sb = i > 1 ? s[i - 2] : 4;
                 double v;
-                ok = update_nc(A, nc, nrows, acol, i, new_acol, sb, T.base, tb, n, m, bw, H,
-                               0, 0, v);
+                ok = update_nc(g, A, nc, nrows, acol, i, new_acol, sb, T.base, tb, 0, 0, v);
                 nc[i - 1] = v;
             }
             if (ok) {
-                const double sc = summax_nc(nc, amin, amax, B, pos + 1, n, m, bw, H);
+                const double sc = summax_nc(g, nc, amin, amax, B, pos + 1);
                 result = (sc == -RF_INF) ? qnan : sc;
             }
         }
@@ -566,7 +635,7 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
     const int first_bcol = acol + (kind == 1 ? 1 : 2);
     const int last_bcol = first_bcol + 2;
     if (kind == 2 && acol == ncols - 1) {
-        out[T.out_idx] = aget(A, nrows - 1, ncols - 2, n, m, bw, H);
+        out[T.out_idx] = g.get(A, nrows - 1, ncols - 2);
         return;
     }
     const bool just_a = last_bcol >= ncols;
@@ -592,14 +661,14 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
     for (int j = 1; j <= n_new && ok; ++j) {
         const int range_col = min(acol + j, ncols);
         int amin, amax;
-        rows0(range_col - 1, n, m, bw, amin, amax);
+        g.rows(range_col - 1, amin, amax);
         amin += 1;
         amax += 1;
         for (int i = amin; i <= amax && ok; ++i) {
             const int sb = i > 1 ? s[i - 2] : 4;
             double v;
-            ok = update_nc(A, nc, nrows, acol, i, acol + j, sb, sub[j - 1], tb, n, m, bw, H,
-                           T.ncins, T.ncdel, v);
+            ok = update_nc(g, A, nc, nrows, acol, i, acol + j, sb, sub[j - 1], tb, T.ncins,
+                           T.ncdel, v);
             nc[(size_t)(i - 1) + (size_t)nrows * (j - 1)] = v;
         }
     }
@@ -615,7 +684,7 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
     for (int j = 1; j <= 3; ++j) {
         const int new_j = n_new - 3 + j;
         int imn, imx;
-        rows0(min(acol + new_j, ncols) - 1, n, m, bw, imn, imx);
+        g.rows(min(acol + new_j, ncols) - 1, imn, imx);
         imn += 1;
         imx += 1;
         const int bj = first_bcol + j - 1;
@@ -623,7 +692,7 @@ __global__ void k_codon(const CodonTask *__restrict__ tasks, int ntasks,
             best = qnan;
             break;
         }
-        const double sc = summax_nc(nc + (size_t)nrows * (new_j - 1), imn, imx, B, bj, n, m, bw, H);
+        const double sc = summax_nc(g, nc + (size_t)nrows * (new_j - 1), imn, imx, B, bj);
         if (sc > best)
             best = sc;
     }
@@ -676,7 +745,14 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
     const uint8_t *s = bases + T.sb;
     const uint8_t *tt = bases + T.tb;
     const double *tb = tabs + T.tab;
-    const int n = T.n, m = T.m, bw = T.bw, H = T.H;
+    const int n = T.n, m = T.m;
+    Geo g;
+    g.n = n;
+    g.m = m;
+    g.bw = T.bw;
+    g.H = T.H;
+    g.P = T.P;
+    g.c = max(m - n, 0) + T.bw;
     const double *t_cins = tb + 4 * (size_t)n + 1;
     const double *t_cdel = t_cins + T.ncins;
     const bool skew = T.flags & 2, trim = T.flags & 4;
@@ -695,24 +771,24 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
             is = 0.0;
         double best = -RF_INF, x;
         int mv = 0;
-        if (inband0(ii - 1, jj - 1, n, m, bw, H)) {
-            x = aget(A, ii - 1, jj - 1, n, m, bw, H) + ms;
+        if (g.inband(ii - 1, jj - 1)) {
+            x = g.get(A, ii - 1, jj - 1) + ms;
             if (x > best) { best = x; mv = 1; }
         }
-        if (inband0(ii - 1, jj, n, m, bw, H)) {
-            x = aget(A, ii - 1, jj, n, m, bw, H) + is;
+        if (g.inband(ii - 1, jj)) {
+            x = g.get(A, ii - 1, jj) + is;
             if (x > best) { best = x; mv = 2; }
         }
-        if (inband0(ii, jj - 1, n, m, bw, H)) {
-            x = aget(A, ii, jj - 1, n, m, bw, H) + ds;
+        if (g.inband(ii, jj - 1)) {
+            x = g.get(A, ii, jj - 1) + ds;
             if (x > best) { best = x; mv = 3; }
         }
-        if (T.ncins > 0 && ii >= 3 && inband0(ii - 3, jj, n, m, bw, H)) {
-            x = aget(A, ii - 3, jj, n, m, bw, H) + t_cins[ii - 3];
+        if (T.ncins > 0 && ii >= 3 && g.inband(ii - 3, jj)) {
+            x = g.get(A, ii - 3, jj) + t_cins[ii - 3];
             if (x > best) { best = x; mv = 4; }
         }
-        if (T.ncdel > 0 && jj >= 3 && inband0(ii, jj - 3, n, m, bw, H)) {
-            x = aget(A, ii, jj - 3, n, m, bw, H) + t_cdel[ii];
+        if (T.ncdel > 0 && jj >= 3 && g.inband(ii, jj - 3)) {
+            x = g.get(A, ii, jj - 3) + t_cdel[ii];
             if (x > best) { best = x; mv = 5; }
         }
         if (mv == 0 || cnt >= n + m) {
@@ -815,7 +891,7 @@ struct rf_ctx {
         uint64_t gen = 0;
         std::vector<int32_t> slot_off, slots;
         size_t nitems = 0;
-        int max_reads = 0, ngroups = 0;
+        int max_reads = 0, ngroups = 0, lds_elems = 0;
         int64_t dense_total = 0, split_total = 0;
     } dplan;
 };
@@ -961,6 +1037,22 @@ int check_err(rf_ctx *ctx)
 }
 
 int band_rows(int n, int m, int bw) { return 2 * bw + std::abs(n - m) + 1; }
+
+// k_score stages the kappa rows of a work item through LDS; size the
+// per-band buffer for the 90th-percentile window (at most 24 KB per band,
+// two bands per single-wave block), larger windows read in place.
+int score_lds_elems(const std::vector<ScoreRead> &reads)
+{
+    if (reads.empty())
+        return 0;
+    std::vector<int> w;
+    w.reserve(reads.size());
+    for (const auto &R : reads)
+        w.push_back((2 * SCORE_C + R.H) * R.P);
+    const size_t q = (w.size() * 9) / 10;
+    std::nth_element(w.begin(), w.begin() + q, w.end());
+    return std::min(w[q], 24 * 1024 / 8);
+}
 
 }  // namespace
 
@@ -1154,7 +1246,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const TplObj &T = ctx->tpls[tpl[k]];
                 Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
                 const int H = band_rows(S.n + 1, T.m + 1, bw[k]);
-                if (int e = region_ensure(ctx, ctx->band_arena, b.r, (int64_t)H * (T.m + 1) * 8))
+                if (int e = region_ensure(ctx, ctx->band_arena, b.r,
+                                          band_K(H, T.m) * band_P(H) * 8))
                     return e;
                 b.valid = true;
                 b.seq = seq[k];
@@ -1194,6 +1287,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // out_score: forward scores win when both directions run
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
+                t.P = band_P(t.H);
                 // classes by lanes per task (W): H <= 32 -> 16, <= 64 -> 32, else 64
                 if (t.H <= 32)
                     c16.push_back(t);
@@ -1248,7 +1342,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     if (P.n16) {
         const int n = (int)P.n16;
         const int ld = 32 + 6;
-        hipLaunchKernelGGL((k_dp<16, false>), dim3((n + 15) / 16), dim3(256), 16 + 16 * 4 * ld * 8,
+        hipLaunchKernelGGL((k_dp<16, false>), dim3((n + 3) / 4), dim3(64), 4 * 4 * ld * 8,
                            ctx->stream, d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                            ld, nullptr);
         at += n;
@@ -1256,7 +1350,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     if (P.n32) {
         const int n = (int)P.n32;
         const int ld = 64 + 6;
-        hipLaunchKernelGGL((k_dp<32, false>), dim3((n + 7) / 8), dim3(256), 16 + 8 * 4 * ld * 8,
+        hipLaunchKernelGGL((k_dp<32, false>), dim3((n + 1) / 2), dim3(64), 2 * 4 * ld * 8,
                            ctx->stream, d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                            ld, nullptr);
         at += n;
@@ -1264,7 +1358,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     if (P.n64) {
         const int n = (int)P.n64;
         const int ld = P.hmax64 + 6;
-        hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 16 + 4 * ld * 8, ctx->stream,
+        hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, ctx->stream,
                            d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
         at += n;
     }
@@ -1273,7 +1367,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         const int ld = P.hmaxg + 6;
         if (int e = ensure_buf(ctx, ctx->scratch[10], (size_t)n * 4 * ld * 8))
             return e;
-        hipLaunchKernelGGL((k_dp<64, true>), dim3(n), dim3(64), 16, ctx->stream, d_tasks + at, n,
+        hipLaunchKernelGGL((k_dp<64, true>), dim3(n), dim3(64), 0, ctx->stream, d_tasks + at, n,
                            d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld,
                            (double *)ctx->scratch[10].p);
         at += n;
@@ -1321,6 +1415,7 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
         t.ncdel = S.ncdel;
         t.flags = (b.flags & RF_SKEW ? 2 : 0) | (b.flags & RF_TRIM ? 4 : 0);
         t.idx = k;
+        t.P = band_P(b.H);
         offs[k] = total;
         total += b.n + b.m;
     }
@@ -1429,6 +1524,8 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             R.H = A.H;
             R.c = std::max(A.m - A.n, 0) + A.bw;
             R.vb = std::max(A.n - A.m, 0) + A.bw;
+            R.P = band_P(A.H);
+            R.K = (int32_t)band_K(A.H, A.m);
             reads.push_back(R);
         }
         const int32_t r1 = (int32_t)reads.size();
@@ -1488,6 +1585,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                 t.H = A.H;
                 t.ncins = S.ncins;
                 t.ncdel = S.ncdel;
+                t.P = band_P(A.H);
                 t.kind = kd;
                 t.pos = ps;
                 t.base = b;
@@ -1561,10 +1659,11 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     if (!items.empty()) {
         dim3 grid((unsigned)items.size(), split ? (unsigned)max_reads : 1u);
-        hipLaunchKernelGGL(k_score, grid, dim3(64), 0, ctx->stream,
+        const int lds = score_lds_elems(reads);
+        hipLaunchKernelGGL(k_score, grid, dim3(64), 2 * lds * 8, ctx->stream,
                            (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
                            (const ScoreRead *)ctx->scratch[2].p, d_bases, d_tabs, d_bands, d_dense,
-                           d_split, split ? 1 : 0);
+                           d_split, split ? 1 : 0, lds);
         if (split && dense_total > 0)
             hipLaunchKernelGGL(k_reduce, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[1].p, ngroups, d_gstart,
@@ -1681,6 +1780,8 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
                 R.H = A.H;
                 R.c = std::max(A.m - A.n, 0) + A.bw;
                 R.vb = std::max(A.n - A.m, 0) + A.bw;
+                R.P = band_P(A.H);
+                R.K = (int32_t)band_K(A.H, A.m);
                 reads.push_back(R);
             }
             G.r1 = (int32_t)reads.size();
@@ -1712,6 +1813,7 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
         P.max_reads = max_reads;
         P.dense_total = dense_total;
         P.split_total = split_total;
+        P.lds_elems = score_lds_elems(reads);
     }
     bool split = (int64_t)P.nitems < 2048 && P.max_reads > 1;
     if (const char *mode = std::getenv("RIFRAF_SCORE_MODE")) {
@@ -1729,11 +1831,11 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     if (P.nitems) {
         dim3 grid((unsigned)P.nitems, split ? (unsigned)P.max_reads : 1u);
-        hipLaunchKernelGGL(k_score, grid, dim3(64), 0, ctx->stream,
+        hipLaunchKernelGGL(k_score, grid, dim3(64), 2 * P.lds_elems * 8, ctx->stream,
                            (const WorkItem *)ctx->scratch[11].p, (const ScoreGroup *)ctx->scratch[12].p,
                            (const ScoreRead *)ctx->scratch[13].p, (const uint8_t *)ctx->bytes_arena.d,
                            (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d, d_dense,
-                           split ? (double *)ctx->scratch[10].p : nullptr, split ? 1 : 0);
+                           split ? (double *)ctx->scratch[10].p : nullptr, split ? 1 : 0, P.lds_elems);
         if (split)
             hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
@@ -1776,9 +1878,16 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     const Band &b = which == RF_BAND_A ? ctx->slots[slot].a : ctx->slots[slot].b;
     if (!b.valid)
         return fail(ctx, RF_ERR_STATE, "rf_download_band: band not computed");
-    HIPCHK(ctx, hipMemcpyAsync(out, ctx->band_arena.d + b.r.off, (size_t)b.H * (b.m + 1) * 8,
+    // kappa-major device layout -> the reference's column-major data
+    const int P = band_P(b.H);
+    const int64_t K = band_K(b.H, b.m);
+    std::vector<double> buf((size_t)K * P);
+    HIPCHK(ctx, hipMemcpyAsync(buf.data(), ctx->band_arena.d + b.r.off, buf.size() * 8,
                                hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int jj = 0; jj <= b.m; ++jj)
+        for (int d = 0; d < b.H; ++d)
+            out[(size_t)jj * b.H + d] = buf[(size_t)(d + 2 * jj) * P + (d >> 1)];
     return 0;
 }
 
