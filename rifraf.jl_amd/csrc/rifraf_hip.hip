@@ -260,6 +260,163 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
 }
 
 // ---------------------------------------------------------------------
+// k_dpr: register-resident variant of k_dp for bands up to H <= 32*NP.
+//
+// Same recurrence, cell order and FP64 sums as k_dp; the anti-diagonals
+// kappa-1..kappa-3 live in registers instead of an LDS ring.  Each task owns
+// one 16-lane DPP row (4 tasks per wave); lane q holds band-row pairs
+// q*NP .. q*NP+NP-1, and the only cross-lane traffic per step is the pair
+// at each block edge, moved with DPP row shifts (v_mov_b32_dpp row_shr /
+// row_shl).  Lanes outside the row read the -Inf "bound" value, i.e. an
+// out-of-band predecessor, exactly like the ring's sentinels.
+// ---------------------------------------------------------------------
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)0xFFF00000, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+#define DPP_FROM_L1 0x111   // row_shr:1 -> value of lane q-1
+#define DPP_FROM_L2 0x112   // row_shr:2 -> lane q-2
+#define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
+#define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
+
+template <int NP>
+__global__ void __launch_bounds__(64)
+k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
+      const double *__restrict__ tabs, double *__restrict__ bands,
+      double *__restrict__ out_score, int *__restrict__ err)
+{
+    const int q = threadIdx.x & 15;
+    const int tid = blockIdx.x * 4 + (threadIdx.x >> 4);
+    DPTask T = {};
+    if (tid < ntasks)
+        T = tasks[tid];
+    int kmax = T.klen;
+    for (int off = 32; off >= 1; off >>= 1)
+        kmax = max(kmax, __shfl_xor(kmax, off));
+    const bool codon = __any(T.ncins > 0 || T.ncdel > 0);   // wave-uniform
+
+    const bool rev = T.flags & 1;
+    const bool skew = T.flags & 2;
+    const bool trim = T.flags & 4;
+    const uint8_t *sbase = bases + T.sb;
+    const uint8_t *tbase = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    const double *t_match = tb;
+    const double *t_mism = tb + T.n;
+    const double *t_ins = tb + 2 * (size_t)T.n;
+    const double *t_del = tb + 3 * (size_t)T.n;
+    const double *t_cins = tb + 4 * (size_t)T.n + 1;
+    const double *t_cdel = t_cins + T.ncins;
+    double *band = bands + T.band;
+
+    double v1[NP], v2[NP], v3[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+        v1[r] = -RF_INF;
+        v2[r] = -RF_INF;
+        v3[r] = -RF_INF;
+    }
+    for (int k = 0; k < kmax; ++k) {
+        const int par = k & 1;
+        // block-edge neighbours (uniform control flow: every lane shifts)
+        const double L1 = dpp_f64<DPP_FROM_L1>(v1[NP - 1]);
+        const double R1 = dpp_f64<DPP_FROM_R1>(v1[0]);
+        double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
+        if (codon) {
+            if (NP == 1) {
+                L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
+                L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
+                R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
+                R3b = dpp_f64<DPP_FROM_R2>(v3[0]);
+            } else {
+                L3a = dpp_f64<DPP_FROM_L1>(v3[NP - 1]);
+                L3b = dpp_f64<DPP_FROM_L1>(v3[NP > 1 ? NP - 2 : 0]);
+                R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
+                R3b = dpp_f64<DPP_FROM_R1>(v3[NP > 1 ? 1 : 0]);
+            }
+        }
+        const bool live = k < T.klen;
+        double *row = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
+        double nv[NP];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+            const int d = 2 * (q * NP + r) + par;
+            const int jj = (k - d) >> 1;
+            double v = -RF_INF;
+            const bool stored = live && d < T.H && d <= k;
+            if (stored && jj <= T.m) {
+                const int ii = d + jj - T.c;
+                if (ii >= 0 && ii <= T.n) {
+                    if (ii == 0 && jj == 0) {
+                        v = 0.0;
+                    } else {
+                        // align.jl:64-76 score lookups
+                        const int sb = ii >= 1 ? sbase[rev ? T.n - ii : ii - 1] : 4;
+                        const int tbb = jj >= 1 ? tbase[rev ? T.m - jj : jj - 1] : 4;
+                        const int ks = rev ? min(T.n - 1, T.n - ii) : max(ii - 1, 0);
+                        const int kd = rev ? T.n - ii : ii;
+                        double ms = (sb == tbb) ? t_match[ks] : t_mism[ks];
+                        double is = t_ins[ks];
+                        const double ds = t_del[kd];
+                        if (skew && sb != tbb)
+                            ms *= 0.99;
+                        if (trim && (jj == 0 || jj == T.m))
+                            is = 0.0;
+                        // neighbours: insert (d-1, kappa-1), delete (d+1, kappa-1)
+                        const double x_ins = par ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : L1);
+                        const double x_del = par ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : R1) : v1[r];
+                        // align.jl:77-104, strict '>' in reference order
+                        double best = -RF_INF, x;
+                        x = v2[r] + ms;
+                        if (x > best) best = x;
+                        x = x_ins + is;
+                        if (x > best) best = x;
+                        x = x_del + ds;
+                        if (x > best) best = x;
+                        if (codon) {
+                            if (T.ncins > 0 && ii >= 3) {
+                                // d-3 at kappa-3: pair index q*NP + r - 2 + par
+                                const int idx = r - 2 + par;
+                                const double y = idx >= 0 ? v3[idx >= 0 ? idx : 0] : (idx == -1 ? L3a : L3b);
+                                const int ci = rev ? T.ncins - ii + 2 : ii - 3;
+                                x = y + t_cins[ci];
+                                if (x > best) best = x;
+                            }
+                            if (T.ncdel > 0 && jj >= 3) {
+                                // d+3 at kappa-3: pair index q*NP + r + 1 + par
+                                const int idx = r + 1 + par;
+                                const double y = idx < NP ? v3[idx < NP ? idx : 0] : (idx == NP ? R3a : R3b);
+                                x = y + t_cdel[kd];
+                                if (x > best) best = x;
+                            }
+                        }
+                        if (best == -RF_INF)
+                            set_err(err, 1);  // "new score is invalid"
+                        v = best;
+                    }
+                    if (ii == T.n && jj == T.m && out_score)
+                        out_score[T.out_idx] = v;
+                }
+            }
+            if (stored)
+                row[(rev ? T.H - 1 - d : d) >> 1] = v;
+            nv[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+            v3[r] = v2[r];
+            v2[r] = v1[r];
+            v1[r] = nv[r];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------
 // k_score: dense proposal scoring of batch reads (no codon moves)
 //
 // One lane per consensus position p in [0, m].  For a read it evaluates
@@ -290,106 +447,122 @@ struct BandWin {
     }
 };
 
-__device__ __forceinline__ void score_position(int p, int m, const ScoreRead &R,
-                                               const uint8_t *__restrict__ s,
-                                               const double *__restrict__ tb,
-                                               const BandWin A, const BandWin B, double out[9])
+// HALF 0: Substitution(p, b) chains + Deletion(p)  -> out[0..4]
+// HALF 1: Insertion(p, b) chains                     -> out[5..8]
+// (two waves of one workgroup share the staged A/B window)
+template <int HALF>
+__device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
+                                           const uint8_t *__restrict__ s,
+                                           const double *__restrict__ tb,
+                                           const BandWin A, const BandWin B, double out[5])
 {
-    const int n = R.n, H = R.H, c = R.c, vb = R.vb;
+    const int n = R.n, c = R.c, vb = R.vb;
     const double *t_match = tb;
     const double *t_mism = tb + n;
     const double *t_ins = tb + 2 * (size_t)n;
     const double *t_del = tb + 3 * (size_t)n;
-
+    const double qnan = __builtin_nan("");
     // row ranges (bandedarrays.jl:133-137), 0-based rows
-    const int pI = min(p + 1, m);           // Ins new column's row range
-    const int s0 = max(0, p - c), s1 = min(p + vb, n);             // rows(p)
-    const int i0 = max(0, pI - c), i1 = min(pI + vb, n);           // rows(pI)
-    const int d0 = max(0, p - 1 - c), d1 = min(p - 1 + vb, n);     // rows(p-1)
-    const bool has_sd = p >= 1;
-
-    double sub_prev[4], sub_acc[4], ins_prev[4], ins_acc[4];
-    bool sub_bad[4], ins_bad[4];
+    const int s0 = max(0, p - c), s1 = min(p + vb, n);             // rows(p): new Sub col, B col p
+    if (HALF == 0) {
+        if (p < 1) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        sub_prev[b] = -RF_INF;
-        sub_acc[b] = -RF_INF;
-        ins_prev[b] = -RF_INF;
-        ins_acc[b] = -RF_INF;
-        sub_bad[b] = false;
-        ins_bad[b] = false;
-    }
-    double del_acc = -RF_INF;
-
-    // A(p-1, ii) in band iff ii in rows(p-1); A(p, ii), B(p, ii) iff ii in rows(p)
-    auto Am1 = [&](int ii) { return (has_sd && ii >= d0 && ii <= d1) ? A.at(ii - (p - 1) + c, p - 1) : -RF_INF; };
-    auto A0 = [&](int ii) { return (ii >= s0 && ii <= s1) ? A.at(ii - p + c, p) : -RF_INF; };
-
-    const int lo = has_sd ? d0 : s0;
-    const int hi = i1;
-    double am1_prev = lo >= 1 ? Am1(lo - 1) : -RF_INF;
-    double a0_prev = lo >= 1 ? A0(lo - 1) : -RF_INF;
-    for (int ii = lo; ii <= hi; ++ii) {
-        const double am1 = Am1(ii);
-        const double a0 = A0(ii);
-        const bool in_s = ii >= s0 && ii <= s1;
-        const double b0 = in_s ? B.at(ii - p + c, p) : -RF_INF;
-        const int sb = ii >= 1 ? s[ii - 1] : 4;
-        const int ks = max(ii - 1, 0);
-        const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
-        const double ds = t_del[ii];
-        if (has_sd && in_s) {
+            for (int k = 0; k < 5; ++k)
+                out[k] = qnan;
+            return;
+        }
+        const int d0 = max(0, p - 1 - c), d1 = min(p - 1 + vb, n);  // rows(p-1): A col p-1
+        double prev[4], acc[4];
+        bool bad[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            prev[b] = -RF_INF;
+            acc[b] = -RF_INF;
+            bad[b] = false;
+        }
+        double del_acc = -RF_INF;
+        // A(p-1, ii) in band iff ii in rows(p-1)
+        double am1_prev = (s0 - 1 >= d0) ? A.at(s0 - 1 - (p - 1) + c, p - 1) : -RF_INF;
+        for (int ii = s0; ii <= s1; ++ii) {
+            const double am1 = (ii <= d1) ? A.at(ii - (p - 1) + c, p - 1) : -RF_INF;
+            const double b0 = B.at(ii - p + c, p);
+            const int sb = ii >= 1 ? s[ii - 1] : 4;
+            const int ks = max(ii - 1, 0);
+            const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
+            const double ds = t_del[ii];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
+                // update(A, i, p+1, s[i-1], b; newcols, acol=p), align.jl:50-112
                 const double ms = (sb == b) ? mt : mm;
                 double best = -RF_INF, x;
                 x = am1_prev + ms;
                 if (x > best) best = x;
-                x = sub_prev[b] + is;
+                x = prev[b] + is;
                 if (x > best) best = x;
                 x = am1 + ds;
                 if (x > best) best = x;
-                sub_bad[b] |= (best == -RF_INF);
-                sub_prev[b] = best;
-                sub_acc[b] = fmax(sub_acc[b], best + b0);
+                bad[b] |= (best == -RF_INF);
+                prev[b] = best;
+                acc[b] = fmax(acc[b], best + b0);     // summax, util.jl:40-48
             }
+            if (ii <= d1)
+                del_acc = fmax(del_acc, am1 + b0);    // seq_score_deletion, model.jl:227-236
+            am1_prev = am1;
         }
-        if (ii >= i0 && ii <= i1) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            out[b] = (bad[b] || acc[b] == -RF_INF) ? qnan : acc[b];
+        out[4] = del_acc;
+    } else {
+        const int pI = min(p + 1, m);                                // new Ins col's row range
+        const int i0 = max(0, pI - c), i1 = min(pI + vb, n);
+        double prev[4], acc[4];
+        bool bad[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            prev[b] = -RF_INF;
+            acc[b] = -RF_INF;
+            bad[b] = false;
+        }
+        // A(p, ii) in band iff ii in rows(p)
+        double a0_prev = (i0 - 1 >= s0) ? A.at(i0 - 1 - p + c, p) : -RF_INF;
+        for (int ii = i0; ii <= i1; ++ii) {
+            const bool in_s = ii <= s1;
+            const double a0 = in_s ? A.at(ii - p + c, p) : -RF_INF;
+            const double b0 = in_s ? B.at(ii - p + c, p) : -RF_INF;
+            const int sb = ii >= 1 ? s[ii - 1] : 4;
+            const int ks = max(ii - 1, 0);
+            const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
+            const double ds = t_del[ii];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
+                // update(A, i, p+2, s[i-1], b; newcols, acol=p+1)
                 const double ms = (sb == b) ? mt : mm;
                 double best = -RF_INF, x;
                 x = a0_prev + ms;
                 if (x > best) best = x;
-                x = ins_prev[b] + is;
+                x = prev[b] + is;
                 if (x > best) best = x;
                 x = a0 + ds;
                 if (x > best) best = x;
-                ins_bad[b] |= (best == -RF_INF);
-                ins_prev[b] = best;
-                if (in_s)
-                    ins_acc[b] = fmax(ins_acc[b], best + b0);
+                bad[b] |= (best == -RF_INF);
+                prev[b] = best;
+                acc[b] = fmax(acc[b], best + b0);
             }
+            a0_prev = a0;
         }
-        if (has_sd && in_s && ii >= d0 && ii <= d1)
-            del_acc = fmax(del_acc, am1 + b0);
-        am1_prev = am1;
-        a0_prev = a0;
-    }
-    const double qnan = __builtin_nan("");
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        out[b] = (!has_sd || sub_bad[b] || sub_acc[b] == -RF_INF) ? qnan : sub_acc[b];
-        out[5 + b] = (ins_bad[b] || ins_acc[b] == -RF_INF) ? qnan : ins_acc[b];
+        for (int b = 0; b < 4; ++b)
+            out[b] = (bad[b] || acc[b] == -RF_INF) ? qnan : acc[b];
     }
-    out[4] = has_sd ? del_acc : qnan;
 }
 
-// grid.x = work items (group, chunk of SCORE_C positions); grid.y = read
-// index in split mode.  Fused mode folds all reads of the group in batch
-// order.  lds_rows: kappa rows the dynamic LDS holds per band (0 = never
-// stage).
-__global__ void __launch_bounds__(64)
+// One workgroup = 2 waves x 64 lanes: lane l of wave h handles position
+// p0 + l, wave 0 the Substitution/Deletion proposals, wave 1 the
+// Insertions.  grid.x = work items (group, chunk of SCORE_C positions);
+// grid.y = read index in split mode.  Fused mode folds all reads of the
+// group in batch order.  lds_elems: doubles the dynamic LDS holds per band.
+__global__ void __launch_bounds__(128)
 k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
         const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
         const double *__restrict__ tabs, const double *__restrict__ bands,
@@ -398,7 +571,9 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const WorkItem w = items[blockIdx.x];
     const ScoreGroup G = groups[w.group];
-    const int p = w.p0 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int half = threadIdx.x >> 6;
+    const int p = w.p0 + lane;
     int r0 = G.r0, r1 = G.r1;
     if (split_mode) {
         r0 = G.r0 + blockIdx.y;
@@ -406,9 +581,9 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
             return;
         r1 = r0 + 1;
     }
-    double tot[9];
+    double tot[5];
 #pragma unroll
-    for (int k = 0; k < 9; ++k)
+    for (int k = 0; k < 5; ++k)
         tot[k] = 0.0;
     double *sA = smem;
     double *sB = smem + lds_elems;
@@ -417,42 +592,72 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
         const ScoreRead R = reads[r];
         const double *A = bands + R.A;
         const double *B = bands + R.B;
-        const int kend = min(k0 + 2 * SCORE_C + R.H, R.K);
-        const int kbeg = max(k0, 0);
-        const int nel = (kend - kbeg) * R.P;
-        const bool stage = (k0 + 2 * SCORE_C + R.H - k0) * R.P <= lds_elems;
-        double s[9];
+        const bool stage = (2 * SCORE_C + R.H) * R.P <= lds_elems;
+        double sc[5];
         if (stage) {
-            // contiguous kappa rows -> LDS, coalesced
+            // contiguous kappa rows -> LDS, coalesced, 16 loads in flight per lane
+            const int kbeg = max(k0, 0);
+            const int kend = min(k0 + 2 * SCORE_C + R.H, R.K);
+            const int nel = (kend - kbeg) * R.P;
             const int off = (kbeg - k0) * R.P;
             const double *ga = A + (size_t)kbeg * R.P;
             const double *gb = B + (size_t)kbeg * R.P;
-            for (int e = threadIdx.x; e < nel; e += 64) {
-                sA[off + e] = ga[e];
-                sB[off + e] = gb[e];
+            for (int e0 = 0; e0 < nel; e0 += 128 * 8) {
+                double ra[8], rb[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * 128 + threadIdx.x;
+                    if (e < nel) {
+                        ra[u] = ga[e];
+                        rb[u] = gb[e];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * 128 + threadIdx.x;
+                    if (e < nel) {
+                        sA[off + e] = ra[u];
+                        sB[off + e] = rb[u];
+                    }
+                }
             }
-            wave_sync();
-            if (p <= G.m)
-                score_position(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{sA, k0, R.P},
-                               BandWin{sB, k0, R.P}, s);
-            wave_sync();
+            __syncthreads();
+            if (p <= G.m) {
+                if (half == 0)
+                    score_half<0>(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{sA, k0, R.P},
+                                  BandWin{sB, k0, R.P}, sc);
+                else
+                    score_half<1>(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{sA, k0, R.P},
+                                  BandWin{sB, k0, R.P}, sc);
+            }
+            __syncthreads();
         } else if (p <= G.m) {
-            score_position(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{A, 0, R.P},
-                           BandWin{B, 0, R.P}, s);
+            if (half == 0)
+                score_half<0>(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{A, 0, R.P},
+                              BandWin{B, 0, R.P}, sc);
+            else
+                score_half<1>(p, G.m, R, bases + R.sb, tabs + R.tab, BandWin{A, 0, R.P},
+                              BandWin{B, 0, R.P}, sc);
         }
         if (p <= G.m) {
 #pragma unroll
-            for (int k = 0; k < 9; ++k)
-                tot[k] += s[k];
+            for (int k = 0; k < 5; ++k)
+                tot[k] += sc[k];
         }
     }
     if (p > G.m)
         return;
     double *dst = split_mode ? split + G.split_off + ((size_t)blockIdx.y * (G.m + 1) + p) * 9
                              : dense + G.dense_off + (size_t)p * 9;
+    if (half == 0) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k)
-        dst[k] = tot[k];
+        for (int k = 0; k < 5; ++k)
+            dst[k] = tot[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[5 + k] = tot[k];
+    }
 }
 
 // split mode: ordered fold over reads, one lane per (group position slot)
@@ -883,7 +1088,7 @@ struct rf_ctx {
         uint64_t gen = 0;
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
-        size_t n16 = 0, n32 = 0, n64 = 0, ng = 0;
+        size_t n16 = 0, n32 = 0, n128 = 0, n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
     } rplan;
     struct {
@@ -1261,7 +1466,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> c16, c32, c64, cg;
+        std::vector<DPTask> c16, c32, c128, c64, cg;
         int hmax64 = 0, hmaxg = 0;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
@@ -1293,6 +1498,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     c16.push_back(t);
                 else if (t.H <= 64)
                     c32.push_back(t);
+                else if (t.H <= 128)
+                    c128.push_back(t);
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
@@ -1305,12 +1512,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
         std::stable_sort(c16.begin(), c16.end(), by_len);
         std::stable_sort(c32.begin(), c32.end(), by_len);
+        std::stable_sort(c128.begin(), c128.end(), by_len);
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         std::vector<DPTask> all;
-        all.reserve(c16.size() + c32.size() + c64.size() + cg.size());
+        all.reserve(c16.size() + c32.size() + c128.size() + c64.size() + cg.size());
         all.insert(all.end(), c16.begin(), c16.end());
         all.insert(all.end(), c32.begin(), c32.end());
+        all.insert(all.end(), c128.begin(), c128.end());
         all.insert(all.end(), c64.begin(), c64.end());
         all.insert(all.end(), cg.begin(), cg.end());
         if (int e = upload(ctx, ctx->scratch[8], all))
@@ -1324,6 +1533,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         P.bw.assign(bw, bw + njobs);
         P.n16 = c16.size();
         P.n32 = c32.size();
+        P.n128 = c128.size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -1341,18 +1551,20 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     size_t at = 0;
     if (P.n16) {
         const int n = (int)P.n16;
-        const int ld = 32 + 6;
-        hipLaunchKernelGGL((k_dp<16, false>), dim3((n + 3) / 4), dim3(64), 4 * 4 * ld * 8,
-                           ctx->stream, d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
-                           ld, nullptr);
+        hipLaunchKernelGGL((k_dpr<1>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
+                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
         at += n;
     }
     if (P.n32) {
         const int n = (int)P.n32;
-        const int ld = 64 + 6;
-        hipLaunchKernelGGL((k_dp<32, false>), dim3((n + 1) / 2), dim3(64), 2 * 4 * ld * 8,
-                           ctx->stream, d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
-                           ld, nullptr);
+        hipLaunchKernelGGL((k_dpr<2>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
+                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
+        at += n;
+    }
+    if (P.n128) {
+        const int n = (int)P.n128;
+        hipLaunchKernelGGL((k_dpr<4>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
+                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
         at += n;
     }
     if (P.n64) {
@@ -1660,7 +1872,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     if (!items.empty()) {
         dim3 grid((unsigned)items.size(), split ? (unsigned)max_reads : 1u);
         const int lds = score_lds_elems(reads);
-        hipLaunchKernelGGL(k_score, grid, dim3(64), 2 * lds * 8, ctx->stream,
+        hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * lds * 8, ctx->stream,
                            (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
                            (const ScoreRead *)ctx->scratch[2].p, d_bases, d_tabs, d_bands, d_dense,
                            d_split, split ? 1 : 0, lds);
@@ -1831,7 +2043,7 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     if (P.nitems) {
         dim3 grid((unsigned)P.nitems, split ? (unsigned)P.max_reads : 1u);
-        hipLaunchKernelGGL(k_score, grid, dim3(64), 2 * P.lds_elems * 8, ctx->stream,
+        hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * P.lds_elems * 8, ctx->stream,
                            (const WorkItem *)ctx->scratch[11].p, (const ScoreGroup *)ctx->scratch[12].p,
                            (const ScoreRead *)ctx->scratch[13].p, (const uint8_t *)ctx->bytes_arena.d,
                            (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d, d_dense,

@@ -1,0 +1,713 @@
+"""RIFRAF consensus stage machine (src/model.jl) over the MI355X engine.
+
+Host logic -- RifrafParams, the stage machine (initial -> frame-correction ->
+refinement -> scoring), resampling, candidate handling -- follows the
+reference function by function (file:line cited on each).  Every alignment
+fill, backtrace and proposal score runs on the HIP engine (rf_realign,
+rf_backtrace, rf_score); there is no CPU numeric path here.
+
+Engine id mapping for one rifraf() call (N reads):
+  sequences 0..N-1 = reads, N = reference, N+1 = scratch (edit_distance)
+  template  0      = consensus
+  slots     0..    = batch positions (state.As[k] / Bs[k] / Amoves[k]),
+            N = reference (A_ref / B_ref), N+1 = scratch
+"""
+from __future__ import annotations
+
+import math
+import sys
+from dataclasses import dataclass, field
+from enum import IntEnum
+
+import numpy as np
+
+from .align import (TRACE_CODON_DELETE, TRACE_CODON_INSERT, TRACE_DELETE, TRACE_INSERT, TRACE_MATCH,
+                    moves_to_proposals_np)
+from .engine import RF_BAND_A, RF_BWD, RF_FWD, RF_SKEW, Engine, RifrafError
+from .errormodel import ErrorModel, Scores, phred_to_log_p
+from .poisson import cquantile_poisson
+from .proposals import (DEL, INS, SUB, Deletion, Insertion, Proposal, ScoredProposal, Substitution,
+                        apply_proposals, choose_candidates, to_arrays)
+from .rifrafsequences import RifrafSequence
+from .types import BASES, CODON_LENGTH, DNASeq, dna_str
+
+
+class Stage(IntEnum):                          # model.jl:1-5
+    INIT = 1
+    FRAME = 2
+    REFINE = 3
+    SCORE = 4
+
+
+@dataclass
+class EstimatedProbs:                          # model.jl:20-24
+    sub: np.ndarray
+    dele: np.ndarray
+    ins: np.ndarray
+
+
+@dataclass
+class RifrafParams:                            # model.jl:97-164
+    scores: Scores = field(default_factory=lambda: Scores.from_errors(ErrorModel(1.0, 2.0, 2.0, 0.0, 0.0)))
+    ref_scores: Scores = field(default_factory=lambda: Scores.from_errors(ErrorModel(10.0, 1e-1, 1e-1, 1.0, 1.0)))
+    ref_indel_mult: float = 3.0
+    max_ref_indel_mults: int = 5
+    ref_error_mult: float = 1.0
+    do_init: bool = True
+    do_frame: bool = True
+    do_refine: bool = True
+    do_score: bool = False
+    do_alignment_proposals: bool = True
+    seed_indels: bool = True
+    indel_correction_only: bool = True
+    use_ref_for_qvs: bool = False
+    bandwidth: int = 3 * CODON_LENGTH
+    bandwidth_pvalue: float = 0.1
+    min_dist: int = 5 * CODON_LENGTH
+    batch_fixed: bool = True
+    batch_fixed_size: int = 5
+    batch_size: int = 20
+    batch_randomness: float = 0.9
+    batch_mult: float = 0.7
+    batch_threshold: float = 0.1
+    max_iters: int = 100
+    verbose: int = 0
+    seed: int | None = None                    # RNG for resample! (Julia's global RNG)
+
+
+@dataclass
+class RifrafState:                             # model.jl:167-193
+    consensus: np.ndarray
+    ref_scores: Scores
+    reference: RifrafSequence
+    batch_fixed_size: int
+    batch_size: int
+    base_batch_size: int
+    sequences: list
+    maxlen: int
+    score: float = -math.inf
+    ref_error_rate: float = -math.inf
+    n_ref_indel_mults: int = 0
+    batch_randomness: float = 0.9
+    batch_seqs: list = field(default_factory=list)       # indices into sequences
+    n_slots: int = 0                                     # length(state.As)
+    slot_scores: list = field(default_factory=list)      # A[end, end] per slot
+    ref_score: float = -math.inf                         # A_ref[end, end]
+    realign_As: bool = True
+    realign_Bs: bool = True
+    penalties_increased: bool = False
+    stage: Stage = Stage.INIT
+    stage_iterations: list = field(default_factory=lambda: [0, 0, 0, 0])
+    converged: bool = False
+
+
+@dataclass
+class RifrafResult:                            # model.jl:216-225
+    consensus: np.ndarray
+    params: RifrafParams
+    state: RifrafState
+    consensus_stages: list
+    error_probs: EstimatedProbs | None = None
+    aln_error_probs: np.ndarray | None = None
+
+
+class _Run:
+    """Engine bindings of one rifraf() call (ids per the module docstring)."""
+
+    def __init__(self, engine: Engine, nseqs: int):
+        self.e = engine
+        self.N = nseqs
+        self.REF = nseqs
+        self.SCRATCH = nseqs + 1
+        self.tpl_version = None
+
+    def set_consensus(self, cons):
+        self.e.set_templates(0, [cons])
+
+
+def log(params, level, msg):
+    if params.verbose >= level:
+        print(msg, file=sys.stderr)
+
+
+# ---------------------------------------------------------------------
+# checks and initial state
+# ---------------------------------------------------------------------
+
+def check_params(scores: Scores, reference, params: RifrafParams):   # model.jl:842-896
+    if (scores.mismatch >= 0.0 or scores.mismatch == -math.inf or scores.insertion >= 0.0
+            or scores.insertion == -math.inf or scores.deletion >= 0.0 or scores.deletion == -math.inf):
+        raise RifrafError("scores must be between -Inf and 0.0")
+    if scores.codon_insertion > -math.inf or scores.codon_deletion > -math.inf:
+        raise RifrafError("error model cannot allow codon indels")
+    if len(reference) > 0:
+        if params.ref_error_mult <= 0.0:
+            raise RifrafError("ref_error_mult must be > 0.0")
+        if params.ref_indel_mult <= 0.0:
+            raise RifrafError("ref_indel_mult must be > 0.0")
+        rs = params.ref_scores
+        if (rs.mismatch >= 0.0 or rs.insertion >= 0.0 or rs.deletion >= 0.0 or rs.codon_insertion >= 0.0
+                or rs.codon_deletion >= 0.0):
+            raise RifrafError("ref scores cannot be >= 0")
+        if -math.inf in (rs.mismatch, rs.insertion, rs.deletion, rs.codon_insertion, rs.codon_deletion):
+            raise RifrafError("ref scores cannot be -Inf")
+        if params.max_ref_indel_mults < 0:
+            raise RifrafError("ref_indel_increases must be >= 0")
+    if not any([params.do_init, params.do_frame, params.do_refine, params.do_score]):
+        raise RifrafError("no stages enabled")
+    if params.max_iters < 1:
+        raise RifrafError(f"invalid max iters: {params.max_iters}")
+    if params.batch_fixed and params.batch_fixed_size <= 1:
+        raise RifrafError("batch_fixed_size must be > 1")
+    if params.batch_randomness < 0.0 or params.batch_randomness > 1.0:
+        raise RifrafError("batch_randomness must be between 0.0 and 1.0")
+    if params.batch_mult < 0.0 or params.batch_mult > 1.0:
+        raise RifrafError("batch_mult must be between 0.0 and 1.0")
+    if params.batch_threshold < 0.0 or params.batch_mult > 1.0:
+        raise RifrafError("batch_threshold must be between 0.0 and 1.0")
+
+
+def logsumexp10(x):                            # util.jl:28-38
+    x = np.asarray(x, np.float64)
+    if x.size == 0:
+        return -math.inf
+    u = float(np.max(x))
+    if abs(u) == math.inf:
+        return math.nan if np.isnan(x).any() else u
+    s = 0.0
+    for v in x:
+        s += 10.0 ** (v - u)
+    return math.log10(s) + u
+
+
+def initial_state(consensus, sequences, reference, params: RifrafParams) -> RifrafState:  # :564-615
+    batch_size = params.batch_size if params.batch_size > 1 else len(sequences)
+    batch_size = min(batch_size, len(sequences))
+    batch_fixed_size = min(params.batch_fixed_size, len(sequences))
+    if len(consensus) == 0:
+        scores = [logsumexp10(s.match_scores) for s in sequences]
+        idx = int(np.argmax(scores))              # indmax: first maximum
+        consensus = sequences[idx].seq.copy()
+    maxlen = max(len(s) for s in sequences)
+    ref_error_log_p = np.zeros(len(reference))    # placeholder, :601-603
+    refseq = RifrafSequence(reference, ref_error_log_p, params.bandwidth, params.ref_scores) \
+        if len(reference) > 0 else RifrafSequence()
+    return RifrafState(consensus=DNASeq(consensus), ref_scores=params.ref_scores, reference=refseq,
+                       batch_fixed_size=batch_fixed_size, batch_size=batch_size,
+                       base_batch_size=batch_size, sequences=sequences, maxlen=maxlen,
+                       batch_randomness=params.batch_randomness)
+
+
+def use_ref(ref: RifrafSequence, stage: Stage, use_ref_for_qvs: bool) -> bool:   # :617-628
+    if len(ref) == 0:
+        return False
+    if stage == Stage.FRAME:
+        return True
+    return stage == Stage.SCORE and use_ref_for_qvs
+
+
+# ---------------------------------------------------------------------
+# realign / rescore (model.jl:630-719)
+# ---------------------------------------------------------------------
+
+def rescore(state: RifrafState, run: _Run, use_ref_for_qvs: bool):   # :630-635
+    # sum over all state.As (left fold, including stale slots), + A_ref
+    total = state.slot_scores[0]
+    for v in state.slot_scores[1:state.n_slots]:
+        total += v
+    state.score = total
+    if use_ref(state.reference, state.stage, use_ref_for_qvs):
+        state.score += state.ref_score
+
+
+def smart_forward_moves(run: _Run, jobs, seqs, consensus_len, pvalue):   # :643-672
+    """Batched smart_forward_moves!: jobs = [(slot, seq_id)], seqs = their
+    RifrafSequences.  Returns A[end,end] per job."""
+    e = run.e
+    n = len(jobs)
+    max_bw = [s.bandwidth if s.bandwidth_fixed else min(s.bandwidth * 2 ** 5, consensus_len, len(s))
+              for s in seqs]
+    scores = np.empty(n)
+    old_err = [sys.maxsize] * n
+    n_err = [sys.maxsize] * n
+    pending = list(range(n))
+    while pending:
+        sl = np.array([jobs[k][0] for k in pending], np.int32)
+        ids = np.array([jobs[k][1] for k in pending], np.int32)
+        bws = np.array([seqs[k].bandwidth for k in pending], np.int32)
+        out = e.realign(sl, ids, 0, bws, RF_FWD)
+        scores[pending] = out
+        check = [k for k in pending if not (seqs[k].bandwidth_fixed or seqs[k].bandwidth >= max_bw[k])]
+        if not check:
+            break
+        _, nerr = e.backtrace(np.array([jobs[k][0] for k in check], np.int32), want_moves=False)
+        nxt = []
+        for k, ne in zip(check, nerr):
+            old_err[k] = n_err[k]
+            n_err[k] = int(ne)
+            threshold = cquantile_poisson(seqs[k].est_n_errors, pvalue)
+            if n_err[k] > threshold and n_err[k] < old_err[k]:
+                seqs[k].bandwidth = min(seqs[k].bandwidth * 2, max_bw[k])
+                nxt.append(k)
+        pending = nxt
+    for s in seqs:
+        s.bandwidth_fixed = True
+    return scores
+
+
+def realign(state: RifrafState, run: _Run, params: RifrafParams):   # :679-714
+    seqs = [state.sequences[i] for i in state.batch_seqs]
+    while state.n_slots < len(seqs):                 # grow As/Bs/Amoves
+        state.slot_scores.append(0.0)                # A[end,end] of a fresh (zero) BandedArray
+        state.n_slots += 1
+    ref_on = use_ref(state.reference, state.stage, params.use_ref_for_qvs)
+    if state.realign_As:
+        log(params, 2, "    realigning As")
+        jobs = [(k, i) for k, i in enumerate(state.batch_seqs)]
+        sc = smart_forward_moves(run, jobs, seqs, len(state.consensus), params.bandwidth_pvalue)
+        for k in range(len(jobs)):
+            state.slot_scores[k] = float(sc[k])
+        if ref_on:
+            sc = smart_forward_moves(run, [(run.REF, run.REF)], [state.reference], len(state.consensus),
+                                     params.bandwidth_pvalue)
+            state.ref_score = float(sc[0])
+    if state.realign_Bs:
+        log(params, 2, "    realigning Bs")
+        slots = np.arange(len(seqs), dtype=np.int32)
+        run.e.realign(slots, np.array(state.batch_seqs, np.int32), 0,
+                      np.array([s.bandwidth for s in seqs], np.int32), RF_BWD)
+        if ref_on:
+            run.e.realign([run.REF], [run.REF], 0, [state.reference.bandwidth], RF_BWD)
+
+
+def realign_rescore(state, run, params):       # :716-719
+    realign(state, run, params)
+    rescore(state, run, params.use_ref_for_qvs)
+
+
+# ---------------------------------------------------------------------
+# proposals (model.jl:401-562)
+# ---------------------------------------------------------------------
+
+def all_proposals(stage: Stage, consensus, indel_correction_only: bool, indel_seeds=(),
+                  seed_neighborhood: int = CODON_LENGTH):           # :401-456
+    length = len(consensus)
+    ins_positions, del_positions = set(), set()
+    for p in indel_seeds:
+        if p.kind == INS:
+            ins_positions.update(range(max(p.pos - seed_neighborhood, 0), min(p.pos + seed_neighborhood, length) + 1))
+        else:
+            del_positions.update(range(max(p.pos - seed_neighborhood, 1), min(p.pos + seed_neighborhood, length) + 1))
+    do_subs = stage != Stage.FRAME or not indel_correction_only
+    do_indels = stage in (Stage.INIT, Stage.FRAME, Stage.SCORE)
+    no_seeds = len(indel_seeds) == 0
+    results = []
+    if do_indels:
+        results += [Insertion(0, b) for b in range(4)]
+    for j in range(1, length + 1):
+        if do_subs:
+            results += [Substitution(j, b) for b in range(4) if consensus[j - 1] != b]
+        if do_indels:
+            if no_seeds or j in del_positions:
+                results.append(Deletion(j))
+            if no_seeds or j in ins_positions:
+                results += [Insertion(j, b) for b in range(4)]
+    return results
+
+
+def alignment_proposals(state: RifrafState, run: _Run, do_indels: bool):   # :483-497
+    """Union of the proposals seen in the batch alignments.  The reference
+    collects a Julia Set (hash order); this mirror returns them sorted by
+    (pos, kind, base), a documented deterministic order."""
+    slots = np.arange(len(state.batch_seqs), dtype=np.int32)
+    moves, _ = run.e.backtrace(slots)
+    cons = state.consensus
+    found = set()
+    for mv, i in zip(moves, state.batch_seqs):
+        k, p, b = moves_to_proposals_np(mv, cons, state.sequences[i].seq)
+        if not do_indels:
+            keep = k == SUB
+            k, p, b = k[keep], p[keep], b[keep]
+        found.update(zip(k.tolist(), p.tolist(), b.tolist()))
+    return [Proposal(k, p, b) for (k, p, b) in sorted(found, key=lambda t: (t[1], t[0], t[2]))]
+
+
+def _align_ref_moves(state: RifrafState, run: _Run, skew: bool):
+    """align_moves(consensus, reference; skew_matches) on the engine
+    (align.jl:337-344): forward_moves! of the reference (rows) against the
+    consensus with the reference's own bandwidth, then backtrace."""
+    ref = state.reference
+    run.e.set_sequences(run.REF, [ref])
+    run.e.realign([run.SCRATCH], [run.REF], 0, [ref.bandwidth], RF_FWD | (RF_SKEW if skew else 0))
+    moves, _ = run.e.backtrace([run.SCRATCH])
+    return moves[0]
+
+
+def has_single_indels(state, run) -> bool:                         # :532-536
+    moves = _align_ref_moves(state, run, skew=False)
+    return bool(((moves == TRACE_INSERT) | (moves == TRACE_DELETE)).any())
+
+
+def single_indel_proposals(state, run):                            # :538-562
+    moves = _align_ref_moves(state, run, skew=True)
+    results = []
+    cons_idx = ref_idx = 0
+    refseq = state.reference.seq
+    for mv in moves.tolist():
+        if mv == TRACE_MATCH:
+            cons_idx += 1
+            ref_idx += 1
+        elif mv == TRACE_INSERT:
+            ref_idx += 1
+            results.append(Insertion(cons_idx, int(refseq[ref_idx - 1])))
+        elif mv == TRACE_DELETE:
+            cons_idx += 1
+            results.append(Deletion(cons_idx))
+        elif mv == TRACE_CODON_INSERT:
+            ref_idx += 3
+        elif mv == TRACE_CODON_DELETE:
+            cons_idx += 3
+    return results
+
+
+def score_proposals(state: RifrafState, run: _Run, proposals, with_ref: bool):
+    """score_proposal(m, state, newcols, use_ref) for a proposal list
+    (model.jl:385-399): batch fold (+ reference last) on the engine."""
+    if not proposals:
+        return np.zeros(0)
+    slots = np.arange(len(state.batch_seqs), dtype=np.int32)
+    return run.e.score([(slots, run.REF if with_ref else -1, to_arrays(proposals))])[0]
+
+
+def get_candidates(state: RifrafState, run: _Run, params: RifrafParams, indel_seeds=()):   # :499-526
+    use_ref_ = state.stage == Stage.FRAME
+    if state.stage in (Stage.INIT, Stage.REFINE) and params.do_alignment_proposals:
+        proposals = alignment_proposals(state, run, state.stage == Stage.INIT)
+    else:
+        proposals = all_proposals(state.stage, state.consensus, params.indel_correction_only, indel_seeds)
+    totals = score_proposals(state, run, proposals, use_ref_)
+    return [ScoredProposal(p, float(s)) for p, s in zip(proposals, totals) if s > state.score]
+
+
+# ---------------------------------------------------------------------
+# stage machine (model.jl:898-1114)
+# ---------------------------------------------------------------------
+
+def _set_consensus(state, run, cons):
+    state.consensus = DNASeq(cons)
+    run.set_consensus(state.consensus)
+
+
+def handle_candidates(candidates, state: RifrafState, run: _Run, params: RifrafParams):   # :898-935
+    old_consensus = state.consensus
+    chosen = choose_candidates(candidates, params.min_dist)
+    log(params, 2, f"    found {len(candidates)} candidates; filtered to {len(chosen)}")
+    log(params, 3, f"    chosen: {chosen}")
+    _set_consensus(state, run, apply_proposals(old_consensus, [c.proposal for c in chosen]))
+    state.realign_As = True
+    state.realign_Bs = False
+    realign_rescore(state, run, params)
+    if len(chosen) > 1 and (state.score < chosen[0].score or
+                            math.isclose(state.score, chosen[0].score, rel_tol=math.sqrt(sys.float_info.epsilon))):
+        log(params, 2, "    rejecting multiple candidates in favor of best")
+        chosen = [chosen[0]]
+        _set_consensus(state, run, apply_proposals(old_consensus, [c.proposal for c in chosen]))
+    else:
+        state.realign_As = False
+    state.realign_Bs = True
+    return chosen
+
+
+def edit_distance_engine(t, s, run: _Run):                        # align.jl:253-260
+    from .align import Scratch, edit_distance
+    return edit_distance(t, s, scratch=Scratch(run.e, run.SCRATCH, 1, run.SCRATCH))
+
+
+def finish_stage(state: RifrafState, run: _Run, params: RifrafParams):   # :937-995
+    log(params, 2, f"    no candidates found in {state.stage.name}.")
+    if state.stage == Stage.INIT:
+        if len(state.reference) == 0 or not params.do_frame:
+            state.converged = True
+        else:
+            state.stage = Stage.FRAME
+            edit_dist = edit_distance_engine(state.consensus, state.reference.seq, run)
+            ref_error_rate = edit_dist / max(len(state.reference), len(state.consensus))
+            ref_error_rate *= params.ref_error_mult
+            state.ref_error_rate = min(max(ref_error_rate, 1e-10), 0.5)
+            ref_error_log_p = np.full(len(state.reference), math.log10(state.ref_error_rate))
+            state.reference = RifrafSequence(state.reference.seq, ref_error_log_p, params.bandwidth,
+                                             state.ref_scores)
+            run.e.set_sequences(run.REF, [state.reference])
+            if not has_single_indels(state, run):
+                state.converged = True
+    elif state.stage == Stage.FRAME:
+        if not has_single_indels(state, run):
+            state.stage = Stage.REFINE
+        elif state.n_ref_indel_mults == params.max_ref_indel_mults:
+            log(params, 2, "    NOTE: alignment had single indels but reached penalty limit.")
+            state.stage = Stage.REFINE
+        else:
+            state.penalties_increased = True
+            if state.n_ref_indel_mults < params.max_ref_indel_mults:
+                state.n_ref_indel_mults += 1
+            else:
+                raise RifrafError("Tried to illegally increase n_ref_indel_mults")
+            mult = params.ref_indel_mult ** state.n_ref_indel_mults
+            rs = state.ref_scores
+            state.ref_scores = Scores(rs.mismatch, rs.insertion * mult, rs.deletion * mult,
+                                      rs.codon_insertion, rs.codon_deletion)
+            state.reference = RifrafSequence.rescored(state.reference, state.ref_scores)
+            run.e.set_sequences(run.REF, [state.reference])
+            log(params, 2, "    NOTE: alignment to reference had single indels. increasing penalty.")
+    elif state.stage == Stage.REFINE:
+        state.converged = True
+    else:
+        raise RifrafError(f"  invalid stage: {state.stage}")
+
+
+def reweight(wv, n, randomness):                                   # :1017-1036
+    if randomness < 0.0 or randomness > 1.0:
+        raise RifrafError("randomness must be between 0.0 and 1.0")
+    wv = np.asarray(wv, np.float64)
+    wv = wv / wv.sum()
+    indices = np.argsort(wv, kind="stable")[::-1][:n]
+    endpoint = wv
+    weight = 0.0
+    if randomness > 0.5:
+        weight = (randomness - 0.5) * 2.0
+        endpoint = np.full(len(wv), 1.0 / len(wv))
+    elif randomness < 0.5:
+        weight = 1.0 - randomness * 2.0
+        endpoint = np.zeros(len(wv))
+        endpoint[indices] = 1.0 / n
+    return weight * endpoint + (1.0 - weight) * wv
+
+
+def resample(state: RifrafState, params: RifrafParams, rng: np.random.Generator):   # :1038-1066
+    err_weights = np.array([s.est_n_errors for s in state.sequences])
+    if state.stage in (Stage.INIT, Stage.FRAME) and params.batch_fixed:
+        state.batch_seqs = np.argsort(err_weights, kind="stable")[:state.batch_fixed_size].tolist()
+        log(params, 2, "    kept fixed batch")
+        return
+    wv = reweight(1.0 - err_weights / err_weights.sum(), state.batch_size, state.batch_randomness)
+    n = state.batch_size
+    if n < len(state.sequences):
+        # StatsBase.sample(data, Weights, n, replace=false): weighted sampling
+        # without replacement (RNG stream not reproducible: parity unpinned)
+        state.batch_seqs = rng.choice(len(state.sequences), size=n, replace=False, p=wv / wv.sum()).tolist()
+        state.realign_As = True
+        log(params, 2, f"    sampled {n} new sequences")
+    else:
+        state.batch_seqs = list(range(len(state.sequences)))
+        log(params, 2, "    sampled all sequences")
+
+
+def check_score(state: RifrafState, run: _Run, params: RifrafParams, old_score: float, rng) -> bool:  # :1074-1114
+    log(params, 2, f"    score: {state.score}")
+    if (not state.penalties_increased and state.batch_size == len(state.sequences)
+            and state.stage_iterations[int(state.stage) - 1] > 1):
+        if state.score < old_score:
+            log(params, 2, "    WARNING: not using batches, but score decreased.")
+        elif state.score == old_score:
+            log(params, 2, "    score did not change. ending stage.")
+            return False
+    if ((state.score - old_score) / old_score > params.batch_threshold and not state.penalties_increased
+            and state.batch_size < len(state.sequences) and state.stage_iterations[int(state.stage) - 1] > 1):
+        state.batch_size = min(state.batch_size + state.base_batch_size, len(state.sequences))
+        log(params, 2, f"    NOTE: increased batch size to {state.batch_size}.")
+        resample(state, params, rng)
+        state.realign_As = True
+        state.realign_Bs = True
+        realign_rescore(state, run, params)
+        log(params, 2, f"    new score: {state.score}")
+    return True
+
+
+# ---------------------------------------------------------------------
+# quality scores (model.jl:721-840)
+# ---------------------------------------------------------------------
+
+def normalize_log_differences(sub_scores, del_scores, ins_scores, state_score):   # :722-735
+    pos_scores = np.hstack([sub_scores, del_scores[:, None]])
+    pos_exp = np.power(10.0, pos_scores)
+    pos_probs = pos_exp / pos_exp.sum(axis=1, keepdims=True)
+    ins_exp = np.power(10.0, ins_scores)
+    ins_probs = ins_exp / (10.0 ** state_score + ins_exp.sum(axis=1, keepdims=True))
+    return EstimatedProbs(pos_probs[:, :4], pos_probs[:, 4], ins_probs)
+
+
+def estimate_probs(state: RifrafState, run: _Run, use_ref_for_qvs: bool) -> EstimatedProbs:   # :737-791
+    m = len(state.consensus)
+    sub_scores = np.zeros((m, 4)) + state.score
+    del_scores = np.zeros(m) + state.score
+    ins_scores = np.zeros((m + 1, 4))
+    use_ref_ = len(state.reference) > 0 and use_ref_for_qvs
+    props = all_proposals(Stage.SCORE, state.consensus, False)
+    scores = score_proposals(state, run, props, use_ref_)
+    for p, sc in zip(props, scores):
+        if p.kind == SUB:
+            sub_scores[p.pos - 1, p.base] = sc
+        elif p.kind == DEL:
+            del_scores[p.pos - 1] = sc
+        else:
+            ins_scores[p.pos, p.base] = sc
+    max_score = max(sub_scores.max(), del_scores.max(), ins_scores.max())
+    sub_scores = sub_scores - max_score
+    del_scores = del_scores - max_score
+    ins_scores = ins_scores - max_score
+    if sub_scores.max() > 0.0:
+        raise RifrafError("sub scores cannot be positive")
+    if del_scores.max() > 0.0:
+        raise RifrafError("deletion scores cannot be positive")
+    if ins_scores.max() > 0.0:
+        raise RifrafError("insertion scores cannot be positive")
+    return normalize_log_differences(sub_scores, del_scores, ins_scores, state.score - max_score)
+
+
+def base_distribution(base, ilp):                                  # :804-809
+    lp = math.log10(1.0 - 10.0 ** ilp)
+    result = np.full(4, lp - math.log10(3))
+    result[base] = ilp
+    return result
+
+
+def alignment_error_probs(tlen, state: RifrafState, run: _Run):   # :817-840
+    probs = np.zeros((tlen, 4))
+    slots = np.arange(len(state.batch_seqs), dtype=np.int32)
+    moves, _ = run.e.backtrace(slots)
+    for mv, idx in zip(moves, state.batch_seqs):
+        s = state.sequences[idx]
+        i = j = 1
+        for move in mv.tolist():
+            a, b = {1: (1, 1), 2: (1, 0), 3: (0, 1), 4: (3, 0), 5: (0, 3)}[move]
+            i, j = i + a, j + b
+            if move == TRACE_MATCH:
+                probs[j - 2, :] += base_distribution(int(s.seq[i - 2]), s.match_scores[i - 2])
+    probs = np.power(10.0, probs)
+    probs = 1.0 - (probs / probs.sum(axis=1, keepdims=True)).max(axis=1)
+    return probs
+
+
+# ---------------------------------------------------------------------
+# rifraf (model.jl:1116-1287)
+# ---------------------------------------------------------------------
+
+def rifraf(dnaseqs, phreds=None, *, error_log_ps=None, consensus=None, reference=None,
+           params: RifrafParams | None = None, engine: Engine | None = None) -> RifrafResult:
+    """rifraf(dnaseqs, phreds; consensus, reference, params) -> RifrafResult.
+    Pass `error_log_ps` instead of `phreds` for the log-probability method
+    (model.jl:1116)."""
+    params = params or RifrafParams()
+    if error_log_ps is None:                                         # model.jl:1277-1287
+        if any(np.min(p) < 0 for p in phreds):
+            raise RifrafError("phred score cannot be negative")
+        error_log_ps = [phred_to_log_p(p) for p in phreds]
+    dnaseqs = [DNASeq(s) for s in dnaseqs]
+    consensus = DNASeq(consensus) if consensus is not None else np.zeros(0, np.uint8)
+    reference = DNASeq(reference) if reference is not None else np.zeros(0, np.uint8)
+    check_params(params.scores, reference, params)
+    sequences = [RifrafSequence(s, p, params.bandwidth, params.scores) for s, p in zip(dnaseqs, error_log_ps)]
+    state = initial_state(consensus, sequences, reference, params)
+    rng = np.random.default_rng(params.seed)
+    if engine is None:
+        from .align import default_engine
+        engine = default_engine()
+    run = _Run(engine, len(sequences))
+    engine.set_sequences(0, sequences)
+    if len(state.reference) > 0:
+        engine.set_sequences(run.REF, [state.reference])
+    run.set_consensus(state.consensus)
+
+    enabled = set()
+    if params.do_init:
+        enabled.add(Stage.INIT)
+    if params.do_frame:
+        enabled.add(Stage.FRAME)
+    if params.do_refine:
+        enabled.add(Stage.REFINE)
+    if params.do_score:
+        enabled.add(Stage.SCORE)
+    consensus_stages = [[] for _ in range(int(Stage.SCORE) - 1)]
+    state.realign_As = True
+    state.realign_Bs = True
+    old_score = -math.inf
+
+    for it in range(1, params.max_iters + 1):
+        while state.stage < Stage.SCORE and state.stage not in enabled:
+            state.stage = Stage(int(state.stage) + 1)
+        if state.stage == Stage.SCORE:
+            break
+        state.stage_iterations[int(state.stage) - 1] += 1
+        consensus_stages[int(state.stage) - 1].append(state.consensus.copy())
+        log(params, 1, f"iteration {it} : {state.stage.name} : {state.score}")
+        if params.verbose >= 3:
+            log(params, 3, f"  consensus: {dna_str(state.consensus)}")
+        else:
+            log(params, 2, f"  consensus length: {len(state.consensus)}")
+        log(params, 2, "  step: resample")
+        resample(state, params, rng)
+        log(params, 2, "  step: realign and rescore")
+        realign_rescore(state, run, params)
+        log(params, 2, "  step: check score")
+        if check_score(state, run, params, old_score, rng):
+            old_score = state.score
+            state.penalties_increased = False
+            indel_seeds = (single_indel_proposals(state, run)
+                           if state.stage == Stage.FRAME and params.seed_indels else [])
+            candidates = get_candidates(state, run, params, indel_seeds)
+            state.realign_As = True
+            if candidates:
+                log(params, 2, "  step: handle candidates")
+                handle_candidates(candidates, state, run, params)
+            else:
+                log(params, 2, "  step: finish_stage")
+                finish_stage(state, run, params)
+        else:
+            finish_stage(state, run, params)
+        if state.converged:
+            break
+        if ((not params.batch_fixed or (state.stage == Stage.REFINE and state.stage_iterations[2] > 1))
+                and state.batch_size < len(state.sequences)):
+            state.batch_randomness *= params.batch_mult
+            log(params, 2, f"  batch randomness decreased to {state.batch_randomness}")
+    state.stage = Stage.SCORE
+    result = RifrafResult(consensus=state.consensus, params=params, state=state,
+                          consensus_stages=consensus_stages)
+    if params.do_score:
+        log(params, 2, "computing consensus quality scores")
+        state.realign_As = True
+        state.realign_Bs = True
+        realign_rescore(state, run, params)
+        result.error_probs = estimate_probs(state, run, params.use_ref_for_qvs)
+        result.aln_error_probs = alignment_error_probs(len(state.consensus), state, run)
+    log(params, 1, f"done. converged: {state.converged}")
+    return result
+
+
+def correct_shifts(consensus, reference, log_p: float = -1.0, bandwidth: int = -1,
+                   scores: Scores | None = None, engine: Engine | None = None):   # :1303-1316
+    """rifraf-style fast frameshift correction."""
+    scores = scores or Scores.from_errors(ErrorModel(10.0, 1e-5, 1e-5, 1.0, 1.0))
+    consensus, reference = DNASeq(consensus), DNASeq(reference)
+    log_ps = np.full(len(reference), log_p)
+    if bandwidth < 0:
+        bandwidth = int(math.ceil(min(len(consensus), len(reference)) * 0.1))
+    refseq = RifrafSequence(reference, log_ps, bandwidth, scores)
+    if engine is None:
+        from .align import default_engine
+        engine = default_engine()
+    run = _Run(engine, 0)
+    run.set_consensus(consensus)
+    state = RifrafState(consensus=consensus, ref_scores=scores, reference=refseq, batch_fixed_size=0,
+                        batch_size=0, base_batch_size=0, sequences=[], maxlen=0)
+    engine.set_sequences(run.REF, [refseq])
+    proposals = single_indel_proposals(state, run)
+    return apply_proposals(consensus, proposals)
+
+
+def calibrate_phreds(s, phred, consensus, engine: Engine | None = None):   # :1295-1300
+    from .align import Scratch, edit_distance
+    e = engine or None
+    n_errors = edit_distance(consensus, s, scratch=Scratch(e) if e else None)
+    errors = np.power(10.0, phred_to_log_p(phred))
+    return errors * float(n_errors) / errors.sum()

@@ -1,0 +1,130 @@
+"""CPU stand-in for rifraf_amd.engine.Engine built on the oracle.
+
+TEST INFRASTRUCTURE ONLY: lets the host stage machine (rifraf_amd.model)
+run end to end on CPU, and gives GPU-vs-oracle whole-run comparisons.  Same
+method signatures and semantics as Engine (slots own A/B bands, forward
+flags, left-fold scoring)."""
+import copy
+
+import numpy as np
+
+import oracle
+from rifraf_amd.bandedarrays import BandedArray
+from rifraf_amd.engine import RF_BAND_A, RF_BWD, RF_FWD, RF_SKEW, RF_TRIM, RifrafError
+from rifraf_amd.proposals import to_arrays
+
+
+class OracleEngine:
+    def __init__(self):
+        self.seqs, self.tpls, self.slots = {}, {}, {}
+        self.version = 0
+
+    def close(self):
+        pass
+
+    def set_sequences(self, first, seqs):
+        for k, s in enumerate(seqs):
+            self.seqs[first + k] = copy.copy(s)
+
+    def set_templates(self, first, tpls):
+        for k, t in enumerate(tpls):
+            self.version += 1
+            self.tpls[first + k] = (np.asarray(t, np.uint8).copy(), self.version)
+
+    def realign(self, slots, seqs, tpls, bws, flags):
+        slots = np.atleast_1d(np.asarray(slots, np.int32))
+        n = len(slots)
+        seqs = np.broadcast_to(seqs, (n,))
+        tpls = np.broadcast_to(tpls, (n,))
+        bws = np.broadcast_to(bws, (n,))
+        out = np.empty(n)
+        for k in range(n):
+            s = self.seqs[int(seqs[k])]
+            t, ver = self.tpls[int(tpls[k])]
+            bw = int(bws[k])
+            if bw < 1:
+                raise RifrafError("bandwidth must be positive")
+            ent = self.slots.setdefault(int(slots[k]), {})
+            key = (int(seqs[k]), int(tpls[k]), ver, bw)
+            try:
+                if flags & RF_FWD:
+                    A, mv = oracle.forward(t, s, moves=True, skew=bool(flags & RF_SKEW),
+                                           trim=bool(flags & RF_TRIM), bandwidth=bw)
+                    ent["A"] = (A, mv, key, len(s), len(t))
+                if flags & RF_BWD:
+                    B = oracle.backward(t, s, bandwidth=bw)
+                    ent["B"] = (B, None, key, len(s), len(t))
+            except oracle.OracleError as e:
+                raise RifrafError(str(e))
+            band = ent["A"] if flags & RF_FWD else ent["B"]
+            data = band[0]
+            H = data.shape[0]
+            if flags & RF_FWD:
+                d = len(s) - len(t) + max(len(t) - len(s), 0) + bw
+                out[k] = data[d, len(t)]
+            else:
+                out[k] = data[max(len(t) - len(s), 0) + bw, 0]
+        return out
+
+    def backtrace(self, slots, want_moves=True):
+        mvs, errs = [], []
+        for sl in np.atleast_1d(slots):
+            A, mv, key, n, m = self.slots[int(sl)]["A"]
+            moves = oracle.backtrace(mv, n + 1, m + 1, key[3])
+            t = self.tpls[key[1]][0]
+            s = self.seqs[key[0]]
+            mvs.append(moves)
+            errs.append(oracle.count_errors(moves, t, s.seq))
+        return (mvs if want_moves else None), np.array(errs, np.int32)
+
+    def _check_slot(self, sl):
+        ent = self.slots.get(int(sl), {})
+        if "A" not in ent or "B" not in ent or ent["A"][2] != ent["B"][2]:
+            raise RifrafError("A and B bands were computed for different alignments")
+        return ent
+
+    def score(self, groups, per_seq=False):
+        totals, mats = [], []
+        for bslots, ref, props in groups:
+            k, p, b = props if isinstance(props, tuple) else to_arrays(props)
+            ents = [self._check_slot(s) for s in bslots]
+            reads = [(e["A"][0], e["B"][0], self._seq_bw(e)) for e in ents]
+            rent = self._check_slot(ref) if ref >= 0 else None
+            tot = np.empty(len(k))
+            mat = np.empty((len(k), len(ents) + (1 if rent else 0)))
+            for i in range(len(k)):
+                acc = 0.0
+                for r, (A, B, (s, t)) in enumerate(reads):
+                    v = self._score1(k[i], p[i], b[i], A, B, t, s)
+                    mat[i, r] = v
+                    acc += v
+                if rent is not None:
+                    s, t = self._seq_bw(rent)
+                    v = self._score1(k[i], p[i], b[i], rent["A"][0], rent["B"][0], t, s)
+                    mat[i, -1] = v
+                    acc += v
+                tot[i] = acc
+            totals.append(tot)
+            mats.append(mat)
+        return (totals, mats) if per_seq else totals
+
+    @staticmethod
+    def _score1(kind, pos, base, A, B, t, s):
+        try:
+            return oracle.score_proposal(int(kind), int(pos), int(base), A, B, t, s)
+        except oracle.OracleError as e:
+            raise RifrafError(str(e))
+
+    def _seq_bw(self, ent):
+        key = ent["A"][2]
+        s = copy.copy(self.seqs[key[0]])
+        s.bandwidth = key[3]
+        return s, self.tpls[key[1]][0]
+
+    def geometry(self, slot, which=RF_BAND_A):
+        A, mv, key, n, m = self.slots[int(slot)]["A" if which == RF_BAND_A else "B"]
+        return n + 1, m + 1, key[3], A.shape[0]
+
+    def download_band(self, slot, which=RF_BAND_A, default=-np.inf):
+        data, _, key, n, m = self.slots[int(slot)]["A" if which == RF_BAND_A else "B"]
+        return BandedArray((n + 1, m + 1), key[3], default=default, data=np.asfortranarray(data))

@@ -36,9 +36,13 @@ DP_CASES = [
     (60, 0.05, 9, 4, False),
     (120, 0.03, 9, 12, False),      # H up to 32 -> W=16 class
     (200, 0.03, 20, 10, False),     # W=32 class
-    (300, 0.05, 40, 30, False),     # W=64 class
+    (300, 0.05, 40, 30, False),     # H in (64, 128]: register kernel, 4 pairs per lane
+    (500, 0.05, 80, 20, False),     # H > 128: LDS-ring kernel (W = 64)
     (90, 0.05, 9, 0, True),         # codon moves (reference-style tables)
     (150, 0.10, 15, 6, True),
+    (200, 0.10, 30, 8, True),       # codon moves with 2 pairs per lane
+    (260, 0.10, 45, 10, True),      # codon moves with 4 pairs per lane
+    (400, 0.10, 70, 10, True),      # codon moves on the LDS-ring kernel
 ]
 
 
