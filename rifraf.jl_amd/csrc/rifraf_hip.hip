@@ -284,6 +284,97 @@ __device__ __forceinline__ double dpp_f64(double x)
 #define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
 #define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
 
+// Shift an int / double across the 16-lane DPP row (lanes outside the row
+// read `bound`).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x, int bound)
+{
+    return __builtin_amdgcn_update_dpp(bound, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_any(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// Per-row inputs of the recurrence (align.jl:64-76, :87-103): the read base
+// and the score-table entries row ii uses, in forward or reverse indexing.
+struct RowRec {
+    int sb;
+    double mt, mm, is, ds, ci, cd;
+};
+
+__device__ __forceinline__ RowRec load_row(const DPTask &T, bool rev, const uint8_t *sbase,
+                                           const double *tb, int ii, bool codon)
+{
+    RowRec r;
+    if (ii < 0 || ii > T.n) {
+        r.sb = 4;
+        r.mt = r.mm = r.is = r.ds = r.ci = r.cd = -RF_INF;
+        return r;
+    }
+    r.sb = ii >= 1 ? sbase[rev ? T.n - ii : ii - 1] : 4;
+    const int ks = rev ? min(T.n - 1, T.n - ii) : max(ii - 1, 0);
+    const int kd = rev ? T.n - ii : ii;
+    r.mt = tb[ks];
+    r.mm = tb[T.n + ks];
+    r.is = tb[2 * (size_t)T.n + ks];
+    r.ds = tb[3 * (size_t)T.n + kd];
+    r.ci = -RF_INF;
+    r.cd = -RF_INF;
+    if (codon) {
+        const double *t_cins = tb + 4 * (size_t)T.n + 1;
+        if (T.ncins > 0 && ii >= 3)
+            r.ci = t_cins[rev ? T.ncins - ii + 2 : ii - 3];
+        if (T.ncdel > 0)
+            r.cd = t_cins[T.ncins + kd];
+    }
+    return r;
+}
+
+__device__ __forceinline__ int load_col(const DPTask &T, bool rev, const uint8_t *tbase, int jj)
+{
+    return (jj >= 1 && jj <= T.m) ? tbase[rev ? T.m - jj : jj - 1] : 4;
+}
+
+template <int CTRL>
+__device__ __forceinline__ RowRec dpp_row(const RowRec &x, bool codon)
+{
+    RowRec r;
+    r.sb = dpp_i32<CTRL>(x.sb, 4);
+    r.mt = dpp_f64_any<CTRL>(x.mt);
+    r.mm = dpp_f64_any<CTRL>(x.mm);
+    r.is = dpp_f64_any<CTRL>(x.is);
+    r.ds = dpp_f64_any<CTRL>(x.ds);
+    if (codon) {
+        r.ci = dpp_f64_any<CTRL>(x.ci);
+        r.cd = dpp_f64_any<CTRL>(x.cd);
+    } else {
+        r.ci = r.cd = -RF_INF;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------
+// k_dpr: register-resident, systolic variant of k_dp for H <= 32*NP.
+//
+// Same recurrence, cell values and FP64 sums as k_dp.  Each task owns one
+// 16-lane DPP row (4 tasks per wave); lane q holds band-row pairs
+// q*NP .. q*NP+NP-1.  With pp = q*NP + r the cell of pair pp at step kappa is
+//   row ii = pp + ceil(kappa/2) - c,   column jj = floor(kappa/2) - pp,
+// so at odd steps every pair moves down one read row and at even steps one
+// template column.  The anti-diagonals kappa-1..kappa-3, the per-row score
+// tables and the template base therefore all move systolically through
+// registers: a pair takes the row record of the pair above it and the
+// column base of the pair before it (DPP row_shl / row_shr across lanes);
+// only lane 15 loads a new row (one step ahead) and lane 0 a new column.
+// Out-of-row DPP sources read -Inf, i.e. an out-of-band predecessor, exactly
+// like the ring's sentinels.
+// ---------------------------------------------------------------------
+
 template <int NP>
 __global__ void __launch_bounds__(64)
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
@@ -306,23 +397,42 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     const uint8_t *sbase = bases + T.sb;
     const uint8_t *tbase = bases + T.tb;
     const double *tb = tabs + T.tab;
-    const double *t_match = tb;
-    const double *t_mism = tb + T.n;
-    const double *t_ins = tb + 2 * (size_t)T.n;
-    const double *t_del = tb + 3 * (size_t)T.n;
-    const double *t_cins = tb + 4 * (size_t)T.n + 1;
-    const double *t_cdel = t_cins + T.ncins;
     double *band = bands + T.band;
 
     double v1[NP], v2[NP], v3[NP];
+    RowRec row[NP];
+    int col[NP];
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
         v1[r] = -RF_INF;
         v2[r] = -RF_INF;
         v3[r] = -RF_INF;
+        const int pp = q * NP + r;
+        row[r] = load_row(T, rev, sbase, tb, pp - T.c, codon);   // kappa = 0
+        col[r] = load_col(T, rev, tbase, -pp);
     }
+    // lane 15 prefetches the row entering at the next odd step
+    const int top = 16 * NP - 1;
+    RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);
+
     for (int k = 0; k < kmax; ++k) {
         const int par = k & 1;
+        if (par) {
+            // rows advance: pair pp takes pair pp+1's row; lane 15 takes nxt
+            const RowRec up = dpp_row<DPP_FROM_R1>(row[0], codon);
+#pragma unroll
+            for (int r = 0; r < NP - 1; ++r)
+                row[r] = row[r + 1];
+            row[NP - 1] = (q == 15) ? nxt : up;
+            nxt = load_row(T, rev, sbase, tb, top + (k + 1) / 2 + 1 - T.c, codon);
+        } else if (k > 0) {
+            // columns advance: pair pp takes pair pp-1's column; lane 0 loads
+            const int lo = dpp_i32<DPP_FROM_L1>(col[NP - 1], 4);
+#pragma unroll
+            for (int r = NP - 1; r > 0; --r)
+                col[r] = col[r - 1];
+            col[0] = (q == 0) ? load_col(T, rev, tbase, k / 2) : lo;
+        }
         // block-edge neighbours (uniform control flow: every lane shifts)
         const double L1 = dpp_f64<DPP_FROM_L1>(v1[NP - 1]);
         const double R1 = dpp_f64<DPP_FROM_R1>(v1[0]);
@@ -341,70 +451,56 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             }
         }
         const bool live = k < T.klen;
-        double *row = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
+        double *orow = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
         double nv[NP];
 #pragma unroll
         for (int r = 0; r < NP; ++r) {
             const int d = 2 * (q * NP + r) + par;
             const int jj = (k - d) >> 1;
-            double v = -RF_INF;
+            const int ii = d + jj - T.c;
             const bool stored = live && d < T.H && d <= k;
-            if (stored && jj <= T.m) {
-                const int ii = d + jj - T.c;
-                if (ii >= 0 && ii <= T.n) {
-                    if (ii == 0 && jj == 0) {
-                        v = 0.0;
-                    } else {
-                        // align.jl:64-76 score lookups
-                        const int sb = ii >= 1 ? sbase[rev ? T.n - ii : ii - 1] : 4;
-                        const int tbb = jj >= 1 ? tbase[rev ? T.m - jj : jj - 1] : 4;
-                        const int ks = rev ? min(T.n - 1, T.n - ii) : max(ii - 1, 0);
-                        const int kd = rev ? T.n - ii : ii;
-                        double ms = (sb == tbb) ? t_match[ks] : t_mism[ks];
-                        double is = t_ins[ks];
-                        const double ds = t_del[kd];
-                        if (skew && sb != tbb)
-                            ms *= 0.99;
-                        if (trim && (jj == 0 || jj == T.m))
-                            is = 0.0;
-                        // neighbours: insert (d-1, kappa-1), delete (d+1, kappa-1)
-                        const double x_ins = par ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : L1);
-                        const double x_del = par ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : R1) : v1[r];
-                        // align.jl:77-104, strict '>' in reference order
-                        double best = -RF_INF, x;
-                        x = v2[r] + ms;
-                        if (x > best) best = x;
-                        x = x_ins + is;
-                        if (x > best) best = x;
-                        x = x_del + ds;
-                        if (x > best) best = x;
-                        if (codon) {
-                            if (T.ncins > 0 && ii >= 3) {
-                                // d-3 at kappa-3: pair index q*NP + r - 2 + par
-                                const int idx = r - 2 + par;
-                                const double y = idx >= 0 ? v3[idx >= 0 ? idx : 0] : (idx == -1 ? L3a : L3b);
-                                const int ci = rev ? T.ncins - ii + 2 : ii - 3;
-                                x = y + t_cins[ci];
-                                if (x > best) best = x;
-                            }
-                            if (T.ncdel > 0 && jj >= 3) {
-                                // d+3 at kappa-3: pair index q*NP + r + 1 + par
-                                const int idx = r + 1 + par;
-                                const double y = idx < NP ? v3[idx < NP ? idx : 0] : (idx == NP ? R3a : R3b);
-                                x = y + t_cdel[kd];
-                                if (x > best) best = x;
-                            }
-                        }
-                        if (best == -RF_INF)
-                            set_err(err, 1);  // "new score is invalid"
-                        v = best;
-                    }
-                    if (ii == T.n && jj == T.m && out_score)
-                        out_score[T.out_idx] = v;
+            const bool valid = stored && jj <= T.m && ii >= 0 && ii <= T.n;
+            const RowRec &R = row[r];
+            const int tbb = col[r];
+            double ms = (R.sb == tbb) ? R.mt : R.mm;
+            double is = R.is;
+            if (skew && R.sb != tbb)
+                ms *= 0.99;
+            if (trim && (jj == 0 || jj == T.m))
+                is = 0.0;
+            // neighbours: insert (d-1, kappa-1), delete (d+1, kappa-1)
+            const double x_ins = par ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : L1);
+            const double x_del = par ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : R1) : v1[r];
+            // align.jl:77-104, strict '>' in reference order
+            double best = -RF_INF, x;
+            x = v2[r] + ms;
+            if (x > best) best = x;
+            x = x_ins + is;
+            if (x > best) best = x;
+            x = x_del + R.ds;
+            if (x > best) best = x;
+            if (codon) {
+                if (ii >= 3) {   // codon insert: d-3 at kappa-3 = pair q*NP + r - 2 + par
+                    const int idx = r - 2 + par;
+                    const double y = idx >= 0 ? v3[idx >= 0 ? idx : 0] : (idx == -1 ? L3a : L3b);
+                    x = y + R.ci;
+                    if (x > best) best = x;
+                }
+                if (jj >= 3) {   // codon delete: d+3 at kappa-3 = pair q*NP + r + 1 + par
+                    const int idx = r + 1 + par;
+                    const double y = idx < NP ? v3[idx < NP ? idx : 0] : (idx == NP ? R3a : R3b);
+                    x = y + R.cd;
+                    if (x > best) best = x;
                 }
             }
+            const bool origin = ii == 0 && jj == 0;
+            double v = valid ? (origin ? 0.0 : best) : -RF_INF;
+            if (valid && !origin && best == -RF_INF)
+                set_err(err, 1);  // "new score is invalid"
+            if (valid && ii == T.n && jj == T.m && out_score)
+                out_score[T.out_idx] = v;
             if (stored)
-                row[(rev ? T.H - 1 - d : d) >> 1] = v;
+                orow[(rev ? T.H - 1 - d : d) >> 1] = v;
             nv[r] = v;
         }
 #pragma unroll
