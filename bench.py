@@ -119,9 +119,11 @@ def main():
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    import torch
-    dist = None
+    dist = torch = None
     if world > 1:
+        # torch only for the process group (RCCL over xGMI / gloo): the engine
+        # calls are synchronous on their own HIP stream
+        import torch
         import torch.distributed as dist
         backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -173,18 +175,17 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    sync = (lambda: torch.cuda.synchronize()) if (torch is not None and torch.cuda.is_available()) else (lambda: None)
     if dist is not None:
         dist.barrier()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     dps, scs = [], []
     for _ in range(args.steps):
         a, b = step()
         dps.append(a)
         scs.append(b)
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -340,18 +340,24 @@ __device__ __forceinline__ int load_col(const DPTask &T, bool rev, const uint8_t
     return (jj >= 1 && jj <= T.m) ? tbase[rev ? T.m - jj : jj - 1] : 4;
 }
 
-template <int CTRL>
-__device__ __forceinline__ RowRec dpp_row(const RowRec &x, bool codon)
+// Row record of the lane above (row_shl:1); lane 15 receives `edge`.
+__device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &edge, bool codon)
 {
     RowRec r;
-    r.sb = dpp_i32<CTRL>(x.sb, 4);
-    r.mt = dpp_f64_any<CTRL>(x.mt);
-    r.mm = dpp_f64_any<CTRL>(x.mm);
-    r.is = dpp_f64_any<CTRL>(x.is);
-    r.ds = dpp_f64_any<CTRL>(x.ds);
+    r.sb = __builtin_amdgcn_update_dpp(edge.sb, x.sb, DPP_FROM_R1, 0xF, 0xF, false);
+    auto sh = [](double v, double e) {
+        const long long b = __double_as_longlong(v), eb = __double_as_longlong(e);
+        const int lo = __builtin_amdgcn_update_dpp((int)eb, (int)b, DPP_FROM_R1, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_update_dpp((int)(eb >> 32), (int)(b >> 32), DPP_FROM_R1, 0xF, 0xF, false);
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    };
+    r.mt = sh(x.mt, edge.mt);
+    r.mm = sh(x.mm, edge.mm);
+    r.is = sh(x.is, edge.is);
+    r.ds = sh(x.ds, edge.ds);
     if (codon) {
-        r.ci = dpp_f64_any<CTRL>(x.ci);
-        r.cd = dpp_f64_any<CTRL>(x.cd);
+        r.ci = sh(x.ci, edge.ci);
+        r.cd = sh(x.cd, edge.cd);
     } else {
         r.ci = r.cd = -RF_INF;
     }
@@ -361,19 +367,103 @@ __device__ __forceinline__ RowRec dpp_row(const RowRec &x, bool codon)
 // ---------------------------------------------------------------------
 // k_dpr: register-resident, systolic variant of k_dp for H <= 32*NP.
 //
-// Same recurrence, cell values and FP64 sums as k_dp.  Each task owns one
-// 16-lane DPP row (4 tasks per wave); lane q holds band-row pairs
-// q*NP .. q*NP+NP-1.  With pp = q*NP + r the cell of pair pp at step kappa is
+// Same recurrence and cell values as k_dp.  Each task owns one 16-lane DPP
+// row (4 tasks per wave); lane q holds band-row pairs q*NP .. q*NP+NP-1.
+// With pp = q*NP + r the cell of pair pp at anti-diagonal kappa is
 //   row ii = pp + ceil(kappa/2) - c,   column jj = floor(kappa/2) - pp,
 // so at odd steps every pair moves down one read row and at even steps one
 // template column.  The anti-diagonals kappa-1..kappa-3, the per-row score
-// tables and the template base therefore all move systolically through
-// registers: a pair takes the row record of the pair above it and the
-// column base of the pair before it (DPP row_shl / row_shr across lanes);
-// only lane 15 loads a new row (one step ahead) and lane 0 a new column.
-// Out-of-row DPP sources read -Inf, i.e. an out-of-band predecessor, exactly
-// like the ring's sentinels.
+// tables and the template base all move systolically through registers: a
+// pair takes the row record of the pair above it and the column base of the
+// pair before it (DPP row_shl / row_shr); the DPP "old" operand hands lane 15
+// its prefetched row and lane 0 its new column.  Out-of-row DPP sources read
+// -Inf, i.e. an out-of-band predecessor, exactly like the ring's sentinels.
+// The loop is unrolled over (even, odd) anti-diagonals so the parity is
+// static.  The cell value of the reference's strict-'>' candidate chain
+// (align.jl:43, :77-104) is the maximum of the candidates, and FP64 max of
+// the same sums is exact (no NaN, no signed zero among candidates), so
+// fmax yields bit-identical cells; the move is recomputed in k_backtrace
+// with the strict order.
 // ---------------------------------------------------------------------
+
+template <int NP, int PAR>
+__device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool codon, bool rev,
+                                         bool skew, bool trim, double (&v1)[NP], double (&v2)[NP],
+                                         double (&v3)[NP], const RowRec (&row)[NP],
+                                         const int (&col)[NP], double *__restrict__ band,
+                                         double *__restrict__ out_score, int *__restrict__ err)
+{
+    // block-edge neighbours at kappa-1 (every lane shifts: uniform control flow)
+    double E1;
+    if (PAR == 0)
+        E1 = dpp_f64<DPP_FROM_L1>(v1[NP - 1]);   // (d-1) of pair 0 = lane q-1's last pair
+    else
+        E1 = dpp_f64<DPP_FROM_R1>(v1[0]);        // (d+1) of the last pair = lane q+1's pair 0
+    double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
+    if (codon) {
+        if (NP == 1) {
+            L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
+            L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
+            R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
+            R3b = dpp_f64<DPP_FROM_R2>(v3[0]);
+        } else {
+            L3a = dpp_f64<DPP_FROM_L1>(v3[NP - 1]);
+            L3b = dpp_f64<DPP_FROM_L1>(v3[NP > 1 ? NP - 2 : 0]);
+            R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
+            R3b = dpp_f64<DPP_FROM_R1>(v3[NP > 1 ? 1 : 0]);
+        }
+    }
+    const bool live = k < T.klen;
+    double *orow = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
+    double nv[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+        const int d = 2 * (q * NP + r) + PAR;
+        const int jj = (k - d) >> 1;
+        const int ii = d + jj - T.c;
+        const bool stored = live && d < T.H && d <= k;
+        const bool valid = stored && jj <= T.m && ii >= 0 && ii <= T.n;
+        const RowRec &R = row[r];
+        const int tbb = col[r];
+        double ms = (R.sb == tbb) ? R.mt : R.mm;
+        double is = R.is;
+        if (skew && R.sb != tbb)
+            ms *= 0.99;
+        if (trim && (jj == 0 || jj == T.m))
+            is = 0.0;
+        // insert (d-1, kappa-1) and delete (d+1, kappa-1)
+        const double x_ins = PAR ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : E1);
+        const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
+        double best = fmax(fmax(v2[r] + ms, x_ins + is), x_del + R.ds);
+        if (codon) {
+            if (ii >= 3) {   // codon insert: d-3 at kappa-3 = pair q*NP + r - 2 + PAR
+                const int idx = r - 2 + PAR;
+                const double y = idx >= 0 ? v3[idx >= 0 ? idx : 0] : (idx == -1 ? L3a : L3b);
+                best = fmax(best, y + R.ci);
+            }
+            if (jj >= 3) {   // codon delete: d+3 at kappa-3 = pair q*NP + r + 1 + PAR
+                const int idx = r + 1 + PAR;
+                const double y = idx < NP ? v3[idx < NP ? idx : 0] : (idx == NP ? R3a : R3b);
+                best = fmax(best, y + R.cd);
+            }
+        }
+        const bool origin = ii == 0 && jj == 0;
+        const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
+        if (valid && !origin && best == -RF_INF)
+            set_err(err, 1);  // "new score is invalid"
+        if (valid && ii == T.n && jj == T.m && out_score)
+            out_score[T.out_idx] = v;
+        if (stored)
+            orow[(rev ? T.H - 1 - d : d) >> 1] = v;
+        nv[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+        v3[r] = v2[r];
+        v2[r] = v1[r];
+        v1[r] = nv[r];
+    }
+}
 
 template <int NP>
 __global__ void __launch_bounds__(64)
@@ -390,7 +480,6 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     for (int off = 32; off >= 1; off >>= 1)
         kmax = max(kmax, __shfl_xor(kmax, off));
     const bool codon = __any(T.ncins > 0 || T.ncdel > 0);   // wave-uniform
-
     const bool rev = T.flags & 1;
     const bool skew = T.flags & 2;
     const bool trim = T.flags & 4;
@@ -411,103 +500,30 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         row[r] = load_row(T, rev, sbase, tb, pp - T.c, codon);   // kappa = 0
         col[r] = load_col(T, rev, tbase, -pp);
     }
-    // lane 15 prefetches the row entering at the next odd step
     const int top = 16 * NP - 1;
-    RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);
+    RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);   // enters at kappa = 1
 
-    for (int k = 0; k < kmax; ++k) {
-        const int par = k & 1;
-        if (par) {
-            // rows advance: pair pp takes pair pp+1's row; lane 15 takes nxt
-            const RowRec up = dpp_row<DPP_FROM_R1>(row[0], codon);
-#pragma unroll
-            for (int r = 0; r < NP - 1; ++r)
-                row[r] = row[r + 1];
-            row[NP - 1] = (q == 15) ? nxt : up;
-            nxt = load_row(T, rev, sbase, tb, top + (k + 1) / 2 + 1 - T.c, codon);
-        } else if (k > 0) {
-            // columns advance: pair pp takes pair pp-1's column; lane 0 loads
-            const int lo = dpp_i32<DPP_FROM_L1>(col[NP - 1], 4);
+    for (int k = 0; k < kmax; k += 2) {
+        if (k > 0) {
+            // even step: columns advance; lane 0 receives column k/2
+            const int edge = load_col(T, rev, tbase, k / 2);
+            const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
 #pragma unroll
             for (int r = NP - 1; r > 0; --r)
                 col[r] = col[r - 1];
-            col[0] = (q == 0) ? load_col(T, rev, tbase, k / 2) : lo;
+            col[0] = from;
         }
-        // block-edge neighbours (uniform control flow: every lane shifts)
-        const double L1 = dpp_f64<DPP_FROM_L1>(v1[NP - 1]);
-        const double R1 = dpp_f64<DPP_FROM_R1>(v1[0]);
-        double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
-        if (codon) {
-            if (NP == 1) {
-                L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
-                L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
-                R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
-                R3b = dpp_f64<DPP_FROM_R2>(v3[0]);
-            } else {
-                L3a = dpp_f64<DPP_FROM_L1>(v3[NP - 1]);
-                L3b = dpp_f64<DPP_FROM_L1>(v3[NP > 1 ? NP - 2 : 0]);
-                R3a = dpp_f64<DPP_FROM_R1>(v3[0]);
-                R3b = dpp_f64<DPP_FROM_R1>(v3[NP > 1 ? 1 : 0]);
-            }
-        }
-        const bool live = k < T.klen;
-        double *orow = band + (size_t)(rev ? T.klen - 1 - k : k) * T.P;
-        double nv[NP];
+        dpr_step<NP, 0>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err);
+        if (k + 1 < kmax) {
+            // odd step: rows advance; lane 15 receives the prefetched row
+            const RowRec up = row_from_above(row[0], nxt, codon);
 #pragma unroll
-        for (int r = 0; r < NP; ++r) {
-            const int d = 2 * (q * NP + r) + par;
-            const int jj = (k - d) >> 1;
-            const int ii = d + jj - T.c;
-            const bool stored = live && d < T.H && d <= k;
-            const bool valid = stored && jj <= T.m && ii >= 0 && ii <= T.n;
-            const RowRec &R = row[r];
-            const int tbb = col[r];
-            double ms = (R.sb == tbb) ? R.mt : R.mm;
-            double is = R.is;
-            if (skew && R.sb != tbb)
-                ms *= 0.99;
-            if (trim && (jj == 0 || jj == T.m))
-                is = 0.0;
-            // neighbours: insert (d-1, kappa-1), delete (d+1, kappa-1)
-            const double x_ins = par ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : L1);
-            const double x_del = par ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : R1) : v1[r];
-            // align.jl:77-104, strict '>' in reference order
-            double best = -RF_INF, x;
-            x = v2[r] + ms;
-            if (x > best) best = x;
-            x = x_ins + is;
-            if (x > best) best = x;
-            x = x_del + R.ds;
-            if (x > best) best = x;
-            if (codon) {
-                if (ii >= 3) {   // codon insert: d-3 at kappa-3 = pair q*NP + r - 2 + par
-                    const int idx = r - 2 + par;
-                    const double y = idx >= 0 ? v3[idx >= 0 ? idx : 0] : (idx == -1 ? L3a : L3b);
-                    x = y + R.ci;
-                    if (x > best) best = x;
-                }
-                if (jj >= 3) {   // codon delete: d+3 at kappa-3 = pair q*NP + r + 1 + par
-                    const int idx = r + 1 + par;
-                    const double y = idx < NP ? v3[idx < NP ? idx : 0] : (idx == NP ? R3a : R3b);
-                    x = y + R.cd;
-                    if (x > best) best = x;
-                }
-            }
-            const bool origin = ii == 0 && jj == 0;
-            double v = valid ? (origin ? 0.0 : best) : -RF_INF;
-            if (valid && !origin && best == -RF_INF)
-                set_err(err, 1);  // "new score is invalid"
-            if (valid && ii == T.n && jj == T.m && out_score)
-                out_score[T.out_idx] = v;
-            if (stored)
-                orow[(rev ? T.H - 1 - d : d) >> 1] = v;
-            nv[r] = v;
-        }
-#pragma unroll
-        for (int r = 0; r < NP; ++r) {
-            v3[r] = v2[r];
-            v2[r] = v1[r];
-            v1[r] = nv[r];
+            for (int r = 0; r < NP - 1; ++r)
+                row[r] = row[r + 1];
+            row[NP - 1] = up;
+            nxt = load_row(T, rev, sbase, tb, top + (k + 2) / 2 + 1 - T.c, codon);
+            dpr_step<NP, 1>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
+                            out_score, err);
         }
     }
 }
@@ -545,7 +561,12 @@ struct BandWin {
 
 // HALF 0: Substitution(p, b) chains + Deletion(p)  -> out[0..4]
 // HALF 1: Insertion(p, b) chains                     -> out[5..8]
-// (two waves of one workgroup share the staged A/B window)
+// (two waves of one workgroup share the staged A/B window).
+// update() of a new column (align.jl:50-112) keeps the first strictly-best
+// of {match, insert, delete}; its value is the FP64 max of the three sums
+// (no NaN / signed zero among candidates), and the sums are formed from the
+// same operands as the reference, so fmax is bit-exact.  A chain that hits
+// -Inf ("new score is invalid") is detected by the running minimum.
 template <int HALF>
 __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
                                            const uint8_t *__restrict__ s,
@@ -560,6 +581,13 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
     const double qnan = __builtin_nan("");
     // row ranges (bandedarrays.jl:133-137), 0-based rows
     const int s0 = max(0, p - c), s1 = min(p + vb, n);             // rows(p): new Sub col, B col p
+    double prev[4], acc[4], mn[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        prev[b] = -RF_INF;
+        acc[b] = -RF_INF;
+        mn[b] = RF_INF;
+    }
     if (HALF == 0) {
         if (p < 1) {
 #pragma unroll
@@ -568,14 +596,6 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
             return;
         }
         const int d0 = max(0, p - 1 - c), d1 = min(p - 1 + vb, n);  // rows(p-1): A col p-1
-        double prev[4], acc[4];
-        bool bad[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            prev[b] = -RF_INF;
-            acc[b] = -RF_INF;
-            bad[b] = false;
-        }
         double del_acc = -RF_INF;
         // A(p-1, ii) in band iff ii in rows(p-1)
         double am1_prev = (s0 - 1 >= d0) ? A.at(s0 - 1 - (p - 1) + c, p - 1) : -RF_INF;
@@ -584,20 +604,14 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
             const double b0 = B.at(ii - p + c, p);
             const int sb = ii >= 1 ? s[ii - 1] : 4;
             const int ks = max(ii - 1, 0);
-            const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
-            const double ds = t_del[ii];
+            const double dm = am1_prev + t_match[ks];     // match predecessor (i-1, p)
+            const double dx = am1_prev + t_mism[ks];      //   ... mismatching base
+            const double is = t_ins[ks];
+            const double dl = am1 + t_del[ii];            // delete predecessor (i, p)
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                // update(A, i, p+1, s[i-1], b; newcols, acol=p), align.jl:50-112
-                const double ms = (sb == b) ? mt : mm;
-                double best = -RF_INF, x;
-                x = am1_prev + ms;
-                if (x > best) best = x;
-                x = prev[b] + is;
-                if (x > best) best = x;
-                x = am1 + ds;
-                if (x > best) best = x;
-                bad[b] |= (best == -RF_INF);
+                const double best = fmax(fmax(sb == b ? dm : dx, prev[b] + is), dl);
+                mn[b] = fmin(mn[b], best);
                 prev[b] = best;
                 acc[b] = fmax(acc[b], best + b0);     // summax, util.jl:40-48
             }
@@ -607,19 +621,11 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            out[b] = (bad[b] || acc[b] == -RF_INF) ? qnan : acc[b];
+            out[b] = (mn[b] == -RF_INF || acc[b] == -RF_INF) ? qnan : acc[b];
         out[4] = del_acc;
     } else {
         const int pI = min(p + 1, m);                                // new Ins col's row range
         const int i0 = max(0, pI - c), i1 = min(pI + vb, n);
-        double prev[4], acc[4];
-        bool bad[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            prev[b] = -RF_INF;
-            acc[b] = -RF_INF;
-            bad[b] = false;
-        }
         // A(p, ii) in band iff ii in rows(p)
         double a0_prev = (i0 - 1 >= s0) ? A.at(i0 - 1 - p + c, p) : -RF_INF;
         for (int ii = i0; ii <= i1; ++ii) {
@@ -628,20 +634,14 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
             const double b0 = in_s ? B.at(ii - p + c, p) : -RF_INF;
             const int sb = ii >= 1 ? s[ii - 1] : 4;
             const int ks = max(ii - 1, 0);
-            const double mt = t_match[ks], mm = t_mism[ks], is = t_ins[ks];
-            const double ds = t_del[ii];
+            const double dm = a0_prev + t_match[ks];
+            const double dx = a0_prev + t_mism[ks];
+            const double is = t_ins[ks];
+            const double dl = a0 + t_del[ii];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                // update(A, i, p+2, s[i-1], b; newcols, acol=p+1)
-                const double ms = (sb == b) ? mt : mm;
-                double best = -RF_INF, x;
-                x = a0_prev + ms;
-                if (x > best) best = x;
-                x = prev[b] + is;
-                if (x > best) best = x;
-                x = a0 + ds;
-                if (x > best) best = x;
-                bad[b] |= (best == -RF_INF);
+                const double best = fmax(fmax(sb == b ? dm : dx, prev[b] + is), dl);
+                mn[b] = fmin(mn[b], best);
                 prev[b] = best;
                 acc[b] = fmax(acc[b], best + b0);
             }
@@ -649,7 +649,7 @@ __device__ __forceinline__ void score_half(int p, int m, const ScoreRead &R,
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            out[b] = (bad[b] || acc[b] == -RF_INF) ? qnan : acc[b];
+            out[b] = (mn[b] == -RF_INF || acc[b] == -RF_INF) ? qnan : acc[b];
     }
 }
 
@@ -1115,6 +1115,30 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 }
 
 // ---------------------------------------------------------------------
+// k_scatter: one staged upload -> per-object device regions (a block per
+// segment), so a batch upload is one H2D copy instead of one per object.
+// ---------------------------------------------------------------------
+struct alignas(16) Segment {
+    int64_t src, dst, len;   // bytes
+    int64_t pad;
+};
+
+__global__ void k_scatter(const Segment *__restrict__ segs, const uint8_t *__restrict__ src,
+                          uint8_t *__restrict__ dst)
+{
+    const Segment S = segs[blockIdx.x];
+    if ((S.src | S.dst | S.len) % 8 == 0) {
+        const uint64_t *a = reinterpret_cast<const uint64_t *>(src + S.src);
+        uint64_t *b = reinterpret_cast<uint64_t *>(dst + S.dst);
+        for (int64_t e = threadIdx.x; e < S.len / 8; e += blockDim.x)
+            b[e] = a[e];
+    } else {
+        for (int64_t e = threadIdx.x; e < S.len; e += blockDim.x)
+            dst[S.dst + e] = src[S.src + e];
+    }
+}
+
+// ---------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------
 
@@ -1438,7 +1462,8 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     (void)hipSetDevice(ctx->device);
     if ((int64_t)first + nseq > (int64_t)ctx->seqs.size())
         ctx->seqs.resize(first + nseq);
-    std::vector<double> host;
+    // 1. regions (arena growth may move earlier regions: offsets are read after)
+    int64_t nb = 0, nt = 0;
     for (int32_t k = 0; k < nseq; ++k) {
         SeqObj &S = ctx->seqs[first + k];
         const int64_t n = off[k + 1] - off[k];
@@ -1449,27 +1474,52 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
         S.n = (int32_t)n;
         S.ncins = (int32_t)nci;
         S.ncdel = (int32_t)ncd;
-        const int64_t ntab = 4 * n + 1 + nci + ncd;
         if (int e = region_ensure(ctx, ctx->bytes_arena, S.bases, n))
             return e;
-        if (int e = region_ensure(ctx, ctx->tab_arena, S.tabs, ntab * 8))
+        if (int e = region_ensure(ctx, ctx->tab_arena, S.tabs, (4 * n + 1 + nci + ncd) * 8))
             return e;
-        host.resize(ntab);
-        std::memcpy(host.data(), match + off[k], n * 8);
-        std::memcpy(host.data() + n, mismatch + off[k], n * 8);
-        std::memcpy(host.data() + 2 * n, ins + off[k], n * 8);
-        std::memcpy(host.data() + 3 * n, del + off[k] + k, (n + 1) * 8);
-        if (nci)
-            std::memcpy(host.data() + 4 * n + 1, cins + cins_off[k], nci * 8);
-        if (ncd)
-            std::memcpy(host.data() + 4 * n + 1 + nci, cdel + cdel_off[k], ncd * 8);
-        HIPCHK(ctx, hipMemcpyAsync(ctx->bytes_arena.d + S.bases.off, bases + off[k], n,
-                                   hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->tab_arena.d + S.tabs.off, host.data(), ntab * 8,
-                                   hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        S.valid = true;
+        nb += n;
+        nt += 4 * n + 1 + nci + ncd;
     }
+    // 2. pack: bases as given; tables [match|mismatch|ins|del|cins|cdel] per sequence
+    std::vector<double> host((size_t)std::max<int64_t>(nt, 1));
+    std::vector<Segment> sb(nseq), st(nseq);
+    int64_t at = 0;
+    for (int32_t k = 0; k < nseq; ++k) {
+        const SeqObj &S = ctx->seqs[first + k];
+        const int64_t n = S.n, nci = S.ncins, ncd = S.ncdel;
+        double *h = host.data() + at;
+        std::memcpy(h, match + off[k], n * 8);
+        std::memcpy(h + n, mismatch + off[k], n * 8);
+        std::memcpy(h + 2 * n, ins + off[k], n * 8);
+        std::memcpy(h + 3 * n, del + off[k] + k, (n + 1) * 8);
+        if (nci)
+            std::memcpy(h + 4 * n + 1, cins + cins_off[k], nci * 8);
+        if (ncd)
+            std::memcpy(h + 4 * n + 1 + nci, cdel + cdel_off[k], ncd * 8);
+        const int64_t len = 4 * n + 1 + nci + ncd;
+        st[k] = {at * 8, S.tabs.off, len * 8, 0};
+        sb[k] = {off[k] - off[0], S.bases.off, n, 0};
+        at += len;
+    }
+    // 3. one H2D copy each + device scatter
+    if (int e = ensure_buf(ctx, ctx->scratch[6], (size_t)std::max<int64_t>(nt * 8, 16))) return e;
+    if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
+    if (nseq > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[6].p, host.data(), nt * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, bases + off[0], nb, hipMemcpyHostToDevice, ctx->stream));
+        if (int e = upload(ctx, ctx->scratch[5], st)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[6].p, (uint8_t *)ctx->tab_arena.d);
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // scratch[5] is reused below
+        if (int e = upload(ctx, ctx->scratch[5], sb)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    for (int32_t k = 0; k < nseq; ++k)
+        ctx->seqs[first + k].valid = true;
     ++ctx->layout_gen;
     return 0;
 }
@@ -1489,13 +1539,23 @@ int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl, const uint8_t *ba
             return fail(ctx, RF_ERR_ARG, "rf_set_templates: empty template");
         if (int e = region_ensure(ctx, ctx->bytes_arena, T.bases, m))
             return e;
-        HIPCHK(ctx, hipMemcpyAsync(ctx->bytes_arena.d + T.bases.off, bases + off[k], m,
-                                   hipMemcpyHostToDevice, ctx->stream));
         if (T.m != (int32_t)m)
             ++ctx->layout_gen;
         T.m = (int32_t)m;
         T.version = ++ctx->tpl_counter;
         T.valid = true;
+    }
+    if (ntpl > 0) {
+        std::vector<Segment> sg(ntpl);
+        for (int32_t k = 0; k < ntpl; ++k)
+            sg[k] = {off[k] - off[0], ctx->tpls[first + k].bases.off, off[k + 1] - off[k], 0};
+        const int64_t nb = off[ntpl] - off[0];
+        if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, bases + off[0], nb, hipMemcpyHostToDevice, ctx->stream));
+        if (int e = upload(ctx, ctx->scratch[5], sg)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(ntpl), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
+        HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
