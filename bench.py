@@ -106,6 +106,23 @@ def cpu_baseline(clusters, budget_s=12.0, max_threads=16):
                       f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads"}
 
 
+def shard_seed(seed: int, rank: int) -> int:
+    """Each rank simulates its own clusters (weak scaling, no shared input)."""
+    return seed * 1000003 + rank
+
+
+def aggregate(elapsed: float, units, device="cpu"):
+    """Whole-job figures: the slowest rank's time and the units of all ranks.
+    The only cross-rank traffic of the benchmark (clusters are independent)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(u) for u in units], dtype=torch.float64, device=device)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), [float(x) for x in c.tolist()]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,7 +151,7 @@ def main():
     if args.clusters is not None:
         nclu = args.clusters
     t_gen = time.perf_counter()
-    clusters = make_workload(nclu, nreads, length, err, bw, seed=args.seed * 1000003 + rank)
+    clusters = make_workload(nclu, nreads, length, err, bw, seed=shard_seed(args.seed, rank))
     gen_s = time.perf_counter() - t_gen
 
     from rifraf_amd.engine import RF_BWD, RF_FWD, Engine
@@ -189,15 +206,11 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    tot_cells, tot_props, tot_pairs = cells, nprops, npairs
+    # per-step units of this rank; the timed region ran args.steps steps
+    tot_cells, tot_props, tot_pairs = cells * args.steps, nprops * args.steps, npairs * args.steps
     if dist is not None:
         dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([cells, nprops, npairs], dtype=torch.float64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        tot_cells, tot_props, tot_pairs = (float(x) for x in c.tolist())
+        elapsed, (tot_cells, tot_props, tot_pairs) = aggregate(elapsed, [tot_cells, tot_props, tot_pairs], dev)
 
     ms_step = elapsed / args.steps * 1e3
     dp_ms = float(np.mean(dps))

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -465,7 +466,56 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     }
 }
 
-template <int NP>
+// Whole-row DPP rotate of an f64 (no "old" operand: every lane has a source).
+template <int CTRL>
+__device__ __forceinline__ double dpp_rot_f64(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+#define DPP_ROT_L1 0x121   // row_ror:1  -> lane (q-1) mod 16
+#define DPP_ROT_R1 0x12F   // row_ror:15 -> lane (q+1) mod 16
+
+// One anti-diagonal of the lean interior (LEAN kernels, kappa in [klo, khi]):
+// no codon / skew / trim, and every cell of an active diagonal is inside the
+// matrix, so the per-cell range checks, the origin and A[end,end] cases of
+// dpr_step drop out.  Inactive diagonals (d >= H, or no cell in the matrix)
+// get lb = -Inf, which keeps them at -Inf exactly like dpr_step's masking
+// (x + 0.0 == x for every cell value: no cell is -0.0).  The block-edge
+// neighbour comes from a row *rotate*: the lane it wraps from holds diagonal
+// 32*NP-1 >= H (host guarantees H <= 32*NP-1), i.e. -Inf.  A cell whose
+// candidates are all -Inf ("new score is invalid", align.jl:105-107) is
+// collected in `bad` and reported after the loop.
+template <int NP, int PAR>
+__device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], const RowRec (&row)[NP],
+                                         const int (&col)[NP], const double (&lb)[NP],
+                                         const bool (&st)[NP], const bool (&act)[NP], double *o,
+                                         int ostep, unsigned long long &bad)
+{
+    const double E1 = PAR == 0 ? dpp_rot_f64<DPP_ROT_L1>(v1[NP - 1]) : dpp_rot_f64<DPP_ROT_R1>(v1[0]);
+    double nv[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+        const RowRec &R = row[r];
+        const double ms = (R.sb == col[r]) ? R.mt : R.mm;
+        const double x_ins = PAR ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : E1);
+        const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
+        const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
+        bad |= __ballot(act[r] && raw == -RF_INF);
+        nv[r] = raw + lb[r];
+        if (st[r])
+            o[r * ostep] = nv[r];
+    }
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+        v2[r] = v1[r];
+        v1[r] = nv[r];
+    }
+}
+
+template <int NP, bool LEAN>
 __global__ void __launch_bounds__(64)
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
@@ -479,10 +529,11 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     int kmax = T.klen;
     for (int off = 32; off >= 1; off >>= 1)
         kmax = max(kmax, __shfl_xor(kmax, off));
-    const bool codon = __any(T.ncins > 0 || T.ncdel > 0);   // wave-uniform
+    kmax = __builtin_amdgcn_readfirstlane(kmax);
+    const bool codon = LEAN ? false : __any(T.ncins > 0 || T.ncdel > 0);   // wave-uniform
     const bool rev = T.flags & 1;
-    const bool skew = T.flags & 2;
-    const bool trim = T.flags & 4;
+    const bool skew = LEAN ? false : (T.flags & 2);
+    const bool trim = LEAN ? false : (T.flags & 4);
     const uint8_t *sbase = bases + T.sb;
     const uint8_t *tbase = bases + T.tb;
     const double *tb = tabs + T.tab;
@@ -503,7 +554,100 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     const int top = 16 * NP - 1;
     RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);   // enters at kappa = 1
 
+    // Lean interior [klo, khi]: the kappa range in which every cell of every
+    // active diagonal of the wave's four tasks is inside the matrix, minus the
+    // origin and the final cell.  Diagonal d holds cells jj in
+    // [max(0, c-d), min(m, n+c-d)], i.e. kappa in [d + 2 jlo, d + 2 jhi].
+    int klo = INT_MAX, khi = -1;
+    double lb[2][NP];
+    bool st[2][NP], act[2][NP];
+    if (LEAN) {
+        int lo = 0, hi = INT_MAX;
+        bool ok = true;
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+            for (int r = 0; r < NP; ++r) {
+                const int d = 2 * (q * NP + r) + par;
+                const int jlo = max(0, T.c - d), jhi = min(T.m, T.n + T.c - d);
+                const bool a = tid < ntasks && d < T.H && jlo <= jhi;
+                act[par][r] = a;
+                st[par][r] = tid < ntasks && d < T.H;
+                lb[par][r] = a ? 0.0 : -RF_INF;
+                if (a) {
+                    lo = max(lo, d + 2 * jlo);
+                    hi = min(hi, d + 2 * jhi);
+                }
+            }
+        if (tid < ntasks) {
+            lo = max(lo, T.c + 1);
+            hi = min(hi, T.klen - 2);
+            ok = T.c <= T.m;   // diagonal 0 holds cells: edge rows stay >= 1
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo = max(lo, __shfl_xor(lo, off));
+            hi = min(hi, __shfl_xor(hi, off));
+        }
+        if (__all(ok)) {
+            klo = __builtin_amdgcn_readfirstlane((lo + 1) & ~1);   // wave-uniform: scalar loop
+            khi = __builtin_amdgcn_readfirstlane(hi);
+        }
+    }
+    unsigned long long bad = 0;
+
     for (int k = 0; k < kmax; k += 2) {
+        if (LEAN && k == klo && k + 1 <= khi) {
+            const int P = T.P;
+            double *o0 = band + (ptrdiff_t)(rev ? T.klen - 1 - k : k) * P +
+                         (rev ? (T.H - 1 - 2 * q * NP) >> 1 : q * NP);
+            double *o1 = band + (ptrdiff_t)(rev ? T.klen - 2 - k : k + 1) * P +
+                         (rev ? (T.H - 2 - 2 * q * NP) >> 1 : q * NP);
+            const ptrdiff_t s2 = rev ? -2 * (ptrdiff_t)P : 2 * (ptrdiff_t)P;
+            const int ostep = rev ? -1 : 1;
+            const int top_c = 16 * NP + 1 - T.c;
+            // column bases entering lane 0, one period ahead (clamped like the
+            // edge rows; >= 1 also for padding tasks)
+            auto col_edge = [&](int kk) {
+                const int jj = max(1, min(kk >> 1, T.m));
+                return (int)tbase[rev ? T.m - jj : jj - 1];
+            };
+            int nedge = col_edge(k);
+            for (; k + 1 <= khi; k += 2) {
+                {   // even step: columns advance (column k/2 >= 1 enters lane 0)
+                    const int edge = nedge;
+                    nedge = col_edge(k + 2);
+                    const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
+#pragma unroll
+                    for (int r = NP - 1; r > 0; --r)
+                        col[r] = col[r - 1];
+                    col[0] = from;
+                }
+                dpl_step<NP, 0>(v1, v2, row, col, lb[0], st[0], act[0], o0, ostep, bad);
+                {   // odd step: rows advance; lane 15 receives the prefetched row
+                    const RowRec up = row_from_above(row[0], nxt, false);
+#pragma unroll
+                    for (int r = 0; r < NP - 1; ++r)
+                        row[r] = row[r + 1];
+                    row[NP - 1] = up;
+                    // next edge row (clamped: a row past the read only reaches
+                    // cells outside the matrix, which are never active here
+                    // and are masked in the general steps)
+                    const int ii = max(1, min(top_c + (k >> 1), T.n));
+                    const int ks = rev ? T.n - ii : ii - 1;
+                    const int kd = rev ? ks : ks + 1;
+                    nxt.sb = sbase[ks];
+                    nxt.mt = tb[ks];
+                    nxt.mm = tb[T.n + ks];
+                    nxt.is = tb[2 * (size_t)T.n + ks];
+                    nxt.ds = tb[3 * (size_t)T.n + kd];
+                }
+                dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], act[1], o1, ostep, bad);
+                o0 += s2;
+                o1 += s2;
+            }
+            if (k >= kmax)
+                break;
+        }
         if (k > 0) {
             // even step: columns advance; lane 0 receives column k/2
             const int edge = load_col(T, rev, tbase, k / 2);
@@ -526,6 +670,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                             out_score, err);
         }
     }
+    if (LEAN && bad != 0 && threadIdx.x == 0)
+        set_err(err, 1);   // "new score is invalid"
 }
 
 // ---------------------------------------------------------------------
@@ -1199,6 +1345,7 @@ struct rf_ctx {
     uint64_t tpl_counter = 0;
     uint64_t layout_gen = 1;   // bumped whenever a device offset / length may change
     DevBuf scratch[16];
+    DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0;
     // host-side plan caches: a repeated call with identical arguments and an
@@ -1208,7 +1355,8 @@ struct rf_ctx {
         uint64_t gen = 0;
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
-        size_t n16 = 0, n32 = 0, n128 = 0, n64 = 0, ng = 0;
+        size_t nr[3][2] = {};   // k_dpr<1,2,4> x {general, lean}
+        size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
     } rplan;
     struct {
@@ -1310,6 +1458,11 @@ int arena_grow(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
     char *d = nullptr;
     HIPCHK(ctx, hipMalloc((void **)&d, cap));
     std::sort(regs.begin(), regs.end(), [](Region *x, Region *y) { return x->off < y->off; });
+    // compaction = one scatter launch (one block per live region), not one
+    // copy dispatch per region: a batch upload that grows an arena log(N)
+    // times would otherwise issue O(N log N) tiny copies
+    std::vector<Segment> segs;
+    segs.reserve(regs.size());
     int64_t top = 0;
     for (auto *r : regs) {
         if (r == skip) {
@@ -1318,10 +1471,16 @@ int arena_grow(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
             continue;
         }
         if (r->cap > 0)
-            HIPCHK(ctx, hipMemcpyAsync(d + top, a.d + r->off, r->cap, hipMemcpyDeviceToDevice,
-                                       ctx->stream));
+            segs.push_back({r->off, top, r->cap, 0});
         r->off = top;
         top += r->cap;
+    }
+    if (!segs.empty()) {
+        if (int e = upload(ctx, ctx->grow_segs, segs))
+            return e;
+        hipLaunchKernelGGL(k_scatter, dim3((unsigned)segs.size()), dim3(256), 0, ctx->stream,
+                           (const Segment *)ctx->grow_segs.p, (const uint8_t *)a.d, (uint8_t *)d);
+        HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (a.d)
@@ -1421,6 +1580,8 @@ int rf_destroy(rf_ctx *ctx)
     for (auto &b : ctx->scratch)
         if (b.p)
             (void)hipFree(b.p);
+    if (ctx->grow_segs.p)
+        (void)hipFree(ctx->grow_segs.p);
     if (ctx->d_err)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
@@ -1462,6 +1623,24 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     (void)hipSetDevice(ctx->device);
     if ((int64_t)first + nseq > (int64_t)ctx->seqs.size())
         ctx->seqs.resize(first + nseq);
+    // 0. grow each arena at most once for the whole batch
+    {
+        int64_t need_b = 0, need_t = 0;
+        for (int32_t k = 0; k < nseq; ++k) {
+            const SeqObj &S = ctx->seqs[first + k];
+            const int64_t n = off[k + 1] - off[k];
+            const int64_t nci = cins_off ? cins_off[k + 1] - cins_off[k] : 0;
+            const int64_t ncd = cdel_off ? cdel_off[k + 1] - cdel_off[k] : 0;
+            const int64_t bb = align_up(std::max<int64_t>(n, 16), 256);
+            const int64_t tb = align_up(std::max<int64_t>((4 * n + 1 + nci + ncd) * 8, 16), 256);
+            if (!(S.bases.off >= 0 && S.bases.cap >= bb)) need_b += bb;
+            if (!(S.tabs.off >= 0 && S.tabs.cap >= tb)) need_t += tb;
+        }
+        if (ctx->bytes_arena.top + need_b > ctx->bytes_arena.cap)
+            if (int e = arena_grow(ctx, ctx->bytes_arena, need_b, nullptr)) return e;
+        if (ctx->tab_arena.top + need_t > ctx->tab_arena.cap)
+            if (int e = arena_grow(ctx, ctx->tab_arena, need_t, nullptr)) return e;
+    }
     // 1. regions (arena growth may move earlier regions: offsets are read after)
     int64_t nb = 0, nt = 0;
     for (int32_t k = 0; k < nseq; ++k) {
@@ -1622,7 +1801,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> c16, c32, c128, c64, cg;
+        std::vector<DPTask> cr[3][2], c64, cg;
         int hmax64 = 0, hmaxg = 0;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
@@ -1649,13 +1828,15 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
                 t.P = band_P(t.H);
-                // classes by lanes per task (W): H <= 32 -> 16, <= 64 -> 32, else 64
-                if (t.H <= 32)
-                    c16.push_back(t);
-                else if (t.H <= 64)
-                    c32.push_back(t);
-                else if (t.H <= 128)
-                    c128.push_back(t);
+                // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4), lean when
+                // there are no codon moves and no skew / trim; k_dp beyond
+                const int lean = (S.ncins == 0 && S.ncdel == 0 && !(t.flags & 6)) ? 1 : 0;
+                if (t.H <= 31)
+                    cr[0][lean].push_back(t);
+                else if (t.H <= 63)
+                    cr[1][lean].push_back(t);
+                else if (t.H <= 127)
+                    cr[2][lean].push_back(t);
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
@@ -1666,16 +1847,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
-        std::stable_sort(c16.begin(), c16.end(), by_len);
-        std::stable_sort(c32.begin(), c32.end(), by_len);
-        std::stable_sort(c128.begin(), c128.end(), by_len);
+        std::vector<DPTask> all;
+        for (auto &cc : cr)
+            for (auto &c : cc) {
+                std::stable_sort(c.begin(), c.end(), by_len);
+                all.insert(all.end(), c.begin(), c.end());
+            }
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
-        std::vector<DPTask> all;
-        all.reserve(c16.size() + c32.size() + c128.size() + c64.size() + cg.size());
-        all.insert(all.end(), c16.begin(), c16.end());
-        all.insert(all.end(), c32.begin(), c32.end());
-        all.insert(all.end(), c128.begin(), c128.end());
         all.insert(all.end(), c64.begin(), c64.end());
         all.insert(all.end(), cg.begin(), cg.end());
         if (int e = upload(ctx, ctx->scratch[8], all))
@@ -1687,9 +1866,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         P.seq.assign(seq, seq + njobs);
         P.tpl.assign(tpl, tpl + njobs);
         P.bw.assign(bw, bw + njobs);
-        P.n16 = c16.size();
-        P.n32 = c32.size();
-        P.n128 = c128.size();
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 2; ++b)
+                P.nr[a][b] = cr[a][b].size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -1705,23 +1884,19 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
 
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     size_t at = 0;
-    if (P.n16) {
-        const int n = (int)P.n16;
-        hipLaunchKernelGGL((k_dpr<1>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
-                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
-        at += n;
-    }
-    if (P.n32) {
-        const int n = (int)P.n32;
-        hipLaunchKernelGGL((k_dpr<2>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
-                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
-        at += n;
-    }
-    if (P.n128) {
-        const int n = (int)P.n128;
-        hipLaunchKernelGGL((k_dpr<4>), dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
-                           d_bases, d_tabs, d_bands, d_out, ctx->d_err);
-        at += n;
+    {
+        using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *);
+        const KFn kr[3][2] = {{k_dpr<1, false>, k_dpr<1, true>},
+                              {k_dpr<2, false>, k_dpr<2, true>},
+                              {k_dpr<4, false>, k_dpr<4, true>}};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 2; ++b)
+                if (P.nr[a][b]) {
+                    const int n = (int)P.nr[a][b];
+                    hipLaunchKernelGGL(kr[a][b], dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
+                                       d_bases, d_tabs, d_bands, d_out, ctx->d_err);
+                    at += n;
+                }
     }
     if (P.n64) {
         const int n = (int)P.n64;

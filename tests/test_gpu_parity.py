@@ -85,6 +85,60 @@ def test_dp_bands_bitexact(engine, L, err, bw, jit, codon):
         assert nerr[0] == oracle.count_errors(ref_moves, t, s.seq)
 
 
+def _check_bands(engine, t, seqs, bws):
+    n = len(seqs)
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    scores = engine.realign(np.arange(n), np.arange(n), 0, bws, RF_FWD | RF_BWD)
+    L = len(t)
+    for k, s in enumerate(seqs):
+        A_exp, _ = oracle.forward(t, s, bandwidth=bws[k])
+        B_exp = oracle.backward(t, s, bandwidth=bws[k])
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(s) + 1, L + 1, bws[k])
+        assert_band_equal(engine.download_band(k, RF_BAND_B), B_exp, len(s) + 1, L + 1, bws[k])
+        d_end = len(s) - L + max(L - len(s), 0) + bws[k]
+        assert scores[k] == A_exp[d_end, L]
+
+
+def test_dp_class_boundaries(engine):
+    """H = 2bw + |n-m| + 1 on both sides of every kernel-class edge (31/32,
+    63/64, 127/128), reads longer and shorter than the template, mixed in one
+    launch so waves hold tasks of different geometry (lean interior bounds are
+    the intersection over a wave's four tasks)."""
+    rng = np.random.default_rng(77)
+    t = random_seq(180, rng)
+    seqs, bws = [], []
+    for H in (29, 30, 31, 32, 33, 61, 62, 63, 64, 65, 125, 126, 127, 128, 129):
+        for delta in (0, 1, 4, -3):
+            bw = (H - 1 - abs(delta)) // 2
+            if bw < 1:
+                continue
+            r = make_read(t, rng, 0.04, bw)
+            s = r.seq
+            want = len(t) + delta
+            if len(s) > want:
+                s = s[:want]
+                lp = r.error_log_p[:want]
+            else:
+                extra = random_seq(want - len(s), rng)
+                s = np.concatenate([s, extra])
+                lp = np.concatenate([r.error_log_p, np.full(len(extra), -1.2)])
+            seqs.append(RifrafSequence(s, lp, bw, SEQ_SCORES))
+            bws.append(bw)
+    _check_bands(engine, t, seqs, bws)
+
+
+@pytest.mark.parametrize("m,n,bw", [(3, 40, 9), (8, 8, 9), (1, 1, 1), (2, 30, 2), (40, 3, 9), (25, 60, 6)])
+def test_dp_short_and_skewed_shapes(engine, m, n, bw):
+    """Templates shorter than the bandwidth (c > m: no lean interior) and very
+    unequal lengths, several copies per launch."""
+    rng = np.random.default_rng(m * 100 + n)
+    t = random_seq(m, rng)
+    seqs = [RifrafSequence(random_seq(n, rng), np.log10(rng.uniform(0.01, 0.3, n)), bw, SEQ_SCORES)
+            for _ in range(7)]
+    _check_bands(engine, t, seqs, [bw] * len(seqs))
+
+
 @pytest.mark.parametrize("flags", [RF_SKEW, RF_TRIM, RF_SKEW | RF_TRIM])
 def test_dp_skew_trim(engine, flags):
     rng = np.random.default_rng(flags)
