@@ -485,14 +485,14 @@ __device__ __forceinline__ double dpp_rot_f64(double x)
 // get lb = -Inf, which keeps them at -Inf exactly like dpr_step's masking
 // (x + 0.0 == x for every cell value: no cell is -0.0).  The block-edge
 // neighbour comes from a row *rotate*: the lane it wraps from holds diagonal
-// 32*NP-1 >= H (host guarantees H <= 32*NP-1), i.e. -Inf.  A cell whose
-// candidates are all -Inf ("new score is invalid", align.jl:105-107) is
-// collected in `bad` and reported after the loop.
+// 32*NP-1 >= H (host guarantees H <= 32*NP-1), i.e. -Inf.  Lean tasks have
+// finite match/mismatch/ins/del tables, so every in-band cell is finite (each
+// has an in-band predecessor chain to the origin) and the "new score is
+// invalid" check (align.jl:105-107) cannot fire here; the general steps keep it.
 template <int NP, int PAR>
 __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], const double (&lb)[NP],
-                                         const bool (&st)[NP], const bool (&act)[NP], double *o,
-                                         int ostep, unsigned long long &bad)
+                                         const bool (&st)[NP], double *o, int ostep)
 {
     const double E1 = PAR == 0 ? dpp_rot_f64<DPP_ROT_L1>(v1[NP - 1]) : dpp_rot_f64<DPP_ROT_R1>(v1[0]);
     double nv[NP];
@@ -503,7 +503,6 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double x_ins = PAR ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : E1);
         const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
         const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
-        bad |= __ballot(act[r] && raw == -RF_INF);
         nv[r] = raw + lb[r];
         if (st[r])
             o[r * ostep] = nv[r];
@@ -514,6 +513,21 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         v1[r] = nv[r];
     }
 }
+
+// Blocked lean interior: per task an LDS slice of DPL_B edge records (the
+// row entering lane 15 and the column entering lane 0 per period) and
+// 2*DPL_B kappa rows of band output, flushed as one contiguous chunk.
+constexpr int DPL_B = 8;
+struct alignas(16) EdgeRec {
+    double mt, mm, is, ds;
+    int sb, col, pad0, pad1;
+};
+__host__ __device__ constexpr int dpl_pmax(int np) { return (16 * np) | 1; }   // band_P(32*NP-1)
+__host__ __device__ constexpr int dpl_task_bytes(int np)
+{
+    return (int)(DPL_B * sizeof(EdgeRec)) + 2 * DPL_B * dpl_pmax(np) * 8;
+}
+extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
 template <int NP, bool LEAN>
 __global__ void __launch_bounds__(64)
@@ -560,7 +574,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     // [max(0, c-d), min(m, n+c-d)], i.e. kappa in [d + 2 jlo, d + 2 jhi].
     int klo = INT_MAX, khi = -1;
     double lb[2][NP];
-    bool st[2][NP], act[2][NP];
+    bool st[2][NP];
     if (LEAN) {
         int lo = 0, hi = INT_MAX;
         bool ok = true;
@@ -571,7 +585,6 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 const int d = 2 * (q * NP + r) + par;
                 const int jlo = max(0, T.c - d), jhi = min(T.m, T.n + T.c - d);
                 const bool a = tid < ntasks && d < T.H && jlo <= jhi;
-                act[par][r] = a;
                 st[par][r] = tid < ntasks && d < T.H;
                 lb[par][r] = a ? 0.0 : -RF_INF;
                 if (a) {
@@ -593,58 +606,90 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             khi = __builtin_amdgcn_readfirstlane(hi);
         }
     }
-    unsigned long long bad = 0;
+    // whole blocks of the interior; the remainder runs as general steps
+    const int nblk = (LEAN && khi >= klo) ? (khi - klo + 1) / (2 * DPL_B) : 0;
 
     for (int k = 0; k < kmax; k += 2) {
-        if (LEAN && k == klo && k + 1 <= khi) {
+        if (LEAN && k == klo && nblk > 0) {
+            // ---- blocked lean interior: DPL_B periods (2*DPL_B anti-diagonals)
+            // per block, inputs and outputs staged in this task's LDS slice
             const int P = T.P;
-            double *o0 = band + (ptrdiff_t)(rev ? T.klen - 1 - k : k) * P +
-                         (rev ? (T.H - 1 - 2 * q * NP) >> 1 : q * NP);
-            double *o1 = band + (ptrdiff_t)(rev ? T.klen - 2 - k : k + 1) * P +
-                         (rev ? (T.H - 2 - 2 * q * NP) >> 1 : q * NP);
-            const ptrdiff_t s2 = rev ? -2 * (ptrdiff_t)P : 2 * (ptrdiff_t)P;
+            const int t = threadIdx.x >> 4;
+            EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP));
+            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP) + DPL_B * sizeof(EdgeRec));
+            // this lane's LDS slot per parity; a block's 2*DPL_B rows are the
+            // contiguous global chunk (reverse: flipped rows)
+            const int sl0 = rev ? (T.H - 1 - 2 * q * NP) >> 1 : q * NP;
+            const int sl1 = rev ? (T.H - 2 - 2 * q * NP) >> 1 : q * NP;
             const int ostep = rev ? -1 : 1;
-            const int top_c = 16 * NP + 1 - T.c;
-            // column bases entering lane 0, one period ahead (clamped like the
-            // edge rows; >= 1 also for padding tasks)
-            auto col_edge = [&](int kk) {
+            const int top_c = 16 * NP - T.c;
+            auto edge_load = [&](int kb) {   // lane q < DPL_B: the period kb + 2q edge row and column
+                EdgeRec e;
+                const int kk = kb + 2 * min(q, DPL_B - 1);
+                const int ii = max(1, min(top_c + (kk >> 1), T.n));   // clamped: see dpl_step
+                const int ks = rev ? T.n - ii : ii - 1;
+                const int kd = rev ? ks : ks + 1;
+                e.sb = sbase[ks];
+                e.mt = tb[ks];
+                e.mm = tb[T.n + ks];
+                e.is = tb[2 * (size_t)T.n + ks];
+                e.ds = tb[3 * (size_t)T.n + kd];
                 const int jj = max(1, min(kk >> 1, T.m));
-                return (int)tbase[rev ? T.m - jj : jj - 1];
+                e.col = tbase[rev ? T.m - jj : jj - 1];
+                return e;
             };
-            int nedge = col_edge(k);
-            for (; k + 1 <= khi; k += 2) {
-                {   // even step: columns advance (column k/2 >= 1 enters lane 0)
-                    const int edge = nedge;
-                    nedge = col_edge(k + 2);
-                    const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
+            EdgeRec pend = edge_load(k);
+            if (q < DPL_B)
+                ein[q] = pend;
+            if (nblk > 1)
+                pend = edge_load(k + 2 * DPL_B);
+            wave_sync();
+            for (int b = 0; b < nblk; ++b) {
 #pragma unroll
-                    for (int r = NP - 1; r > 0; --r)
-                        col[r] = col[r - 1];
-                    col[0] = from;
-                }
-                dpl_step<NP, 0>(v1, v2, row, col, lb[0], st[0], act[0], o0, ostep, bad);
-                {   // odd step: rows advance; lane 15 receives the prefetched row
-                    const RowRec up = row_from_above(row[0], nxt, false);
+                for (int p = 0; p < DPL_B; ++p) {
+                    const EdgeRec &E = ein[p];   // LDS broadcast within the task
+                    {   // even step: column k/2 enters lane 0
+                        const int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
 #pragma unroll
-                    for (int r = 0; r < NP - 1; ++r)
-                        row[r] = row[r + 1];
-                    row[NP - 1] = up;
-                    // next edge row (clamped: a row past the read only reaches
-                    // cells outside the matrix, which are never active here
-                    // and are masked in the general steps)
-                    const int ii = max(1, min(top_c + (k >> 1), T.n));
-                    const int ks = rev ? T.n - ii : ii - 1;
-                    const int kd = rev ? ks : ks + 1;
-                    nxt.sb = sbase[ks];
-                    nxt.mt = tb[ks];
-                    nxt.mm = tb[T.n + ks];
-                    nxt.is = tb[2 * (size_t)T.n + ks];
-                    nxt.ds = tb[3 * (size_t)T.n + kd];
+                        for (int r = NP - 1; r > 0; --r)
+                            col[r] = col[r - 1];
+                        col[0] = from;
+                    }
+                    const int i0 = rev ? 2 * DPL_B - 1 - 2 * p : 2 * p;
+                    dpl_step<NP, 0>(v1, v2, row, col, lb[0], st[0], ob + i0 * P + sl0, ostep);
+                    {   // odd step: rows advance; lane 15 receives the edge row
+                        RowRec e;
+                        e.sb = E.sb;
+                        e.mt = E.mt;
+                        e.mm = E.mm;
+                        e.is = E.is;
+                        e.ds = E.ds;
+                        const RowRec up = row_from_above(row[0], e, false);
+#pragma unroll
+                        for (int r = 0; r < NP - 1; ++r)
+                            row[r] = row[r + 1];
+                        row[NP - 1] = up;
+                    }
+                    const int i1 = rev ? 2 * DPL_B - 2 - 2 * p : 2 * p + 1;
+                    dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], ob + i1 * P + sl1, ostep);
                 }
-                dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], act[1], o1, ostep, bad);
-                o0 += s2;
-                o1 += s2;
+                wave_sync();
+                // next block's edges (loaded one block ago) -> LDS
+                if (b + 1 < nblk && q < DPL_B)
+                    ein[q] = pend;
+                // flush: 2*DPL_B kappa rows = one contiguous chunk of the band
+                if (tid < ntasks) {
+                    double *g = band + (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
+                    for (int e = q; e < 2 * DPL_B * P; e += 16)
+                        g[e] = ob[e];
+                }
+                if (b + 2 < nblk)
+                    pend = edge_load(k + 4 * DPL_B);
+                wave_sync();
+                k += 2 * DPL_B;
             }
+            // back to the general steps: the edge row they expect
+            nxt = load_row(T, rev, sbase, tb, top + k / 2 + 1 - T.c, false);
             if (k >= kmax)
                 break;
         }
@@ -670,8 +715,6 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                             out_score, err);
         }
     }
-    if (LEAN && bad != 0 && threadIdx.x == 0)
-        set_err(err, 1);   // "new score is invalid"
 }
 
 // ---------------------------------------------------------------------
@@ -1302,6 +1345,7 @@ struct Arena {
 
 struct SeqObj {
     bool valid = false;
+    bool finite = false;   // match / mismatch / ins / del tables hold no -Inf (lean DP eligible)
     int32_t n = 0, ncins = 0, ncdel = 0;
     Region bases, tabs;
 };
@@ -1677,6 +1721,10 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
         if (ncd)
             std::memcpy(h + 4 * n + 1 + nci, cdel + cdel_off[k], ncd * 8);
         const int64_t len = 4 * n + 1 + nci + ncd;
+        bool fin = true;
+        for (int64_t e = 0; e < 4 * n + 1; ++e)
+            fin = fin && std::isfinite(h[e]);
+        ctx->seqs[first + k].finite = fin;
         st[k] = {at * 8, S.tabs.off, len * 8, 0};
         sb[k] = {off[k] - off[0], S.bases.off, n, 0};
         at += len;
@@ -1830,7 +1878,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.P = band_P(t.H);
                 // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4), lean when
                 // there are no codon moves and no skew / trim; k_dp beyond
-                const int lean = (S.ncins == 0 && S.ncdel == 0 && !(t.flags & 6)) ? 1 : 0;
+                const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
                 if (t.H <= 31)
                     cr[0][lean].push_back(t);
                 else if (t.H <= 63)
@@ -1893,7 +1941,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             for (int b = 0; b < 2; ++b)
                 if (P.nr[a][b]) {
                     const int n = (int)P.nr[a][b];
-                    hipLaunchKernelGGL(kr[a][b], dim3((n + 3) / 4), dim3(64), 0, ctx->stream, d_tasks + at, n,
+                    const int np = 1 << a;
+                    const size_t lds = b ? 4 * (size_t)dpl_task_bytes(np) : 0;
+                    hipLaunchKernelGGL(kr[a][b], dim3((n + 3) / 4), dim3(64), lds, ctx->stream, d_tasks + at, n,
                                        d_bases, d_tabs, d_bands, d_out, ctx->d_err);
                     at += n;
                 }
