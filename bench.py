@@ -212,6 +212,9 @@ def main():
         dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
         elapsed, (tot_cells, tot_props, tot_pairs) = aggregate(elapsed, [tot_cells, tot_props, tot_pairs], dev)
 
+    # attainable streaming-read bandwidth over the same band arena (diagnostic)
+    probe_ms = eng.probe_stream(band_bytes, 3)
+    probe_gbs = band_bytes / (probe_ms * 1e-3) / 1e9 if probe_ms > 0 else None
     ms_step = elapsed / args.steps * 1e3
     dp_ms = float(np.mean(dps))
     sc_ms = float(np.mean(scs))
@@ -256,6 +259,7 @@ def main():
                                     "bytes": dp_bytes, "ms": dp_ms},
                            "k_score": {"achieved": sc_gbs, "frac": sc_gbs / HBM_PEAK_GBS,
                                        "bytes": score_bytes, "ms": sc_ms}},
+        "stream_read_gbs": probe_gbs,
         "setup_s": gen_s,
     }
     if rank == 0:

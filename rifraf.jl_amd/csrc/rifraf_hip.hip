@@ -972,6 +972,566 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
 }
 
 // ---------------------------------------------------------------------
+// k_score_lean: the same dense scoring, one new-column chain per lane
+//
+// A new column built from A column a (0-based) with base b over the rows of
+// column min(a+1, m) serves two proposals (model.jl:250-270):
+//   Substitution(a+1, b)  acol = a+1 (1-based) -> summax with B column a+1
+//   Insertion(a, b)       acol = a+1 (1-based) -> summax with B column a
+// (same A column, same rows, same base: the chains are identical), and the
+// lane also folds Deletion(a+1) = max_i A(i, a) + B(i, a+1) (model.jl:227-236).
+// So lane a writes slots 5-8 of position a and slots 0-4 of position a+1.
+//
+// Eligible when every read of the launch has finite match / mismatch / ins /
+// del tables (the lean DP condition): then every in-band A and B cell is
+// finite, a new column can never hold -Inf, and the reference's "new score
+// is invalid" check cannot fire; an empty summax still reports NaN.
+//
+// Per read, the kappa rows of the work item's columns (one contiguous block
+// per band) are staged in LDS with 16-B loads -- the next read's block is
+// prefetched into VGPRs while the current one is scored -- and the per-row tables are staged once as {sub A,C,G,T, ins, del} records
+// (sub_b = match if the read base is b, else mismatch), so the inner loop is
+// LDS reads + FP64 max-plus only.  A read whose window exceeds the LDS budget
+// is processed in sub-passes over fewer lanes.  Work items are remapped so
+// that consecutive chunks of one group run on the same XCD (shared L2 for the
+// H overlapping kappa rows of neighbouring chunks).
+// ---------------------------------------------------------------------
+
+// doubles of LDS a sub-pass over L lanes needs for a read of band height H
+#ifndef LEAN_NPF
+#define LEAN_NPF 12
+#endif
+
+__host__ __device__ inline int lean_need(int L, int H, int P)
+{
+    const int win = ((2 * L + H + 1) * P + 3) & ~1;   // kappa rows + alignment shift, even
+    return 2 * win + (L + H + 1) * 6;
+}
+
+// v_max_f64 without the NaN-quieting self-max hipcc adds in front of every
+// fmax whose operand is a loop-carried value; the operands here are never NaN
+// (finite tables, finite in-band cells, -Inf sentinels), so the result is
+// the same FP64 maximum.
+__device__ __forceinline__ double vmax(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+// Geometry of one staged (read, lanes [la0, la1]) window.
+struct LeanWin {
+    int kw0, shift, n16, win;   // kappa rows from kw0, 16-B chunks per band, doubles per band slot
+    int t0, t1;                 // table rows
+};
+
+__device__ __forceinline__ LeanWin lean_win(const ScoreRead &R, int m, int la0, int la1)
+{
+    LeanWin w;
+    w.kw0 = 2 * la0;
+    const int kw1 = min(2 * (la1 + 1) + R.H, R.K);
+    w.shift = (w.kw0 * R.P) & 1;
+    w.n16 = (w.shift + (kw1 - w.kw0) * R.P + 1) >> 1;
+    w.win = (2 * w.n16 + 1) & ~1;
+    w.t0 = max(0, min(la0 + 1, m) - R.c);
+    w.t1 = min(min(la1 + 1, m) + R.vb, R.n);
+    return w;
+}
+
+// one {sub A, C, G, T, ins, del} record per read row i (align.jl:60-69)
+__device__ __forceinline__ void lean_row(double *rec, int sbse, double mt, double mm, double ins, double del)
+{
+    double2 *r2 = (double2 *)rec;
+    r2[0] = make_double2(sbse == 0 ? mt : mm, sbse == 1 ? mt : mm);
+    r2[1] = make_double2(sbse == 2 ? mt : mm, sbse == 3 ? mt : mm);
+    r2[2] = make_double2(ins, del);
+}
+
+// Synchronous staging of a window (bands and tables through VGPRs).
+template <int Q>
+__device__ __forceinline__ void lean_stage(const ScoreRead &R, const LeanWin &w, int tid,
+                                           const double *__restrict__ bands, const double *__restrict__ tabs,
+                                           const uint8_t *__restrict__ bases, double *sA, double *sB, double *sT)
+{
+    // plain 16-B loads + ds_write (no LDS-DMA: a global_load_lds anywhere in
+    // the kernel makes hipcc wait vmcnt(0) before every LDS read, which would
+    // drain the cross-read prefetch at the start of each chain)
+    const dvec2 *ga = (const dvec2 *)(bands + R.A + (size_t)w.kw0 * R.P - w.shift);
+    const dvec2 *gb = (const dvec2 *)(bands + R.B + (size_t)w.kw0 * R.P - w.shift);
+    dvec2 *la = (dvec2 *)sA, *lb = (dvec2 *)sB;
+    for (int e0 = 0; e0 < w.n16; e0 += 4 * Q) {
+        dvec2 va[4], vb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * Q + tid;
+            if (e < w.n16) {
+                va[u] = ga[e];
+                vb[u] = gb[e];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * Q + tid;
+            if (e < w.n16) {
+                la[e] = va[u];
+                lb[e] = vb[u];
+            }
+        }
+    }
+    const int n = R.n;
+    const double *tm = tabs + R.tab;
+    const uint8_t *sq = bases + R.sb;
+    for (int e = tid; e <= w.t1 - w.t0; e += Q) {
+        const int i = w.t0 + e;
+        const int ks = max(i - 1, 0);
+        lean_row(sT + 6 * e, i >= 1 ? sq[i - 1] : 4, tm[ks], tm[n + ks], tm[2 * (size_t)n + ks],
+                 tm[3 * (size_t)n + i]);
+    }
+}
+
+// One new-column chain (lane column a) over the staged window; accumulates
+// into the lane's totals.  Row values are software-pipelined one row ahead.
+__device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w, int a, int m,
+                                           const double *sA, const double *sB, const double *sT,
+                                           double tI[4], double tS[4], double &tD)
+{
+    const int c = R.c, vb = R.vb, P = R.P;
+    const int jn = min(a + 1, m);
+    const int i0 = max(0, jn - c);
+    const int i1 = min(jn + vb, R.n);
+    const int ilast = min(i1, a + vb);                  // last row of rows(a)
+    int d = i0 - a + c;
+    int idx = w.shift + (d + 2 * a - w.kw0) * P + (d >> 1);
+    double aprev = (d >= 1 && i0 >= 1) ? sA[idx - P - 1 + (d & 1)] : -RF_INF;
+    // B(i, a+1) sits at idx + P - 1 + (d & 1); the last column (a = m) has no
+    // Substitution(m+1): it reads B(i, a) there and masks the sum to -Inf
+    const bool hasS = a < m;
+    const int sofs = hasS ? P - 1 : 0;
+    const int sodd = hasS ? 1 : 0;
+    const double smask = hasS ? 0.0 : -RF_INF;
+    const double *tr = sT + 6 * (i0 - w.t0);
+    double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        prev[k] = -RF_INF;
+        accI[k] = -RF_INF;
+        accS[k] = -RF_INF;
+    }
+    double ac = sA[idx], bI = sB[idx], bSr = sB[idx + sofs + (sodd & d)];
+    double2 u0 = ((const double2 *)tr)[0], u1 = ((const double2 *)tr)[1], u2 = ((const double2 *)tr)[2];
+    for (int i = i0; i <= ilast; ++i) {
+        // next row's operands (row ilast + 1 is the peeled row below)
+        idx += P + (d & 1);
+        ++d;
+        tr += 6;
+        const double acn = sA[idx], bIn = sB[idx], bSn = sB[idx + sofs + (sodd & d)];
+        const double2 v0 = ((const double2 *)tr)[0], v1 = ((const double2 *)tr)[1],
+                      v2 = ((const double2 *)tr)[2];
+        const double bS = bSr + smask;
+        const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+        const double dl = ac + u2.y;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
+            prev[k] = best;
+            accI[k] = vmax(accI[k], best + bI);
+            accS[k] = vmax(accS[k], best + bS);
+        }
+        dd = vmax(dd, ac + bS);
+        aprev = ac;
+        ac = acn;
+        bI = bIn;
+        bSr = bSn;
+        u0 = v0;
+        u1 = v1;
+        u2 = v2;
+    }
+    if (i1 > ilast) {
+        // last row of the new column lies below A/B column a's band (a < m)
+        const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+    }
+    const double qnan = __builtin_nan("");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+        tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+    }
+    tD += dd;
+}
+
+template <int NW>
+__device__ __forceinline__ void lean_barrier()
+{
+    if (NW > 1)
+        __syncthreads();
+    else
+        wave_sync();
+}
+
+// NPF: 16-byte chunks per band and lane the cross-read register prefetch
+// holds; a read whose full window needs more (or does not fit the LDS
+// budget) is staged synchronously, in sub-passes if needed.
+template <int NW, int NPF>
+__global__ void __launch_bounds__(64 * NW)
+k_score_lean(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+             const double *__restrict__ tabs, const double *__restrict__ bands,
+             double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int Q = 64 * NW;
+    // XCD-aware remap (blocks are dealt round-robin over the 8 XCDs)
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int xq = nb >> 3, xr = nb & 7, x = b & 7;
+    const int item = x * xq + min(x, xr) + (b >> 3);
+    const WorkItem wi = items[item];
+    const ScoreGroup G = groups[wi.group];
+    const int tid = threadIdx.x;
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int a = a0 + tid;
+    const int la1f = min(a0 + Q - 1, m);
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + blockIdx.y;
+        if (r0 >= G.r1)
+            return;
+        r1 = r0 + 1;
+    }
+    double tI[4], tS[4], tD = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] = 0.0;
+        tS[k] = 0.0;
+    }
+    // a read takes the prefetch path when its full window fits both budgets
+    auto fast = [&](const ScoreRead &R, const LeanWin &w) {
+        return lean_need(Q, R.H, R.P) <= lds_elems && w.n16 <= NPF * Q && w.t1 - w.t0 < 2 * Q;
+    };
+    dvec2 pa[NPF], pb[NPF];
+    double pm[2], px[2], pn[2], pd[2];
+    int ps[2];
+    // Issue read rr's full window + table rows into registers (no wait).
+    auto issue = [&](int rr) -> bool {
+        const ScoreRead R2 = reads[rr];
+        const LeanWin w2 = lean_win(R2, m, a0, la1f);
+        if (!fast(R2, w2))
+            return false;
+        const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
+        const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
+#pragma unroll
+        for (int u = 0; u < NPF; ++u) {
+            const int e = min(u * Q + tid, w2.n16 - 1);
+            pa[u] = ga[e];
+            pb[u] = gb[e];
+        }
+        const double *tm = tabs + R2.tab;
+        const int n2 = R2.n;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = min(w2.t0 + tid + k * Q, w2.t1);
+            const int ks = max(i - 1, 0);
+            pm[k] = tm[ks];
+            px[k] = tm[n2 + ks];
+            pn[k] = tm[2 * (size_t)n2 + ks];
+            pd[k] = tm[3 * (size_t)n2 + i];
+            ps[k] = bases[R2.sb + ks];
+        }
+        // keep the loads here (a memory clobber: no sinking into the commit)
+        asm volatile("" ::: "memory");
+        return true;
+    };
+    bool pf = r0 < r1 ? issue(r0) : false;
+    for (int r = r0; r < r1; ++r) {
+        const ScoreRead R = reads[r];
+        const LeanWin wf = lean_win(R, m, a0, la1f);
+        if (pf) {
+            // ---- commit the prefetched window, start the next read's, score this one
+            {
+                dvec2 *sA = (dvec2 *)smem;
+                dvec2 *sB = (dvec2 *)(smem + wf.win);
+                double *sT = smem + 2 * wf.win;
+#pragma unroll
+                for (int u = 0; u < NPF; ++u) {
+                    const int e = u * Q + tid;
+                    if (e < wf.n16) {
+                        sA[e] = pa[u];
+                        sB[e] = pb[u];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int e = tid + k * Q;
+                    const int i = wf.t0 + e;
+                    if (i <= wf.t1)
+                        lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
+                }
+            }
+            lean_barrier<NW>();
+            pf = r + 1 < r1 ? issue(r + 1) : false;
+            if (a <= m && !(split_mode & 2))
+                lean_chain(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
+            lean_barrier<NW>();
+        } else {
+            // ---- wide read: synchronous sub-passes over L lanes
+            int L = Q;
+            while (L > 1 && lean_need(L, R.H, R.P) > lds_elems)
+                L >>= 1;
+            for (int s0 = 0; s0 < Q; s0 += L) {
+                const int la0 = a0 + s0;
+                if (la0 > m)
+                    break;
+                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
+                lean_stage<Q>(R, w, tid, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
+                lean_barrier<NW>();
+                if (tid >= s0 && tid < s0 + L && a <= m)
+                    lean_chain(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
+                lean_barrier<NW>();
+            }
+            pf = r + 1 < r1 ? issue(r + 1) : false;
+        }
+    }
+    if (a > m)
+        return;
+    const double qnan = __builtin_nan("");
+    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
+                                    : dense + G.dense_off;
+    double *dst = base + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[5 + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[9 + k] = tS[k];
+        dst[13] = tD;
+    }
+    if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
+// ---------------------------------------------------------------------
+// k_score_ws: the lean scorer with wave specialization (the default)
+//
+// 512 threads: waves 0-3 are the chain waves (256 chain columns per work
+// item, totals in their VGPRs); waves 4-7 are loader waves that hold the
+// NEXT read's window and table rows in their own VGPRs while the chain waves
+// score the current read from LDS, then write it to LDS between two
+// barriers.  The two roles run separate loops (so the loaders' registers
+// never constrain the chains) that meet at the same s_barrier sequence:
+// two barriers per read, or per sub-pass of a read too wide for the
+// prefetch (staged synchronously by the loaders).
+// ---------------------------------------------------------------------
+
+__device__ __forceinline__ void wg_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+#ifndef WS_NPF
+#define WS_NPF 22
+#endif
+
+template <int NPF>
+__global__ void __launch_bounds__(512)
+k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+           const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+           const double *__restrict__ tabs, const double *__restrict__ bands,
+           double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int Q = 256;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int xq = nb >> 3, xr = nb & 7, x = b & 7;
+    const int item = x * xq + min(x, xr) + (b >> 3);
+    const WorkItem wi = items[item];
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int la1f = min(a0 + Q - 1, m);
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + blockIdx.y;
+        if (r0 >= G.r1)
+            return;
+        r1 = r0 + 1;
+    }
+    // same decision in both roles (block-uniform)
+    auto fast = [&](const ScoreRead &R, const LeanWin &w) {
+        return lean_need(Q, R.H, R.P) <= lds_elems && w.n16 <= NPF * Q && w.t1 - w.t0 < 2 * Q;
+    };
+    auto sub_L = [&](const ScoreRead &R) {
+        int L = Q;
+        while (L > 1 && lean_need(L, R.H, R.P) > lds_elems)
+            L >>= 1;
+        return L;
+    };
+    if (threadIdx.x >= Q) {
+        // =========================== loader waves ===========================
+        const int lt = threadIdx.x - Q;
+        dvec2 pa[NPF], pb[NPF];
+        double pm[2], px[2], pn[2], pd[2];
+        int ps[2];
+        auto issue = [&](const ScoreRead &R2, const LeanWin &w2) {
+            const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
+            const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
+#pragma unroll
+            for (int u = 0; u < NPF; ++u) {
+                const int e = min(u * Q + lt, w2.n16 - 1);
+                pa[u] = ga[e];
+                pb[u] = gb[e];
+            }
+            const double *tm = tabs + R2.tab;
+            const int n2 = R2.n;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = min(w2.t0 + lt + k * Q, w2.t1);
+                const int ks = max(i - 1, 0);
+                pm[k] = tm[ks];
+                px[k] = tm[n2 + ks];
+                pn[k] = tm[2 * (size_t)n2 + ks];
+                pd[k] = tm[3 * (size_t)n2 + i];
+                ps[k] = bases[R2.sb + ks];
+            }
+        };
+        bool held = false;   // registers hold read r
+        for (int r = r0; r < r1; ++r) {
+            const ScoreRead R = reads[r];
+            const LeanWin wf = lean_win(R, m, a0, la1f);
+            if (fast(R, wf)) {
+                if (!held)
+                    issue(R, wf);
+                dvec2 *sA = (dvec2 *)smem;
+                dvec2 *sB = (dvec2 *)(smem + wf.win);
+                double *sT = smem + 2 * wf.win;
+#pragma unroll
+                for (int u = 0; u < NPF; ++u) {
+                    const int e = u * Q + lt;
+                    if (e < wf.n16) {
+                        sA[e] = pa[u];
+                        sB[e] = pb[u];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int e = lt + k * Q;
+                    const int i = wf.t0 + e;
+                    if (i <= wf.t1)
+                        lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
+                }
+                wg_barrier();                        // window r ready
+                held = false;
+                if (r + 1 < r1) {
+                    const ScoreRead R2 = reads[r + 1];
+                    const LeanWin w2 = lean_win(R2, m, a0, la1f);
+                    if (fast(R2, w2)) {
+                        issue(R2, w2);
+                        held = true;
+                    }
+                }
+                wg_barrier();                        // chains of r done
+            } else {
+                const int L = sub_L(R);
+                for (int s0 = 0; s0 < Q; s0 += L) {
+                    const int la0 = a0 + s0;
+                    if (la0 > m)
+                        break;
+                    const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
+                    lean_stage<Q>(R, w, lt, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
+                    wg_barrier();
+                    wg_barrier();
+                }
+                held = false;
+            }
+        }
+        return;
+    }
+    // ============================ chain waves =============================
+    const int tid = threadIdx.x;
+    const int a = a0 + tid;
+    double tI[4], tS[4], tD = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] = 0.0;
+        tS[k] = 0.0;
+    }
+    for (int r = r0; r < r1; ++r) {
+        const ScoreRead R = reads[r];
+        const LeanWin wf = lean_win(R, m, a0, la1f);
+        if (fast(R, wf)) {
+            wg_barrier();                            // window r ready
+            if (a <= m && !(split_mode & 2))
+                lean_chain(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
+            wg_barrier();                            // chains of r done
+        } else {
+            const int L = sub_L(R);
+            for (int s0 = 0; s0 < Q; s0 += L) {
+                const int la0 = a0 + s0;
+                if (la0 > m)
+                    break;
+                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
+                wg_barrier();
+                if (tid >= s0 && tid < s0 + L && a <= m)
+                    lean_chain(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
+                wg_barrier();
+            }
+        }
+    }
+    if (a > m)
+        return;
+    const double qnan = __builtin_nan("");
+    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
+                                    : dense + G.dense_off;
+    double *dst = base + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[5 + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[9 + k] = tS[k];
+        dst[13] = tD;
+    }
+    if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
+// Read-bandwidth probe over the band arena (calibrates the HBM roofline of
+// the scorer on the same allocation): grid-stride 16-B loads, 8 in flight.
+__global__ void __launch_bounds__(256) k_probe_stream(const dvec2 *__restrict__ src, int64_t n16,
+                                                      double *__restrict__ sink)
+{
+    const int64_t stride = (int64_t)gridDim.x * 256 * 8;
+    double acc = 0.0;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * 8 + threadIdx.x; base < n16; base += stride) {
+        dvec2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t e = base + u * 256;
+            v[u] = e < n16 ? src[e] : dvec2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            acc += v[u].x + v[u].y;
+    }
+    if (acc == 12345.678)   // never true for band data; keeps the loads alive
+        sink[0] = acc;
+}
+
+// ---------------------------------------------------------------------
 // k_codon: codon-move scoring, one lane per proposal (model.jl:302-383)
 // ---------------------------------------------------------------------
 
@@ -1368,6 +1928,14 @@ struct Slot {
     Band a, b;
 };
 
+// Choice of dense scorer for one launch.
+struct ScorePick {
+    bool lean = false;
+    int nw = 1;     // lean: waves per workgroup (64 * nw chain columns per work item)
+    int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
+    int q() const { return nw == 8 ? 256 : 64 * nw; }   // chain columns per work item
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -1408,8 +1976,10 @@ struct rf_ctx {
         uint64_t gen = 0;
         std::vector<int32_t> slot_off, slots;
         size_t nitems = 0;
-        int max_reads = 0, ngroups = 0, lds_elems = 0;
+        int max_reads = 0, ngroups = 0;
         int64_t dense_total = 0, split_total = 0;
+        ScorePick pick;
+        std::string envkey;
     } dplan;
 };
 
@@ -1582,6 +2152,87 @@ int score_lds_elems(const std::vector<ScoreRead> &reads)
     return std::min(w[q], 24 * 1024 / 8);
 }
 
+
+int env_int(const char *name, int dflt)
+{
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// environment knobs of the scorer choice, as a plan-cache key
+std::string scorer_env_key()
+{
+    std::string k;
+    for (const char *n : {"RIFRAF_SCORE_KERNEL", "RIFRAF_LEAN_NW", "RIFRAF_LEAN_LDS_KB"}) {
+        const char *v = std::getenv(n);
+        k += v ? v : "-";
+        k += '|';
+    }
+    return k;
+}
+
+ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
+{
+    ScorePick p;
+    const char *kern = std::getenv("RIFRAF_SCORE_KERNEL");
+    const bool force_general = kern && !std::strcmp(kern, "general");
+    if (all_finite && !force_general && !reads.empty()) {
+        int need1 = 0;
+        for (const auto &R : reads)
+            need1 = std::max(need1, lean_need(1, R.H, R.P));
+        // 8 = wave-specialized k_score_ws (256 chain lanes + 256 loader lanes)
+        int nw = env_int("RIFRAF_LEAN_NW", 8);
+        nw = nw >= 8 ? 8 : (nw >= 4 ? 4 : (nw >= 2 ? 2 : 1));
+        const int lds = std::max(env_int("RIFRAF_LEAN_LDS_KB", nw >= 4 ? 160 : 40 * nw) * 1024 / 8, need1);
+        if (lds <= 160 * 1024 / 8) {
+            p.lean = true;
+            p.nw = nw;
+            p.lds = lds;
+            return p;
+        }
+    }
+    p.lds = score_lds_elems(reads);
+    return p;
+}
+
+// work items: chunks of q consecutive positions of every group
+std::vector<WorkItem> make_items(const std::vector<ScoreGroup> &groups, int q)
+{
+    std::vector<WorkItem> items;
+    for (int g = 0; g < (int)groups.size(); ++g)
+        if (groups[g].r1 > groups[g].r0)
+            for (int p0 = 0; p0 <= groups[g].m; p0 += q)
+                items.push_back({g, p0});
+    return items;
+}
+
+void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned gy, const WorkItem *items,
+                   const ScoreGroup *groups, const ScoreRead *reads, double *dense, double *split)
+{
+    const uint8_t *d_bases = (const uint8_t *)ctx->bytes_arena.d;
+    const double *d_tabs = (const double *)ctx->tab_arena.d;
+    const double *d_bands = (const double *)ctx->band_arena.d;
+    // RIFRAF_LEAN_NOCOMP=1: diagnostics only -- the lean scorer stages every
+    // window but skips the chains (measures its load pipeline alone)
+    const int sm = (split ? 1 : 0) | (env_int("RIFRAF_LEAN_NOCOMP", 0) ? 2 : 0);
+    dim3 grid(nitems, gy);
+    if (!pk.lean)
+        hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
+                           d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    else if (pk.nw == 8)
+        hipLaunchKernelGGL((k_score_ws<WS_NPF>), grid, dim3(512), pk.lds * 8, ctx->stream, items, groups,
+                           reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    else if (pk.nw == 1)
+        hipLaunchKernelGGL((k_score_lean<1, LEAN_NPF>), grid, dim3(64), pk.lds * 8, ctx->stream, items,
+                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    else if (pk.nw == 2)
+        hipLaunchKernelGGL((k_score_lean<2, LEAN_NPF>), grid, dim3(128), pk.lds * 8, ctx->stream, items,
+                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    else
+        hipLaunchKernelGGL((k_score_lean<4, LEAN_NPF>), grid, dim3(256), pk.lds * 8, ctx->stream, items,
+                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1608,6 +2259,15 @@ int rf_create(int device, rf_ctx **out)
     }
     for (auto &e : ctx->ev)
         (void)hipEventCreate(&e);
+    // the lean scorer may use up to the whole 160 KiB LDS of a CU
+    (void)hipFuncSetAttribute((const void *)k_score_lean<1, LEAN_NPF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_score_lean<2, LEAN_NPF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_score_lean<4, LEAN_NPF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
 }
@@ -2092,6 +2752,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     std::vector<int64_t> gstart(ngroups + 1, 0);
     int64_t dense_total = 0, split_total = 0, scratch_total = 0;
     int max_reads = 0;
+    bool all_finite = true;
     for (int32_t g = 0; g < ngroups; ++g) {
         int32_t tpl = -1;
         std::string why;
@@ -2104,6 +2765,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             const SeqObj &S = ctx->seqs[A.seq];
             if (S.ncins > 0 || S.ncdel > 0)
                 return fail(ctx, RF_ERR_ARG, "error model cannot allow codon indels");
+            all_finite = all_finite && S.finite;
             if (tpl >= 0 && A.tpl != tpl)
                 return fail(ctx, RF_ERR_ARG, "rf_score: batch slots use different templates");
             tpl = A.tpl;
@@ -2198,6 +2860,10 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             split = true;
     }
 
+    const ScorePick pick = pick_scorer(reads, all_finite);
+    if (pick.lean && pick.q() != 64)
+        items = make_items(groups, pick.q());
+
     std::vector<int32_t> pgroup(nprops);
     for (int32_t g = 0; g < ngroups; ++g)
         for (int64_t k = prop_off[g]; k < prop_off[g + 1]; ++k)
@@ -2251,12 +2917,9 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
 
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     if (!items.empty()) {
-        dim3 grid((unsigned)items.size(), split ? (unsigned)max_reads : 1u);
-        const int lds = score_lds_elems(reads);
-        hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * lds * 8, ctx->stream,
-                           (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
-                           (const ScoreRead *)ctx->scratch[2].p, d_bases, d_tabs, d_bands, d_dense,
-                           d_split, split ? 1 : 0, lds);
+        launch_scorer(ctx, pick, (unsigned)items.size(), split ? (unsigned)max_reads : 1u,
+                      (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
+                      (const ScoreRead *)ctx->scratch[2].p, d_dense, d_split);
         if (split && dense_total > 0)
             hipLaunchKernelGGL(k_reduce, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[1].p, ngroups, d_gstart,
@@ -2345,7 +3008,8 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
         }
     }
     auto &P = ctx->dplan;
-    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups &&
+    const std::string envkey = scorer_env_key();
+    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.envkey == envkey &&
                       P.slots.size() == (size_t)nslots &&
                       !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
                       (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
@@ -2356,6 +3020,7 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
         reads.reserve(nslots);
         int64_t dense_total = 0, split_total = 0;
         int max_reads = 0;
+        bool all_finite = true;
         for (int32_t g = 0; g < ngroups; ++g) {
             ScoreGroup &G = groups[g];
             G.r0 = (int32_t)reads.size();
@@ -2363,6 +3028,7 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
                 const Band &A = ctx->slots[slots[k]].a;
                 const Band &B = ctx->slots[slots[k]].b;
                 const SeqObj &S = ctx->seqs[A.seq];
+                all_finite = all_finite && S.finite;
                 ScoreRead R{};
                 R.A = A.r.off / 8;
                 R.B = B.r.off / 8;
@@ -2406,7 +3072,13 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
         P.max_reads = max_reads;
         P.dense_total = dense_total;
         P.split_total = split_total;
-        P.lds_elems = score_lds_elems(reads);
+        P.pick = pick_scorer(reads, all_finite);
+        P.envkey = envkey;
+        if (P.pick.lean && P.pick.q() != 64) {
+            items = make_items(groups, P.pick.q());
+            if (int e = upload(ctx, ctx->scratch[11], items)) return e;
+            P.nitems = items.size();
+        }
     }
     bool split = (int64_t)P.nitems < 2048 && P.max_reads > 1;
     if (const char *mode = std::getenv("RIFRAF_SCORE_MODE")) {
@@ -2424,11 +3096,9 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     if (P.nitems) {
         dim3 grid((unsigned)P.nitems, split ? (unsigned)P.max_reads : 1u);
-        hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * P.lds_elems * 8, ctx->stream,
-                           (const WorkItem *)ctx->scratch[11].p, (const ScoreGroup *)ctx->scratch[12].p,
-                           (const ScoreRead *)ctx->scratch[13].p, (const uint8_t *)ctx->bytes_arena.d,
-                           (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d, d_dense,
-                           split ? (double *)ctx->scratch[10].p : nullptr, split ? 1 : 0, P.lds_elems);
+        launch_scorer(ctx, P.pick, grid.x, grid.y, (const WorkItem *)ctx->scratch[11].p,
+                      (const ScoreGroup *)ctx->scratch[12].p, (const ScoreRead *)ctx->scratch[13].p,
+                      d_dense, split ? (double *)ctx->scratch[10].p : nullptr);
         if (split)
             hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
@@ -2481,6 +3151,31 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     for (int jj = 0; jj <= b.m; ++jj)
         for (int d = 0; d < b.H; ++d)
             out[(size_t)jj * b.H + d] = buf[(size_t)(d + 2 * jj) * P + (d >> 1)];
+    return 0;
+}
+
+int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms)
+{
+    if (!ctx || bytes < 0 || reps < 1 || !ms)
+        return fail(ctx, RF_ERR_ARG, "rf_probe_stream: bad arguments");
+    (void)hipSetDevice(ctx->device);
+    bytes = std::min<int64_t>(bytes, ctx->band_arena.cap) & ~(int64_t)15;
+    if (bytes == 0) {
+        *ms = 0;
+        return 0;
+    }
+    if (int e = ensure_buf(ctx, ctx->scratch[9], 64)) return e;
+    const unsigned blocks = 256 * 8;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(k_probe_stream, dim3(blocks), dim3(256), 0, ctx->stream,
+                           (const dvec2 *)ctx->band_arena.d, bytes / 16, (double *)ctx->scratch[9].p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
+    *ms = t / reps;
     return 0;
 }
 

@@ -212,6 +212,12 @@ class Engine:
         data = np.asfortranarray(buf.reshape(ncols, H).T)
         return BandedArray((nrows, ncols), bw, default=default, data=data)
 
+    def probe_stream(self, nbytes: int, reps: int = 5) -> float:
+        """Mean ms to stream-read nbytes of the band arena (roofline calibration)."""
+        ms = c_double()
+        self._check(self.lib.rf_probe_stream(self.ctx, int(nbytes), int(reps), byref(ms)))
+        return ms.value
+
     def last_timing(self):
         a, b, c = c_double(), c_double(), c_double()
         self._check(self.lib.rf_last_timing(self.ctx, byref(a), byref(b), byref(c)))

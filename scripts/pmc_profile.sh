@@ -17,6 +17,7 @@ for p in $PASSES; do
     write) C="WRITE_SIZE" ;;
     inst)  C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" ;;
     wait)  C="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE" ;;
+    lds)   C="SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM TA_BUSY_avr TA_BUSY_max" ;;
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/pmc/${TAG}_$p -o p \

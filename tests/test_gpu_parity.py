@@ -352,3 +352,94 @@ def test_plan_cache_follows_template_content(engine):
     s3 = engine.realign(sl, sl, 0, [9] * 4, RF_FWD | RF_BWD)
     np.testing.assert_array_equal(s3, s1)
     np.testing.assert_array_equal(engine.score_dense([sl])[0][1:, 5:], d1[1:, 5:])
+
+
+SCORER_CONFIGS = [
+    # (RIFRAF_SCORE_KERNEL, RIFRAF_LEAN_NW, RIFRAF_LEAN_LDS_KB)
+    ("general", None, None),
+    (None, "1", None),
+    (None, "2", None),
+    (None, "1", "8"),      # windows exceed the budget: sub-passes over fewer lanes
+    (None, "2", "12"),
+    (None, "4", None),
+    (None, "4", "24"),
+    (None, "8", None),
+    (None, "8", "40"),
+]
+
+
+@pytest.mark.parametrize("kern,nw,lds", SCORER_CONFIGS)
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
+    """Both dense scorers (general and lean chain-per-column) over ragged
+    clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the oracle."""
+    for k, v in (("RIFRAF_SCORE_KERNEL", kern), ("RIFRAF_LEAN_NW", nw), ("RIFRAF_LEAN_LDS_KB", lds)):
+        if v is None:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    rng = np.random.default_rng(77)
+    templates, seqs, bws = [], [], []
+    shapes = [(150, 9, 0), (40, 3, 25), (260, 20, -30), (130, 9, 0), (70, 5, 12), (1, 1, 0)]
+    for c, (L, bw, skew) in enumerate(shapes):
+        t = random_seq(L, rng)
+        templates.append(t)
+        rs = []
+        for _ in range(int(rng.integers(1, 6))):
+            r = make_read(t, rng, 0.04, bw)
+            if skew > 0:
+                extra = random_seq(int(rng.integers(0, skew + 1)), rng)
+                r = RifrafSequence(np.concatenate([r.seq, extra]),
+                                   np.concatenate([r.error_log_p, np.full(len(extra), -1.0)]), bw, SEQ_SCORES)
+            elif skew < 0 and len(r.seq) > -skew + 5:
+                cut = int(rng.integers(0, -skew + 1))
+                r = RifrafSequence(r.seq[:len(r.seq) - cut], r.error_log_p[:len(r.seq) - cut], bw, SEQ_SCORES)
+            rs.append(r)
+        seqs.append(rs)
+        bws += [bw] * len(rs)
+    flat = [r for rs in seqs for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), tpl, bws, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in seqs:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    got = engine.score_dense(groups)
+    for c in range(len(templates)):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        t = templates[c]
+        mask = np.ones_like(ref_tot, bool)
+        mask[0, :5] = False
+        for j in range(1, len(t) + 1):
+            mask[j, t[j - 1]] = False
+        np.testing.assert_array_equal(got[c][mask], ref_tot[mask], err_msg=f"cluster {c}")
+    # the proposal-list path (rf_score) through the same scorer
+    props = [all_proposals_arrays(t) for t in templates]
+    tots = engine.score([(groups[c], -1, props[c]) for c in range(len(templates))])
+    for c in range(len(templates)):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        k, p, b = props[c]
+        np.testing.assert_array_equal(tots[c], ref_tot[p, dense_slot(k, b)], err_msg=f"cluster {c}")
+
+
+def test_score_lean_ineligible_tables(engine):
+    """A read with an infinite table entry (phred 0 -> match = -Inf) keeps the
+    launch on the general scorer; results stay bit-exact."""
+    rng = np.random.default_rng(5)
+    t = random_seq(90, rng)
+    rs = [make_read(t, rng, 0.03, 9) for _ in range(3)]
+    lp = rs[1].error_log_p.copy()
+    lp[10] = 0.0
+    rs[1] = RifrafSequence(rs[1].seq, lp, 9, SEQ_SCORES)
+    engine.set_sequences(0, rs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(3), np.arange(3), 0, [9] * 3, RF_FWD | RF_BWD)
+    props = all_proposals_arrays(t)
+    got = engine.score([(np.arange(3), -1, props)])[0]
+    ref_tot, _ = oracle.cpu_pass(t, rs, nthreads=4)
+    exp = ref_tot[props[1], dense_slot(props[0], props[2])]
+    np.testing.assert_array_equal(got, exp)
