@@ -50,6 +50,16 @@
 // column-major `data` is produced on download (rf_download_band).
 // ---------------------------------------------------------------------
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+// Band stores of the DP fill: nontemporal (streamed once, read back by the
+// scorer much later; measured ~5 % faster than plain stores on MI355X)
+#ifndef RIFRAF_DP_PLAIN_STORES
+#define DP_STORE(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define DP_STORE(p, v) (*(p) = (v))
+#endif
+
 __host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
 __host__ __device__ inline int64_t band_K(int H, int m) { return (int64_t)H + 2 * (int64_t)m; }
 
@@ -517,15 +527,29 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 // Blocked lean interior: per task an LDS slice of DPL_B edge records (the
 // row entering lane 15 and the column entering lane 0 per period) and
 // 2*DPL_B kappa rows of band output, flushed as one contiguous chunk.
-constexpr int DPL_B = 8;
+#ifndef DPL_BLOCK
+#define DPL_BLOCK 16
+#endif
+#ifndef DP_STAGGER
+#define DP_STAGGER 0   // measured: no gain (flush convoys are not the limiter)
+#endif
+constexpr int DPL_B = DPL_BLOCK;   // periods per block (<= 16: one edge record per lane)
 struct alignas(16) EdgeRec {
     double mt, mm, is, ds;
     int sb, col, pad0, pad1;
 };
 __host__ __device__ constexpr int dpl_pmax(int np) { return (16 * np) | 1; }   // band_P(32*NP-1)
+// carry slots on either side of a task's band-output rows: a flush writes
+// whole 128-B lines only and carries the partial line into the next block
+constexpr int DPL_CARRY = 16;
 __host__ __device__ constexpr int dpl_task_bytes(int np)
 {
-    return (int)(DPL_B * sizeof(EdgeRec)) + 2 * DPL_B * dpl_pmax(np) * 8;
+    return (int)(DPL_B * sizeof(EdgeRec)) + (2 * DPL_B * dpl_pmax(np) + 2 * DPL_CARRY) * 8;
+}
+// 16-B stores per lane of one flush: at most 2*DPL_B*P + DPL_CARRY doubles
+__host__ __device__ constexpr int dpl_flush_stores(int np)
+{
+    return (DPL_B * dpl_pmax(np) + DPL_CARRY / 2 + 15) / 16;
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
@@ -533,7 +557,7 @@ template <int NP, bool LEAN>
 __global__ void __launch_bounds__(64)
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
-      double *__restrict__ out_score, int *__restrict__ err)
+      double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink)
 {
     const int q = threadIdx.x & 15;
     const int tid = blockIdx.x * 4 + (threadIdx.x >> 4);
@@ -602,7 +626,11 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             hi = min(hi, __shfl_xor(hi, off));
         }
         if (__all(ok)) {
-            klo = __builtin_amdgcn_readfirstlane((lo + 1) & ~1);   // wave-uniform: scalar loop
+            // stagger: waves of one CU (blocks b, b+8, b+16, ... share an XCD) enter
+            // the blocked interior a quarter block apart, so that their band
+            // flushes do not all hit the store path at once (RIFRAF_DP_STAGGER)
+            const int stag = ((blockIdx.x >> 3) & 3) * (DPL_B / 2) * DP_STAGGER;
+            klo = __builtin_amdgcn_readfirstlane(((lo + 1) & ~1) + stag);   // wave-uniform: scalar loop
             khi = __builtin_amdgcn_readfirstlane(hi);
         }
     }
@@ -616,7 +644,17 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const int P = T.P;
             const int t = threadIdx.x >> 4;
             EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP));
-            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP) + DPL_B * sizeof(EdgeRec));
+            // line-aligned flushes: `fl` is the band position (doubles from the
+            // band start, which is 256-B aligned) up to which (forward) or down
+            // from which (reverse) the interior has been written.  A block's
+            // first position g0 is even forward (even kappa x any P) but can be
+            // odd in reverse (odd H): `ob` is shifted by g0's parity so that LDS
+            // and global 16-B pairs line up.
+            const int blk = 2 * DPL_B * P;
+            const ptrdiff_t g00 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
+            ptrdiff_t fl = g00 + (rev ? blk : 0);
+            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP) + DPL_B * sizeof(EdgeRec)) +
+                         DPL_CARRY + (int)(g00 & 1);
             // this lane's LDS slot per parity; a block's 2*DPL_B rows are the
             // contiguous global chunk (reverse: flipped rows)
             const int sl0 = rev ? (T.H - 1 - 2 * q * NP) >> 1 : q * NP;
@@ -641,8 +679,18 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             EdgeRec pend = edge_load(k);
             if (q < DPL_B)
                 ein[q] = pend;
-            if (nblk > 1)
-                pend = edge_load(k + 2 * DPL_B);
+            pend = edge_load(k + 2 * DPL_B);
+            {
+                // as many stores behind this load as the loop puts behind its
+                // own (to the sink), so that hipcc's wait for `pend` is vmcnt(FL)
+                // on every path into the loop, not vmcnt(0)
+                constexpr int FL = dpl_flush_stores(NP);
+                dvec2 *g = (dvec2 *)sink;
+                const dvec2 z = {0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < FL; ++j)
+                    g[q + 16 * j] = z;
+            }
             wave_sync();
             for (int b = 0; b < nblk; ++b) {
 #pragma unroll
@@ -674,17 +722,65 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], ob + i1 * P + sl1, ostep);
                 }
                 wave_sync();
-                // next block's edges (loaded one block ago) -> LDS
-                if (b + 1 < nblk && q < DPL_B)
+                // next block's edges (loaded one block ago) -> LDS (harmless past
+                // the last block: ein is not read again)
+                if (q < DPL_B)
                     ein[q] = pend;
-                // flush: 2*DPL_B kappa rows = one contiguous chunk of the band
-                if (tid < ntasks) {
-                    double *g = band + (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
-                    for (int e = q; e < 2 * DPL_B * P; e += 16)
-                        g[e] = ob[e];
+                // the block after next: issued BEFORE this block's stores.  vmcnt
+                // is one in-order counter for loads and stores, so a load issued
+                // after the stores could only be waited for by draining them
+                // (clamped rows: past the interior it reads valid, unused rows)
+                pend = edge_load(k + 4 * DPL_B);
+                // flush: the block's 2*DPL_B kappa rows are one contiguous run of the
+                // band [g0, g0 + blk).  Only whole 128-B lines are written (a partial
+                // line would leave L2 as a partial HBM write): the part past the last
+                // full line is carried into the next block (LDS slots before /
+                // after `ob`); the last block writes everything.  A fixed number of
+                // 16-B stores per lane (lanes past the end repeat the last pair;
+                // tasks past ntasks write the sink) keeps hipcc's wait for the next
+                // edge load at vmcnt(FL) instead of draining these stores.
+                {
+                    constexpr int FL = dpl_flush_stores(NP);
+                    const ptrdiff_t g0 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
+                    const bool last = b + 1 == nblk;
+                    ptrdiff_t lo, hi;
+                    if (!rev) {
+                        lo = fl;
+                        hi = last ? g0 + blk : ((g0 + blk) & ~(ptrdiff_t)15);
+                        fl = hi;
+                    } else {
+                        hi = fl;
+                        lo = last ? g0 : ((g0 + 15) & ~(ptrdiff_t)15);
+                        fl = lo;
+                    }
+                    // whole 16-B pairs [lo2, hi2); an odd end (reverse, odd g0: only
+                    // the first and last blocks) is one 8-B store
+                    const ptrdiff_t lo2 = (lo + 1) & ~(ptrdiff_t)1, hi2 = hi & ~(ptrdiff_t)1;
+                    const int nu = (int)((hi2 - lo2) >> 1);
+                    // (flags 512: diagnostics, every flush goes to the sink)
+                    const bool real = tid < ntasks && !(T.flags & 512);
+                    dvec2 *g = real ? (dvec2 *)(band + lo2) : (dvec2 *)sink;
+                    const dvec2 *o2 = (const dvec2 *)(ob + (lo2 - g0));
+#pragma unroll
+                    for (int j = 0; j < FL; ++j) {
+                        const int e = min(q + 16 * j, nu - 1);
+                        DP_STORE(g + e, o2[e]);
+                    }
+                    if (real && q == 0 && (lo & 1))
+                        band[lo] = ob[lo - g0];
+                    if (real && q == 1 && (hi & 1))
+                        band[hi - 1] = ob[hi - 1 - g0];
+                    // carry the unwritten partial line next to the next block's rows
+                    if (!rev) {
+                        const int c = (int)(g0 + blk - fl), src = (int)(fl - g0);
+                        if (q < c)
+                            ob[src - blk + q] = ob[src + q];
+                    } else {
+                        const int c = (int)(fl - g0);
+                        if (q < c)
+                            ob[blk + q] = ob[q];
+                    }
                 }
-                if (b + 2 < nblk)
-                    pend = edge_load(k + 4 * DPL_B);
                 wave_sync();
                 k += 2 * DPL_B;
             }
@@ -1019,7 +1115,6 @@ __device__ __forceinline__ double vmax(double a, double b)
     return r;
 }
 
-typedef double dvec2 __attribute__((ext_vector_type(2)));
 
 // Geometry of one staged (read, lanes [la0, la1]) window.
 struct LeanWin {
@@ -2532,6 +2627,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.ncdel = S.ncdel;
                 t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (flags & RF_SKEW) ? 2 : 0) |
                           (dir == 0 && (flags & RF_TRIM) ? 4 : 0);
+                // RIFRAF_DP_SINK=1: diagnostics only -- the blocked interior's band
+                // stores all go to one small sink buffer (bands are then invalid)
+                if (env_int("RIFRAF_DP_SINK", 0))
+                    t.flags |= 512;
                 // out_score: forward scores win when both directions run
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
@@ -2593,7 +2692,11 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     size_t at = 0;
     {
-        using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *);
+        using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
+                             double *);
+        // store sink of the blocked interior's padding tasks (past ntasks)
+        if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))
+            return e;
         const KFn kr[3][2] = {{k_dpr<1, false>, k_dpr<1, true>},
                               {k_dpr<2, false>, k_dpr<2, true>},
                               {k_dpr<4, false>, k_dpr<4, true>}};
@@ -2604,7 +2707,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     const int np = 1 << a;
                     const size_t lds = b ? 4 * (size_t)dpl_task_bytes(np) : 0;
                     hipLaunchKernelGGL(kr[a][b], dim3((n + 3) / 4), dim3(64), lds, ctx->stream, d_tasks + at, n,
-                                       d_bases, d_tabs, d_bands, d_out, ctx->d_err);
+                                       d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
                     at += n;
                 }
     }
@@ -3151,6 +3254,54 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     for (int jj = 0; jj <= b.m; ++jj)
         for (int d = 0; d < b.H; ++d)
             out[(size_t)jj * b.H + d] = buf[(size_t)(d + 2 * jj) * P + (d >> 1)];
+    return 0;
+}
+
+// Write-bandwidth probes over the band arena (destroys its contents):
+// mode 1: grid-stride 16-B stores (sequential); mode 2: the DP fill's
+// pattern -- 16-lane streams (4 per wave), each writing its own contiguous
+// region in chunks of `chunk16` 16-B units.
+__global__ void __launch_bounds__(64) k_probe_write(dvec2 *__restrict__ dst, int64_t n16, int mode,
+                                                    int chunk16, int nstreams)
+{
+    const dvec2 v = {1.0, 2.0};
+    if (mode == 1) {
+        const int64_t stride = (int64_t)gridDim.x * 64;
+        for (int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x; e < n16; e += stride)
+            dst[e] = v;
+        return;
+    }
+    const int sid = blockIdx.x * 4 + (threadIdx.x >> 4);
+    const int q = threadIdx.x & 15;
+    if (sid >= nstreams)
+        return;
+    const int64_t per = n16 / nstreams;
+    dvec2 *g = dst + (int64_t)sid * per;
+    for (int64_t c0 = 0; c0 + chunk16 <= per; c0 += chunk16) {
+        for (int e = q; e < chunk16; e += 16)
+            g[c0 + e] = v;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes, int32_t nstreams,
+                   double *ms)
+{
+    if (!ctx || bytes < 0 || !ms || (mode != 1 && mode != 2) || (mode == 2 && (chunk_bytes < 16 || nstreams < 1)))
+        return fail(ctx, RF_ERR_ARG, "rf_probe_write: bad arguments");
+    (void)hipSetDevice(ctx->device);
+    bytes = std::min<int64_t>(bytes, ctx->band_arena.cap) & ~(int64_t)15;
+    const int64_t n16 = bytes / 16;
+    const unsigned blocks = mode == 1 ? 256 * 32 : (unsigned)((nstreams + 3) / 4);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    hipLaunchKernelGGL(k_probe_write, dim3(blocks), dim3(64), 0, ctx->stream, (dvec2 *)ctx->band_arena.d, n16,
+                       mode, chunk_bytes / 16, nstreams);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
+    *ms = t;
     return 0;
 }
 

@@ -218,6 +218,13 @@ class Engine:
         self._check(self.lib.rf_probe_stream(self.ctx, int(nbytes), int(reps), byref(ms)))
         return ms.value
 
+    def probe_write(self, mode: int, nbytes: int, chunk_bytes: int = 0, nstreams: int = 0) -> float:
+        """ms for one write pass over the band arena (destroys band contents)."""
+        ms = c_double()
+        self._check(self.lib.rf_probe_write(self.ctx, int(mode), int(nbytes), int(chunk_bytes),
+                                            int(nstreams), byref(ms)))
+        return ms.value
+
     def last_timing(self):
         a, b, c = c_double(), c_double(), c_double()
         self._check(self.lib.rf_last_timing(self.ctx, byref(a), byref(b), byref(c)))

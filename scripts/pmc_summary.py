@@ -15,7 +15,11 @@ import sys
 
 def kname(full):
     base = full.split("(")[0].replace("void ", "")
-    return "k_dp" if base.startswith("k_dpr") or base.startswith("k_dp<") else base
+    if base.startswith("k_dpr") or base.startswith("k_dp<"):
+        return "k_dp"                 # every DP class of one rf_realign
+    if base.startswith("k_score"):
+        return "k_score"              # k_score / k_score_lean / k_score_ws*
+    return base
 
 
 def per_launch(path):

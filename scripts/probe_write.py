@@ -1,0 +1,16 @@
+#!/usr/bin/env python
+"""Write-bandwidth probes over a band arena the size of the c4 bench's (diagnostics)."""
+import json, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rifraf.jl_amd"))
+from rifraf_amd.engine import Engine
+nbytes = int(float(sys.argv[1])) if len(sys.argv) > 1 else 38 << 30
+e = Engine(0)
+e.reserve(nbytes + (64 << 20))
+res = {"bytes": nbytes, "read_gbs": nbytes / (e.probe_stream(nbytes, 3) * 1e-3) / 1e9}
+res["write_seq_gbs"] = nbytes / (e.probe_write(1, nbytes) * 1e-3) / 1e9
+for chunk in (256, 1664, 4096, 16384):
+    for ns in (16384, 65536):
+        ms = e.probe_write(2, nbytes, chunk, ns)
+        res[f"write_chunk{chunk}_s{ns}_gbs"] = nbytes / (ms * 1e-3) / 1e9
+print(json.dumps(res, indent=1))
+e.close()

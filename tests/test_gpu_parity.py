@@ -365,6 +365,7 @@ SCORER_CONFIGS = [
     (None, "4", "24"),
     (None, "8", None),
     (None, "8", "40"),
+    (None, "8", "60"),
 ]
 
 
