@@ -140,6 +140,13 @@ int rf_score(rf_ctx *ctx, int32_t ngroups,
 int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
                    const int32_t *slots, double *out);
 
+/* rf_score_dense with the totals written to DEVICE memory of the context's
+ * device (dev_out: at least sum_g (m_g + 1) * 9 doubles, e.g. a torch tensor).
+ * For the read-sharded exchange: each rank's partial fold
+ * goes straight into the RCCL all-gather buffer without a host round trip. */
+int rf_score_dense_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
+                       const int32_t *slots, double *dev_out);
+
 /* Geometry of a slot's band: nrows = n+1, ncols = m+1, bandwidth, H. */
 int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,
                      int32_t *nrows, int32_t *ncols, int32_t *bw, int32_t *H);

@@ -2041,7 +2041,9 @@ struct DevBuf {
 struct rf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side[3] = {};   // concurrent DP class launches (fork/join on `stream`)
     hipEvent_t ev[6];
+    hipEvent_t fork = nullptr, join[3] = {};
     std::string err;
     Arena bytes_arena;  // sequence + template bases
     Arena tab_arena;    // sequence tables
@@ -2354,6 +2356,11 @@ int rf_create(int device, rf_ctx **out)
     }
     for (auto &e : ctx->ev)
         (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    for (int i = 0; i < 3; ++i) {
+        (void)hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
+        (void)hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
+    }
     // the lean scorer may use up to the whole 160 KiB LDS of a CU
     (void)hipFuncSetAttribute((const void *)k_score_lean<1, LEAN_NPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2385,6 +2392,16 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
         (void)hipEventDestroy(e);
+    for (int i = 0; i < 3; ++i) {
+        if (ctx->side[i]) {
+            (void)hipStreamSynchronize(ctx->side[i]);
+            (void)hipStreamDestroy(ctx->side[i]);
+        }
+        if (ctx->join[i])
+            (void)hipEventDestroy(ctx->join[i]);
+    }
+    if (ctx->fork)
+        (void)hipEventDestroy(ctx->fork);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -2690,43 +2707,79 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     double *d_bands = (double *)ctx->band_arena.d;
 
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
-    size_t at = 0;
+    // Each kernel class is its own launch.  The classes are independent (disjoint
+    // bands), so the smaller ones run on side streams concurrently with the
+    // largest: the machine stays full through every launch's tail.
+    struct Launch {
+        int kind;      // 0..5 = k_dpr<1<<(kind>>1), kind&1>, 6 = k_dp<64,false>, 7 = k_dp<64,true>
+        size_t at, n;
+    };
+    std::vector<Launch> launches;
     {
-        using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
-                             double *);
-        // store sink of the blocked interior's padding tasks (past ntasks)
-        if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))
-            return e;
-        const KFn kr[3][2] = {{k_dpr<1, false>, k_dpr<1, true>},
-                              {k_dpr<2, false>, k_dpr<2, true>},
-                              {k_dpr<4, false>, k_dpr<4, true>}};
+        size_t at = 0;
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 2; ++b)
                 if (P.nr[a][b]) {
-                    const int n = (int)P.nr[a][b];
-                    const int np = 1 << a;
-                    const size_t lds = b ? 4 * (size_t)dpl_task_bytes(np) : 0;
-                    hipLaunchKernelGGL(kr[a][b], dim3((n + 3) / 4), dim3(64), lds, ctx->stream, d_tasks + at, n,
-                                       d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
-                    at += n;
+                    launches.push_back({2 * a + b, at, P.nr[a][b]});
+                    at += P.nr[a][b];
                 }
+        if (P.n64) {
+            launches.push_back({6, at, P.n64});
+            at += P.n64;
+        }
+        if (P.ng)
+            launches.push_back({7, at, P.ng});
     }
-    if (P.n64) {
-        const int n = (int)P.n64;
-        const int ld = P.hmax64 + 6;
-        hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, ctx->stream,
-                           d_tasks + at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
-        at += n;
-    }
+    if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))  // lean padding-task sink
+        return e;
     if (P.ng) {
-        const int n = (int)P.ng;
-        const int ld = P.hmaxg + 6;
-        if (int e = ensure_buf(ctx, ctx->scratch[10], (size_t)n * 4 * ld * 8))
+        if (int e = ensure_buf(ctx, ctx->scratch[10], P.ng * 4 * (size_t)(P.hmaxg + 6) * 8))
             return e;
-        hipLaunchKernelGGL((k_dp<64, true>), dim3(n), dim3(64), 0, ctx->stream, d_tasks + at, n,
-                           d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld,
-                           (double *)ctx->scratch[10].p);
-        at += n;
+    }
+    // the largest launch stays on the main stream
+    size_t big = 0;
+    for (size_t i = 1; i < launches.size(); ++i)
+        if (launches[i].n > launches[big].n)
+            big = i;
+    const bool concurrent = launches.size() > 1 && env_int("RIFRAF_DP_STREAMS", 1);
+    if (concurrent)
+        HIPCHK(ctx, hipEventRecord(ctx->fork, ctx->stream));
+    int nside = 0;
+    std::vector<int> used_side;
+    for (size_t i = 0; i < launches.size(); ++i) {
+        const Launch &L = launches[i];
+        hipStream_t st = ctx->stream;
+        if (concurrent && i != big) {
+            const int si = nside++ % 3;
+            st = ctx->side[si];
+            if (nside <= 3) {
+                HIPCHK(ctx, hipStreamWaitEvent(st, ctx->fork, 0));
+                used_side.push_back(si);
+            }
+        }
+        const int n = (int)L.n;
+        if (L.kind < 6) {
+            using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
+                                 double *);
+            const KFn kr[6] = {k_dpr<1, false>, k_dpr<1, true>, k_dpr<2, false>,
+                               k_dpr<2, true>,  k_dpr<4, false>, k_dpr<4, true>};
+            const int np = 1 << (L.kind >> 1);
+            const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
+            hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
+                               d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
+        } else if (L.kind == 6) {
+            const int ld = P.hmax64 + 6;
+            hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
+                               d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
+        } else {
+            const int ld = P.hmaxg + 6;
+            hipLaunchKernelGGL((k_dp<64, true>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
+                               d_bands, d_out, ctx->d_err, ld, (double *)ctx->scratch[10].p);
+        }
+    }
+    for (int si : used_side) {
+        HIPCHK(ctx, hipEventRecord(ctx->join[si], ctx->side[si]));
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->join[si], 0));
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
@@ -3080,8 +3133,8 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     return check_err(ctx);
 }
 
-int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
-                   double *out)
+static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                            double *out, hipMemcpyKind out_kind)
 {
     if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots)))
         return fail(ctx, RF_ERR_ARG, "rf_score_dense: bad arguments");
@@ -3211,14 +3264,27 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const 
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     if (out && P.dense_total > 0)
-        HIPCHK(ctx, hipMemcpyAsync(out, d_dense, sizeof(double) * P.dense_total, hipMemcpyDeviceToHost,
-                                   ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(out, d_dense, sizeof(double) * P.dense_total, out_kind, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
     ctx->score_ms = ms;
     ctx->gather_ms = 0;
     return 0;
+}
+
+int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                   double *out)
+{
+    return score_dense_impl(ctx, ngroups, slot_off, slots, out, hipMemcpyDeviceToHost);
+}
+
+int rf_score_dense_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                       double *dev_out)
+{
+    if (!dev_out)
+        return fail(ctx, RF_ERR_ARG, "rf_score_dense_dev: null device buffer");
+    return score_dense_impl(ctx, ngroups, slot_off, slots, dev_out, hipMemcpyDeviceToDevice);
 }
 
 int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which, int32_t *nrows, int32_t *ncols,

@@ -199,6 +199,16 @@ class Engine:
             at += r
         return res
 
+    def score_dense_dev(self, groups, dev_ptr: int):
+        """rf_score_dense_dev: dense totals written to device memory at
+        dev_ptr (sum_g (m_g+1)*9 doubles on this engine's device)."""
+        G = len(groups)
+        slot_off = np.zeros(G + 1, np.int32)
+        for g, sl in enumerate(groups):
+            slot_off[g + 1] = slot_off[g] + len(sl)
+        slots = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in groups]), np.int32)
+        self._check(self.lib.rf_score_dense_dev(self.ctx, G, ptr(slot_off), ptr(slots), c_void_p(int(dev_ptr))))
+
     def geometry(self, slot: int, which: int = RF_BAND_A):
         nr, nc, bw, H = c_int32(), c_int32(), c_int32(), c_int32()
         self._check(self.lib.rf_slot_geometry(self.ctx, int(slot), int(which), byref(nr), byref(nc),

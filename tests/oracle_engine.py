@@ -128,3 +128,13 @@ class OracleEngine:
     def download_band(self, slot, which=RF_BAND_A, default=-np.inf):
         data, _, key, n, m = self.slots[int(slot)]["A" if which == RF_BAND_A else "B"]
         return BandedArray((n + 1, m + 1), key[3], default=default, data=np.asfortranarray(data))
+
+    def score_dense(self, groups, to_host=True, rows=None):
+        """rf_score_dense on the oracle: all STAGE_SCORE proposals, (m+1, 9)
+        totals per group (oracle.cpu_pass refills the bands itself)."""
+        res = []
+        for sl in groups:
+            sb = [self._seq_bw(self._check_slot(s)) for s in sl]
+            tot, _ = oracle.cpu_pass(sb[0][1], [s for s, _ in sb], nthreads=2)
+            res.append(tot)
+        return res if to_host else None

@@ -1,0 +1,193 @@
+"""Read-sharded rifraf() (rifraf_amd.sharded) on CPU with
+gloo: world sizes 2 and 3, every rank wrapping the oracle engine.
+
+* whole rifraf() runs through ShardedEngine give the same consensus at every
+  iteration, the same final score and the same quality estimates as one
+  unsharded engine -- bit-exact, because the per-proposal fold is carried
+  from rank to rank in the reference's order (model.jl:389-397);
+* the dense exchange (per-rank partial fold + all-gather + rank-order sum)
+  agrees with the one-process fold within the north_star's 1e-9 relative.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G1 = os.path.join(HERE, "golden", "config1")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    errs = [g for g in got if g[1] == "error"]
+    assert not errs, errs[0][2]
+    return dict((r, v) for r, _, v in got)
+
+
+def _entry(fn, rank, world, port, q, *args):
+    import traceback
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, "ok", fn(rank, world, *args)))
+    except Exception:
+        q.put((rank, "error", traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------
+def _config1(engine_factory, f, refid):
+    from rifraf_amd import ErrorModel, Scores, cap_phreds
+    from rifraf_amd.fastxio import read_fasta_records, read_fastq
+    from rifraf_amd.model import RifrafParams, rifraf
+    refs = dict(read_fasta_records(os.path.join(G1, "references.fasta")))
+    seqs, phreds, _ = read_fastq(os.path.join(G1, f))
+    phreds = [cap_phreds(p, 30) for p in phreds]
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)),
+                          ref_scores=Scores.from_errors(ErrorModel(8, 0.1, 0.1, 1, 1)), max_iters=100,
+                          do_score=True)
+    res = rifraf(seqs, phreds, reference=refs[refid], params=params, engine=engine_factory(len(seqs)))
+    return summary(res)
+
+
+def _sampled(engine_factory, seed):
+    from rifraf_amd.model import RifrafParams, rifraf
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    _, _, _, reads, _, phreds, _, _ = sample_sequences(7, 70, error_rate=0.03, rng=rng)
+    params = RifrafParams(do_score=True, max_iters=30)
+    res = rifraf(reads, phreds, params=params, engine=engine_factory(len(reads)))
+    return summary(res)
+
+
+def summary(res):
+    st = res.state
+    return {"consensus": np.asarray(res.consensus).copy(), "score": st.score,
+            "stages": [[np.asarray(c).copy() for c in s] for s in res.consensus_stages],
+            "iters": list(st.stage_iterations), "converged": st.converged,
+            "sub": None if res.error_probs is None else res.error_probs.sub.copy(),
+            "ins": None if res.error_probs is None else res.error_probs.ins.copy(),
+            "aln": None if res.aln_error_probs is None else np.asarray(res.aln_error_probs).copy()}
+
+
+def _sharded_factory(n):
+    from oracle_engine import OracleEngine
+    from rifraf_amd.sharded import ShardedEngine
+    return ShardedEngine(OracleEngine(), n)
+
+
+def _plain_factory(n):
+    from oracle_engine import OracleEngine
+    return OracleEngine()
+
+
+def _w_config1(rank, world, f, refid):
+    return _config1(_sharded_factory, f, refid)
+
+
+def _w_sampled(rank, world, seed):
+    return _sampled(_sharded_factory, seed)
+
+
+def assert_same_run(a, b):
+    np.testing.assert_array_equal(a["consensus"], b["consensus"])
+    assert a["score"] == b["score"]
+    assert a["iters"] == b["iters"] and a["converged"] == b["converged"]
+    assert len(a["stages"]) == len(b["stages"])
+    for x, y in zip(a["stages"], b["stages"]):
+        assert len(x) == len(y)
+        for c1, c2 in zip(x, y):
+            np.testing.assert_array_equal(c1, c2)
+    for k in ("sub", "ins", "aln"):
+        if a[k] is None:
+            assert b[k] is None
+        else:
+            np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_config1_with_reference(world):
+    """Reference-informed run (FRAME stage, codon scoring on the last rank's
+    reference slot) with quality scores: identical to one engine."""
+    f = "input-reads-1.fastq"
+    refmap = dict(line.split() for line in open(os.path.join(G1, "ref-map.tsv")) if line.strip())
+    refid = refmap[f]
+    single = _config1(_plain_factory, f, refid)
+    got = _spawn(_w_config1, world, f, refid)
+    for r in range(world):
+        assert_same_run(got[r], single)
+
+
+def test_sharded_sampled_cluster():
+    single = _sampled(_plain_factory, 5)
+    got = _spawn(_w_sampled, 2, 5)
+    for r in range(2):
+        assert_same_run(got[r], single)
+
+
+# ----------------------------------------------------------------------
+def _w_dense(rank, world, seed):
+    from _util import make_read
+    from oracle_engine import OracleEngine
+    from rifraf_amd.engine import RF_BWD, RF_FWD
+    from rifraf_amd.sample import random_seq
+    from rifraf_amd.sharded import ShardedEngine
+    rng = np.random.default_rng(seed)
+    tpls = [random_seq(int(rng.integers(40, 70)), rng) for _ in range(2)]
+    reads = [[make_read(t, rng, 0.04, 6) for _ in range(int(rng.integers(3, 7)))] for t in tpls]
+    flat = [r for rs in reads for r in rs]
+    e = ShardedEngine(OracleEngine(), len(flat))
+    e.set_sequences(0, flat)
+    e.set_templates(0, tpls)
+    tpl_of = np.concatenate([[c] * len(rs) for c, rs in enumerate(reads)])
+    n = len(flat)
+    e.realign(np.arange(n), np.arange(n), tpl_of, [6] * n, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in reads:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    return e.score_dense(groups), tpls, reads
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_dense_exchange(world):
+    import oracle
+    got = _spawn(_w_dense, world, 17)
+    dense0, tpls, reads = got[0]
+    for r in range(1, world):
+        for a, b in zip(got[r][0], dense0):
+            np.testing.assert_array_equal(a, b)        # every rank holds the same totals
+    for c, t in enumerate(tpls):
+        exp, _ = oracle.cpu_pass(t, reads[c], nthreads=2)
+        mask = np.isfinite(exp)
+        assert (np.isfinite(dense0[c]) == mask).all()
+        # regrouped sum: 1e-9 relative is the north_star bar; the bound here is far tighter
+        np.testing.assert_allclose(dense0[c][mask], exp[mask], rtol=1e-12, atol=0)
+
+
+def test_shard_bounds_and_owner():
+    from rifraf_amd.sharded import shard_bounds
+    for n, w in [(10, 3), (5000, 8), (3, 4), (1, 1)]:
+        b = shard_bounds(n, w)
+        assert b[0] == 0 and b[-1] == n and all(x <= y for x, y in zip(b, b[1:]))
+        sizes = np.diff(b)
+        assert sizes.max() - sizes.min() <= 1

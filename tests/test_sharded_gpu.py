@@ -1,0 +1,67 @@
+"""Read-sharded rifraf() on the HIP engine.
+
+Two gloo ranks on the one GPU of the test box, each with its own rf_ctx,
+run whole rifraf() calls through ShardedEngine; the results must equal one
+unsharded HIP engine bit for bit (the proposal fold is carried from rank to
+rank in the reference's order).  rf_score_dense_dev (the device-side partial
+of the RCCL exchange) must equal rf_score_dense.
+"""
+import numpy as np
+import pytest
+
+from test_sharded import _config1, _sampled, _spawn, assert_same_run, G1
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip_sharded_factory(n):
+    from rifraf_amd.engine import Engine
+    from rifraf_amd.sharded import ShardedEngine
+    return ShardedEngine(Engine(0), n)
+
+
+def _w_hip_config1(rank, world, f, refid):
+    return _config1(_hip_sharded_factory, f, refid)
+
+
+def _w_hip_sampled(rank, world, seed):
+    return _sampled(_hip_sharded_factory, seed)
+
+
+def test_sharded_hip_config1_two_ranks(engine):
+    import os
+    f = "input-reads-2.fastq"
+    refmap = dict(line.split() for line in open(os.path.join(G1, "ref-map.tsv")) if line.strip())
+    single = _config1(lambda n: engine, f, refmap[f])
+    got = _spawn(_w_hip_config1, 2, f, refmap[f])
+    for r in range(2):
+        assert_same_run(got[r], single)
+
+
+def test_sharded_hip_sampled_two_ranks(engine):
+    single = _sampled(lambda n: engine, 9)
+    got = _spawn(_w_hip_sampled, 2, 9)
+    for r in range(2):
+        assert_same_run(got[r], single)
+
+
+def test_score_dense_dev_matches_host(engine):
+    import torch
+    from _util import make_read
+    from rifraf_amd.engine import RF_BWD, RF_FWD
+    from rifraf_amd.sample import random_seq
+    rng = np.random.default_rng(4)
+    tpls = [random_seq(120, rng), random_seq(75, rng)]
+    reads = [[make_read(t, rng, 0.03, 9) for _ in range(4)] for t in tpls]
+    flat = [r for rs in reads for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, tpls)
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), np.repeat([0, 1], 4), [9] * n, RF_FWD | RF_BWD)
+    groups = [np.arange(0, 4), np.arange(4, 8)]
+    host = engine.score_dense(groups)
+    buf = torch.full(((121 + 76) * 9,), 7.0, dtype=torch.float64, device="cuda:0")
+    engine.score_dense_dev(groups, buf.data_ptr())
+    dev = buf.cpu().numpy()
+    np.testing.assert_array_equal(dev[:121 * 9].reshape(121, 9), host[0])
+    np.testing.assert_array_equal(dev[121 * 9:].reshape(76, 9), host[1])
