@@ -758,17 +758,20 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     const ptrdiff_t lo2 = (lo + 1) & ~(ptrdiff_t)1, hi2 = hi & ~(ptrdiff_t)1;
                     const int nu = (int)((hi2 - lo2) >> 1);
                     // (flags 512: diagnostics, every flush goes to the sink)
-                    const bool real = tid < ntasks && !(T.flags & 512);
+                    // padding tasks (T = {}: nu = 0) and the diagnostics sink write
+                    // slots [0, 16*FL) of the sink -- never index -1
+                    const bool task_real = tid < ntasks && !(T.flags & 512);
+                    const bool real = task_real && nu > 0;
                     dvec2 *g = real ? (dvec2 *)(band + lo2) : (dvec2 *)sink;
                     const dvec2 *o2 = (const dvec2 *)(ob + (lo2 - g0));
 #pragma unroll
                     for (int j = 0; j < FL; ++j) {
-                        const int e = min(q + 16 * j, nu - 1);
-                        DP_STORE(g + e, o2[e]);
+                        const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
+                        DP_STORE(g + e, real ? o2[e] : o2[0]);
                     }
-                    if (real && q == 0 && (lo & 1))
+                    if (task_real && q == 0 && (lo & 1))
                         band[lo] = ob[lo - g0];
-                    if (real && q == 1 && (hi & 1))
+                    if (task_real && q == 1 && (hi & 1))
                         band[hi - 1] = ob[hi - 1 - g0];
                     // carry the unwritten partial line next to the next block's rows
                     if (!rev) {
