@@ -65,6 +65,13 @@ def band_cells(n: int, m: int, bw: int) -> int:
     return int(np.sum(stop - start + 1))
 
 
+def band_bytes(n: int, m: int, bw: int) -> int:
+    """Device bytes of one kappa-major band (rifraf_hip.hip band_K x band_P, 256-B aligned)."""
+    H = 2 * bw + abs(n - m) + 1
+    P = ((H + 1) >> 1) | 1
+    return ((H + 2 * m) * P * 8 + 255) // 256 * 256
+
+
 def make_workload(nclusters, nreads, length, error_rate, bw, seed):
     """Synthetic clusters from the restated sample module (sample.jl)."""
     from rifraf_amd import ErrorModel, RifrafSequence, Scores
@@ -334,10 +341,13 @@ def run_read_sharded(args, rank, world, local, dist, torch):
     t_gen = time.perf_counter()
     t, reads = make_read_shard(nreads, length, err, bw, args.seed, lo, hi)
     gen_s = time.perf_counter() - t_gen
-    eng = Engine(local)
     nloc = len(reads)
-    guess = sum(2 * 8 * (2 * 2 * bw + abs(len(r) - length) + 2) * (length + 1) * 11 // 10 for r in reads)
-    eng.reserve(guess + (256 << 20))
+    # band doubling on a first context sized for one forward band per read at
+    # bw and 2*bw; the timed context is then sized exactly for A + B at the
+    # final bandwidths (an arena that grows by compaction needs old + new)
+    eng = Engine(local)
+    eng.reserve(sum(band_bytes(len(r), length, bw) + band_bytes(len(r), length, 2 * bw) for r in reads)
+                + (256 << 20))
     for a in range(0, nloc, 1024):
         eng.set_sequences(a, reads[a:a + 1024])
     eng.set_templates(0, [t])
@@ -345,6 +355,12 @@ def run_read_sharded(args, rank, world, local, dist, torch):
     cells_first = sum(band_cells(len(r), length, r.bandwidth) for r in reads)
     smart_forward_moves(SimpleNamespace(e=eng), [(k, k) for k in range(nloc)], reads, length, 0.1)
     dbl_s = time.perf_counter() - t_dbl
+    eng.close()
+    eng = Engine(local)
+    eng.reserve(sum(2 * band_bytes(len(r), length, r.bandwidth) for r in reads) + (256 << 20))
+    for a in range(0, nloc, 1024):
+        eng.set_sequences(a, reads[a:a + 1024])
+    eng.set_templates(0, [t])
     slots = np.arange(nloc, dtype=np.int32)
     bws = np.array([r.bandwidth for r in reads], np.int32)
     cells = sum(2 * band_cells(len(r), length, r.bandwidth) for r in reads)
