@@ -533,7 +533,10 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 #ifndef DP_STAGGER
 #define DP_STAGGER 0   // measured: no gain (flush convoys are not the limiter)
 #endif
-constexpr int DPL_B = DPL_BLOCK;   // periods per block (<= 16: one edge record per lane)
+// periods per block (<= 16: one edge record per lane); NP = 8 tasks take 4 so
+// that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
+// several waves per CU
+__host__ __device__ constexpr int dpl_b(int np) { return np >= 8 ? 4 : DPL_BLOCK; }
 struct alignas(16) EdgeRec {
     double mt, mm, is, ds;
     int sb, col, pad0, pad1;
@@ -544,12 +547,12 @@ __host__ __device__ constexpr int dpl_pmax(int np) { return (16 * np) | 1; }   /
 constexpr int DPL_CARRY = 16;
 __host__ __device__ constexpr int dpl_task_bytes(int np)
 {
-    return (int)(DPL_B * sizeof(EdgeRec)) + (2 * DPL_B * dpl_pmax(np) + 2 * DPL_CARRY) * 8;
+    return (int)(dpl_b(np) * sizeof(EdgeRec)) + (2 * dpl_b(np) * dpl_pmax(np) + 2 * DPL_CARRY) * 8;
 }
 // 16-B stores per lane of one flush: at most 2*DPL_B*P + DPL_CARRY doubles
 __host__ __device__ constexpr int dpl_flush_stores(int np)
 {
-    return (DPL_B * dpl_pmax(np) + DPL_CARRY / 2 + 15) / 16;
+    return (dpl_b(np) * dpl_pmax(np) + DPL_CARRY / 2 + 15) / 16;
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
@@ -559,6 +562,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
       const double *__restrict__ tabs, double *__restrict__ bands,
       double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink)
 {
+    constexpr int DPL_B = dpl_b(NP);
     const int q = threadIdx.x & 15;
     const int tid = blockIdx.x * 4 + (threadIdx.x >> 4);
     DPTask T = {};
@@ -2067,7 +2071,7 @@ struct rf_ctx {
         uint64_t gen = 0;
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
-        size_t nr[3][2] = {};   // k_dpr<1,2,4> x {general, lean}
+        size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
     } rplan;
@@ -2624,7 +2628,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[3][2], c64, cg;
+        std::vector<DPTask> cr[4][2], c64, cg;
         int hmax64 = 0, hmaxg = 0;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
@@ -2655,7 +2659,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
                 t.P = band_P(t.H);
-                // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4), lean when
+                // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4, 8), lean when
                 // there are no codon moves and no skew / trim; k_dp beyond
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
                 if (t.H <= 31)
@@ -2664,6 +2668,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     cr[1][lean].push_back(t);
                 else if (t.H <= 127)
                     cr[2][lean].push_back(t);
+                else if (t.H <= 255 && !env_int("RIFRAF_DP_NO_NP8", 0))
+                    cr[3][env_int("RIFRAF_DP_NP8_LEAN", 1) ? lean : 0].push_back(t);
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
@@ -2693,7 +2699,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         P.seq.assign(seq, seq + njobs);
         P.tpl.assign(tpl, tpl + njobs);
         P.bw.assign(bw, bw + njobs);
-        for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 2; ++b)
                 P.nr[a][b] = cr[a][b].size();
         P.n64 = c64.size();
@@ -2714,24 +2720,24 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // bands), so the smaller ones run on side streams concurrently with the
     // largest: the machine stays full through every launch's tail.
     struct Launch {
-        int kind;      // 0..5 = k_dpr<1<<(kind>>1), kind&1>, 6 = k_dp<64,false>, 7 = k_dp<64,true>
+        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<64,true>
         size_t at, n;
     };
     std::vector<Launch> launches;
     {
         size_t at = 0;
-        for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 2; ++b)
                 if (P.nr[a][b]) {
                     launches.push_back({2 * a + b, at, P.nr[a][b]});
                     at += P.nr[a][b];
                 }
         if (P.n64) {
-            launches.push_back({6, at, P.n64});
+            launches.push_back({8, at, P.n64});
             at += P.n64;
         }
         if (P.ng)
-            launches.push_back({7, at, P.ng});
+            launches.push_back({9, at, P.ng});
     }
     if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))  // lean padding-task sink
         return e;
@@ -2761,16 +2767,16 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         const int n = (int)L.n;
-        if (L.kind < 6) {
+        if (L.kind < 8) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *);
-            const KFn kr[6] = {k_dpr<1, false>, k_dpr<1, true>, k_dpr<2, false>,
-                               k_dpr<2, true>,  k_dpr<4, false>, k_dpr<4, true>};
+            const KFn kr[8] = {k_dpr<1, false>, k_dpr<1, true>, k_dpr<2, false>, k_dpr<2, true>,
+                               k_dpr<4, false>, k_dpr<4, true>, k_dpr<8, false>, k_dpr<8, true>};
             const int np = 1 << (L.kind >> 1);
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
-        } else if (L.kind == 6) {
+        } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);

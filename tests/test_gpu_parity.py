@@ -108,7 +108,7 @@ def test_dp_class_boundaries(engine):
     rng = np.random.default_rng(77)
     t = random_seq(180, rng)
     seqs, bws = [], []
-    for H in (29, 30, 31, 32, 33, 61, 62, 63, 64, 65, 125, 126, 127, 128, 129):
+    for H in (29, 30, 31, 32, 33, 61, 62, 63, 64, 65, 125, 126, 127, 128, 129, 254, 255, 256, 257):
         for delta in (0, 1, 4, -3):
             bw = (H - 1 - abs(delta)) // 2
             if bw < 1:
