@@ -556,8 +556,13 @@ __host__ __device__ constexpr int dpl_flush_stores(int np)
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
+#ifdef DPR_WAVES
+#define DPR_ATTR __attribute__((amdgpu_waves_per_eu(DPR_WAVES)))
+#else
+#define DPR_ATTR
+#endif
 template <int NP, bool LEAN>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) DPR_ATTR
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
       double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink)
