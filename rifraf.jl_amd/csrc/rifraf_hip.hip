@@ -1616,6 +1616,181 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
     }
 }
 
+// ---------------------------------------------------------------------
+// k_score_seg: the lean chains for bands too wide for k_score_ws's window
+//
+// Same per-lane chain as lean_chain (one new column per lane a: Sub(a+1, b),
+// Ins(a, b), Del(a+1); identical operands, order and FP64 max-plus, so
+// identical results), but the rows are walked in segments of SEG_S band
+// diagonals.  In column a's frame a row is d = i - a + c, and every interior
+// lane walks the same d range [1, H], so one segment [D, D+SEG_S) of all
+// SEG_L lanes touches kappa rows [D + 2*a0 - 1, D + SEG_S + 2*(a0+SEG_L) - 2]
+// and, in each, only the SEG_S/2 + 1 elements of diagonals [D-1, D+SEG_S).
+// That (SEG_S + 2*SEG_L) x (SEG_S/2 + 1) slice per band is staged in LDS --
+// independent of H, unlike the full kappa-row window (2L + H) x H/2 -- and
+// each band element is loaded about once per work item.
+// ---------------------------------------------------------------------
+constexpr int SEG_L = 64;                       // lanes (columns) per work item
+constexpr int SEG_S = 16;                       // diagonals per segment
+constexpr int SEG_W = SEG_S / 2 + 1;            // staged doubles per kappa row (odd)
+constexpr int SEG_NR = SEG_S + 2 * SEG_L;       // staged kappa rows per band
+constexpr int SEG_NT = SEG_S + SEG_L + 1;       // staged table rows
+
+__global__ void __launch_bounds__(64)
+k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+            const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+            const double *__restrict__ tabs, const double *__restrict__ bands,
+            double *__restrict__ dense, double *__restrict__ split, int split_mode)
+{
+    __shared__ double sA[SEG_NR * SEG_W];
+    __shared__ double sB[SEG_NR * SEG_W];
+    __shared__ __attribute__((aligned(16))) double sT[SEG_NT * 6];
+    const int nb = gridDim.x, bx = blockIdx.x;
+    const int xq = nb >> 3, xr = nb & 7, x = bx & 7;
+    const WorkItem wi = items[x * xq + min(x, xr) + (bx >> 3)];   // XCD-aware, as k_score_ws
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int tid = threadIdx.x;
+    const int a = a0 + tid;
+    const bool active = a <= m;
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + blockIdx.y;
+        if (r0 >= G.r1)
+            return;
+        r1 = r0 + 1;
+    }
+    const bool hasS = a < m;
+    const double smask = hasS ? 0.0 : -RF_INF;
+    double tI[4], tS[4], tD = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] = 0.0;
+        tS[k] = 0.0;
+    }
+    for (int r = r0; r < r1; ++r) {
+        const ScoreRead R = reads[r];
+        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
+        // this lane's rows (lean_chain): [i0, ilast] in the loop, i1 = ilast + 1 peeled
+        const int jn = min(a + 1, m);
+        const int i0 = max(0, jn - c);
+        const int i1 = min(jn + vb, n);
+        const int ilast = min(i1, a + vb);
+        const int dfirst = i0 - a + c, dlast = ilast - a + c;
+        const bool peel = i1 > ilast;
+        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
+        for (int off = 32; off >= 1; off >>= 1) {
+            dlo = min(dlo, __shfl_xor(dlo, off));
+            dhi = max(dhi, __shfl_xor(dhi, off));
+        }
+        dlo = __builtin_amdgcn_readfirstlane(dlo) & ~1;   // even segment starts
+        dhi = __builtin_amdgcn_readfirstlane(dhi);
+        const double *gA = bands + R.A;
+        const double *gB = bands + R.B;
+        const double *tm = tabs + R.tab;
+        const uint8_t *sq = bases + R.sb;
+        double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            prev[k] = -RF_INF;
+            accI[k] = -RF_INF;
+            accS[k] = -RF_INF;
+        }
+        for (int D = dlo; D <= dhi; D += SEG_S) {
+            const int kb = D + 2 * a0 - 1;          // first staged kappa row
+            const int e0 = (D - 1) >> 1;            // first staged element (diagonal D-1)
+            const int ib = a0 - c + D;              // first staged table row
+            wave_sync();                            // previous segment's chains are done
+            for (int t = tid; t < SEG_NR * SEG_W; t += 64) {
+                const int row = t / SEG_W, col = t - row * SEG_W;
+                const int kap = kb + row, e = e0 + col;
+                const bool ok = kap >= 0 && kap < K && e >= 0 && e < P;
+                const size_t g = (size_t)kap * P + e;
+                sA[t] = ok ? gA[g] : -RF_INF;
+                sB[t] = ok ? gB[g] : -RF_INF;
+            }
+            for (int t = tid; t < SEG_NT; t += 64) {
+                const int i = ib + t;
+                if (i >= 0 && i <= n) {
+                    const int ks = max(i - 1, 0);
+                    lean_row(sT + 6 * t, i >= 1 ? sq[i - 1] : 4, tm[ks], tm[n + ks], tm[2 * (size_t)n + ks],
+                             tm[3 * (size_t)n + i]);
+                }
+            }
+            wave_sync();
+            if (!active)
+                continue;
+            const int lo = max(D, dfirst), hi = min(D + SEG_S - 1, dlast);
+            for (int d = lo; d <= hi; ++d) {
+                const int kr = d + 2 * a - kb;                       // staged row of (d, a)
+                const int ec = (d >> 1) - e0, ep = ((d - 1) >> 1) - e0;
+                const int i = a - c + d;
+                const double ac = sA[kr * SEG_W + ec];
+                const double bI = sB[kr * SEG_W + ec];
+                const double aprev = (d >= 1 && i >= 1) ? sA[(kr - 1) * SEG_W + ep] : -RF_INF;
+                const double bS = (hasS ? sB[(kr + 1) * SEG_W + ep] : bI) + smask;
+                const double2 *rec = (const double2 *)(sT + 6 * (i - ib));
+                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
+                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+                const double dl = ac + u2.y;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
+                    prev[k] = best;
+                    accI[k] = vmax(accI[k], best + bI);
+                    accS[k] = vmax(accS[k], best + bS);
+                }
+                dd = vmax(dd, ac + bS);
+            }
+            const int dp = dlast + 1;
+            if (peel && dp >= D && dp < D + SEG_S) {
+                // last row of the new column lies below A/B column a's band (a < m)
+                const int kr = dp + 2 * a - kb;
+                const int ep = ((dp - 1) >> 1) - e0;
+                const int i = a - c + dp;
+                const double aprev = sA[(kr - 1) * SEG_W + ep];
+                const double bSr = sB[(kr + 1) * SEG_W + ep];
+                const double2 *rec = (const double2 *)(sT + 6 * (i - ib));
+                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
+                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+            }
+        }
+        if (active) {
+            const double qnan = __builtin_nan("");
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+                tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+            }
+            tD += dd;
+        }
+    }
+    if (!active)
+        return;
+    const double qnan = __builtin_nan("");
+    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
+                                    : dense + G.dense_off;
+    double *dst = base + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[5 + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[9 + k] = tS[k];
+        dst[13] = tD;
+    }
+    if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
 // Read-bandwidth probe over the band arena (calibrates the HBM roofline of
 // the scorer on the same allocation): grid-stride 16-B loads, 8 in flight.
 __global__ void __launch_bounds__(256) k_probe_stream(const dvec2 *__restrict__ src, int64_t n16,
@@ -2038,6 +2213,7 @@ struct Slot {
 // Choice of dense scorer for one launch.
 struct ScorePick {
     bool lean = false;
+    bool seg = false;   // k_score_seg: wide bands (window too large for LDS), finite tables
     int nw = 1;     // lean: waves per workgroup (64 * nw chain columns per work item)
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
     int q() const { return nw == 8 ? 256 : 64 * nw; }   // chain columns per work item
@@ -2285,7 +2461,8 @@ ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
     ScorePick p;
     const char *kern = std::getenv("RIFRAF_SCORE_KERNEL");
     const bool force_general = kern && !std::strcmp(kern, "general");
-    if (all_finite && !force_general && !reads.empty()) {
+    const bool force_seg = kern && !std::strcmp(kern, "seg");
+    if (all_finite && !force_general && !force_seg && !reads.empty()) {
         int need1 = 0;
         for (const auto &R : reads)
             need1 = std::max(need1, lean_need(1, R.H, R.P));
@@ -2299,6 +2476,11 @@ ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
             p.lds = lds;
             return p;
         }
+    }
+    // wide bands: the row-segment scorer (same chains, H-independent LDS)
+    if (all_finite && !force_general && !reads.empty()) {
+        p.seg = true;
+        return p;
     }
     p.lds = score_lds_elems(reads);
     return p;
@@ -2325,7 +2507,10 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     // window but skips the chains (measures its load pipeline alone)
     const int sm = (split ? 1 : 0) | (env_int("RIFRAF_LEAN_NOCOMP", 0) ? 2 : 0);
     dim3 grid(nitems, gy);
-    if (!pk.lean)
+    if (pk.seg)
+        hipLaunchKernelGGL(k_score_seg, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
+                           d_bands, dense, split, sm);
+    else if (!pk.lean)
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     else if (pk.nw == 8)

@@ -357,6 +357,7 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (RIFRAF_SCORE_KERNEL, RIFRAF_LEAN_NW, RIFRAF_LEAN_LDS_KB)
     ("general", None, None),
+    ("seg", None, None),       # row-segment scorer (wide bands) on every shape
     (None, "1", None),
     (None, "2", None),
     (None, "1", "8"),      # windows exceed the budget: sub-passes over fewer lanes
@@ -444,3 +445,54 @@ def test_score_lean_ineligible_tables(engine):
     ref_tot, _ = oracle.cpu_pass(t, rs, nthreads=4)
     exp = ref_tot[props[1], dense_slot(props[0], props[2])]
     np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("kern", [None, "general"])
+def test_score_wide_bands(engine, monkeypatch, mode, kern):
+    """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
+    shorter than the template, plus a narrow read in the same launch): the
+    row-segment scorer k_score_seg (default) and the in-place k_score
+    ("general") are both bit-exact against the oracle."""
+    if kern is None:
+        monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("RIFRAF_SCORE_KERNEL", kern)
+    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    rng = np.random.default_rng(404)
+    templates, seqs, bws = [], [], []
+    for L, bw_list, skew in [(320, (100, 60, 9), 40), (250, (45, 120), -35), (90, (70,), 0)]:
+        t = random_seq(L, rng)
+        templates.append(t)
+        rs = []
+        for bw in bw_list:
+            r = make_read(t, rng, 0.05, bw)
+            if skew > 0:
+                extra = random_seq(int(rng.integers(skew // 2, skew + 1)), rng)
+                r = RifrafSequence(np.concatenate([r.seq, extra]),
+                                   np.concatenate([r.error_log_p, np.full(len(extra), -1.0)]), bw, SEQ_SCORES)
+            elif skew < 0:
+                cut = int(rng.integers(-skew // 2, -skew + 1))
+                r = RifrafSequence(r.seq[:len(r.seq) - cut], r.error_log_p[:len(r.seq) - cut], bw, SEQ_SCORES)
+            rs.append(r)
+            bws.append(bw)
+        seqs.append(rs)
+    flat = [r for rs in seqs for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), tpl, bws, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in seqs:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    got = engine.score_dense(groups)
+    for c in range(len(templates)):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        t = templates[c]
+        mask = np.ones_like(ref_tot, bool)
+        mask[0, :5] = False
+        for j in range(1, len(t) + 1):
+            mask[j, t[j - 1]] = False
+        np.testing.assert_array_equal(got[c][mask], ref_tot[mask], err_msg=f"cluster {c}")
