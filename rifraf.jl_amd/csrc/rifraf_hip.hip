@@ -1697,28 +1697,66 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
             accI[k] = -RF_INF;
             accS[k] = -RF_INF;
         }
+        // segment staging, software-pipelined: the next segment's band slices
+        // and table rows are loaded into registers while this one is scored
+        constexpr int NL = (SEG_NR * SEG_W + 63) / 64;   // band elements per lane
+        constexpr int NTL = (SEG_NT + 63) / 64;           // table rows per lane
+        double ra[NL], rb[NL], tmt[NTL], tmm[NTL], tin[NTL], tdl[NTL];
+        int tsb[NTL];
+        auto load_seg = [&](int D) {
+            const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, ib = a0 - c + D;
+#pragma unroll
+            for (int u = 0; u < NL; ++u) {
+                const int t = tid + 64 * u;
+                const int row = t / SEG_W, col = t - row * SEG_W;
+                const int kap = kb + row, e = e0 + col;
+                const bool ok = t < SEG_NR * SEG_W && kap >= 0 && kap < K && e >= 0 && e < P;
+                const size_t g = ok ? (size_t)kap * P + e : 0;
+                ra[u] = gA[g];
+                rb[u] = gB[g];
+                if (!ok) {
+                    ra[u] = -RF_INF;
+                    rb[u] = -RF_INF;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < NTL; ++u) {
+                const int i = min(max(ib + tid + 64 * u, 0), n);
+                const int ks = max(i - 1, 0);
+                tsb[u] = i >= 1 ? sq[i - 1] : 4;
+                tmt[u] = tm[ks];
+                tmm[u] = tm[n + ks];
+                tin[u] = tm[2 * (size_t)n + ks];
+                tdl[u] = tm[3 * (size_t)n + i];
+            }
+        };
+        auto store_seg = [&]() {
+#pragma unroll
+            for (int u = 0; u < NL; ++u) {
+                const int t = tid + 64 * u;
+                if (t < SEG_NR * SEG_W) {
+                    sA[t] = ra[u];
+                    sB[t] = rb[u];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < NTL; ++u) {
+                const int t = tid + 64 * u;
+                if (t < SEG_NT)
+                    lean_row(sT + 6 * t, tsb[u], tmt[u], tmm[u], tin[u], tdl[u]);
+            }
+        };
+        if (dlo <= dhi)
+            load_seg(dlo);
         for (int D = dlo; D <= dhi; D += SEG_S) {
             const int kb = D + 2 * a0 - 1;          // first staged kappa row
             const int e0 = (D - 1) >> 1;            // first staged element (diagonal D-1)
             const int ib = a0 - c + D;              // first staged table row
             wave_sync();                            // previous segment's chains are done
-            for (int t = tid; t < SEG_NR * SEG_W; t += 64) {
-                const int row = t / SEG_W, col = t - row * SEG_W;
-                const int kap = kb + row, e = e0 + col;
-                const bool ok = kap >= 0 && kap < K && e >= 0 && e < P;
-                const size_t g = (size_t)kap * P + e;
-                sA[t] = ok ? gA[g] : -RF_INF;
-                sB[t] = ok ? gB[g] : -RF_INF;
-            }
-            for (int t = tid; t < SEG_NT; t += 64) {
-                const int i = ib + t;
-                if (i >= 0 && i <= n) {
-                    const int ks = max(i - 1, 0);
-                    lean_row(sT + 6 * t, i >= 1 ? sq[i - 1] : 4, tm[ks], tm[n + ks], tm[2 * (size_t)n + ks],
-                             tm[3 * (size_t)n + i]);
-                }
-            }
+            store_seg();
             wave_sync();
+            if (D + SEG_S <= dhi)
+                load_seg(D + SEG_S);
             if (!active)
                 continue;
             const int lo = max(D, dfirst), hi = min(D + SEG_S - 1, dlast);
