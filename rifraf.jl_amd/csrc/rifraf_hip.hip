@@ -1445,19 +1445,21 @@ __device__ __forceinline__ void wg_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+#ifndef WS_NPF128
+#define WS_NPF128 20
+#endif
 #ifndef WS_NPF
 #define WS_NPF 22
 #endif
 
-template <int NPF>
-__global__ void __launch_bounds__(512)
+template <int NPF, int Q>
+__global__ void __launch_bounds__(2 * Q)
 k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
            const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
            const double *__restrict__ tabs, const double *__restrict__ bands,
            double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int Q = 256;
     const int nb = gridDim.x, b = blockIdx.x;
     const int xq = nb >> 3, xr = nb & 7, x = b & 7;
     const int item = x * xq + min(x, xr) + (b >> 3);
@@ -2254,7 +2256,8 @@ struct ScorePick {
     bool seg = false;   // k_score_seg: wide bands (window too large for LDS), finite tables
     int nw = 1;     // lean: waves per workgroup (64 * nw chain columns per work item)
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
-    int q() const { return nw == 8 ? 256 : 64 * nw; }   // chain columns per work item
+    int wsq = 256;  // ws: chain lanes per workgroup (256: 1 workgroup per CU; 128: 2)
+    int q() const { return nw == 8 ? wsq : 64 * nw; }   // chain columns per work item
 };
 
 struct DevBuf {
@@ -2486,7 +2489,7 @@ int env_int(const char *name, int dflt)
 std::string scorer_env_key()
 {
     std::string k;
-    for (const char *n : {"RIFRAF_SCORE_KERNEL", "RIFRAF_LEAN_NW", "RIFRAF_LEAN_LDS_KB"}) {
+    for (const char *n : {"RIFRAF_SCORE_KERNEL", "RIFRAF_LEAN_NW", "RIFRAF_LEAN_LDS_KB", "RIFRAF_WS_Q"}) {
         const char *v = std::getenv(n);
         k += v ? v : "-";
         k += '|';
@@ -2507,10 +2510,15 @@ ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
         // 8 = wave-specialized k_score_ws (256 chain lanes + 256 loader lanes)
         int nw = env_int("RIFRAF_LEAN_NW", 8);
         nw = nw >= 8 ? 8 : (nw >= 4 ? 4 : (nw >= 2 ? 2 : 1));
-        const int lds = std::max(env_int("RIFRAF_LEAN_LDS_KB", nw >= 4 ? 160 : 40 * nw) * 1024 / 8, need1);
+        // k_score_ws with 128 chain lanes: two workgroups (two windows in
+        // flight) per CU, each with half the LDS
+        const int wsq = (nw == 8 && env_int("RIFRAF_WS_Q", 256) == 128) ? 128 : 256;
+        const int dflt_kb = nw >= 4 ? (wsq == 128 ? 80 : 160) : 40 * nw;
+        const int lds = std::max(env_int("RIFRAF_LEAN_LDS_KB", dflt_kb) * 1024 / 8, need1);
         if (lds <= 160 * 1024 / 8) {
             p.lean = true;
             p.nw = nw;
+            p.wsq = wsq;
             p.lds = lds;
             return p;
         }
@@ -2552,8 +2560,14 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     else if (pk.nw == 8)
-        hipLaunchKernelGGL((k_score_ws<WS_NPF>), grid, dim3(512), pk.lds * 8, ctx->stream, items, groups,
-                           reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    {
+        if (pk.wsq == 128)
+            hipLaunchKernelGGL((k_score_ws<WS_NPF128, 128>), grid, dim3(256), pk.lds * 8, ctx->stream, items,
+                               groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+        else
+            hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
+                               groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    }
     else if (pk.nw == 1)
         hipLaunchKernelGGL((k_score_lean<1, LEAN_NPF>), grid, dim3(64), pk.lds * 8, ctx->stream, items,
                            groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
@@ -2603,7 +2617,9 @@ int rf_create(int device, rf_ctx **out)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_score_lean<4, LEAN_NPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF>,
+    (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF128, 128>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
