@@ -22,6 +22,7 @@ exactly the cluster that raised it.
 from __future__ import annotations
 
 import threading
+import time
 
 import numpy as np
 
@@ -80,6 +81,7 @@ class _Hub:
         self.pending = []
         self.live = 0
         self.launches = 0
+        self.engine_s = 0.0          # wall time inside batched engine calls
 
     # ---------------- id maps (local -> global) ----------------
     def seq(self, k, x):
@@ -113,7 +115,9 @@ class _Hub:
                 if self.live == 0 and not self.pending:
                     return
                 batch, self.pending = self.pending, []
+            t0 = time.perf_counter()
             self._execute(batch)
+            self.engine_s += time.perf_counter() - t0
             with self.cv:
                 for r in batch:
                     r.done = True
@@ -203,6 +207,9 @@ class _Hub:
             at += n
 
 
+STATS = {"launches": 0, "engine_s": 0.0}
+
+
 def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
     """rifraf() over many independent clusters, batched on one engine.
 
@@ -240,6 +247,8 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
         hub.serve()
         for t in threads:
             t.join()
+        STATS["launches"] += hub.launches
+        STATS["engine_s"] += hub.engine_s
         for e in errors:
             if e is not None:
                 raise e

@@ -572,17 +572,33 @@ def base_distribution(base, ilp):                                  # :804-809
 
 
 def alignment_error_probs(tlen, state: RifrafState, run: _Run):   # :817-840
+    """Per consensus position, 1 - max normalised base probability over the
+    batch alignments.  Vectorised per read; every column still receives its
+    base_distribution rows in batch order, so the sums are the loop's."""
     probs = np.zeros((tlen, 4))
     slots = np.arange(len(state.batch_seqs), dtype=np.int32)
     moves, _ = run.e.backtrace(slots)
+    memo = {}
     for mv, idx in zip(moves, state.batch_seqs):
         s = state.sequences[idx]
-        i = j = 1
-        for move in mv.tolist():
-            a, b = {1: (1, 1), 2: (1, 0), 3: (0, 1), 4: (3, 0), 5: (0, 3)}[move]
-            i, j = i + a, j + b
-            if move == TRACE_MATCH:
-                probs[j - 2, :] += base_distribution(int(s.seq[i - 2]), s.match_scores[i - 2])
+        mv = np.asarray(mv, np.int64)
+        di = np.where((mv == 1) | (mv == 2), 1, np.where(mv == 4, 3, 0))
+        dj = np.where((mv == 1) | (mv == 3), 1, np.where(mv == 5, 3, 0))
+        i = 1 + np.cumsum(di)
+        j = 1 + np.cumsum(dj)
+        match = mv == TRACE_MATCH
+        ii, jj = i[match] - 2, j[match] - 2
+        bases = s.seq[ii]
+        ilps = np.asarray(s.match_scores)[ii]
+        ulp, inv = np.unique(ilps, return_inverse=True)
+        table = np.empty((4, len(ulp), 4))
+        for u, lp in enumerate(ulp.tolist()):
+            for b in range(4):
+                d = memo.get((b, lp))
+                if d is None:
+                    d = memo[(b, lp)] = base_distribution(b, lp)
+                table[b, u] = d
+        probs[jj] += table[bases, inv.reshape(-1)]   # one row per column per read
     probs = np.power(10.0, probs)
     probs = 1.0 - (probs / probs.sum(axis=1, keepdims=True)).max(axis=1)
     return probs

@@ -13,7 +13,7 @@ REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [REPO, os.path.join(REPO, "rifraf.jl_amd"), os.path.join(REPO, "tests"), os.path.join(REPO, "oracle")]
 import numpy as np  # noqa: E402
 
-from rifraf_amd.batch import rifraf_batch  # noqa: E402
+from rifraf_amd.batch import STATS, rifraf_batch  # noqa: E402
 from rifraf_amd.model import RifrafParams, rifraf  # noqa: E402
 from rifraf_amd.sample import sample_sequences  # noqa: E402
 
@@ -46,4 +46,5 @@ if ncpu > 0:
            "cores": 1, "same_consensus_as_gpu": same}
 print(json.dumps({"workload": "c4-e2e", "clusters": nclu, "reads_per_cluster": 50, "template_len": 1500,
                   "gpu_clusters_per_s": nclu / gpu_s, "gpu_seconds": gpu_s, "stage_iterations": iters,
-                  "consensus_equals_template": ok, "setup_s": gen_s, "cpu_baseline": cpu}))
+                  "consensus_equals_template": ok,
+                  "engine_calls": STATS["launches"], "engine_s": STATS["engine_s"], "setup_s": gen_s, "cpu_baseline": cpu}))
