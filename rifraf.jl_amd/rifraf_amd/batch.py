@@ -31,11 +31,11 @@ from .proposals import to_arrays
 
 
 class _Request:
-    __slots__ = ("k", "kind", "args", "done", "result", "error")
+    __slots__ = ("k", "kind", "args", "ev", "result", "error")
 
     def __init__(self, k, kind, args):
         self.k, self.kind, self.args = k, kind, args
-        self.done = False
+        self.ev = threading.Event()      # set by the hub: only this worker wakes
         self.result = None
         self.error = None
 
@@ -101,8 +101,9 @@ class _Hub:
         req = _Request(k, kind, args)
         with self.cv:
             self.pending.append(req)
-            self.cv.notify_all()
-            self.cv.wait_for(lambda: req.done)
+            if len(self.pending) == self.live:
+                self.cv.notify()             # the hub is the only waiter on cv
+        req.ev.wait()
         if req.error is not None:
             raise req.error
         return req.result
@@ -118,10 +119,8 @@ class _Hub:
             t0 = time.perf_counter()
             self._execute(batch)
             self.engine_s += time.perf_counter() - t0
-            with self.cv:
-                for r in batch:
-                    r.done = True
-                self.cv.notify_all()
+            for r in batch:
+                r.ev.set()
 
     def _execute(self, batch):
         kinds = {}
@@ -238,7 +237,8 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
             finally:
                 with hub.cv:
                     hub.live -= 1
-                    hub.cv.notify_all()
+                    if len(hub.pending) == hub.live:
+                        hub.cv.notify()
 
         hub.live = len(part)
         threads = [threading.Thread(target=worker, args=(k, kw), daemon=True) for k, kw in enumerate(part)]
