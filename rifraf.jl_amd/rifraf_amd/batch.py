@@ -217,8 +217,10 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
     `reference`).  Returns the list of RifrafResult in input order (an
     exception raised by a cluster is re-raised after the wave finishes).
     Clusters run in waves of at most `wave` (their bands share the device)."""
+    import os
     from .model import RifrafParams, rifraf
     params = params or RifrafParams()
+    profile_dir = os.environ.get("RIFRAF_BATCH_PROFILE")
     if engine is None:
         from .align import default_engine
         engine = default_engine()
@@ -231,7 +233,13 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
 
         def worker(k, kw):
             try:
-                results[w0 + k] = rifraf(params=params, engine=ClusterEngine(hub, k), **kw)
+                if profile_dir and k == 0:       # diagnostics: host profile of one cluster thread
+                    import cProfile
+                    pr = cProfile.Profile()
+                    results[w0 + k] = pr.runcall(rifraf, params=params, engine=ClusterEngine(hub, k), **kw)
+                    pr.dump_stats(f"{profile_dir}/batch_worker0.prof")
+                else:
+                    results[w0 + k] = rifraf(params=params, engine=ClusterEngine(hub, k), **kw)
             except Exception as e:  # noqa: BLE001 -- handed back to the caller
                 errors[k] = e
             finally:

@@ -174,9 +174,8 @@ def logsumexp10(x):                            # util.jl:28-38
     u = float(np.max(x))
     if abs(u) == math.inf:
         return math.nan if np.isnan(x).any() else u
-    s = 0.0
-    for v in x:
-        s += 10.0 ** (v - u)
+    # sequential accumulation in index order (cumsum), as the reference's loop
+    s = float(np.cumsum(np.power(10.0, x - u))[-1])
     return math.log10(s) + u
 
 
@@ -536,21 +535,42 @@ def normalize_log_differences(sub_scores, del_scores, ins_scores, state_score): 
     return EstimatedProbs(pos_probs[:, :4], pos_probs[:, 4], ins_probs)
 
 
+def score_proposal_arrays(m: int, consensus):
+    """all_proposals(STAGE_SCORE, consensus, false) without seeds
+    (model.jl:401-456) as (kind, pos, base) arrays in the same order:
+    Ins(0, ACGT); then per position j: Sub(j, b != cons[j]), Del(j), Ins(j, ACGT)."""
+    cons = np.asarray(consensus, np.int64)
+    # per position: 4 sub candidates (the consensus base's is dropped), del, 4 ins
+    j9 = np.repeat(np.arange(1, m + 1), 9)
+    s9 = np.tile(np.arange(9), m)
+    keep = ~((s9 < 4) & (s9 == cons[j9 - 1]))
+    j9, s9 = j9[keep], s9[keep]
+    kind = np.where(s9 < 4, SUB, np.where(s9 == 4, DEL, INS))
+    base = np.where(s9 < 4, s9, np.where(s9 == 4, 0, s9 - 5))
+    kind = np.concatenate([np.full(4, INS), kind]).astype(np.uint8)
+    pos = np.concatenate([np.zeros(4, np.int64), j9]).astype(np.int32)
+    base = np.concatenate([np.arange(4), base]).astype(np.uint8)
+    return kind, pos, base
+
+
 def estimate_probs(state: RifrafState, run: _Run, use_ref_for_qvs: bool) -> EstimatedProbs:   # :737-791
     m = len(state.consensus)
     sub_scores = np.zeros((m, 4)) + state.score
     del_scores = np.zeros(m) + state.score
     ins_scores = np.zeros((m + 1, 4))
     use_ref_ = len(state.reference) > 0 and use_ref_for_qvs
-    props = all_proposals(Stage.SCORE, state.consensus, False)
-    scores = score_proposals(state, run, props, use_ref_)
-    for p, sc in zip(props, scores):
-        if p.kind == SUB:
-            sub_scores[p.pos - 1, p.base] = sc
-        elif p.kind == DEL:
-            del_scores[p.pos - 1] = sc
-        else:
-            ins_scores[p.pos, p.base] = sc
+    kind, pos, base = score_proposal_arrays(m, state.consensus)
+    slots = np.arange(len(state.batch_seqs), dtype=np.int32)
+    scores = run.e.score([(slots, run.REF if use_ref_ else -1, (kind, pos, base))])[0]
+    k = kind.astype(np.int64)
+    p = pos.astype(np.int64)
+    b = base.astype(np.int64)
+    sub = k == SUB
+    dele = k == DEL
+    ins = k == INS
+    sub_scores[p[sub] - 1, b[sub]] = scores[sub]
+    del_scores[p[dele] - 1] = scores[dele]
+    ins_scores[p[ins], b[ins]] = scores[ins]
     max_score = max(sub_scores.max(), del_scores.max(), ins_scores.max())
     sub_scores = sub_scores - max_score
     del_scores = del_scores - max_score

@@ -3,7 +3,10 @@
 stage logic, batch = all 50 reads, quality scores on) over many 50 x 1.5 kb
 clusters, batched on one GPU with rifraf_batch, against the same runs on the
 CPU oracle engine.  Prints one JSON line.
-usage: scripts/e2e_batch.py [CLUSTERS] [CPU_CLUSTERS]"""
+usage: scripts/e2e_batch.py [CLUSTERS] [CPU_CLUSTERS] [PROCS]
+PROCS > 1: that many worker processes, each with its own engine context on
+GPU 0 and a contiguous share of the clusters (the reference's pmap workers,
+scripts/rifraf.jl:190); the host stage machine is the per-process limit."""
 import json
 import os
 import sys
@@ -28,23 +31,49 @@ for k in range(nclu):
     templates.append(t)
 gen_s = time.perf_counter() - t0
 
-from rifraf_amd.engine import Engine  # noqa: E402
-eng = Engine(0)
-t0 = time.perf_counter()
-res = rifraf_batch(clusters, params=params, engine=eng)
-gpu_s = time.perf_counter() - t0
-ok = sum(int(np.array_equal(r.consensus, t)) for r, t in zip(res, templates))
-iters = sum(sum(r.state.stage_iterations) for r in res)
+nproc = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+
+
+def _shard(args):
+    lo, hi = args
+    from rifraf_amd.batch import STATS as st
+    from rifraf_amd.engine import Engine
+    e = Engine(0)
+    out = rifraf_batch(clusters[lo:hi], params=params, engine=e)
+    e.close()
+    return [(r.consensus, sum(r.state.stage_iterations)) for r in out], st["launches"], st["engine_s"]
+
+
+if nproc <= 1:
+    from rifraf_amd.engine import Engine  # noqa: E402
+    eng = Engine(0)
+    t0 = time.perf_counter()
+    res = rifraf_batch(clusters, params=params, engine=eng)
+    gpu_s = time.perf_counter() - t0
+    cons = [r.consensus for r in res]
+    iters = sum(sum(r.state.stage_iterations) for r in res)
+else:
+    import multiprocessing as mp
+    bounds = [k * nclu // nproc for k in range(nproc + 1)]
+    with mp.get_context("fork").Pool(nproc) as pool:      # fork before any HIP call
+        t0 = time.perf_counter()
+        parts = pool.map(_shard, list(zip(bounds[:-1], bounds[1:])))
+        gpu_s = time.perf_counter() - t0
+    cons = [c for part, _, _ in parts for c, _ in part]
+    iters = sum(i for part, _, _ in parts for _, i in part)
+    STATS["launches"] = sum(p[1] for p in parts)
+    STATS["engine_s"] = sum(p[2] for p in parts)
+ok = sum(int(np.array_equal(c, t)) for c, t in zip(cons, templates))
 cpu = None
 if ncpu > 0:
     from oracle_engine import OracleEngine
     t0 = time.perf_counter()
     cres = [rifraf(params=params, engine=OracleEngine(), **kw) for kw in clusters[:ncpu]]
     cpu_s = time.perf_counter() - t0
-    same = all(np.array_equal(a.consensus, b.consensus) for a, b in zip(cres, res[:ncpu]))
+    same = all(np.array_equal(a.consensus, b) for a, b in zip(cres, cons[:ncpu]))
     cpu = {"clusters_per_s": ncpu / cpu_s, "clusters": ncpu, "seconds": cpu_s, "kind": "port",
            "cores": 1, "same_consensus_as_gpu": same}
-print(json.dumps({"workload": "c4-e2e", "clusters": nclu, "reads_per_cluster": 50, "template_len": 1500,
+print(json.dumps({"workload": "c4-e2e", "clusters": nclu, "procs": nproc, "reads_per_cluster": 50, "template_len": 1500,
                   "gpu_clusters_per_s": nclu / gpu_s, "gpu_seconds": gpu_s, "stage_iterations": iters,
                   "consensus_equals_template": ok,
                   "engine_calls": STATS["launches"], "engine_s": STATS["engine_s"], "setup_s": gen_s, "cpu_baseline": cpu}))
