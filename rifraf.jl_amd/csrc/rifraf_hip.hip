@@ -533,10 +533,11 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 #ifndef DP_STAGGER
 #define DP_STAGGER 0   // measured: no gain (flush convoys are not the limiter)
 #endif
-// periods per block (<= 16: one edge record per lane); NP = 8 tasks take 4 so
+// periods per block (<= 16: one edge record per lane); NP = 2, 4 take 8 and NP = 8
+// takes 4 (measured: NP = 2/4 at 16 need 280/430 VGPRs -> one wave per SIMD), so
 // that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
 // several waves per CU
-__host__ __device__ constexpr int dpl_b(int np) { return np >= 8 ? 4 : DPL_BLOCK; }
+__host__ __device__ constexpr int dpl_b(int np) { return np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK); }
 struct alignas(16) EdgeRec {
     double mt, mm, is, ds;
     int sb, col, pad0, pad1;
