@@ -12,6 +12,8 @@
  *                        src/align.jl:114-141,155-179,196-202;
  *                        realign! src/model.jl:679-714
  *   rf_backtrace      <- backtrace + count_errors   src/align.jl:229-245
+ *   rf_alignment_proposals <- alignment_proposals / moves_to_proposals
+ *                        src/model.jl:458-497
  *   rf_score          <- score_proposal(m, state, newcols, use_ref) summed
  *                        over the batch, as called by get_candidates and
  *                        estimate_probs  src/model.jl:385-399,499-526,737-791
@@ -111,6 +113,16 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot,
 int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot,
                  int8_t *moves, const int64_t *moves_off,
                  int32_t *nmoves, int32_t *nerrors);
+
+/* alignment_proposals (model.jl:483-497 over moves_to_proposals :458-480)
+ * on the device: backtrace every batch slot of each group (one cluster) and
+ * mark the proposals its alignment implies -- Substitution at mismatching
+ * matches, and if do_indels, Insertion / Deletion -- in the group's dense
+ * mask out_mask[(row_g + p) * 9 + k] (0/1 bytes, slots as rf_score_dense,
+ * row_g = sum over h < g of (m_h + 1)).  The mask is the reference's Set
+ * union over the batch; position-major order is (pos, kind, base) order. */
+int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
+                           const int32_t *slots, int32_t do_indels, uint8_t *out_mask);
 
 /* Proposal scoring.  Group g (one cluster) = batch slots
  * slots[slot_off[g] .. slot_off[g+1]) in batch order, an optional

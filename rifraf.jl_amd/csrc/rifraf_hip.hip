@@ -2187,6 +2187,57 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 }
 
 // ---------------------------------------------------------------------
+// k_aln_props: alignment_proposals / moves_to_proposals (model.jl:458-497)
+// on the device.  One lane per batch read walks its forward move list (left
+// by k_backtrace) and marks every proposal the alignment implies in its
+// cluster's dense mask [(m+1) x 9] (slots as rf_score_dense: 0-3 Sub A..T,
+// 4 Del, 5-8 Ins A..T).  The mask is the reference's Set union over the
+// batch; reading it position-major gives the (pos, kind, base) order.
+// ---------------------------------------------------------------------
+struct alignas(16) PropTask {
+    int64_t sb, tb, mv, mask;   // read bases, template bases, moves, mask offset (bytes)
+    int32_t n, m, idx, pad;
+};
+
+__global__ void k_aln_props(const PropTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
+                            const int8_t *__restrict__ moves, const int32_t *__restrict__ nmoves,
+                            uint8_t *__restrict__ mask, int do_indels)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ntasks)
+        return;
+    const PropTask T = tasks[k];
+    const uint8_t *s = bases + T.sb;
+    const uint8_t *t = bases + T.tb;
+    const int8_t *mv = moves + T.mv;
+    uint8_t *out = mask + T.mask;
+    const int cnt = nmoves[T.idx];
+    int i = 0, j = 0;
+    for (int e = 0; e < cnt; ++e) {
+        switch (mv[e]) {
+        case 1:   // TRACE_MATCH: Substitution(j, s[i]) where the bases differ
+            ++i;
+            ++j;
+            if (s[i - 1] != t[j - 1])
+                out[(size_t)j * 9 + s[i - 1]] = 1;
+            break;
+        case 2:   // TRACE_INSERT: Insertion(j, s[i])
+            ++i;
+            if (do_indels)
+                out[(size_t)j * 9 + 5 + s[i - 1]] = 1;
+            break;
+        case 3:   // TRACE_DELETE: Deletion(j)
+            ++j;
+            if (do_indels)
+                out[(size_t)j * 9 + 4] = 1;
+            break;
+        case 4: i += 3; break;   // codon moves propose nothing (model.jl:469-476)
+        default: j += 3; break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------
 // k_scatter: one staged upload -> per-object device regions (a block per
 // segment), so a batch upload is one H2D copy instead of one per object.
 // ---------------------------------------------------------------------
@@ -3118,6 +3169,56 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
         if (moves)
             std::memcpy(moves + moves_off[k], all.data() + offs[k], cnt[k]);
     }
+    return 0;
+}
+
+int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                           int32_t do_indels, uint8_t *out_mask)
+{
+    if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !out_mask)))
+        return fail(ctx, RF_ERR_ARG, "rf_alignment_proposals: bad arguments");
+    const int32_t nslots = ngroups > 0 ? slot_off[ngroups] : 0;
+    // 1. device backtraces of every batch slot (moves stay in scratch[3],
+    //    counts in scratch[4]; offsets = prefix sums of n + m, as rf_backtrace)
+    if (int e = rf_backtrace(ctx, nslots, slots, nullptr, nullptr, nullptr, nullptr))
+        return e;
+    std::vector<PropTask> tasks(nslots);
+    int64_t mv_at = 0, mask_total = 0;
+    for (int32_t g = 0; g < ngroups; ++g) {
+        int32_t tpl = -1, m = 0;
+        for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
+            const Band &b = ctx->slots[slots[k]].a;
+            if (tpl >= 0 && b.tpl != tpl)
+                return fail(ctx, RF_ERR_ARG, "rf_alignment_proposals: batch slots use different templates");
+            tpl = b.tpl;
+            m = b.m;
+            PropTask &t = tasks[k];
+            t.sb = ctx->seqs[b.seq].bases.off;
+            t.tb = ctx->tpls[b.tpl].bases.off;
+            t.mv = mv_at;
+            t.mask = mask_total;
+            t.n = b.n;
+            t.m = b.m;
+            t.idx = k;
+            mv_at += b.n + b.m;
+        }
+        if (slot_off[g + 1] > slot_off[g])
+            mask_total += (int64_t)(m + 1) * 9;
+    }
+    if (nslots == 0)
+        return 0;
+    if (int e = upload(ctx, ctx->scratch[1], tasks))
+        return e;
+    if (int e = ensure_buf(ctx, ctx->scratch[2], std::max<int64_t>(mask_total, 16)))
+        return e;
+    HIPCHK(ctx, hipMemsetAsync(ctx->scratch[2].p, 0, mask_total, ctx->stream));
+    hipLaunchKernelGGL(k_aln_props, dim3((nslots + 63) / 64), dim3(64), 0, ctx->stream,
+                       (const PropTask *)ctx->scratch[1].p, nslots, (const uint8_t *)ctx->bytes_arena.d,
+                       (const int8_t *)ctx->scratch[3].p, (const int32_t *)ctx->scratch[4].p,
+                       (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
 

@@ -34,6 +34,7 @@ _SIGNATURES = {
     "rf_backtrace": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_score": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p]),
+    "rf_alignment_proposals": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p]),
     "rf_score_dense": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "rf_score_dense_dev": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "rf_slot_geometry": (c_int, [c_void_p, c_int32, c_int32, POINTER(c_int32), POINTER(c_int32),

@@ -62,6 +62,9 @@ class ClusterEngine:
     def score(self, groups, per_seq=False):
         return self.hub.call(self.k, "score", groups, per_seq)
 
+    def alignment_proposals(self, groups, do_indels):
+        return self.hub.call(self.k, "aln_props", groups, do_indels)
+
     def geometry(self, slot, which=0):
         return self.hub.call(self.k, "geometry", slot, which)
 
@@ -126,10 +129,11 @@ class _Hub:
         kinds = {}
         for r in batch:
             key = (r.kind, r.args[4]) if r.kind == "realign" else (
-                (r.kind, bool(r.args[1])) if r.kind in ("backtrace", "score") else (r.kind, id(r)))
+                (r.kind, bool(r.args[1])) if r.kind in ("backtrace", "score", "aln_props") else (r.kind, id(r)))
             kinds.setdefault(key, []).append(r)
         for (kind, _), reqs in kinds.items():
-            fn = {"realign": self._realign, "backtrace": self._backtrace, "score": self._score}.get(kind)
+            fn = {"realign": self._realign, "backtrace": self._backtrace, "score": self._score,
+                  "aln_props": self._aln_props}.get(kind)
             if fn is not None and len(reqs) > 1:
                 try:
                     fn(reqs)
@@ -186,6 +190,17 @@ class _Hub:
         for r, s in zip(reqs, sl):
             n = len(s)
             r.result = (moves[at:at + n] if want else None, nerr[at:at + n].copy())
+            at += n
+
+    def _aln_props(self, reqs):
+        groups, cnt = [], []
+        for r in reqs:
+            cnt.append(len(r.args[0]))
+            groups += [self.seq(r.k, np.asarray(sl, np.int32)) for sl in r.args[0]]
+        res = self.e.alignment_proposals(groups, bool(reqs[0].args[1]))
+        at = 0
+        for r, n in zip(reqs, cnt):
+            r.result = res[at:at + n]
             at += n
 
     def _score(self, reqs):

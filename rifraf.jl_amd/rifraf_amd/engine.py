@@ -132,6 +132,24 @@ class Engine:
         self._check(self.lib.rf_backtrace(self.ctx, n, ptr(slots), None, None, ptr(nmoves), ptr(nerr)))
         return None, nerr[:n].copy()
 
+    def alignment_proposals(self, groups, do_indels: bool):
+        """rf_alignment_proposals: per group (batch slots of one cluster) the
+        (m+1, 9) 0/1 mask of the proposals its alignments imply."""
+        G = len(groups)
+        slot_off = np.zeros(G + 1, np.int32)
+        for g, sl in enumerate(groups):
+            slot_off[g + 1] = slot_off[g] + len(sl)
+        slots = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in groups]), np.int32)
+        rows = [self.geometry(int(sl[0]), RF_BAND_A)[1] for sl in groups]
+        out = np.zeros(max(int(sum(rows)) * 9, 1), np.uint8)
+        self._check(self.lib.rf_alignment_proposals(self.ctx, G, ptr(slot_off), ptr(slots), int(bool(do_indels)),
+                                                    ptr(out)))
+        res, at = [], 0
+        for r in rows:
+            res.append(out[at * 9:(at + r) * 9].reshape(r, 9))
+            at += r
+        return res
+
     def score(self, groups, per_seq: bool = False):
         """Score proposals.  groups: list of (batch_slots, ref_slot, proposals)
         with ref_slot = -1 for none.  Returns a list of total arrays (and of

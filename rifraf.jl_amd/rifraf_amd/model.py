@@ -317,8 +317,11 @@ def all_proposals(stage: Stage, consensus, indel_correction_only: bool, indel_se
 def alignment_proposals(state: RifrafState, run: _Run, do_indels: bool):   # :483-497
     """Union of the proposals seen in the batch alignments.  The reference
     collects a Julia Set (hash order); this mirror returns them sorted by
-    (pos, kind, base), a documented deterministic order."""
+    (pos, kind, base), a documented deterministic order.  Engines with a
+    device-side union (rf_alignment_proposals) return it as a dense mask."""
     slots = np.arange(len(state.batch_seqs), dtype=np.int32)
+    if hasattr(run.e, "alignment_proposals"):
+        return mask_to_proposals(run.e.alignment_proposals([slots], do_indels)[0])
     moves, _ = run.e.backtrace(slots)
     cons = state.consensus
     found = set()
@@ -329,6 +332,21 @@ def alignment_proposals(state: RifrafState, run: _Run, do_indels: bool):   # :48
             k, p, b = k[keep], p[keep], b[keep]
         found.update(zip(k.tolist(), p.tolist(), b.tolist()))
     return [Proposal(k, p, b) for (k, p, b) in sorted(found, key=lambda t: (t[1], t[0], t[2]))]
+
+
+# dense slot -> (kind, base) in (kind, base) order within a position: Sub A..T, Ins A..T, Del
+_MASK_ORDER = [(0, SUB, 0), (1, SUB, 1), (2, SUB, 2), (3, SUB, 3),
+               (5, INS, 0), (6, INS, 1), (7, INS, 2), (8, INS, 3), (4, DEL, 0)]
+
+
+def mask_to_proposals(mask):
+    """(m+1, 9) proposal mask -> Proposal list sorted by (pos, kind, base)."""
+    mask = np.asarray(mask)
+    order = np.array([c for c, _, _ in _MASK_ORDER])
+    kinds = np.array([k for _, k, _ in _MASK_ORDER])
+    bases = np.array([b for _, _, b in _MASK_ORDER])
+    pos, col = np.nonzero(mask[:, order])
+    return [Proposal(int(kinds[c]), int(p), int(bases[c])) for p, c in zip(pos.tolist(), col.tolist())]
 
 
 def _align_ref_moves(state: RifrafState, run: _Run, skew: bool):

@@ -172,6 +172,27 @@ class ShardedEngine:
                     moves[i] = m[k]
         return moves, nerr
 
+    def alignment_proposals(self, groups, do_indels: bool):
+        """Per-rank masks of the owned batch slots, OR-ed over the ranks (the
+        union is order-free, so the result equals one GPU's)."""
+        err, masks = None, {}
+        local = [(g, np.asarray(sl, np.int32)[self.owned(sl)]) for g, sl in enumerate(groups)]
+        local = [(g, s) for g, s in local if len(s)]
+        if local:
+            try:
+                res = self.e.alignment_proposals([s for _, s in local], do_indels)
+                masks = {g: m for (g, _), m in zip(local, res)}
+            except RifrafError as e:
+                err = str(e)
+        parts = self._gather((err, masks))
+        out = [None] * len(groups)
+        for e, ms in parts:
+            if e is not None:
+                raise RifrafError(e)
+            for g, m in ms.items():
+                out[g] = m.copy() if out[g] is None else (out[g] | m)
+        return out
+
     def geometry(self, slot: int, which: int = RF_BAND_A):
         src = self.owner(slot)
         obj = [self.e.geometry(slot, which) if self.rank == src else None]

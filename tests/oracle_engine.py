@@ -138,3 +138,22 @@ class OracleEngine:
             tot, _ = oracle.cpu_pass(sb[0][1], [s for s, _ in sb], nthreads=2)
             res.append(tot)
         return res if to_host else None
+
+    def alignment_proposals(self, groups, do_indels):
+        """rf_alignment_proposals on the oracle: dense (m+1, 9) masks."""
+        from rifraf_amd.align import moves_to_proposals_np
+        out = []
+        for sl in groups:
+            moves, _ = self.backtrace(sl)
+            m = self.slots[int(sl[0])]["A"][4]
+            mask = np.zeros((m + 1, 9), np.uint8)
+            for s, mv in zip(sl, moves):
+                key = self.slots[int(s)]["A"][2]
+                k, p, b = moves_to_proposals_np(mv, self.tpls[key[1]][0], self.seqs[key[0]].seq)
+                if not do_indels:
+                    keep = k == 0
+                    k, p, b = k[keep], p[keep], b[keep]
+                col = np.where(k == 0, b, np.where(k == 2, 4, 5 + b))
+                mask[p, col] = 1
+            out.append(mask)
+        return out

@@ -502,3 +502,38 @@ def test_score_wide_bands(engine, monkeypatch, mode, kern):
         for j in range(1, len(t) + 1):
             mask[j, t[j - 1]] = False
         np.testing.assert_array_equal(got[c][mask], ref_tot[mask], err_msg=f"cluster {c}")
+
+
+@pytest.mark.parametrize("do_indels", [True, False])
+def test_alignment_proposals_device(engine, do_indels):
+    """rf_alignment_proposals (device moves_to_proposals + Set union) equals the
+    host union of moves_to_proposals over the oracle's backtraces."""
+    from rifraf_amd.align import moves_to_proposals_np
+    rng = np.random.default_rng(55 + do_indels)
+    templates, seqs = [], []
+    for c in range(4):
+        t = random_seq(int(rng.integers(60, 160)), rng)
+        templates.append(t)
+        seqs.append([make_read(t, rng, 0.06, 9) for _ in range(int(rng.integers(1, 7)))])
+    flat = [r for rs in seqs for r in rs]
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), tpl, [9] * n, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in seqs:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    masks = engine.alignment_proposals(groups, do_indels)
+    for c, t in enumerate(templates):
+        exp = np.zeros((len(t) + 1, 9), np.uint8)
+        for s in seqs[c]:
+            _, mv = oracle.forward(t, s, moves=True)
+            moves = oracle.backtrace(mv, len(s) + 1, len(t) + 1, 9)
+            k, p, b = moves_to_proposals_np(moves, t, s.seq)
+            if not do_indels:
+                keep = k == 0
+                k, p, b = k[keep], p[keep], b[keep]
+            exp[p, np.where(k == 0, b, np.where(k == 2, 4, 5 + b))] = 1
+        np.testing.assert_array_equal(masks[c], exp, err_msg=f"cluster {c}")
