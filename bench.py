@@ -182,22 +182,30 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    dist = torch = None
+    dist = torch = coll = None
+    gpu = local
     if world > 1:
         # torch only for the process group (RCCL over xGMI / gloo): the engine
         # calls are synchronous on their own HIP stream
         import torch
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = args.backend
+        if backend == "auto":
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        ndev = torch.cuda.device_count()
+        gpu = local % ndev if ndev else local      # gloo rehearsals: several ranks per GPU
         if backend == "nccl":
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
+        coll = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
 
     if args.config == "c5":
-        return run_read_sharded(args, rank, world, local, dist, torch)
+        return run_read_sharded(args, rank, world, gpu, dist, torch, coll)
     nclu, nreads, length, err, bw, label = CONFIGS[args.config]
     if args.clusters is not None:
         nclu = args.clusters
@@ -206,7 +214,7 @@ def main():
     gen_s = time.perf_counter() - t_gen
 
     from rifraf_amd.engine import RF_BWD, RF_FWD, Engine
-    eng = Engine(local)
+    eng = Engine(gpu)
     reads = [r for _, rs in clusters for r in rs]
     tpl_of = np.concatenate([[c] * len(rs) for c, (_, rs) in enumerate(clusters)]).astype(np.int32)
     nr = len(reads)
@@ -260,8 +268,7 @@ def main():
     # per-step units of this rank; the timed region ran args.steps steps
     tot_cells, tot_props, tot_pairs = cells * args.steps, nprops * args.steps, npairs * args.steps
     if dist is not None:
-        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        elapsed, (tot_cells, tot_props, tot_pairs) = aggregate(elapsed, [tot_cells, tot_props, tot_pairs], dev)
+        elapsed, (tot_cells, tot_props, tot_pairs) = aggregate(elapsed, [tot_cells, tot_props, tot_pairs], coll)
 
     # attainable streaming-read bandwidth over the same band arena (diagnostic)
     probe_ms = eng.probe_stream(band_bytes, 3)
@@ -324,7 +331,7 @@ def main():
         dist.destroy_process_group()
 
 
-def run_read_sharded(args, rank, world, local, dist, torch):
+def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     """configs[4]: ONE cluster whose reads are split over the ranks.  Setup
     (untimed): each rank simulates and uploads its block of reads and runs the
     band-doubling first realign (smart_forward_moves!, model.jl:643-672).
@@ -369,8 +376,7 @@ def run_read_sharded(args, rank, world, local, dist, torch):
     score_bytes = 8 * cells + sum(33 * (len(r) + 1) for r in reads) + 72 * (length + 1)
     partial = None
     if world > 1:
-        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        partial = torch.zeros((length + 1) * 9, dtype=torch.float64, device=dev)
+        partial = torch.zeros((length + 1) * 9, dtype=torch.float64, device=coll)
 
     def step():
         eng.realign(slots, slots, 0, bws, RF_FWD | RF_BWD)
@@ -405,8 +411,7 @@ def run_read_sharded(args, rank, world, local, dist, torch):
     doubled = int(np.sum(bws > bw))
     units = [cells * args.steps, nloc * nprops * args.steps, doubled, nloc]
     if dist is not None:
-        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        elapsed, units = aggregate(elapsed, units, dev)
+        elapsed, units = aggregate(elapsed, units, coll)
     tot_cells, tot_pairs, tot_doubled, tot_reads = units
     dp_ms = float(np.mean([r[0] for r in rec]))
     sc_ms = float(np.mean([r[1] for r in rec]))
