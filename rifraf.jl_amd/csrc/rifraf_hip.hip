@@ -1763,26 +1763,47 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
             if (!active)
                 continue;
             const int lo = max(D, dfirst), hi = min(D + SEG_S - 1, dlast);
-            for (int d = lo; d <= hi; ++d) {
+            // software-pipelined: row d+1's LDS operands are read while row d
+            // is scored; A(d-1, a) of row d+1 is row d's A(d, a)
+            auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
                 const int kr = d + 2 * a - kb;                       // staged row of (d, a)
                 const int ec = (d >> 1) - e0, ep = ((d - 1) >> 1) - e0;
-                const int i = a - c + d;
-                const double ac = sA[kr * SEG_W + ec];
-                const double bI = sB[kr * SEG_W + ec];
-                const double aprev = (d >= 1 && i >= 1) ? sA[(kr - 1) * SEG_W + ep] : -RF_INF;
-                const double bS = (hasS ? sB[(kr + 1) * SEG_W + ep] : bI) + smask;
-                const double2 *rec = (const double2 *)(sT + 6 * (i - ib));
-                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
-                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-                const double dl = ac + u2.y;
+                ac = sA[kr * SEG_W + ec];
+                bI = sB[kr * SEG_W + ec];
+                bS = (hasS ? sB[(kr + 1) * SEG_W + ep] : bI) + smask;
+                const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
+                u0 = rec[0];
+                u1 = rec[1];
+                u2 = rec[2];
+            };
+            if (lo <= hi) {
+                double ac, bI, bS;
+                double2 u0, u1, u2;
+                ld(lo, ac, bI, bS, u0, u1, u2);
+                double aprev = (lo >= 1 && a - c + lo >= 1)
+                                   ? sA[(lo - 1 + 2 * a - kb) * SEG_W + ((lo - 1) >> 1) - e0] : -RF_INF;
+                for (int d = lo; d <= hi; ++d) {
+                    double acn, bIn, bSn;
+                    double2 v0, v1, v2;
+                    ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
+                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+                    const double dl = ac + u2.y;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
-                    prev[k] = best;
-                    accI[k] = vmax(accI[k], best + bI);
-                    accS[k] = vmax(accS[k], best + bS);
+                    for (int k = 0; k < 4; ++k) {
+                        const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
+                        prev[k] = best;
+                        accI[k] = vmax(accI[k], best + bI);
+                        accS[k] = vmax(accS[k], best + bS);
+                    }
+                    dd = vmax(dd, ac + bS);
+                    aprev = ac;
+                    ac = acn;
+                    bI = bIn;
+                    bS = bSn;
+                    u0 = v0;
+                    u1 = v1;
+                    u2 = v2;
                 }
-                dd = vmax(dd, ac + bS);
             }
             const int dp = dlast + 1;
             if (peel && dp >= D && dp < D + SEG_S) {
