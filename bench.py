@@ -68,7 +68,7 @@ def band_cells(n: int, m: int, bw: int) -> int:
 def band_bytes(n: int, m: int, bw: int) -> int:
     """Device bytes of one kappa-major band (rifraf_hip.hip band_K x band_P, 256-B aligned)."""
     H = 2 * bw + abs(n - m) + 1
-    P = (H + 1) >> 1
+    P = ((H + 1) >> 1) | 1
     return ((H + 2 * m) * P * 8 + 255) // 256 * 256
 
 

@@ -42,9 +42,9 @@
 //                          (bandedarrays.jl:109-114), c = h_off + bw
 //   kappa = d + 2*jj       anti-diagonal of cell (ii, jj)
 //   element (d, jj) lives at band[kappa * P + (d >> 1)],
-//   P = ceil(H/2) (no padding: an odd stride for LDS banks cost 4-16 % more
-//   band bytes at c4's H = 19-27; measured net -3.5 % step time), kappa in
-//   [0, K), K = H + 2m.
+//   P = ceil(H/2) | 1 (odd row stride: the scorer's lanes read LDS at stride
+//   2P; an even P measured 3 % slower scoring with no DP gain in a same-box
+//   A/B, despite 4-16 % fewer band bytes), kappa in [0, K), K = H + 2m.
 //
 // A kappa row holds one anti-diagonal (all band rows d of one parity), so the
 // DP fill stores every step as one contiguous run, and a window of columns
@@ -62,7 +62,7 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 #define DP_STORE(p, v) (*(p) = (v))
 #endif
 
-__host__ __device__ inline int band_P(int H) { return (H + 1) >> 1; }
+__host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
 __host__ __device__ inline int64_t band_K(int H, int m) { return (int64_t)H + 2 * (int64_t)m; }
 
 __device__ __forceinline__ size_t bidx(int d, int jj, int P)
