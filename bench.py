@@ -310,6 +310,11 @@ def main():
         "dp_ms": dp_ms,
         "score_ms": sc_ms,
         "dp_gcups_kernel": cells / (dp_ms * 1e-3) / 1e9,
+        # north_star: the DP fill against the FP64 VALU peak (5 non-FMA FP64
+        # ops per cell: 3 adds + 2 max; peak = 78.6 TF FMA / 2 = 39.3 T ops/s)
+        "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
+                    "peak_tops": FP64_VEC_TFLOPS / 2,
+                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2)},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": byt, "launch_ms": ms},
@@ -441,6 +446,11 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         "score_ms": sc_ms,
         "exchange_ms": xch_ms,
         "dp_gcups_kernel": cells / (dp_ms * 1e-3) / 1e9,
+        # north_star: the DP fill against the FP64 VALU peak (5 non-FMA FP64
+        # ops per cell: 3 adds + 2 max; peak = 78.6 TF FMA / 2 = 39.3 T ops/s)
+        "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
+                    "peak_tops": FP64_VEC_TFLOPS / 2,
+                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2)},
         "band_doubling": {"reads_doubled": tot_doubled, "reads": tot_reads,
                           "first_pass_cells_rank0": cells_first, "setup_s_rank0": dbl_s},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
