@@ -2587,6 +2587,7 @@ ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
         nw = nw >= 8 ? 8 : (nw >= 4 ? 4 : (nw >= 2 ? 2 : 1));
         // k_score_ws with 128 chain lanes: two workgroups (two windows in
         // flight) per CU, each with half the LDS
+        // (measured at c4: 128 -> +14 %, 320 / 384 chain lanes -> +50 % scoring time)
         const int wsq = (nw == 8 && env_int("RIFRAF_WS_Q", 256) == 128) ? 128 : 256;
         const int dflt_kb = nw >= 4 ? (wsq == 128 ? 80 : 160) : 40 * nw;
         const int lds = std::max(env_int("RIFRAF_LEAN_LDS_KB", dflt_kb) * 1024 / 8, need1);

@@ -367,8 +367,8 @@ SCORER_CONFIGS = [
     (None, "8", None),
     (None, "8", "40"),
     (None, "8", "60"),
-    (None, "8", "128q"),   # k_score_ws with 128 chain lanes (RIFRAF_WS_Q=128), 80 KB LDS
-    (None, "8", "40q"),    # ... with windows beyond the budget: sub-passes
+    (None, "8", "q128"),     # k_score_ws with 128 chain lanes (RIFRAF_WS_Q=128), 80 KB LDS
+    (None, "8", "q128l40"),  # ... with windows beyond the budget: sub-passes
 ]
 
 
@@ -378,8 +378,9 @@ def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
     """Both dense scorers (general and lean chain-per-column) over ragged
     clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the oracle."""
     wsq = None
-    if lds is not None and lds.endswith("q"):
-        wsq, lds = "128", (None if lds == "128q" else lds[:-1])
+    if lds is not None and lds.startswith("q"):
+        parts = lds[1:].split("l")
+        wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
     for k, v in (("RIFRAF_SCORE_KERNEL", kern), ("RIFRAF_LEAN_NW", nw), ("RIFRAF_LEAN_LDS_KB", lds),
                  ("RIFRAF_WS_Q", wsq)):
         if v is None:
