@@ -1,0 +1,105 @@
+"""Committed golden fixtures (tests/golden/pairs.npz, config2.json; made by
+scripts/make_golden.py from the KAT-pinned oracle).
+
+CPU: the oracle still reproduces them (guards the checker against drift).
+GPU: the HIP engine reproduces them bit for bit -- bands, A[end,end],
+backtrace moves and error counts, every STAGE_SCORE proposal total, and
+whole rifraf() runs (consensus, score)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from _util import REF_SCORES, SEQ_SCORES, inband_mask
+from rifraf_amd import RifrafSequence, dna_str
+from rifraf_amd.engine import RF_BAND_A, RF_BAND_B, RF_BWD, RF_FWD
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _pairs():
+    z = np.load(os.path.join(G, "pairs.npz"))
+    out = []
+    for k in range(int(z["npairs"])):
+        g = {key: z[f"p{k}_{key}"] for key in ("template", "read", "lp", "bw", "codon", "A", "B", "score",
+                                               "moves", "nerr", "kind", "pos", "base", "totals")}
+        codon = bool(g["codon"])
+        g["seq"] = RifrafSequence(g["read"], g["lp"], int(g["bw"]), REF_SCORES if codon else SEQ_SCORES)
+        out.append(g)
+    return out
+
+
+PAIRS = _pairs()
+
+
+def _inband(data, n, m, bw):
+    return np.asarray(data).T[inband_mask(n + 1, m + 1, bw).T]
+
+
+@pytest.mark.parametrize("k", range(len(PAIRS)))
+def test_oracle_reproduces_pairs(k):
+    g = PAIRS[k]
+    t, s, bw = g["template"], g["seq"], int(g["bw"])
+    A, mv = oracle.forward(t, s, moves=True)
+    B = oracle.backward(t, s)
+    n, m = len(s), len(t)
+    np.testing.assert_array_equal(_inband(A, n, m, bw), g["A"])
+    np.testing.assert_array_equal(_inband(B, n, m, bw), g["B"])
+    moves = oracle.backtrace(mv, n + 1, m + 1, bw)
+    np.testing.assert_array_equal(moves, g["moves"])
+    assert oracle.count_errors(moves, t, s.seq) == int(g["nerr"])
+    for i in range(0, len(g["totals"]), 11):
+        assert 0.0 + oracle.score_proposal(int(g["kind"][i]), int(g["pos"][i]), int(g["base"][i]),
+                                           A, B, t, s) == g["totals"][i]
+
+
+def test_oracle_engine_reproduces_config2():
+    from oracle_engine import OracleEngine
+    _check_config2(OracleEngine())
+
+
+def _check_config2(engine):
+    from rifraf_amd.model import RifrafParams, rifraf
+    from rifraf_amd.sample import sample_sequences
+    runs = json.load(open(os.path.join(G, "config2.json")))["runs"]
+    for r in runs:
+        rng = np.random.default_rng(r["seed"])
+        _, t, _, reads, _, phreds, _, _ = sample_sequences(r["nreads"], r["length"], error_rate=r["error_rate"],
+                                                           rng=rng)
+        assert dna_str(t) == r["template"]
+        res = rifraf(reads, phreds, params=RifrafParams(), engine=engine)
+        assert dna_str(res.consensus) == r["consensus"]
+        assert res.state.score.hex() == r["score"]
+        assert list(res.state.stage_iterations) == r["stage_iterations"]
+
+
+@pytest.mark.gpu
+def test_engine_reproduces_pairs(engine):
+    seqs = [g["seq"] for g in PAIRS]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [g["template"] for g in PAIRS])
+    n = len(PAIRS)
+    bws = [int(g["bw"]) for g in PAIRS]
+    scores = engine.realign(np.arange(n), np.arange(n), np.arange(n), bws, RF_FWD | RF_BWD)
+    moves, nerr = engine.backtrace(np.arange(n))
+    for k, g in enumerate(PAIRS):
+        nr, m, bw = len(g["seq"]), len(g["template"]), bws[k]
+        A = engine.download_band(k, RF_BAND_A)
+        B = engine.download_band(k, RF_BAND_B)
+        np.testing.assert_array_equal(_inband(A.data, nr, m, bw), g["A"], err_msg=f"pair {k}")
+        np.testing.assert_array_equal(_inband(B.data, nr, m, bw), g["B"], err_msg=f"pair {k}")
+        assert scores[k] == g["score"]
+        np.testing.assert_array_equal(moves[k], g["moves"])
+        assert nerr[k] == int(g["nerr"])
+        if len(g["totals"]):
+            props = (g["kind"], g["pos"], g["base"])
+            group = ([], k, props) if bool(g["codon"]) else ([k], -1, props)
+            got = engine.score([group])[0]
+            np.testing.assert_array_equal(got, g["totals"], err_msg=f"pair {k}")
+
+
+@pytest.mark.gpu
+def test_engine_reproduces_config2(engine):
+    _check_config2(engine)
