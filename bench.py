@@ -172,6 +172,20 @@ def aggregate(elapsed: float, units, device="cpu"):
     return float(t.item()), [float(x) for x in c.tolist()]
 
 
+def pmc_traffic(config, size, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_<config>.json, scripts/pmc_summary.py), when it was taken at
+    the same size (clusters for c4, reads per rank for c5); else None."""
+    pmc_file = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    try:
+        pm = json.load(open(pmc_file))
+        if pm.get("clusters") == size and kernel in pm.get("kernels", {}):
+            return pm["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -280,15 +294,7 @@ def main():
     sc_gbs = score_bytes / (sc_ms * 1e-3) / 1e9
     dominant = "k_score" if sc_ms >= dp_ms else "k_dp"
     ach, byt, ms = (sc_gbs, score_bytes, sc_ms) if dominant == "k_score" else (dp_gbs, dp_bytes, dp_ms)
-    traffic = None
-    pmc_file = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_file):
-        try:
-            pm = json.load(open(pmc_file))
-            if pm.get("clusters") == nclu and dominant in pm.get("kernels", {}):
-                traffic = pm["kernels"][dominant]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(args.config, nclu, dominant)
     result = {
         "metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
         "value": tot_cells / elapsed / 1e9,
@@ -454,7 +460,8 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         "band_doubling": {"reads_doubled": tot_doubled, "reads": tot_reads,
                           "first_pass_cells_rank0": cells_first, "setup_s_rank0": dbl_s},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("c5", len(reads), dominant),
                      "algorithmic_bytes": byt, "launch_ms": ms},
         "roofline_other": {"k_dp": {"achieved": dp_gbs, "frac": dp_gbs / HBM_PEAK_GBS, "bytes": dp_bytes,
                                     "ms": dp_ms},

@@ -1635,24 +1635,40 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 // independent of H, unlike the full kappa-row window (2L + H) x H/2 -- and
 // each band element is loaded about once per work item.
 // ---------------------------------------------------------------------
+// Fetch efficiency: a kappa row is P doubles at an arbitrary 8-B alignment,
+// so a segment's SEG_S/2 + 1 doubles of it span 1-2 128-B lines, and the
+// neighbouring segments of one row are too far apart in time to hit in L2:
+// HBM bytes are ~3x the useful bytes at SEG_S = 16, ~2.3x at 24, ~2x at 32.
+// Measured at c5 (PMC FETCH_SIZE, one GPU): S = 16 48.9 ms (328 GB),
+// S = 24 45.7 ms (264 GB), S = 32 62.2 ms (214 GB: 48 KB of LDS and 256
+// VGPRs with spills leave 3 workgroups per CU, latency-bound).  Default 24.
 constexpr int SEG_L = 64;                       // lanes (columns) per work item
-constexpr int SEG_S = 16;                       // diagonals per segment
-constexpr int SEG_W = SEG_S / 2 + 1;            // staged doubles per kappa row (odd)
-constexpr int SEG_NR = SEG_S + 2 * SEG_L;       // staged kappa rows per band
-constexpr int SEG_NT = SEG_S + SEG_L + 1;       // staged table rows
 
+template <int SEG_S>
 __global__ void __launch_bounds__(64)
 k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
             const double *__restrict__ tabs, const double *__restrict__ bands,
             double *__restrict__ dense, double *__restrict__ split, int split_mode)
 {
+    constexpr int SEG_W = SEG_S / 2 + 1;            // staged doubles per kappa row (odd)
+    constexpr int SEG_NR = SEG_S + 2 * SEG_L;       // staged kappa rows per band
+    constexpr int SEG_NT = SEG_S + SEG_L + 1;       // staged table rows
     __shared__ double sA[SEG_NR * SEG_W];
     __shared__ double sB[SEG_NR * SEG_W];
     __shared__ __attribute__((aligned(16))) double sT[SEG_NT * 6];
-    const int nb = gridDim.x, bx = blockIdx.x;
-    const int xq = nb >> 3, xr = nb & 7, x = bx & 7;
-    const WorkItem wi = items[x * xq + min(x, xr) + (bx >> 3)];   // XCD-aware, as k_score_ws
+    // XCD-aware over the whole (item, read) grid: workgroups are dealt
+    // round-robin to the 8 XCDs in linear order, so linear id `lin` runs on XCD
+    // lin & 7; give each XCD a contiguous run of (item-fastest) grid cells, so
+    // the neighbouring items of one read, which share S kappa rows per segment,
+    // run at the same time under the same L2 (in split mode the grid is
+    // items x reads and gridDim.x is rarely a multiple of 8)
+    const int nx = gridDim.x;
+    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
+    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
+    const int cell = x * xq + min(x, xr) + (lin >> 3);
+    const int bx = cell % nx, by = cell / nx;
+    const WorkItem wi = items[bx];
     const ScoreGroup G = groups[wi.group];
     const int m = G.m;
     const int a0 = wi.p0;
@@ -1661,7 +1677,7 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
     const bool active = a <= m;
     int r0 = G.r0, r1 = G.r1;
     if (split_mode & 1) {
-        r0 = G.r0 + blockIdx.y;
+        r0 = G.r0 + by;
         if (r0 >= G.r1)
             return;
         r1 = r0 + 1;
@@ -1836,7 +1852,7 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
     if (!active)
         return;
     const double qnan = __builtin_nan("");
-    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
+    double *base = (split_mode & 1) ? split + G.split_off + (size_t)by * (m + 1) * 9
                                     : dense + G.dense_off;
     double *dst = base + (size_t)a * 9;
 #pragma unroll
@@ -2629,9 +2645,19 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     // window but skips the chains (measures its load pipeline alone)
     const int sm = (split ? 1 : 0) | (env_int("RIFRAF_LEAN_NOCOMP", 0) ? 2 : 0);
     dim3 grid(nitems, gy);
-    if (pk.seg)
-        hipLaunchKernelGGL(k_score_seg, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
-                           d_bands, dense, split, sm);
+    if (pk.seg) {
+        // RIFRAF_SEG_S: diagonals per segment (16, 24 or 32)
+        const int segs = env_int("RIFRAF_SEG_S", 24);
+        if (segs == 16)
+            hipLaunchKernelGGL(k_score_seg<16>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm);
+        else if (segs == 24)
+            hipLaunchKernelGGL(k_score_seg<24>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm);
+        else
+            hipLaunchKernelGGL(k_score_seg<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm);
+    }
     else if (!pk.lean)
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);

@@ -358,6 +358,7 @@ SCORER_CONFIGS = [
     # (RIFRAF_SCORE_KERNEL, RIFRAF_LEAN_NW, RIFRAF_LEAN_LDS_KB)
     ("general", None, None),
     ("seg", None, None),       # row-segment scorer (wide bands) on every shape
+    ("seg16", None, None),     # ... with 16-diagonal segments (RIFRAF_SEG_S=16)
     (None, "1", None),
     (None, "2", None),
     (None, "1", "8"),      # windows exceed the budget: sub-passes over fewer lanes
@@ -381,8 +382,11 @@ def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
     if lds is not None and lds.startswith("q"):
         parts = lds[1:].split("l")
         wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
+    segs = None
+    if kern == "seg16":
+        kern, segs = "seg", "16"
     for k, v in (("RIFRAF_SCORE_KERNEL", kern), ("RIFRAF_LEAN_NW", nw), ("RIFRAF_LEAN_LDS_KB", lds),
-                 ("RIFRAF_WS_Q", wsq)):
+                 ("RIFRAF_WS_Q", wsq), ("RIFRAF_SEG_S", segs)):
         if v is None:
             monkeypatch.delenv(k, raising=False)
         else:
@@ -455,14 +459,18 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "general"])
+@pytest.mark.parametrize("kern", [None, "seg16", "general"])
 def test_score_wide_bands(engine, monkeypatch, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
     row-segment scorer k_score_seg (default) and the in-place k_score
     ("general") are both bit-exact against the oracle."""
+    monkeypatch.delenv("RIFRAF_SEG_S", raising=False)
     if kern is None:
         monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
+    elif kern == "seg16":
+        monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
+        monkeypatch.setenv("RIFRAF_SEG_S", "16")
     else:
         monkeypatch.setenv("RIFRAF_SCORE_KERNEL", kern)
     monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
