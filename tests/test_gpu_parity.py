@@ -359,6 +359,7 @@ SCORER_CONFIGS = [
     ("general", None, None),
     ("seg", None, None),       # row-segment scorer (wide bands) on every shape
     ("seg16", None, None),     # ... with 16-diagonal segments (RIFRAF_SEG_S=16)
+    ("seg32", None, None),     # ... with 32-diagonal segments
     (None, "1", None),
     (None, "2", None),
     (None, "1", "8"),      # windows exceed the budget: sub-passes over fewer lanes
@@ -383,8 +384,8 @@ def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
         parts = lds[1:].split("l")
         wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
     segs = None
-    if kern == "seg16":
-        kern, segs = "seg", "16"
+    if kern in ("seg16", "seg32"):
+        kern, segs = "seg", kern[3:]
     for k, v in (("RIFRAF_SCORE_KERNEL", kern), ("RIFRAF_LEAN_NW", nw), ("RIFRAF_LEAN_LDS_KB", lds),
                  ("RIFRAF_WS_Q", wsq), ("RIFRAF_SEG_S", segs)):
         if v is None:
@@ -459,7 +460,7 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seg16", "general"])
+@pytest.mark.parametrize("kern", [None, "seg16", "seg32", "general"])
 def test_score_wide_bands(engine, monkeypatch, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
@@ -468,9 +469,9 @@ def test_score_wide_bands(engine, monkeypatch, mode, kern):
     monkeypatch.delenv("RIFRAF_SEG_S", raising=False)
     if kern is None:
         monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
-    elif kern == "seg16":
+    elif kern in ("seg16", "seg32"):
         monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
-        monkeypatch.setenv("RIFRAF_SEG_S", "16")
+        monkeypatch.setenv("RIFRAF_SEG_S", kern[3:])
     else:
         monkeypatch.setenv("RIFRAF_SCORE_KERNEL", kern)
     monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
