@@ -611,35 +611,55 @@ def base_distribution(base, ilp):                                  # :804-809
 
 def alignment_error_probs(tlen, state: RifrafState, run: _Run):   # :817-840
     """Per consensus position, 1 - max normalised base probability over the
-    batch alignments.  Vectorised per read; every column still receives its
-    base_distribution rows in batch order, so the sums are the loop's."""
+    batch alignments.  The move walk is vectorised over all reads at once and
+    the base_distribution rows are built once per distinct (base, match
+    score); every column still receives its rows in batch order (one fancy
+    add per read), so the sums are the reference loop's."""
     probs = np.zeros((tlen, 4))
     slots = np.arange(len(state.batch_seqs), dtype=np.int32)
     moves, _ = run.e.backtrace(slots)
-    memo = {}
-    for mv, idx in zip(moves, state.batch_seqs):
-        s = state.sequences[idx]
-        mv = np.asarray(mv, np.int64)
-        di = np.where((mv == 1) | (mv == 2), 1, np.where(mv == 4, 3, 0))
-        dj = np.where((mv == 1) | (mv == 3), 1, np.where(mv == 5, 3, 0))
-        i = 1 + np.cumsum(di)
-        j = 1 + np.cumsum(dj)
-        match = mv == TRACE_MATCH
-        ii, jj = i[match] - 2, j[match] - 2
-        bases = s.seq[ii]
-        ilps = np.asarray(s.match_scores)[ii]
-        ulp, inv = np.unique(ilps, return_inverse=True)
-        table = np.empty((4, len(ulp), 4))
-        for u, lp in enumerate(ulp.tolist()):
-            for b in range(4):
-                d = memo.get((b, lp))
-                if d is None:
-                    d = memo[(b, lp)] = base_distribution(b, lp)
-                table[b, u] = d
-        probs[jj] += table[bases, inv.reshape(-1)]   # one row per column per read
+    if moves:
+        _add_base_distributions(probs, moves, [state.sequences[idx] for idx in state.batch_seqs])
     probs = np.power(10.0, probs)
     probs = 1.0 - (probs / probs.sum(axis=1, keepdims=True)).max(axis=1)
     return probs
+
+
+# read / consensus advance of each move code (align.jl:14-18 OFFSETS)
+_MOVE_DI = np.array([0, 1, 1, 0, 3, 0], np.int64)
+_MOVE_DJ = np.array([0, 1, 0, 1, 0, 3], np.int64)
+
+
+def _add_base_distributions(probs, moves, seqs):
+    nr = len(moves)
+    lens = np.array([len(mv) for mv in moves], np.int64)
+    mv = np.concatenate(moves)
+    start = np.zeros(nr + 1, np.int64)
+    np.cumsum(lens, out=start[1:])
+    # i, j after each move (align.jl:286-311 walk), restarted at (1, 1) per read
+    ci = np.zeros(len(mv) + 1, np.int64)
+    cj = np.zeros(len(mv) + 1, np.int64)
+    np.cumsum(_MOVE_DI[mv], out=ci[1:])
+    np.cumsum(_MOVE_DJ[mv], out=cj[1:])
+    match = mv == TRACE_MATCH
+    ii = (ci[1:] - np.repeat(ci[start[:-1]], lens))[match] - 1   # matched read base (0-based)
+    jj = (cj[1:] - np.repeat(cj[start[:-1]], lens))[match] - 1   # consensus column (0-based)
+    owner = np.repeat(np.arange(nr), lens)[match]
+    bases = np.concatenate([s.seq for s in seqs])
+    mscores = np.concatenate([np.asarray(s.match_scores) for s in seqs])
+    soff = np.zeros(len(seqs) + 1, np.int64)
+    np.cumsum([len(s.seq) for s in seqs], out=soff[1:])
+    gi = soff[owner] + ii
+    ilps = mscores[gi]
+    ulp, inv = np.unique(ilps, return_inverse=True)
+    table = np.empty((4, len(ulp), 4))
+    for u, lp in enumerate(ulp.tolist()):
+        for b in range(4):
+            table[b, u] = base_distribution(b, lp)
+    rows = table[bases[gi], inv.reshape(-1)]
+    # bincount adds its weights in input order, i.e. per column in batch order
+    flat = (jj[:, None] * 4 + np.arange(4)).ravel()
+    probs += np.bincount(flat, weights=rows.ravel(), minlength=probs.size).reshape(probs.shape)
 
 
 # ---------------------------------------------------------------------

@@ -123,6 +123,35 @@ def test_alignment_error_probs(eng):                                 # test_mode
     assert list(np.argsort(result, kind="stable") + 1) == [4, 3, 2, 1]
 
 
+def test_alignment_error_probs_matches_loop(eng):
+    """The vectorised alignment_error_probs equals the reference's per-read,
+    per-move loop (model.jl:817-840) bit for bit: ragged noisy reads, so the
+    walk sees matches, inserts and deletes and columns get rows from several
+    reads in batch order."""
+    from rifraf_amd.align import TRACE_MATCH
+    from rifraf_amd.model import base_distribution
+    rng = np.random.default_rng(31)
+    _, t, _, reads, _, phreds, _, _ = sample_sequences(9, 120, error_rate=0.06, rng=rng)
+    scores = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0, 0.0, 0.0))
+    pseqs = [RifrafSequence(r, p, 9, scores) for r, p in zip(reads, phreds)]
+    state, run = _state(eng, dna_str(t), pseqs, RifrafParams(bandwidth=9, batch_size=0, batch_fixed=False))
+    got = alignment_error_probs(len(t), state, run)
+    moves, _ = run.e.backtrace(np.arange(len(state.batch_seqs), dtype=np.int32))
+    probs = np.zeros((len(t), 4))
+    off = {1: (1, 1), 2: (1, 0), 3: (0, 1), 4: (3, 0), 5: (0, 3)}
+    for idx, mv in zip(state.batch_seqs, moves):
+        s = state.sequences[idx]
+        i, j = 1, 1
+        for move in mv.tolist():
+            i, j = i + off[move][0], j + off[move][1]
+            if move == TRACE_MATCH:
+                probs[j - 2] += base_distribution(int(s.seq[i - 2]), float(s.match_scores[i - 2]))
+    probs = np.power(10.0, probs)
+    expect = 1.0 - (probs / probs.sum(axis=1, keepdims=True)).max(axis=1)
+    np.testing.assert_array_equal(got, expect)
+    assert np.count_nonzero(got) > 0
+
+
 def test_smart_forward_moves_widens_band(eng):                       # test_model.jl:451-471
     from rifraf_amd.model import smart_forward_moves
     seq = DNASeq("AAAGGGTTTCCC")
