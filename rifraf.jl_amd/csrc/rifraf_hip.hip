@@ -126,7 +126,8 @@ struct alignas(16) BTTask {
     int64_t A, sb, tab, tb, out;
     int32_t n, m, bw, H;
     int32_t ncins, ncdel, flags, idx;
-    int32_t P, pad[3];
+    int32_t P, pad;
+    int64_t mask;   // k_bt_win with a proposal mask: byte offset of the cluster's (m+1) x 9 mask
 };
 
 // error word: first error code wins (atomicCAS)
@@ -2207,7 +2208,8 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
             set_err(err, 2);  // failed to find a move
             break;
         }
-        out[cnt++] = (int8_t)mv;
+        out[n + m - 1 - cnt] = (int8_t)mv;   // forward order ends at slot n+m-1
+        ++cnt;
         switch (mv) {
         case 1: errs += (sb != tbb); ii -= 1; jj -= 1; break;
         case 2: errs += 1; ii -= 1; break;
@@ -2216,13 +2218,152 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
         default: errs += 3; jj -= 3; break;
         }
     }
-    for (int a = 0, b = cnt - 1; a < b; ++a, --b) {
-        const int8_t tmp = out[a];
-        out[a] = out[b];
-        out[b] = tmp;
-    }
     nmoves[T.idx] = cnt;
     nerr[T.idx] = errs;
+}
+
+// ---------------------------------------------------------------------
+// k_bt_win: backtrace + count_errors (align.jl:229-245) for reads (no codon
+// moves, H <= 255), one wave per read, from an LDS window instead of global
+// memory.  k_backtrace's walk is a chain of dependent global loads (band
+// cells, tables and bases at the current cell, ~1 us per move); here the
+// wave stages a window of kappa rows of the A band (contiguous in the
+// kappa-major layout) plus the table rows and bases the walk can reach from
+// it, and every lane walks the same path through LDS (broadcast reads, no
+// divergence).  The walk only moves to lower kappa, so a window is left
+// downwards and re-staged below.  Same move choice as k_backtrace (strict '>'
+// in the reference's order), same count_errors; moves are written in forward
+// order ending at slot n+m-1 of the read's output.  With a mask, the wave
+// also marks the proposals its alignment implies (moves_to_proposals,
+// model.jl:458-480: k_aln_props fused into the walk -- the set union does not
+// depend on the walk direction).
+// ---------------------------------------------------------------------
+constexpr int BTW_A = 4096;    // doubles of A window (32 KB)
+constexpr int BTW_T = 384;     // staged table rows / bases per window
+
+__global__ void __launch_bounds__(64)
+k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
+         const double *__restrict__ bands, int8_t *__restrict__ moves, int32_t *__restrict__ nmoves,
+         int32_t *__restrict__ nerr, int *__restrict__ err, uint8_t *__restrict__ mask, int do_indels)
+{
+    __shared__ double sA[BTW_A];
+    __shared__ double sTm[BTW_T], sTx[BTW_T], sTi[BTW_T], sTd[BTW_T];
+    __shared__ uint8_t sS[BTW_T], sTt[BTW_T];
+    const BTTask T = tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const double *A = bands + T.A;
+    const uint8_t *s = bases + T.sb;
+    const uint8_t *tt = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    const int n = T.n, m = T.m, H = T.H, P = T.P;
+    const int c = max(m - n, 0) + T.bw;
+    const int K = H + 2 * m;
+    const int W = min(256, BTW_A / P);                 // kappa rows per window
+    const bool skew = T.flags & 2, trim = T.flags & 4;
+    int8_t *out = moves + T.out;
+    uint8_t *mk = mask ? mask + T.mask : nullptr;
+    auto inband = [&](int ii, int jj) {
+        if (ii < 0 || jj < 0 || ii > n || jj > m)
+            return false;
+        const int d = ii - jj + c;
+        return d >= 0 && d < H;
+    };
+    int ii = n, jj = m, cnt = 0, errs = 0;
+    int klo = 0, q0 = 0, r0 = 0;                       // staged: kappa >= klo, table index >= q0, t index >= r0
+    bool staged = false;
+    while (ii > 0 || jj > 0) {
+        const int kap0 = ii + jj + c;                  // kappa of the current cell
+        if (!staged || (klo > 0 && kap0 - 2 < klo) || max(ii - 1, 0) < q0 || (jj >= 1 && jj - 1 < r0)) {
+            // ---- (re)stage below the current cell: rows [klo, khi], tables [q0, q1], bases
+            const int khi = min(kap0 - 1, K - 1);
+            klo = max(0, khi - W + 1);
+            const int q1 = ii;                         // del index ii; ks = ii - 1
+            q0 = max(0, min((klo + 2 - 2 * c) / 2 - 2, q1 - 1));   // <= max(ii - 1, 0): no re-stage loop
+            q0 = max(q0, q1 - BTW_T + 1);
+            const int r1 = max(jj - 1, 0);
+            r0 = max(0, min((klo + 3 - H) / 2 - 2, r1));
+            r0 = max(r0, r1 - BTW_T + 1);
+            wave_sync();                               // every lane is done with the old window
+            const int na = (khi - klo + 1) * P;
+            const double *ga = A + (size_t)klo * P;
+            for (int e = lane; e < na; e += 64)
+                sA[e] = ga[e];
+            for (int e = lane; e <= q1 - q0; e += 64) {
+                const int q = q0 + e;
+                const int ks = min(q, n - 1);
+                sTm[e] = tb[ks];
+                sTx[e] = tb[n + ks];
+                sTi[e] = tb[2 * (size_t)n + ks];
+                sTd[e] = tb[3 * (size_t)n + q];
+                sS[e] = q < n ? s[q] : 4;
+            }
+            for (int e = lane; e <= r1 - r0; e += 64)
+                sTt[e] = r0 + e < m ? tt[r0 + e] : 4;
+            wave_sync();
+            staged = true;
+        }
+        const int sb = ii >= 1 ? sS[ii - 1 - q0] : 4;
+        const int tbb = jj >= 1 ? sTt[jj - 1 - r0] : 4;
+        const int ks = max(ii - 1, 0) - q0;
+        double ms = (sb == tbb) ? sTm[ks] : sTx[ks];
+        double is = sTi[ks];
+        const double ds = sTd[ii - q0];
+        if (skew && sb != tbb)
+            ms *= 0.99;
+        if (trim && (jj == 0 || jj == m))
+            is = 0.0;
+        auto get = [&](int i2, int j2) {
+            const int d = i2 - j2 + c;
+            return sA[(d + 2 * j2 - klo) * P + (d >> 1)];
+        };
+        double best = -RF_INF, x;
+        int mv = 0;
+        if (inband(ii - 1, jj - 1)) {
+            x = get(ii - 1, jj - 1) + ms;
+            if (x > best) { best = x; mv = 1; }
+        }
+        if (inband(ii - 1, jj)) {
+            x = get(ii - 1, jj) + is;
+            if (x > best) { best = x; mv = 2; }
+        }
+        if (inband(ii, jj - 1)) {
+            x = get(ii, jj - 1) + ds;
+            if (x > best) { best = x; mv = 3; }
+        }
+        if (mv == 0 || cnt >= n + m) {
+            if (lane == 0)
+                set_err(err, 2);  // failed to find a move
+            break;
+        }
+        if (lane == 0) {
+            out[n + m - 1 - cnt] = (int8_t)mv;
+            if (mk) {
+                // the forward step of this move ends at (ii, jj) (k_aln_props)
+                if (mv == 1 && sb != tbb)
+                    mk[(size_t)jj * 9 + sb] = 1;
+                else if (mv == 2 && do_indels)
+                    mk[(size_t)jj * 9 + 5 + sb] = 1;
+                else if (mv == 3 && do_indels)
+                    mk[(size_t)jj * 9 + 4] = 1;
+            }
+        }
+        ++cnt;
+        if (mv == 1) {
+            errs += (sb != tbb);
+            --ii;
+            --jj;
+        } else if (mv == 2) {
+            errs += 1;
+            --ii;
+        } else {
+            errs += 1;
+            --jj;
+        }
+    }
+    if (lane == 0) {
+        nmoves[T.idx] = cnt;
+        nerr[T.idx] = errs;
+    }
 }
 
 // ---------------------------------------------------------------------
@@ -2248,9 +2389,9 @@ __global__ void k_aln_props(const PropTask *__restrict__ tasks, int ntasks, cons
     const PropTask T = tasks[k];
     const uint8_t *s = bases + T.sb;
     const uint8_t *t = bases + T.tb;
-    const int8_t *mv = moves + T.mv;
-    uint8_t *out = mask + T.mask;
     const int cnt = nmoves[T.idx];
+    const int8_t *mv = moves + T.mv + (T.n + T.m - cnt);   // end-aligned in the n+m slot
+    uint8_t *out = mask + T.mask;
     int i = 0, j = 0;
     for (int e = 0; e < cnt; ++e) {
         switch (mv[e]) {
@@ -2373,7 +2514,7 @@ struct rf_ctx {
     std::vector<Slot> slots;
     uint64_t tpl_counter = 0;
     uint64_t layout_gen = 1;   // bumped whenever a device offset / length may change
-    DevBuf scratch[16];
+    DevBuf scratch[17];
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0;
@@ -3148,15 +3289,52 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     return check_err(ctx);
 }
 
-int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves,
-                 const int64_t *moves_off, int32_t *nmoves, int32_t *nerrors)
+// k_bt_win takes reads (no codon tables) with H <= 255; the rest (the
+// reference's codon alignments, edit_distance-sized bands) walk in k_backtrace
+static bool bt_windowed(const BTTask &t) { return t.ncins == 0 && t.ncdel == 0 && t.H <= 255; }
+
+// Launch the backtraces of `tasks` (moves into scratch[3] at t.out, counts in
+// scratch[4]); with d_mask, the windowed walks also mark alignment proposals.
+static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d_mask, int do_indels)
 {
-    if (!ctx || nslots < 0 || (nslots > 0 && !slot) || (moves && !moves_off))
-        return fail(ctx, RF_ERR_ARG, "rf_backtrace: bad arguments");
-    (void)hipSetDevice(ctx->device);
-    std::vector<BTTask> tasks(nslots);
+    const int32_t nslots = (int32_t)tasks.size();
+    std::vector<BTTask> win, old;
+    for (const auto &t : tasks)
+        (bt_windowed(t) ? win : old).push_back(t);
+    if (std::getenv("RIFRAF_BT_LEGACY") && !d_mask) {   // diagnostics: every walk in k_backtrace
+        old = tasks;
+        win.clear();
+    }
+    int32_t *d_cnt = (int32_t *)ctx->scratch[4].p;
+    if (!old.empty()) {
+        if (int e = upload(ctx, ctx->scratch[0], old))
+            return e;
+        hipLaunchKernelGGL(k_backtrace, dim3((unsigned)((old.size() + 63) / 64)), dim3(64), 0, ctx->stream,
+                           (const BTTask *)ctx->scratch[0].p, (int)old.size(),
+                           (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
+                           (const double *)ctx->band_arena.d, (int8_t *)ctx->scratch[3].p, d_cnt,
+                           d_cnt + nslots, ctx->d_err);
+    }
+    if (!win.empty()) {
+        if (int e = upload(ctx, ctx->scratch[16], win))
+            return e;
+        hipLaunchKernelGGL(k_bt_win, dim3((unsigned)win.size()), dim3(64), 0, ctx->stream,
+                           (const BTTask *)ctx->scratch[16].p, (const uint8_t *)ctx->bytes_arena.d,
+                           (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d,
+                           (int8_t *)ctx->scratch[3].p, d_cnt, d_cnt + nslots, ctx->d_err, d_mask, do_indels);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    return 0;
+}
+
+// Backtrace descriptors of `nslots` slots (moves slot k at offs[k], n+m bytes)
+// and the scratch buffers for moves and counts.
+static int build_bt_tasks(rf_ctx *ctx, int32_t nslots, const int32_t *slot, std::vector<BTTask> &tasks,
+                          std::vector<int64_t> &offs)
+{
+    tasks.assign(nslots, BTTask{});
+    offs.assign(nslots, 0);
     int64_t total = 0;
-    std::vector<int64_t> offs(nslots);
     for (int32_t k = 0; k < nslots; ++k) {
         if (slot[k] < 0 || slot[k] >= (int32_t)ctx->slots.size() || !ctx->slots[slot[k]].a.valid)
             return fail(ctx, RF_ERR_STATE, "rf_backtrace: slot has no A band");
@@ -3180,23 +3358,32 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
         t.flags = (b.flags & RF_SKEW ? 2 : 0) | (b.flags & RF_TRIM ? 4 : 0);
         t.idx = k;
         t.P = band_P(b.H);
+        t.mask = 0;
         offs[k] = total;
         total += b.n + b.m;
     }
-    if (int e = upload(ctx, ctx->scratch[0], tasks))
-        return e;
     if (int e = ensure_buf(ctx, ctx->scratch[3], std::max<int64_t>(total, 16)))
         return e;
     if (int e = ensure_buf(ctx, ctx->scratch[4], sizeof(int32_t) * 2 * std::max(nslots, 1)))
         return e;
+    return 0;
+}
+
+int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves,
+                 const int64_t *moves_off, int32_t *nmoves, int32_t *nerrors)
+{
+    if (!ctx || nslots < 0 || (nslots > 0 && !slot) || (moves && !moves_off))
+        return fail(ctx, RF_ERR_ARG, "rf_backtrace: bad arguments");
+    (void)hipSetDevice(ctx->device);
+    std::vector<BTTask> tasks;
+    std::vector<int64_t> offs;
+    if (int e = build_bt_tasks(ctx, nslots, slot, tasks, offs))
+        return e;
+    const int64_t total = nslots > 0 ? offs[nslots - 1] + tasks[nslots - 1].n + tasks[nslots - 1].m : 0;
     int32_t *d_cnt = (int32_t *)ctx->scratch[4].p;
     if (nslots > 0)
-        hipLaunchKernelGGL(k_backtrace, dim3((nslots + 63) / 64), dim3(64), 0, ctx->stream,
-                           (const BTTask *)ctx->scratch[0].p, nslots,
-                           (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
-                           (const double *)ctx->band_arena.d, (int8_t *)ctx->scratch[3].p, d_cnt,
-                           d_cnt + nslots, ctx->d_err);
-    HIPCHK(ctx, hipGetLastError());
+        if (int e = launch_backtraces(ctx, tasks, nullptr, 0))
+            return e;
     std::vector<int32_t> cnt(2 * (size_t)nslots);
     if (nslots > 0)
         HIPCHK(ctx, hipMemcpyAsync(cnt.data(), d_cnt, sizeof(int32_t) * 2 * nslots,
@@ -3216,8 +3403,8 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
             nmoves[k] = cnt[k];
         if (nerrors)
             nerrors[k] = cnt[nslots + k];
-        if (moves)
-            std::memcpy(moves + moves_off[k], all.data() + offs[k], cnt[k]);
+        if (moves)   // the walk leaves the moves at the end of the read's n+m slot
+            std::memcpy(moves + moves_off[k], all.data() + offs[k] + tasks[k].n + tasks[k].m - cnt[k], cnt[k]);
     }
     return 0;
 }
@@ -3228,12 +3415,14 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !out_mask)))
         return fail(ctx, RF_ERR_ARG, "rf_alignment_proposals: bad arguments");
     const int32_t nslots = ngroups > 0 ? slot_off[ngroups] : 0;
-    // 1. device backtraces of every batch slot (moves stay in scratch[3],
-    //    counts in scratch[4]; offsets = prefix sums of n + m, as rf_backtrace)
-    if (int e = rf_backtrace(ctx, nslots, slots, nullptr, nullptr, nullptr, nullptr))
+    (void)hipSetDevice(ctx->device);
+    // 1. descriptors: backtrace tasks of every batch slot + each cluster's mask
+    std::vector<BTTask> tasks;
+    std::vector<int64_t> offs;
+    if (int e = build_bt_tasks(ctx, nslots, slots, tasks, offs))
         return e;
-    std::vector<PropTask> tasks(nslots);
-    int64_t mv_at = 0, mask_total = 0;
+    std::vector<PropTask> ptasks;   // reads whose walk runs in k_backtrace (then k_aln_props)
+    int64_t mask_total = 0;
     for (int32_t g = 0; g < ngroups; ++g) {
         int32_t tpl = -1, m = 0;
         for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
@@ -3242,34 +3431,42 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
                 return fail(ctx, RF_ERR_ARG, "rf_alignment_proposals: batch slots use different templates");
             tpl = b.tpl;
             m = b.m;
-            PropTask &t = tasks[k];
-            t.sb = ctx->seqs[b.seq].bases.off;
-            t.tb = ctx->tpls[b.tpl].bases.off;
-            t.mv = mv_at;
-            t.mask = mask_total;
-            t.n = b.n;
-            t.m = b.m;
-            t.idx = k;
-            mv_at += b.n + b.m;
+            tasks[k].mask = mask_total;
+            if (!bt_windowed(tasks[k])) {
+                PropTask t{};
+                t.sb = ctx->seqs[b.seq].bases.off;
+                t.tb = ctx->tpls[b.tpl].bases.off;
+                t.mv = offs[k];
+                t.mask = mask_total;
+                t.n = b.n;
+                t.m = b.m;
+                t.idx = k;
+                ptasks.push_back(t);
+            }
         }
         if (slot_off[g + 1] > slot_off[g])
             mask_total += (int64_t)(m + 1) * 9;
     }
     if (nslots == 0)
         return 0;
-    if (int e = upload(ctx, ctx->scratch[1], tasks))
-        return e;
     if (int e = ensure_buf(ctx, ctx->scratch[2], std::max<int64_t>(mask_total, 16)))
         return e;
     HIPCHK(ctx, hipMemsetAsync(ctx->scratch[2].p, 0, mask_total, ctx->stream));
-    hipLaunchKernelGGL(k_aln_props, dim3((nslots + 63) / 64), dim3(64), 0, ctx->stream,
-                       (const PropTask *)ctx->scratch[1].p, nslots, (const uint8_t *)ctx->bytes_arena.d,
-                       (const int8_t *)ctx->scratch[3].p, (const int32_t *)ctx->scratch[4].p,
-                       (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0);
+    // 2. the walks; windowed ones mark the mask as they go (k_aln_props fused)
+    if (int e = launch_backtraces(ctx, tasks, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0))
+        return e;
+    if (!ptasks.empty()) {
+        if (int e = upload(ctx, ctx->scratch[1], ptasks))
+            return e;
+        hipLaunchKernelGGL(k_aln_props, dim3((unsigned)((ptasks.size() + 63) / 64)), dim3(64), 0, ctx->stream,
+                           (const PropTask *)ctx->scratch[1].p, (int)ptasks.size(),
+                           (const uint8_t *)ctx->bytes_arena.d, (const int8_t *)ctx->scratch[3].p,
+                           (const int32_t *)ctx->scratch[4].p, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0);
+    }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    return check_err(ctx);
 }
 
 int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,

@@ -547,3 +547,46 @@ def test_alignment_proposals_device(engine, do_indels):
                 k, p, b = k[keep], p[keep], b[keep]
             exp[p, np.where(k == 0, b, np.where(k == 2, 4, 5 + b))] = 1
         np.testing.assert_array_equal(masks[c], exp, err_msg=f"cluster {c}")
+
+
+@pytest.mark.parametrize("L,bw,skew", [(700, 9, 0), (400, 40, 30), (300, 120, -40), (260, 9, 60), (90, 3, 0)])
+def test_backtrace_windowed(engine, monkeypatch, L, bw, skew):
+    """k_bt_win (wave per read, LDS windows of kappa rows, re-staged as the
+    walk leaves them) against the oracle's backtrace and count_errors, and the
+    fused proposal marking against the host moves_to_proposals union, on long
+    reads (many windows), wide bands (small windows: P up to 129) and reads
+    longer / shorter than the template; RIFRAF_BT_LEGACY=1 (k_backtrace for
+    every walk) gives the same moves."""
+    from rifraf_amd.align import moves_to_proposals_np
+    rng = np.random.default_rng(L + bw)
+    t = random_seq(L, rng)
+    seqs = []
+    for _ in range(5):
+        r = make_read(t, rng, 0.05, bw)
+        if skew > 0:
+            extra = random_seq(int(rng.integers(skew // 2, skew + 1)), rng)
+            r = RifrafSequence(np.concatenate([r.seq, extra]),
+                               np.concatenate([r.error_log_p, np.full(len(extra), -1.0)]), bw, SEQ_SCORES)
+        elif skew < 0:
+            cut = int(rng.integers(-skew // 2, -skew + 1))
+            r = RifrafSequence(r.seq[:len(r.seq) - cut], r.error_log_p[:len(r.seq) - cut], bw, SEQ_SCORES)
+        seqs.append(r)
+    n = len(seqs)
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
+    monkeypatch.delenv("RIFRAF_BT_LEGACY", raising=False)
+    got, nerr = engine.backtrace(np.arange(n))
+    monkeypatch.setenv("RIFRAF_BT_LEGACY", "1")
+    legacy, nerr_l = engine.backtrace(np.arange(n))
+    monkeypatch.delenv("RIFRAF_BT_LEGACY")
+    exp_mask = np.zeros((L + 1, 9), np.uint8)
+    for k, s in enumerate(seqs):
+        _, mv = oracle.forward(t, s, moves=True, bandwidth=bw)
+        ref = oracle.backtrace(mv, len(s) + 1, L + 1, bw)
+        np.testing.assert_array_equal(got[k], ref)
+        np.testing.assert_array_equal(legacy[k], ref)
+        assert nerr[k] == nerr_l[k] == oracle.count_errors(ref, t, s.seq)
+        kk, p, b = moves_to_proposals_np(ref, t, s.seq)
+        exp_mask[p, np.where(kk == 0, b, np.where(kk == 2, 4, 5 + b))] = 1
+    np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
