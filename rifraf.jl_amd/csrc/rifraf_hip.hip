@@ -2302,34 +2302,36 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             wave_sync();
             staged = true;
         }
-        const int sb = ii >= 1 ? sS[ii - 1 - q0] : 4;
-        const int tbb = jj >= 1 ? sTt[jj - 1 - r0] : 4;
+        // one LDS round trip per move: every operand is read unconditionally
+        // (addresses clamped to the window when a predecessor is out of band),
+        // then the reference's candidate chain is evaluated on registers
+        const bool in1 = inband(ii - 1, jj - 1), in2 = inband(ii - 1, jj), in3 = inband(ii, jj - 1);
+        auto aix = [&](bool in, int i2, int j2) {
+            const int d = i2 - j2 + c;
+            return in ? (d + 2 * j2 - klo) * P + (d >> 1) : 0;
+        };
         const int ks = max(ii - 1, 0) - q0;
-        double ms = (sb == tbb) ? sTm[ks] : sTx[ks];
-        double is = sTi[ks];
-        const double ds = sTd[ii - q0];
+        const int sbv = sS[ii >= 1 ? ii - 1 - q0 : 0];
+        const int tbv = sTt[jj >= 1 ? jj - 1 - r0 : 0];
+        const double tm = sTm[ks], tx = sTx[ks], ti = sTi[ks], ds = sTd[ii - q0];
+        const double a1 = sA[aix(in1, ii - 1, jj - 1)], a2 = sA[aix(in2, ii - 1, jj)], a3 = sA[aix(in3, ii, jj - 1)];
+        const int sb = ii >= 1 ? sbv : 4;
+        const int tbb = jj >= 1 ? tbv : 4;
+        double ms = (sb == tbb) ? tm : tx;
+        double is = ti;
         if (skew && sb != tbb)
             ms *= 0.99;
         if (trim && (jj == 0 || jj == m))
             is = 0.0;
-        auto get = [&](int i2, int j2) {
-            const int d = i2 - j2 + c;
-            return sA[(d + 2 * j2 - klo) * P + (d >> 1)];
-        };
         double best = -RF_INF, x;
         int mv = 0;
-        if (inband(ii - 1, jj - 1)) {
-            x = get(ii - 1, jj - 1) + ms;
-            if (x > best) { best = x; mv = 1; }
-        }
-        if (inband(ii - 1, jj)) {
-            x = get(ii - 1, jj) + is;
-            if (x > best) { best = x; mv = 2; }
-        }
-        if (inband(ii, jj - 1)) {
-            x = get(ii, jj - 1) + ds;
-            if (x > best) { best = x; mv = 3; }
-        }
+        x = a1 + ms;
+        if (in1 && x > best) { best = x; mv = 1; }
+        x = a2 + is;
+        if (in2 && x > best) { best = x; mv = 2; }
+        x = a3 + ds;
+        if (in3 && x > best) { best = x; mv = 3; }
+        mv = __builtin_amdgcn_readfirstlane(mv);
         if (mv == 0 || cnt >= n + m) {
             if (lane == 0)
                 set_err(err, 2);  // failed to find a move
@@ -2515,6 +2517,10 @@ struct rf_ctx {
     uint64_t tpl_counter = 0;
     uint64_t layout_gen = 1;   // bumped whenever a device offset / length may change
     DevBuf scratch[17];
+    // pinned host staging for sequence uploads (pageable H2D copies of a few
+    // MB took ~14 ms per cluster upload on the box: page locking per call)
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0;
@@ -2882,6 +2888,8 @@ int rf_destroy(rf_ctx *ctx)
             (void)hipFree(b.p);
     if (ctx->grow_segs.p)
         (void)hipFree(ctx->grow_segs.p);
+    if (ctx->pinned)
+        (void)hipHostFree(ctx->pinned);
     if (ctx->d_err)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
@@ -2970,14 +2978,27 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
         nb += n;
         nt += 4 * n + 1 + nci + ncd;
     }
-    // 2. pack: bases as given; tables [match|mismatch|ins|del|cins|cdel] per sequence
-    std::vector<double> host((size_t)std::max<int64_t>(nt, 1));
+    // 2. pack into the pinned staging buffer: tables [match|mismatch|ins|del|
+    //    cins|cdel] per sequence, then the bases as given
+    const size_t stage_bytes = (size_t)std::max<int64_t>(nt, 1) * 8 + (size_t)std::max<int64_t>(nb, 1);
+    if (ctx->pinned_bytes < stage_bytes) {
+        if (ctx->pinned)
+            (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        const size_t want = std::max(stage_bytes + stage_bytes / 2, (size_t)1 << 22);
+        if (hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault) != hipSuccess)
+            return fail(ctx, RF_ERR_HIP, "rf_set_sequences: pinned staging allocation failed");
+        ctx->pinned_bytes = want;
+    }
+    double *host_tabs = (double *)ctx->pinned;
+    uint8_t *host_bases = (uint8_t *)ctx->pinned + (size_t)std::max<int64_t>(nt, 1) * 8;
     std::vector<Segment> sb(nseq), st(nseq);
     int64_t at = 0;
     for (int32_t k = 0; k < nseq; ++k) {
         const SeqObj &S = ctx->seqs[first + k];
         const int64_t n = S.n, nci = S.ncins, ncd = S.ncdel;
-        double *h = host.data() + at;
+        double *h = host_tabs + at;
         std::memcpy(h, match + off[k], n * 8);
         std::memcpy(h + n, mismatch + off[k], n * 8);
         std::memcpy(h + 2 * n, ins + off[k], n * 8);
@@ -2999,8 +3020,9 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     if (int e = ensure_buf(ctx, ctx->scratch[6], (size_t)std::max<int64_t>(nt * 8, 16))) return e;
     if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
     if (nseq > 0) {
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[6].p, host.data(), nt * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, bases + off[0], nb, hipMemcpyHostToDevice, ctx->stream));
+        std::memcpy(host_bases, bases + off[0], nb);
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[6].p, host_tabs, nt * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, host_bases, nb, hipMemcpyHostToDevice, ctx->stream));
         if (int e = upload(ctx, ctx->scratch[5], st)) return e;
         hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
                            (const uint8_t *)ctx->scratch[6].p, (uint8_t *)ctx->tab_arena.d);
