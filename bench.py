@@ -149,10 +149,32 @@ def cpu_baseline(clusters, budget_s=12.0, max_threads=16):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
+    # the same pass on one thread (1 thread and all cores), shorter budget
+    c1 = d1 = 0
+    t1 = time.perf_counter()
+    for t, reads in clusters:
+        _, c = oracle.cpu_pass(t, reads, nthreads=1)
+        c1 += c
+        d1 += 1
+        if time.perf_counter() - t1 >= budget_s / 4:
+            break
+    dt1 = time.perf_counter() - t1
     return {"value": cells / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
-            "proposals_per_s": props / dt,
+            "proposals_per_s": props / dt, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{done} cluster(s) x {len(clusters[0][1])} reads x {len(clusters[0][0])} bp, "
-                      f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads"}
+                      f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads",
+            "single_thread": {"value": c1 / dt1 / 1e9, "unit": "GCUPS", "cores": 1,
+                              "sample": f"{d1} cluster(s), {dt1:.1f} s"}}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def shard_seed(seed: int, rank: int) -> int:
