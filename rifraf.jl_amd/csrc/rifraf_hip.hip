@@ -549,14 +549,15 @@ __host__ __device__ constexpr int dpl_pmax(int np) { return (16 * np) | 1; }   /
 // carry slots on either side of a task's band-output rows: a flush writes
 // whole 128-B lines only and carries the partial line into the next block
 constexpr int DPL_CARRY = 16;
-__host__ __device__ constexpr int dpl_task_bytes(int np)
+__host__ __device__ constexpr int dpl_task_bytes(int np, int pm)
 {
-    return (int)(dpl_b(np) * sizeof(EdgeRec)) + (2 * dpl_b(np) * dpl_pmax(np) + 2 * DPL_CARRY) * 8;
+    return (int)(dpl_b(np) * sizeof(EdgeRec)) + (2 * dpl_b(np) * pm + 2 * DPL_CARRY) * 8;
 }
+__host__ __device__ constexpr int dpl_task_bytes(int np) { return dpl_task_bytes(np, dpl_pmax(np)); }
 // 16-B stores per lane of one flush: at most 2*DPL_B*P + DPL_CARRY doubles
-__host__ __device__ constexpr int dpl_flush_stores(int np)
+__host__ __device__ constexpr int dpl_flush_stores(int np, int pm)
 {
-    return (dpl_b(np) * dpl_pmax(np) + DPL_CARRY / 2 + 15) / 16;
+    return (dpl_b(np) * pm + DPL_CARRY / 2 + 15) / 16;
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
@@ -565,7 +566,14 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 #else
 #define DPR_ATTR
 #endif
-template <int NP, bool LEAN>
+// PM: the largest band row stride P of the launch's tasks (default: the
+// class maximum).  The lean flush issues a fixed dpl_flush_stores(NP, PM)
+// 16-B stores per lane (a static count, so hipcc's wait for the next edge
+// load is vmcnt(FL) rather than vmcnt(0)); lanes past a block's end repeat
+// its last pair.  For NP = 1 the host splits the lean class by P (11, 13,
+// 15, 17), so a c4 task with P = 11 issues 12 stores per lane per block
+// instead of 18.
+template <int NP, bool LEAN, int PM = dpl_pmax(NP)>
 __global__ void __launch_bounds__(64) DPR_ATTR
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
@@ -656,7 +664,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // per block, inputs and outputs staged in this task's LDS slice
             const int P = T.P;
             const int t = threadIdx.x >> 4;
-            EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP));
+            EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP, PM));
             // line-aligned flushes: `fl` is the band position (doubles from the
             // band start, which is 256-B aligned) up to which (forward) or down
             // from which (reverse) the interior has been written.  A block's
@@ -666,7 +674,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const int blk = 2 * DPL_B * P;
             const ptrdiff_t g00 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
             ptrdiff_t fl = g00 + (rev ? blk : 0);
-            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP) + DPL_B * sizeof(EdgeRec)) +
+            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP, PM) + DPL_B * sizeof(EdgeRec)) +
                          DPL_CARRY + (int)(g00 & 1);
             // this lane's LDS slot per parity; a block's 2*DPL_B rows are the
             // contiguous global chunk (reverse: flipped rows)
@@ -697,7 +705,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 // as many stores behind this load as the loop puts behind its
                 // own (to the sink), so that hipcc's wait for `pend` is vmcnt(FL)
                 // on every path into the loop, not vmcnt(0)
-                constexpr int FL = dpl_flush_stores(NP);
+                constexpr int FL = dpl_flush_stores(NP, PM);
                 dvec2 *g = (dvec2 *)sink;
                 const dvec2 z = {0.0, 0.0};
 #pragma unroll
@@ -753,7 +761,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 // tasks past ntasks write the sink) keeps hipcc's wait for the next
                 // edge load at vmcnt(FL) instead of draining these stores.
                 {
-                    constexpr int FL = dpl_flush_stores(NP);
+                    constexpr int FL = dpl_flush_stores(NP, PM);
                     const ptrdiff_t g0 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
                     const bool last = b + 1 == nblk;
                     ptrdiff_t lo, hi;
@@ -2532,6 +2540,7 @@ struct rf_ctx {
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
+        size_t nr1p[3] = {};    // lean NP = 1 split by P: k_dpr<1, true, 11 / 13 / 15> (nr[0][1]: P = 17)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
     } rplan;
@@ -3137,8 +3146,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg;
+        std::vector<DPTask> cr[4][2], c64, cg, c1p[3];
         int hmax64 = 0, hmaxg = 0;
+        const bool psplit = env_int("RIFRAF_DP_PSPLIT", 1) != 0;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
                 continue;
@@ -3171,7 +3181,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4, 8), lean when
                 // there are no codon moves and no skew / trim; k_dp beyond
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
-                if (t.H <= 31)
+                if (t.H <= 31 && lean && psplit && t.P <= 15)
+                    c1p[std::max(0, (t.P - 11) >> 1)].push_back(t);   // P <= 11, 13, 15 (P is odd)
+                else if (t.H <= 31)
                     cr[0][lean].push_back(t);
                 else if (t.H <= 63)
                     cr[1][lean].push_back(t);
@@ -3195,6 +3207,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 std::stable_sort(c.begin(), c.end(), by_len);
                 all.insert(all.end(), c.begin(), c.end());
             }
+        for (auto &c : c1p) {
+            std::stable_sort(c.begin(), c.end(), by_len);
+            all.insert(all.end(), c.begin(), c.end());
+        }
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
@@ -3211,6 +3227,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 2; ++b)
                 P.nr[a][b] = cr[a][b].size();
+        for (int a = 0; a < 3; ++a)
+            P.nr1p[a] = c1p[a].size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -3229,7 +3247,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // bands), so the smaller ones run on side streams concurrently with the
     // largest: the machine stays full through every launch's tail.
     struct Launch {
-        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<64,true>
+        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<64,true>,
+                       // 10..12 = k_dpr<1, true, 11 / 13 / 15>
         size_t at, n;
     };
     std::vector<Launch> launches;
@@ -3241,6 +3260,11 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     launches.push_back({2 * a + b, at, P.nr[a][b]});
                     at += P.nr[a][b];
                 }
+        for (int a = 0; a < 3; ++a)
+            if (P.nr1p[a]) {
+                launches.push_back({10 + a, at, P.nr1p[a]});
+                at += P.nr1p[a];
+            }
         if (P.n64) {
             launches.push_back({8, at, P.n64});
             at += P.n64;
@@ -3285,6 +3309,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
+        } else if (L.kind >= 10) {
+            using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
+                                 double *);
+            const KFn kp[3] = {k_dpr<1, true, 11>, k_dpr<1, true, 13>, k_dpr<1, true, 15>};
+            const int pm = 11 + 2 * (L.kind - 10);
+            hipLaunchKernelGGL(kp[L.kind - 10], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1, pm), st,
+                               d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
+                               (double *)ctx->scratch[7].p);
         } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
