@@ -559,6 +559,14 @@ __host__ __device__ constexpr int dpl_flush_stores(int np, int pm)
 {
     return (dpl_b(np) * pm + DPL_CARRY / 2 + 15) / 16;
 }
+// stride classes of the lean DP launches: k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
+// takes the lean tasks of NP class npi with P <= dpr_pm (the largest is the
+// class maximum 16 * NP | 1)
+__host__ __device__ constexpr int dpr_pm(int npi, int pmi)
+{
+    // NP = 1: P <= 17 (H <= 31); NP = 2: 17..33; NP = 4: 33..65; NP = 8: 65..129
+    return npi == 0 ? 11 + 2 * pmi : npi == 1 ? 19 + 4 * pmi + (pmi == 3 ? 2 : 0) : (((16 << npi) * (pmi + 5)) / 8) | 1;
+}
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
 #ifdef DPR_WAVES
@@ -2540,7 +2548,7 @@ struct rf_ctx {
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
-        size_t nr1p[3] = {};    // lean NP = 1 split by P: k_dpr<1, true, 11 / 13 / 15> (nr[0][1]: P = 17)
+        size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
     } rplan;
@@ -3146,9 +3154,27 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, c1p[3];
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4];
         int hmax64 = 0, hmaxg = 0;
-        const bool psplit = env_int("RIFRAF_DP_PSPLIT", 1) != 0;
+        // RIFRAF_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
+        // (default: NP = 1 only, and only when that class holds at least half
+        // of the tasks -- measured: c4 DP -5..9 %; splitting the wide classes,
+        // or a small NP = 1 class next to them (c5), made the fill slower)
+        int psplit = env_int("RIFRAF_DP_PSPLIT", 1);
+        if (!std::getenv("RIFRAF_DP_PSPLIT")) {
+            size_t n1 = 0, nall = 0;
+            for (int dir = 0; dir < 2; ++dir) {
+                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
+                    continue;
+                for (int32_t k = 0; k < njobs; ++k) {
+                    const Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
+                    n1 += b.H <= 31;
+                    ++nall;
+                }
+            }
+            if (2 * n1 < nall)
+                psplit = 0;
+        }
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
                 continue;
@@ -3181,9 +3207,15 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4, 8), lean when
                 // there are no codon moves and no skew / trim; k_dp beyond
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
-                if (t.H <= 31 && lean && psplit && t.P <= 15)
-                    c1p[std::max(0, (t.P - 11) >> 1)].push_back(t);   // P <= 11, 13, 15 (P is odd)
-                else if (t.H <= 31)
+                const int npi = t.H <= 31 ? 0 : t.H <= 63 ? 1 : t.H <= 127 ? 2 : 3;
+                const bool np8 = npi < 3 || (t.H <= 255 && !env_int("RIFRAF_DP_NO_NP8", 0) &&
+                                             env_int("RIFRAF_DP_NP8_LEAN", 1));
+                if (lean && ((psplit >> npi) & 1) && np8) {
+                    int pmi = 0;
+                    while (pmi < 3 && t.P > dpr_pm(npi, pmi))
+                        ++pmi;
+                    cp[npi][pmi].push_back(t);
+                } else if (t.H <= 31)
                     cr[0][lean].push_back(t);
                 else if (t.H <= 63)
                     cr[1][lean].push_back(t);
@@ -3207,10 +3239,11 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 std::stable_sort(c.begin(), c.end(), by_len);
                 all.insert(all.end(), c.begin(), c.end());
             }
-        for (auto &c : c1p) {
-            std::stable_sort(c.begin(), c.end(), by_len);
-            all.insert(all.end(), c.begin(), c.end());
-        }
+        for (auto &cc : cp)
+            for (auto &c : cc) {
+                std::stable_sort(c.begin(), c.end(), by_len);
+                all.insert(all.end(), c.begin(), c.end());
+            }
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
@@ -3227,8 +3260,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 2; ++b)
                 P.nr[a][b] = cr[a][b].size();
-        for (int a = 0; a < 3; ++a)
-            P.nr1p[a] = c1p[a].size();
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                P.nrp[a][b] = cp[a][b].size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -3248,7 +3282,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // largest: the machine stays full through every launch's tail.
     struct Launch {
         int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<64,true>,
-                       // 10..12 = k_dpr<1, true, 11 / 13 / 15>
+                       // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
     };
     std::vector<Launch> launches;
@@ -3260,11 +3294,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     launches.push_back({2 * a + b, at, P.nr[a][b]});
                     at += P.nr[a][b];
                 }
-        for (int a = 0; a < 3; ++a)
-            if (P.nr1p[a]) {
-                launches.push_back({10 + a, at, P.nr1p[a]});
-                at += P.nr1p[a];
-            }
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                if (P.nrp[a][b]) {
+                    launches.push_back({16 + 4 * a + b, at, P.nrp[a][b]});
+                    at += P.nrp[a][b];
+                }
         if (P.n64) {
             launches.push_back({8, at, P.n64});
             at += P.n64;
@@ -3309,13 +3344,16 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
-        } else if (L.kind >= 10) {
+        } else if (L.kind >= 16) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *);
-            const KFn kp[3] = {k_dpr<1, true, 11>, k_dpr<1, true, 13>, k_dpr<1, true, 15>};
-            const int pm = 11 + 2 * (L.kind - 10);
-            hipLaunchKernelGGL(kp[L.kind - 10], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1, pm), st,
-                               d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
+#define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b)>
+            const KFn kp[16] = {KP(0, 0), KP(0, 1), KP(0, 2), KP(0, 3), KP(1, 0), KP(1, 1), KP(1, 2), KP(1, 3),
+                                KP(2, 0), KP(2, 1), KP(2, 2), KP(2, 3), KP(3, 0), KP(3, 1), KP(3, 2), KP(3, 3)};
+#undef KP
+            const int c = L.kind - 16, npi = c >> 2, pmi = c & 3;
+            hipLaunchKernelGGL(kp[c], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)),
+                               st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p);
         } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;
