@@ -1516,9 +1516,19 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
             const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
 #pragma unroll
             for (int u = 0; u < NPF; ++u) {
+#ifdef WS_CLAMP_LOADS
                 const int e = min(u * Q + lt, w2.n16 - 1);
                 pa[u] = ga[e];
                 pb[u] = gb[e];
+#else
+                // predicated: chunks past the window are neither loaded nor
+                // committed (the commit's `e < n16` test)
+                const int e = u * Q + lt;
+                if (e < w2.n16) {
+                    pa[u] = ga[e];
+                    pb[u] = gb[e];
+                }
+#endif
             }
             const double *tm = tabs + R2.tab;
             const int n2 = R2.n;
