@@ -1671,8 +1671,8 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 // VGPRs with spills leave 3 workgroups per CU, latency-bound).  Default 24.
 constexpr int SEG_L = 64;                       // lanes (columns) per work item
 
-template <int SEG_S>
-__global__ void __launch_bounds__(64)
+template <int SEG_S, int SEG_WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SEG_WPE)))
 k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
             const double *__restrict__ tabs, const double *__restrict__ bands,
@@ -2822,15 +2822,24 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     if (pk.seg) {
         // RIFRAF_SEG_S: diagonals per segment (16, 24 or 32)
         const int segs = env_int("RIFRAF_SEG_S", 24);
-        if (segs == 16)
-            hipLaunchKernelGGL(k_score_seg<16>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm);
+        // RIFRAF_SEG_LDS: extra (unused) LDS bytes per workgroup -- caps the
+        // workgroups per CU, i.e. the L2 footprint between a kappa row's reuses
+        const size_t pad = (size_t)env_int("RIFRAF_SEG_LDS", 0);
+        // RIFRAF_SEG_WPE: minimum waves per SIMD the register allocation is
+        // capped for (1: no cap; 2: <= 256 VGPRs)
+        const int wpe = env_int("RIFRAF_SEG_WPE", 1);
+#define RF_SEG_LAUNCH(S, W)                                                                                  \
+    hipLaunchKernelGGL((k_score_seg<S, W>), grid, dim3(64), pad, ctx->stream, items, groups, reads, d_bases, \
+                       d_tabs, d_bands, dense, split, sm)
+        if (segs == 16 && wpe == 2)
+            RF_SEG_LAUNCH(16, 2);
+        else if (segs == 16)
+            RF_SEG_LAUNCH(16, 1);
         else if (segs == 24)
-            hipLaunchKernelGGL(k_score_seg<24>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm);
+            RF_SEG_LAUNCH(24, 1);
         else
-            hipLaunchKernelGGL(k_score_seg<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm);
+            RF_SEG_LAUNCH(32, 1);
+#undef RF_SEG_LAUNCH
     }
     else if (!pk.lean)
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
