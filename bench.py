@@ -112,37 +112,63 @@ def make_read_shard(nreads, length, error_rate, bw, seed, lo, hi):
     return t, reads
 
 
-def cpu_baseline_reads(t, reads, budget_s=12.0, max_threads=16):
+def cpu_threads():
+    """Host cores usable by this process (affinity mask, capped by a cgroup
+    CPU quota when one is set): the CPU baseline runs on all of them."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_baseline_reads(t, reads, budget_s=12.0):
     """Oracle CPU baseline for one read-sharded cluster: realign + all-proposal
-    scoring over chunks of this rank's reads (final bandwidths) until the budget."""
+    scoring over chunks of this rank's reads (final bandwidths) until the
+    budget, on every usable host core.  Also returns the first chunk's totals
+    (the bench's parity check)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
-    threads = max(1, min(max_threads, os.cpu_count() or 1))
+    threads = cpu_threads()
+    chunk = max(16, threads)
     cells = done = 0
+    first = None
     t0 = time.perf_counter()
-    for a in range(0, len(reads), threads):
-        chunk = reads[a:a + threads]
-        _, c = oracle.cpu_pass(t, chunk, nthreads=threads)
+    for a in range(0, len(reads), chunk):
+        tot, c = oracle.cpu_pass(t, reads[a:a + chunk], nthreads=threads)
+        if first is None:
+            first = (a, a + len(reads[a:a + chunk]), tot)
         cells += c
-        done += len(chunk)
+        done += len(reads[a:a + chunk])
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": cells / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{done} reads x {len(t)} bp (final bandwidths), realign + all-proposal scoring "
-                      f"in chunks of {threads}, {dt:.1f} s, OpenMP {threads} threads"}
+                      f"in chunks of {chunk} reads, {dt:.1f} s, OpenMP {threads} threads (all usable cores)"}, first
 
 
-def cpu_baseline(clusters, budget_s=12.0, max_threads=16):
-    """The oracle (C restatement of the reference) on the host cores, over a
-    bounded sample of the same workload (whole clusters until the budget)."""
+def cpu_baseline(clusters, budget_s=12.0):
+    """The oracle (C restatement of the reference) on every usable host core,
+    over a bounded sample of the same workload (whole clusters until the
+    budget), plus the same pass on one thread.  Returns the per-cluster
+    totals of the all-core sample for the bench's parity check."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
-    threads = max(1, min(max_threads, os.cpu_count() or 1))
+    threads = cpu_threads()
     cells = props = done = 0
+    totals = []
     t0 = time.perf_counter()
     for t, reads in clusters:
-        _, c = oracle.cpu_pass(t, reads, nthreads=threads)
+        tot, c = oracle.cpu_pass(t, reads, nthreads=threads)
+        totals.append(tot)
         cells += c
         props += 8 * len(t) + 4
         done += 1
@@ -162,9 +188,23 @@ def cpu_baseline(clusters, budget_s=12.0, max_threads=16):
     return {"value": cells / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
             "proposals_per_s": props / dt, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{done} cluster(s) x {len(clusters[0][1])} reads x {len(clusters[0][0])} bp, "
-                      f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads",
+                      f"realign + all-proposal scoring, {dt:.1f} s, OpenMP {threads} threads (all usable cores)",
             "single_thread": {"value": c1 / dt1 / 1e9, "unit": "GCUPS", "cores": 1,
-                              "sample": f"{d1} cluster(s), {dt1:.1f} s"}}
+                              "sample": f"{d1} cluster(s), {dt1:.1f} s"}}, totals
+
+
+def parity_check(got, expected, templates):
+    """Bench self-check: GPU dense totals vs the oracle's for the clusters the
+    CPU baseline ran (every STAGE_SCORE proposal slot, bit for bit)."""
+    bad = checked = 0
+    for g, e, t in zip(got, expected, templates):
+        mask = np.ones(e.shape, bool)
+        mask[0, :5] = False                                  # p = 0: no sub / del
+        mask[np.arange(1, len(t) + 1), np.asarray(t, np.int64)] = False   # the consensus base
+        a, b = np.asarray(g)[mask], e[mask]
+        bad += int(np.sum(~((a == b) | (np.isnan(a) & np.isnan(b)))))
+        checked += int(mask.sum())
+    return {"clusters": len(expected), "proposal_totals": checked, "mismatches": bad, "bitexact": bad == 0}
 
 
 def _cpu_model():
@@ -217,6 +257,8 @@ def main():
     ap.add_argument("--clusters", type=int, default=None, help="clusters per rank (override)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="c4 only: skip the secondary c5 (10 kb, band doubling) workload")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
@@ -241,7 +283,27 @@ def main():
         coll = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
 
     if args.config == "c5":
-        return run_read_sharded(args, rank, world, gpu, dist, torch, coll)
+        result = run_read_sharded(args, rank, world, gpu, dist, torch, coll)
+    else:
+        result = run_clusters(args, rank, world, gpu, dist, torch, coll)
+        if args.config == "c4" and not args.no_secondary:
+            # configs[4] beside the headline line: driver-measured 10 kb reads
+            # with band doubling, read-sharded over the same ranks
+            result["secondary"] = run_read_sharded(args, rank, world, gpu, dist, torch, coll)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _sync_fn(torch):
+    if torch is not None and torch.cuda.is_available():
+        return lambda: torch.cuda.synchronize()
+    return lambda: None
+
+
+def run_clusters(args, rank, world, gpu, dist, torch, coll):
+    """configs[3] (default): this rank's clusters, realign + dense scoring."""
     nclu, nreads, length, err, bw, label = CONFIGS[args.config]
     if args.clusters is not None:
         nclu = args.clusters
@@ -287,7 +349,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    sync = (lambda: torch.cuda.synchronize()) if (torch is not None and torch.cuda.is_available()) else (lambda: None)
+    sync = _sync_fn(torch)
     if dist is not None:
         dist.barrier()
     sync()
@@ -354,24 +416,51 @@ def main():
         "setup_s": gen_s,
     }
     if rank == 0:
+        # the timed launch's totals (same plan: downloaded, not recomputed)
+        dense = eng.score_dense(groups, rows=[len(t) + 1 for t, _ in clusters])
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(clusters, budget_s=args.cpu_budget)
+            result["cpu_baseline"], ref = cpu_baseline(clusters, budget_s=args.cpu_budget)
         else:
             result["cpu_baseline"] = None
-        print(json.dumps(result), flush=True)
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle  # test infrastructure: the parity check only
+            ref = [oracle.cpu_pass(t, rs, nthreads=cpu_threads())[0] for t, rs in clusters[:2]]
+        result["parity"] = parity_check(dense[:len(ref)], ref, [t for t, _ in clusters[:len(ref)]])
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return result
+
+
+class _TimedEngine:
+    """Engine proxy for smart_forward_moves!: accumulates the kernel time of
+    every band-doubling realign / backtrace and the DP cells it executes."""
+
+    def __init__(self, eng, reads, m):
+        self.e, self.reads, self.m = eng, reads, m
+        self.dp_ms = self.bt_ms = 0.0
+        self.cells = self.rounds = 0
+
+    def realign(self, slots, seqs, tpls, bws, flags):
+        out = self.e.realign(slots, seqs, tpls, bws, flags)
+        self.dp_ms += self.e.last_timing()[0]
+        self.cells += sum(band_cells(len(self.reads[int(k)]), self.m, int(b)) for k, b in zip(seqs, bws))
+        self.rounds += 1
+        return out
+
+    def backtrace(self, slots, want_moves=True):
+        out = self.e.backtrace(slots, want_moves)
+        self.bt_ms += self.e.last_backtrace_ms()
+        return out
 
 
 def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     """configs[4]: ONE cluster whose reads are split over the ranks.  Setup
-    (untimed): each rank simulates and uploads its block of reads and runs the
-    band-doubling first realign (smart_forward_moves!, model.jl:643-672).
-    Step: fwd+bwd DP of the rank's reads at their final bandwidths, the
-    rank's partial fold of every STAGE_SCORE proposal (rf_score_dense_dev),
-    then the exchange: all-gather of the partial totals over RCCL + rank-order
-    sum (rifraf_amd.sharded).  Total work is fixed: strong scaling."""
+    (untimed, reported): each rank simulates and uploads its block of reads
+    and runs the band-doubling first realign (smart_forward_moves!,
+    model.jl:643-672), timed separately with its DP cells.  Step: fwd+bwd DP
+    of the rank's reads at their final bandwidths, the rank's partial fold of
+    every STAGE_SCORE proposal (rf_score_dense_dev), then the exchange:
+    all-gather of the partial totals over RCCL + rank-order sum
+    (rifraf_amd.sharded).  Total work is fixed: strong scaling."""
     from types import SimpleNamespace
     from rifraf_amd.engine import RF_BWD, RF_FWD, Engine
     from rifraf_amd.model import smart_forward_moves
@@ -391,10 +480,17 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     for a in range(0, nloc, 1024):
         eng.set_sequences(a, reads[a:a + 1024])
     eng.set_templates(0, [t])
+    timed = _TimedEngine(eng, reads, length)
     t_dbl = time.perf_counter()
-    cells_first = sum(band_cells(len(r), length, r.bandwidth) for r in reads)
-    smart_forward_moves(SimpleNamespace(e=eng), [(k, k) for k in range(nloc)], reads, length, 0.1)
+    smart_forward_moves(SimpleNamespace(e=timed), [(k, k) for k in range(nloc)], reads, length, 0.1)
     dbl_s = time.perf_counter() - t_dbl
+    # alignment_proposals (model.jl:483-497) over the doubled forward bands:
+    # the walk + proposal marking of every read, one launch
+    sl_all = np.arange(nloc, dtype=np.int32)
+    bws0 = np.array([r.bandwidth for r in reads], np.int32)
+    eng.realign(sl_all, sl_all, 0, bws0, RF_FWD)
+    eng.alignment_proposals([sl_all], True)
+    aln_ms = eng.last_backtrace_ms()
     eng.close()
     eng = Engine(local)
     eng.reserve(sum(2 * band_bytes(len(r), length, r.bandwidth) for r in reads) + (256 << 20))
@@ -431,7 +527,7 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
 
     for _ in range(args.warmup):
         step()
-    sync = (lambda: torch.cuda.synchronize()) if (torch is not None and torch.cuda.is_available()) else (lambda: None)
+    sync = _sync_fn(torch)
     if dist is not None:
         dist.barrier()
     sync()
@@ -442,10 +538,11 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     doubled = int(np.sum(bws > bw))
-    units = [cells * args.steps, nloc * nprops * args.steps, doubled, nloc]
+    units = [cells * args.steps, nloc * nprops * args.steps, doubled, nloc, timed.cells, dbl_s,
+             timed.dp_ms, timed.bt_ms, aln_ms]
     if dist is not None:
         elapsed, units = aggregate(elapsed, units, coll)
-    tot_cells, tot_pairs, tot_doubled, tot_reads = units
+    tot_cells, tot_pairs, tot_doubled, tot_reads, dbl_cells, _, _, _, _ = units
     dp_ms = float(np.mean([r[0] for r in rec]))
     sc_ms = float(np.mean([r[1] for r in rec]))
     xch_ms = float(np.mean([r[2] for r in rec]))
@@ -479,8 +576,17 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
                     "peak_tops": FP64_VEC_TFLOPS / 2,
                     "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2)},
-        "band_doubling": {"reads_doubled": tot_doubled, "reads": tot_reads,
-                          "first_pass_cells_rank0": cells_first, "setup_s_rank0": dbl_s},
+        # smart_forward_moves! (first realign of every read): forward fills at
+        # bw, the backtrace walks that count errors, the redone fills of the
+        # reads whose band doubled -- every executed cell counted (rank 0's
+        # kernel times; cells summed over ranks)
+        "band_doubling": {"reads_doubled": tot_doubled, "reads": tot_reads, "cells_executed": dbl_cells,
+                          "rounds_rank0": timed.rounds, "dp_ms_rank0": timed.dp_ms,
+                          "backtrace_ms_rank0": timed.bt_ms, "wall_s_rank0": dbl_s,
+                          "gcups_kernel_rank0": (timed.cells / (timed.dp_ms * 1e-3) / 1e9) if timed.dp_ms else None},
+        # alignment_proposals (model.jl:483-497): walk + mark every read's
+        # proposals (one rf_alignment_proposals launch, rank 0)
+        "alignment_proposals_ms_rank0": aln_ms,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                      "traffic": pmc_traffic("c5", len(reads), dominant),
@@ -492,12 +598,19 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         "setup_s": gen_s,
     }
     if rank == 0:
-        result["cpu_baseline"] = (cpu_baseline_reads(t, reads, budget_s=args.cpu_budget)
-                                  if world == 1 and not args.no_cpu else None)
-        print(json.dumps(result), flush=True)
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"], first = cpu_baseline_reads(t, reads, budget_s=args.cpu_budget)
+        else:
+            import oracle  # test infrastructure: the parity check only
+            result["cpu_baseline"] = None
+            first = (0, 16, oracle.cpu_pass(t, reads[:16], nthreads=cpu_threads())[0])
+        a, b, ref = first
+        got = eng.score_dense([slots[a:b]])[0]
+        result["parity"] = parity_check([got], [ref], [t])
+        result["parity"]["reads"] = b - a
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

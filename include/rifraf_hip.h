@@ -32,9 +32,14 @@
  *    (Insertion(0, b) inserts before the first base). kind: 0 = Substitution,
  *    1 = Insertion, 2 = Deletion.
  *  - Bands stay device resident between calls.  A "slot" is one alignment
- *    (sequence x template) owning an A band and a B band, each H x (m+1)
- *    FP64, column-major, H = 2*bw + |n-m| + 1 -- the reference layout
- *    data[(i-j)+h_off+bw+1, j] (src/bandedarrays.jl:101-114).
+ *    (sequence x template) owning an A band and a B band: the H x (m+1) FP64
+ *    cells of the reference's data[(i-j)+h_off+bw+1, j]
+ *    (src/bandedarrays.jl:101-114), H = 2*bw + |n-m| + 1.  On the device a
+ *    band is stored anti-diagonal ("kappa") major: cell (d, j) (0-based data
+ *    row d, column j) at kappa = d + 2j, element d >> 1 of a kappa row of
+ *    P = ((H+1) >> 1) | 1 doubles; the B band is stored
+ *    already flipped.  rf_download_band converts to the reference's
+ *    column-major data.
  *  - One context per host thread; calls are synchronous on the context's
  *    HIP stream.  No torch types cross this boundary.
  */
@@ -73,6 +78,26 @@ int rf_abi_version(void);
 int rf_create(int device, rf_ctx **out);
 int rf_destroy(rf_ctx *ctx);
 const char *rf_last_error(const rf_ctx *ctx);
+
+/* Tuning options of a context (rf_set_option / rf_get_option keys).  Every
+ * value selects between code paths with bit-identical results; the defaults
+ * are read once from the RIFRAF_* environment at rf_create.  No reference
+ * counterpart (the reference has one code path). */
+#define RF_OPT_SCORE_MODE   1   /* 0 auto, 1 fused in-kernel fold, 2 split + k_reduce  */
+#define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_seg            */
+#define RF_OPT_LEAN_NW      3   /* 8 = k_score_ws; 1, 2, 4 = k_score_lean waves         */
+#define RF_OPT_LEAN_LDS_KB  4   /* lean scorer LDS budget (0 = default)                */
+#define RF_OPT_WS_Q         5   /* k_score_ws chain lanes: 256 or 128                  */
+#define RF_OPT_SEG_S        6   /* k_score_seg diagonals per segment: 16, 24, 32       */
+#define RF_OPT_SEG_LDS      7   /* k_score_seg extra LDS bytes per workgroup           */
+#define RF_OPT_SEG_WPE      8   /* k_score_seg waves-per-EU register cap: 1, 2         */
+#define RF_OPT_BT_GLOBAL    9   /* 1: every backtrace walk in k_backtrace              */
+#define RF_OPT_DP_PSPLIT   10   /* lean DP stride-class split mask (-1 auto)           */
+#define RF_OPT_DP_NP8      11   /* 0: H 128..255 bands in k_dp<64> instead of k_dpr<8> */
+#define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
+#define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
+int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
+int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 
 /* Pre-size the device band arena (bytes); optional. */
 int rf_reserve(rf_ctx *ctx, int64_t band_bytes);
@@ -182,6 +207,9 @@ int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes
  * context stream), milliseconds; used by bench.py's roofline. */
 int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms,
                    double *gather_ms);
+/* Kernel time of the walks of the last rf_backtrace / rf_alignment_proposals
+ * call (k_bt_win / k_backtrace / k_aln_props), milliseconds. */
+int rf_last_backtrace_ms(const rf_ctx *ctx, double *ms);
 
 #ifdef __cplusplus
 }

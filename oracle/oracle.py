@@ -54,6 +54,9 @@ def lib():
         L.or_score_proposal.argtypes = [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                         POINTER(OrSeq), c_void_p, POINTER(c_double)]
         L.or_score_total.restype = c_int
+        L.or_score_list.restype = c_int
+        L.or_score_list.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int]
         L.or_pass.restype = c_int64
         L.or_pass.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int]
         L.or_seq_tables.restype = None
@@ -176,6 +179,34 @@ def seq_tables(lp, scores):
                         scores.codon_insertion, scores.codon_deletion, *[_p(x) for x in out],
                         ctypes.byref(ne))
     return out, ne.value
+
+
+def score_list(props, As, Bs, rss, t, Aref=None, Bref=None, ref=None, per_seq=False, nthreads=4):
+    """model.jl:385-399 over a proposal list (kind, pos, base arrays) with
+    column-major A/B data per sequence (as forward()/backward() return).
+    Returns totals (and the per-sequence matrix [k, r] if per_seq)."""
+    kind, pos, base = (np.ascontiguousarray(x, np.int32) for x in props)
+    P = len(kind)
+    seqs = [Seq(r) for r in rss]
+    keep = [np.ascontiguousarray(np.asarray(A).T) for A in As] + [np.ascontiguousarray(np.asarray(B).T) for B in Bs]
+    R = len(seqs)
+    aptr = (c_void_p * max(R, 1))(*[k.ctypes.data for k in keep[:R]])
+    bptr = (c_void_p * max(R, 1))(*[k.ctypes.data for k in keep[R:]])
+    arr = (OrSeq * max(R, 1))(*[s.st for s in seqs])
+    rseq = Seq(ref) if ref is not None else None
+    ra = np.ascontiguousarray(np.asarray(Aref).T) if ref is not None else None
+    rb = np.ascontiguousarray(np.asarray(Bref).T) if ref is not None else None
+    width = R + (1 if ref is not None else 0)
+    total = np.zeros(max(P, 1))
+    per = np.zeros((max(P, 1), max(width, 1))) if per_seq else None
+    t = np.ascontiguousarray(t, np.uint8)
+    _chk(lib().or_score_list(P, _p(kind), _p(pos), _p(base), R, ctypes.cast(aptr, c_void_p),
+                             ctypes.cast(bptr, c_void_p), ctypes.cast(arr, c_void_p), _p(ra), _p(rb),
+                             ctypes.cast(ctypes.pointer(rseq.st), c_void_p) if rseq is not None else None, _p(t), len(t),
+                             _p(per), _p(total), int(nthreads)))
+    if per_seq:
+        return total[:P], per[:P, :width]
+    return total[:P]
 
 
 def cpu_pass(t, rss, nthreads=1):

@@ -553,6 +553,55 @@ int or_score_total(int kind, int pos, int base, int nseqs,
     return OR_OK;
 }
 
+/* model.jl:385-399 for a proposal list, proposals in parallel */
+int or_score_list(int nprops, const int32_t *kind, const int32_t *pos, const int32_t *base,
+                  int nseqs, const double *const *As, const double *const *Bs,
+                  const or_seq *seqs, const double *Aref, const double *Bref,
+                  const or_seq *ref, const uint8_t *t, int m,
+                  double *per, double *total, int nthreads)
+{
+    const int width = nseqs + (ref ? 1 : 0);
+    int maxn = ref ? ref->n : 0;
+    for (int r = 0; r < nseqs; r++)
+        maxn = imax(maxn, seqs[r].n);
+    int *errs = (int *)calloc((size_t)(nprops > 0 ? nprops : 1), sizeof(int));
+#ifdef _OPENMP
+    if (nthreads < 1)
+        nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        double *newcols = (double *)malloc(sizeof(double) * (size_t)(maxn + 1) * (CODON_LENGTH + 1));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 16)
+#endif
+        for (int k = 0; k < nprops; k++) {
+            double score = 0.0;
+            int err = 0;
+            for (int r = 0; r < width && !err; r++) {
+                double sc = 0.0;
+                if (r < nseqs)
+                    err = or_score_proposal(kind[k], pos[k], base[k], As[r], Bs[r], t, m, &seqs[r], newcols, &sc);
+                else
+                    err = or_score_proposal(kind[k], pos[k], base[k], Aref, Bref, t, m, ref, newcols, &sc);
+                if (!err) {
+                    score += sc;
+                    if (per)
+                        per[(size_t)k * width + r] = sc;
+                }
+            }
+            errs[k] = err;
+            total[k] = score;
+        }
+        free(newcols);
+    }
+    int first = 0;
+    for (int k = 0; k < nprops && !first; k++)
+        first = errs[k];
+    free(errs);
+    return first;
+}
+
 /* CPU baseline pass: realign (forward_moves! + backward!) every read, then
  * score the dense STAGE_SCORE all_proposals set (model.jl:401-456) with the
  * left-fold total of model.jl:385-399. */

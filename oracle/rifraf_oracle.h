@@ -130,6 +130,18 @@ int or_score_total(int kind, int pos, int base, int nseqs,
  * nthreads > 1 parallelises over reads (DP) and positions (scoring).
  * Returns cells computed; totals laid out [pos 0..m][9] (sub A,C,G,T | del |
  * ins A,C,G,T) matching the engine's dense layout. */
+/* model.jl:385-399 over a proposal list (the get_candidates / estimate_probs
+ * loop, model.jl:519-523, :762-763): total[k] = 0.0 + s_1 + ... + s_R (+ s_ref)
+ * and optionally per[k * width + r] = s_r (width = nseqs + (ref != NULL)).
+ * Proposals are independent (OpenMP over k); the returned error is the one
+ * the reference raises first (the earliest failing proposal, and within it
+ * the earliest failing sequence). */
+int or_score_list(int nprops, const int32_t *kind, const int32_t *pos, const int32_t *base,
+                  int nseqs, const double *const *As, const double *const *Bs,
+                  const or_seq *seqs, const double *Aref, const double *Bref,
+                  const or_seq *ref, const uint8_t *t, int m,
+                  double *per, double *total, int nthreads);
+
 int64_t or_pass(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
                 double *totals, int nthreads);
 

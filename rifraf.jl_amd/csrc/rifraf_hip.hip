@@ -2525,6 +2525,29 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
+// selects between bit-identical code paths; defaults come from the RIFRAF_*
+// environment once, at rf_create, and never from a hot path.
+struct Opts {
+    int score_mode = 0;     // RF_OPT_SCORE_MODE: 0 auto, 1 fused, 2 split
+    int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg
+    int lean_nw = 8;        // RF_OPT_LEAN_NW: 8 = k_score_ws, 1/2/4 = k_score_lean waves
+    int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: 0 = default budget
+    int ws_q = 256;         // RF_OPT_WS_Q: k_score_ws chain lanes (256 or 128)
+    int seg_s = 24;         // RF_OPT_SEG_S: k_score_seg diagonals per segment (16, 24, 32)
+    int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
+    int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
+    int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
+    int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
+    int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
+    int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
+    int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
+#ifdef RIFRAF_DIAG
+    int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
+    int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
+#endif
+};
+
 }  // namespace
 
 struct rf_ctx {
@@ -2549,7 +2572,10 @@ struct rf_ctx {
     size_t pinned_bytes = 0;
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
-    double dp_ms = 0, score_ms = 0, gather_ms = 0;
+    double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
+    Opts opt;
+    uint64_t opt_gen = 0;      // bumped by rf_set_option (scorer plan key)
+    std::vector<BTTask> bt_win, bt_old;   // backtrace descriptors of the last launch
     // host-side plan caches: a repeated call with identical arguments and an
     // unchanged layout reuses the uploaded descriptors (steady-state loops)
     struct {
@@ -2561,6 +2587,7 @@ struct rf_ctx {
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
+        std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
     } rplan;
     struct {
         bool valid = false;
@@ -2570,7 +2597,13 @@ struct rf_ctx {
         int max_reads = 0, ngroups = 0;
         int64_t dense_total = 0, split_total = 0;
         ScorePick pick;
-        std::string envkey;
+        uint64_t opt_gen = 0;
+        // host copies of the uploaded descriptors: alive until the uploads
+        // they source have completed (hipMemcpyAsync from pageable memory)
+        std::vector<WorkItem> items;
+        std::vector<ScoreGroup> groups;
+        std::vector<ScoreRead> reads;
+        std::vector<int64_t> gstart;
     } dplan;
 };
 
@@ -2750,37 +2783,48 @@ int env_int(const char *name, int dflt)
     return (v && *v) ? std::atoi(v) : dflt;
 }
 
-// environment knobs of the scorer choice, as a plan-cache key
-std::string scorer_env_key()
+// option defaults from the environment (rf_create only)
+void load_env_opts(Opts &o)
 {
-    std::string k;
-    for (const char *n : {"RIFRAF_SCORE_KERNEL", "RIFRAF_LEAN_NW", "RIFRAF_LEAN_LDS_KB", "RIFRAF_WS_Q"}) {
-        const char *v = std::getenv(n);
-        k += v ? v : "-";
-        k += '|';
-    }
-    return k;
+    if (const char *k = std::getenv("RIFRAF_SCORE_KERNEL"))
+        o.score_kernel = !std::strcmp(k, "general") ? 1 : !std::strcmp(k, "seg") ? 2 : 0;
+    if (const char *m = std::getenv("RIFRAF_SCORE_MODE"))
+        o.score_mode = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "split") ? 2 : 0;
+    o.lean_nw = env_int("RIFRAF_LEAN_NW", o.lean_nw);
+    o.lean_lds_kb = env_int("RIFRAF_LEAN_LDS_KB", o.lean_lds_kb);
+    o.ws_q = env_int("RIFRAF_WS_Q", o.ws_q);
+    o.seg_s = env_int("RIFRAF_SEG_S", o.seg_s);
+    o.seg_lds = env_int("RIFRAF_SEG_LDS", o.seg_lds);
+    o.seg_wpe = env_int("RIFRAF_SEG_WPE", o.seg_wpe);
+    o.bt_global = env_int("RIFRAF_BT_GLOBAL", o.bt_global);
+    o.dp_psplit = env_int("RIFRAF_DP_PSPLIT", o.dp_psplit);
+    o.dp_np8 = env_int("RIFRAF_DP_NO_NP8", 0) ? 0 : 1;
+    o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
+    o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
+#ifdef RIFRAF_DIAG
+    o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
+    o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
+#endif
 }
 
-ScorePick pick_scorer(const std::vector<ScoreRead> &reads, bool all_finite)
+ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool all_finite)
 {
     ScorePick p;
-    const char *kern = std::getenv("RIFRAF_SCORE_KERNEL");
-    const bool force_general = kern && !std::strcmp(kern, "general");
-    const bool force_seg = kern && !std::strcmp(kern, "seg");
+    const bool force_general = o.score_kernel == 1;
+    const bool force_seg = o.score_kernel == 2;
     if (all_finite && !force_general && !force_seg && !reads.empty()) {
         int need1 = 0;
         for (const auto &R : reads)
             need1 = std::max(need1, lean_need(1, R.H, R.P));
         // 8 = wave-specialized k_score_ws (256 chain lanes + 256 loader lanes)
-        int nw = env_int("RIFRAF_LEAN_NW", 8);
+        int nw = o.lean_nw;
         nw = nw >= 8 ? 8 : (nw >= 4 ? 4 : (nw >= 2 ? 2 : 1));
         // k_score_ws with 128 chain lanes: two workgroups (two windows in
         // flight) per CU, each with half the LDS
         // (measured at c4: 128 -> +14 %, 320 / 384 chain lanes -> +50 % scoring time)
-        const int wsq = (nw == 8 && env_int("RIFRAF_WS_Q", 256) == 128) ? 128 : 256;
+        const int wsq = (nw == 8 && o.ws_q == 128) ? 128 : 256;
         const int dflt_kb = nw >= 4 ? (wsq == 128 ? 80 : 160) : 40 * nw;
-        const int lds = std::max(env_int("RIFRAF_LEAN_LDS_KB", dflt_kb) * 1024 / 8, need1);
+        const int lds = std::max((o.lean_lds_kb > 0 ? o.lean_lds_kb : dflt_kb) * 1024 / 8, need1);
         if (lds <= 160 * 1024 / 8) {
             p.lean = true;
             p.nw = nw;
@@ -2815,19 +2859,23 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     const uint8_t *d_bases = (const uint8_t *)ctx->bytes_arena.d;
     const double *d_tabs = (const double *)ctx->tab_arena.d;
     const double *d_bands = (const double *)ctx->band_arena.d;
-    // RIFRAF_LEAN_NOCOMP=1: diagnostics only -- the lean scorer stages every
-    // window but skips the chains (measures its load pipeline alone)
-    const int sm = (split ? 1 : 0) | (env_int("RIFRAF_LEAN_NOCOMP", 0) ? 2 : 0);
+    int sm = split ? 1 : 0;
+#ifdef RIFRAF_DIAG
+    // RIFRAF_LEAN_NOCOMP=1 (diagnostic builds only): the lean scorer stages
+    // every window but skips the chains (measures its load pipeline alone)
+    if (ctx->opt.diag_lean_nocomp)
+        sm |= 2;
+#endif
     dim3 grid(nitems, gy);
     if (pk.seg) {
-        // RIFRAF_SEG_S: diagonals per segment (16, 24 or 32)
-        const int segs = env_int("RIFRAF_SEG_S", 24);
-        // RIFRAF_SEG_LDS: extra (unused) LDS bytes per workgroup -- caps the
+        // RF_OPT_SEG_S: diagonals per segment (16, 24 or 32)
+        const int segs = ctx->opt.seg_s;
+        // RF_OPT_SEG_LDS: extra (unused) LDS bytes per workgroup -- caps the
         // workgroups per CU, i.e. the L2 footprint between a kappa row's reuses
-        const size_t pad = (size_t)env_int("RIFRAF_SEG_LDS", 0);
-        // RIFRAF_SEG_WPE: minimum waves per SIMD the register allocation is
+        const size_t pad = (size_t)std::max(ctx->opt.seg_lds, 0);
+        // RF_OPT_SEG_WPE: minimum waves per SIMD the register allocation is
         // capped for (1: no cap; 2: <= 256 VGPRs)
-        const int wpe = env_int("RIFRAF_SEG_WPE", 1);
+        const int wpe = ctx->opt.seg_wpe;
 #define RF_SEG_LAUNCH(S, W)                                                                                  \
     hipLaunchKernelGGL((k_score_seg<S, W>), grid, dim3(64), pad, ctx->stream, items, groups, reads, d_bases, \
                        d_tabs, d_bands, dense, split, sm)
@@ -2888,6 +2936,7 @@ int rf_create(int device, rf_ctx **out)
         delete ctx;
         return RF_ERR_HIP;
     }
+    load_env_opts(ctx->opt);
     for (auto &e : ctx->ev)
         (void)hipEventCreate(&e);
     (void)hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
@@ -2946,6 +2995,53 @@ int rf_destroy(rf_ctx *ctx)
 }
 
 const char *rf_last_error(const rf_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+static int *opt_slot(rf_ctx *ctx, int32_t key)
+{
+    Opts &o = ctx->opt;
+    switch (key) {
+    case RF_OPT_SCORE_MODE: return &o.score_mode;
+    case RF_OPT_SCORE_KERNEL: return &o.score_kernel;
+    case RF_OPT_LEAN_NW: return &o.lean_nw;
+    case RF_OPT_LEAN_LDS_KB: return &o.lean_lds_kb;
+    case RF_OPT_WS_Q: return &o.ws_q;
+    case RF_OPT_SEG_S: return &o.seg_s;
+    case RF_OPT_SEG_LDS: return &o.seg_lds;
+    case RF_OPT_SEG_WPE: return &o.seg_wpe;
+    case RF_OPT_BT_GLOBAL: return &o.bt_global;
+    case RF_OPT_DP_PSPLIT: return &o.dp_psplit;
+    case RF_OPT_DP_NP8: return &o.dp_np8;
+    case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
+    case RF_OPT_DP_STREAMS: return &o.dp_streams;
+    default: return nullptr;
+    }
+}
+
+int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value)
+{
+    if (!ctx)
+        return RF_ERR_ARG;
+    int *s = opt_slot(ctx, key);
+    if (!s)
+        return fail(ctx, RF_ERR_ARG, "rf_set_option: unknown option");
+    if (*s != value) {
+        *s = value;
+        ++ctx->opt_gen;
+        ctx->rplan.valid = false;   // DP class split depends on options
+    }
+    return 0;
+}
+
+int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value)
+{
+    if (!ctx || !value)
+        return RF_ERR_ARG;
+    int *s = opt_slot(ctx, key);
+    if (!s)
+        return fail(ctx, RF_ERR_ARG, "rf_get_option: unknown option");
+    *value = *s;
+    return 0;
+}
 
 int rf_reserve(rf_ctx *ctx, int64_t band_bytes)
 {
@@ -3145,11 +3241,13 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
     } else {
+        P.valid = false;
         int32_t maxslot = -1;
         for (int32_t k = 0; k < njobs; ++k)
             maxslot = std::max(maxslot, slot[k]);
         if (maxslot >= (int32_t)ctx->slots.size())
             ctx->slots.resize(maxslot + 1);
+        bool moved = false;   // a band now describes another alignment
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
                 continue;
@@ -3161,6 +3259,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 if (int e = region_ensure(ctx, ctx->band_arena, b.r,
                                           band_K(H, T.m) * band_P(H) * 8))
                     return e;
+                moved = moved || !b.valid || b.seq != seq[k] || b.tpl != tpl[k] || b.bw != bw[k] ||
+                        b.n != S.n || b.m != T.m || b.H != H;
                 b.valid = true;
                 b.seq = seq[k];
                 b.tpl = tpl[k];
@@ -3172,15 +3272,20 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 b.tplver = T.version;
             }
         }
+        // scorer descriptors (rf_score_dense's plan) hold band geometry and
+        // sequence offsets: a band that now describes another read, template or
+        // bandwidth invalidates them even when its region did not move
+        if (moved)
+            ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
         std::vector<DPTask> cr[4][2], c64, cg, cp[4][4];
         int hmax64 = 0, hmaxg = 0;
-        // RIFRAF_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
+        // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
         // of the tasks -- measured: c4 DP -5..9 %; splitting the wide classes,
         // or a small NP = 1 class next to them (c5), made the fill slower)
-        int psplit = env_int("RIFRAF_DP_PSPLIT", 1);
-        if (!std::getenv("RIFRAF_DP_PSPLIT")) {
+        int psplit = ctx->opt.dp_psplit >= 0 ? ctx->opt.dp_psplit : 1;
+        if (ctx->opt.dp_psplit < 0) {
             size_t n1 = 0, nall = 0;
             for (int dir = 0; dir < 2; ++dir) {
                 if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
@@ -3215,10 +3320,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.ncdel = S.ncdel;
                 t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (flags & RF_SKEW) ? 2 : 0) |
                           (dir == 0 && (flags & RF_TRIM) ? 4 : 0);
-                // RIFRAF_DP_SINK=1: diagnostics only -- the blocked interior's band
-                // stores all go to one small sink buffer (bands are then invalid)
-                if (env_int("RIFRAF_DP_SINK", 0))
+#ifdef RIFRAF_DIAG
+                // RIFRAF_DP_SINK=1 (diagnostic builds only): the blocked interior's
+                // band stores all go to one small sink buffer (bands are then invalid)
+                if (ctx->opt.diag_dp_sink)
                     t.flags |= 512;
+#endif
                 // out_score: forward scores win when both directions run
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
@@ -3227,8 +3334,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // there are no codon moves and no skew / trim; k_dp beyond
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
                 const int npi = t.H <= 31 ? 0 : t.H <= 63 ? 1 : t.H <= 127 ? 2 : 3;
-                const bool np8 = npi < 3 || (t.H <= 255 && !env_int("RIFRAF_DP_NO_NP8", 0) &&
-                                             env_int("RIFRAF_DP_NP8_LEAN", 1));
+                const bool np8 = npi < 3 || (t.H <= 255 && ctx->opt.dp_np8 && ctx->opt.dp_np8_lean);
                 if (lean && ((psplit >> npi) & 1) && np8) {
                     int pmi = 0;
                     while (pmi < 3 && t.P > dpr_pm(npi, pmi))
@@ -3240,8 +3346,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     cr[1][lean].push_back(t);
                 else if (t.H <= 127)
                     cr[2][lean].push_back(t);
-                else if (t.H <= 255 && !env_int("RIFRAF_DP_NO_NP8", 0))
-                    cr[3][env_int("RIFRAF_DP_NP8_LEAN", 1) ? lean : 0].push_back(t);
+                else if (t.H <= 255 && ctx->opt.dp_np8)
+                    cr[3][ctx->opt.dp_np8_lean ? lean : 0].push_back(t);
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
@@ -3252,7 +3358,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             }
         }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
-        std::vector<DPTask> all;
+        std::vector<DPTask> &all = P.tasks;
+        all.clear();
         for (auto &cc : cr)
             for (auto &c : cc) {
                 std::stable_sort(c.begin(), c.end(), by_len);
@@ -3337,7 +3444,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     for (size_t i = 1; i < launches.size(); ++i)
         if (launches[i].n > launches[big].n)
             big = i;
-    const bool concurrent = launches.size() > 1 && env_int("RIFRAF_DP_STREAMS", 1);
+    const bool concurrent = launches.size() > 1 && ctx->opt.dp_streams;
     if (concurrent)
         HIPCHK(ctx, hipEventRecord(ctx->fork, ctx->stream));
     int nside = 0;
@@ -3409,14 +3516,17 @@ static bool bt_windowed(const BTTask &t) { return t.ncins == 0 && t.ncdel == 0 &
 static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d_mask, int do_indels)
 {
     const int32_t nslots = (int32_t)tasks.size();
-    std::vector<BTTask> win, old;
+    std::vector<BTTask> &win = ctx->bt_win, &old = ctx->bt_old;   // alive until the caller's sync
+    win.clear();
+    old.clear();
     for (const auto &t : tasks)
         (bt_windowed(t) ? win : old).push_back(t);
-    if (std::getenv("RIFRAF_BT_LEGACY") && !d_mask) {   // diagnostics: every walk in k_backtrace
+    if (ctx->opt.bt_global && !d_mask) {   // RF_OPT_BT_GLOBAL: every walk in k_backtrace
         old = tasks;
         win.clear();
     }
     int32_t *d_cnt = (int32_t *)ctx->scratch[4].p;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     if (!old.empty()) {
         if (int e = upload(ctx, ctx->scratch[0], old))
             return e;
@@ -3435,7 +3545,16 @@ static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d
                            (int8_t *)ctx->scratch[3].p, d_cnt, d_cnt + nslots, ctx->d_err, d_mask, do_indels);
     }
     HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     return 0;
+}
+
+// kernel time of the last launch_backtraces (after the caller's sync)
+static void note_bt_ms(rf_ctx *ctx)
+{
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]) == hipSuccess)
+        ctx->bt_ms = ms;
 }
 
 // Backtrace descriptors of `nslots` slots (moves slot k at offs[k], n+m bytes)
@@ -3507,6 +3626,8 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
                                        ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (nslots > 0)
+        note_bt_ms(ctx);
     if (int e = check_err(ctx))
         return e;
     for (int32_t k = 0; k < nslots; ++k) {
@@ -3577,6 +3698,7 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    note_bt_ms(ctx);
     return check_err(ctx);
 }
 
@@ -3720,16 +3842,14 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     }
     // split mode: not enough (group, chunk) items to fill the chip, or the
     // caller wants per-read scores
-    // RIFRAF_SCORE_MODE=fused|split overrides the choice (tests cover both)
+    // RF_OPT_SCORE_MODE = fused | split overrides the choice (tests cover both)
     bool split = out_per_seq != nullptr || ((int64_t)items.size() < 2048 && max_reads > 1);
-    if (const char *mode = std::getenv("RIFRAF_SCORE_MODE")) {
-        if (!std::strcmp(mode, "fused") && !out_per_seq)
-            split = false;
-        else if (!std::strcmp(mode, "split"))
-            split = true;
-    }
+    if (ctx->opt.score_mode == 1 && !out_per_seq)
+        split = false;
+    else if (ctx->opt.score_mode == 2)
+        split = true;
 
-    const ScorePick pick = pick_scorer(reads, all_finite);
+    const ScorePick pick = pick_scorer(ctx->opt, reads, all_finite);
     if (pick.lean && pick.q() != 64)
         items = make_items(groups, pick.q());
 
@@ -3877,15 +3997,18 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         }
     }
     auto &P = ctx->dplan;
-    const std::string envkey = scorer_env_key();
-    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.envkey == envkey &&
+    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
                       P.slots.size() == (size_t)nslots &&
                       !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
                       (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
     if (!same) {
-        std::vector<ScoreGroup> groups(ngroups);
-        std::vector<ScoreRead> reads;
-        std::vector<WorkItem> items;
+        P.valid = false;
+        std::vector<ScoreGroup> &groups = P.groups;
+        std::vector<ScoreRead> &reads = P.reads;
+        std::vector<WorkItem> &items = P.items;
+        groups.assign(ngroups, ScoreGroup{});
+        reads.clear();
+        items.clear();
         reads.reserve(nslots);
         int64_t dense_total = 0, split_total = 0;
         int max_reads = 0;
@@ -3924,10 +4047,14 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             for (int p0 = 0; p0 <= G.m; p0 += 64)
                 items.push_back({g, p0});
         }
-        std::vector<int64_t> gstart(ngroups + 1);
+        std::vector<int64_t> &gstart = P.gstart;
+        gstart.assign(ngroups + 1, 0);
         for (int32_t g = 0; g < ngroups; ++g)
             gstart[g] = groups[g].dense_off;
         gstart[ngroups] = dense_total;
+        P.pick = pick_scorer(ctx->opt, reads, all_finite);
+        if (P.pick.lean && P.pick.q() != 64)
+            items = make_items(groups, P.pick.q());
         if (int e = upload(ctx, ctx->scratch[11], items)) return e;
         if (int e = upload(ctx, ctx->scratch[12], groups)) return e;
         if (int e = upload(ctx, ctx->scratch[13], reads)) return e;
@@ -3941,21 +4068,13 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         P.max_reads = max_reads;
         P.dense_total = dense_total;
         P.split_total = split_total;
-        P.pick = pick_scorer(reads, all_finite);
-        P.envkey = envkey;
-        if (P.pick.lean && P.pick.q() != 64) {
-            items = make_items(groups, P.pick.q());
-            if (int e = upload(ctx, ctx->scratch[11], items)) return e;
-            P.nitems = items.size();
-        }
+        P.opt_gen = ctx->opt_gen;
     }
     bool split = (int64_t)P.nitems < 2048 && P.max_reads > 1;
-    if (const char *mode = std::getenv("RIFRAF_SCORE_MODE")) {
-        if (!std::strcmp(mode, "fused"))
-            split = false;
-        else if (!std::strcmp(mode, "split"))
-            split = true;
-    }
+    if (ctx->opt.score_mode == 1)
+        split = false;
+    else if (ctx->opt.score_mode == 2)
+        split = true;
     if (int e = ensure_buf(ctx, ctx->scratch[15], sizeof(double) * std::max<int64_t>(P.dense_total, 1)))
         return e;
     if (split)
@@ -4106,6 +4225,14 @@ int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms)
     float t = 0;
     (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
     *ms = t / reps;
+    return 0;
+}
+
+int rf_last_backtrace_ms(const rf_ctx *ctx, double *ms)
+{
+    if (!ctx || !ms)
+        return RF_ERR_ARG;
+    *ms = ctx->bt_ms;
     return 0;
 }
 

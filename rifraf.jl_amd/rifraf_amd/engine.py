@@ -53,6 +53,21 @@ class Engine:
             raise RifrafError(msg)
 
     # ------------------------------------------------------------------
+    def set_option(self, name: str, value):
+        """rf_set_option: select between bit-identical code paths (kernel
+        variants, fused/split fold, ...).  Returns the previous value."""
+        key = _lib.OPTIONS[name]
+        if isinstance(value, str):
+            value = _lib.OPTION_VALUES[name][value]
+        old = self.get_option(name)
+        self._check(self.lib.rf_set_option(self.ctx, key, int(value)))
+        return old
+
+    def get_option(self, name: str) -> int:
+        v = c_int32()
+        self._check(self.lib.rf_get_option(self.ctx, _lib.OPTIONS[name], byref(v)))
+        return v.value
+
     def reserve(self, nbytes: int):
         self._check(self.lib.rf_reserve(self.ctx, int(nbytes)))
 
@@ -252,6 +267,12 @@ class Engine:
         self._check(self.lib.rf_probe_write(self.ctx, int(mode), int(nbytes), int(chunk_bytes),
                                             int(nstreams), byref(ms)))
         return ms.value
+
+    def last_backtrace_ms(self) -> float:
+        """Kernel ms of the last backtrace / alignment_proposals call."""
+        v = c_double()
+        self._check(self.lib.rf_last_backtrace_ms(self.ctx, byref(v)))
+        return v.value
 
     def last_timing(self):
         a, b, c = c_double(), c_double(), c_double()

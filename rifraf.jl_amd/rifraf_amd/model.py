@@ -528,7 +528,10 @@ def check_score(state: RifrafState, run: _Run, params: RifrafParams, old_score: 
         elif state.score == old_score:
             log(params, 2, "    score did not change. ending stage.")
             return False
-    if ((state.score - old_score) / old_score > params.batch_threshold and not state.penalties_increased
+    # IEEE division as in Julia (x / 0.0 is +-Inf or NaN, never an exception)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rel = float(np.float64(state.score - old_score) / np.float64(old_score))
+    if (rel > params.batch_threshold and not state.penalties_increased
             and state.batch_size < len(state.sequences) and state.stage_iterations[int(state.stage) - 1] > 1):
         state.batch_size = min(state.batch_size + state.base_batch_size, len(state.sequences))
         log(params, 2, f"    NOTE: increased batch size to {state.batch_size}.")

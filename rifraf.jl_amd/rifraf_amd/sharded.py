@@ -18,6 +18,14 @@ Ownership:
     live only on its owner, so band memory is sharded;
   - slots >= nslots (the reference and scratch slots of model._Run) belong
     to the last rank.
+  - `nslots` must be the batch size the run actually uses (rifraf() fills
+    batch slots 0..batch_size-1, model.jl:569-573 / :1038-1066), not the
+    read count: `ShardedEngine.for_params` derives it from RifrafParams.  A
+    block partition over the read count would put every batch slot of a
+    20-read batch on rank 0.  The work is then balanced whenever the batch
+    holds >= W reads (REFINE / SCORE, and every stage with batch_size <= 1,
+    the throughput setting of configs 2-5); the fixed 5-read INIT/FRAME
+    batch (batch_fixed_size) is spread over min(W, 5)-ish ranks only.
 
 Exchange and exactness:
   - realign / backtrace results are per job; they are gathered verbatim, so
@@ -57,6 +65,21 @@ class ShardedEngine:
                     else torch.device("cpu"))
         self.bounds = [r * self.nslots // self.world for r in range(self.world + 1)]
         self.last_dense = None
+
+    @classmethod
+    def for_params(cls, local, nreads: int, params=None, group=None):
+        """ShardedEngine sized for the batch rifraf() will use: batch_size
+        (all reads when batch_size <= 1, model.jl:569-573), capped at nreads."""
+        bs = getattr(params, "batch_size", 0) if params is not None else 0
+        nslots = nreads if bs <= 1 else min(bs, nreads)
+        return cls(local, nslots, group)
+
+    def slot_counts(self, slots) -> list:
+        """Number of the given slots each rank owns (load-balance diagnostics)."""
+        counts = [0] * self.world
+        for s in np.asarray(slots).ravel():
+            counts[self.owner(int(s))] += 1
+        return counts
 
     # ------------------------------------------------------------------
     # ownership

@@ -19,3 +19,17 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def opts(engine):
+    """Set engine options (rf_set_option) for one test; restored afterwards."""
+    saved = {}
+
+    def set_(name, value):
+        old = engine.set_option(name, value)
+        saved.setdefault(name, old)
+
+    yield set_
+    for k, v in saved.items():
+        engine.set_option(k, v)

@@ -84,26 +84,28 @@ class OracleEngine:
         return ent
 
     def score(self, groups, per_seq=False):
+        """model.jl:385-399 per proposal (oracle.score_list: the same
+        per-proposal left fold, proposals in parallel in C)."""
         totals, mats = [], []
         for bslots, ref, props in groups:
             k, p, b = props if isinstance(props, tuple) else to_arrays(props)
             ents = [self._check_slot(s) for s in bslots]
-            reads = [(e["A"][0], e["B"][0], self._seq_bw(e)) for e in ents]
+            reads = [self._seq_bw(e) for e in ents]
             rent = self._check_slot(ref) if ref >= 0 else None
-            tot = np.empty(len(k))
-            mat = np.empty((len(k), len(ents) + (1 if rent else 0)))
-            for i in range(len(k)):
-                acc = 0.0
-                for r, (A, B, (s, t)) in enumerate(reads):
-                    v = self._score1(k[i], p[i], b[i], A, B, t, s)
-                    mat[i, r] = v
-                    acc += v
-                if rent is not None:
-                    s, t = self._seq_bw(rent)
-                    v = self._score1(k[i], p[i], b[i], rent["A"][0], rent["B"][0], t, s)
-                    mat[i, -1] = v
-                    acc += v
-                tot[i] = acc
+            t = reads[0][1] if reads else None
+            kw = {}
+            if rent is not None:
+                rs, t = self._seq_bw(rent)
+                kw = dict(Aref=rent["A"][0], Bref=rent["B"][0], ref=rs)
+            if len(k) == 0:
+                totals.append(np.zeros(0))
+                mats.append(np.zeros((0, len(ents) + (1 if rent else 0))))
+                continue
+            try:
+                tot, mat = oracle.score_list((k, p, b), [e["A"][0] for e in ents], [e["B"][0] for e in ents],
+                                             [s for s, _ in reads], t, per_seq=True, nthreads=8, **kw)
+            except oracle.OracleError as e:
+                raise RifrafError(str(e))
             totals.append(tot)
             mats.append(mat)
         return (totals, mats) if per_seq else totals

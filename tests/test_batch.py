@@ -73,3 +73,19 @@ def test_batch_waves_and_errors():
 @pytest.mark.gpu
 def test_batch_matches_separate_runs_hip(engine):
     _check(lambda: engine)
+
+
+@pytest.mark.gpu
+def test_batch_hip_matches_oracle_runs(engine):
+    """HIP-batched clusters (one launch per request kind) against separate
+    rifraf() runs on the CPU oracle engine: same consensus at every
+    iteration, same score, same QVs (error_probs, aln_error_probs)."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import rifraf
+    clusters = _clusters()
+    params = _params()
+    ref = [summary(rifraf(params=params, engine=OracleEngine(), **kw)) for kw in clusters]
+    got = rifraf_batch(clusters, params=params, engine=engine)
+    for r, g in zip(ref, got):
+        assert_same_run(summary(g), r)

@@ -171,8 +171,8 @@ def test_dp_huge_band_global_ring(engine):
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
 @pytest.mark.parametrize("L,nreads,bw", [(40, 3, 9), (150, 7, 9), (260, 5, 25)])
-def test_score_all_proposals_bitexact(engine, monkeypatch, mode, L, nreads, bw):
-    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+def test_score_all_proposals_bitexact(engine, opts, mode, L, nreads, bw):
+    opts("score_mode", mode)
     rng = np.random.default_rng(L + nreads)
     t = random_seq(L, rng)
     seqs = [make_read(t, rng, 0.03, bw) for _ in range(nreads)]
@@ -207,9 +207,9 @@ def test_score_per_read_bitexact(engine):
         assert tot[0][k] == fold
 
 
-def test_score_many_clusters(engine, monkeypatch):
+def test_score_many_clusters(engine, opts):
     """Batched clusters: one group per consensus, fused ordered fold."""
-    monkeypatch.setenv("RIFRAF_SCORE_MODE", "fused")
+    opts("score_mode", "fused")
     rng = np.random.default_rng(99)
     templates, seqs, groups = [], [], []
     for c in range(6):
@@ -296,9 +296,9 @@ def test_errors_are_loud(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-def test_score_dense_clusters(engine, monkeypatch, mode):
+def test_score_dense_clusters(engine, opts, mode):
     """rf_score_dense over several clusters == oracle all-proposals pass."""
-    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    opts("score_mode", mode)
     rng = np.random.default_rng(123)
     templates, seqs = [], []
     for c in range(5):
@@ -355,10 +355,10 @@ def test_plan_cache_follows_template_content(engine):
 
 
 SCORER_CONFIGS = [
-    # (RIFRAF_SCORE_KERNEL, RIFRAF_LEAN_NW, RIFRAF_LEAN_LDS_KB)
+    # (score_kernel, lean_nw, lean_lds_kb) engine options
     ("general", None, None),
     ("seg", None, None),       # row-segment scorer (wide bands) on every shape
-    ("seg16", None, None),     # ... with 16-diagonal segments (RIFRAF_SEG_S=16)
+    ("seg16", None, None),     # ... with 16-diagonal segments (seg_s=16)
     ("seg32", None, None),     # ... with 32-diagonal segments
     (None, "1", None),
     (None, "2", None),
@@ -369,14 +369,14 @@ SCORER_CONFIGS = [
     (None, "8", None),
     (None, "8", "40"),
     (None, "8", "60"),
-    (None, "8", "q128"),     # k_score_ws with 128 chain lanes (RIFRAF_WS_Q=128), 80 KB LDS
+    (None, "8", "q128"),     # k_score_ws with 128 chain lanes (ws_q=128), 80 KB LDS
     (None, "8", "q128l40"),  # ... with windows beyond the budget: sub-passes
 ]
 
 
 @pytest.mark.parametrize("kern,nw,lds", SCORER_CONFIGS)
 @pytest.mark.parametrize("mode", ["fused", "split"])
-def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
+def test_score_dense_kernels(engine, opts, kern, nw, lds, mode):
     """Both dense scorers (general and lean chain-per-column) over ragged
     clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the oracle."""
     wsq = None
@@ -386,13 +386,12 @@ def test_score_dense_kernels(engine, monkeypatch, kern, nw, lds, mode):
     segs = None
     if kern in ("seg16", "seg32"):
         kern, segs = "seg", kern[3:]
-    for k, v in (("RIFRAF_SCORE_KERNEL", kern), ("RIFRAF_LEAN_NW", nw), ("RIFRAF_LEAN_LDS_KB", lds),
-                 ("RIFRAF_WS_Q", wsq), ("RIFRAF_SEG_S", segs)):
-        if v is None:
-            monkeypatch.delenv(k, raising=False)
-        else:
-            monkeypatch.setenv(k, v)
-    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+    opts("score_kernel", kern or "auto")
+    opts("lean_nw", int(nw or 8))
+    opts("lean_lds_kb", int(lds or 0))
+    opts("ws_q", int(wsq or 256))
+    opts("seg_s", int(segs or 24))
+    opts("score_mode", mode)
     rng = np.random.default_rng(77)
     templates, seqs, bws = [], [], []
     shapes = [(150, 9, 0), (40, 3, 25), (260, 20, -30), (130, 9, 0), (70, 5, 12), (1, 1, 0)]
@@ -461,20 +460,20 @@ def test_score_lean_ineligible_tables(engine):
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
 @pytest.mark.parametrize("kern", [None, "seg16", "seg32", "general"])
-def test_score_wide_bands(engine, monkeypatch, mode, kern):
+def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
     row-segment scorer k_score_seg (default) and the in-place k_score
     ("general") are both bit-exact against the oracle."""
-    monkeypatch.delenv("RIFRAF_SEG_S", raising=False)
+    opts("seg_s", 24)
     if kern is None:
-        monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
+        opts("score_kernel", "auto")
     elif kern in ("seg16", "seg32"):
-        monkeypatch.delenv("RIFRAF_SCORE_KERNEL", raising=False)
-        monkeypatch.setenv("RIFRAF_SEG_S", kern[3:])
+        opts("score_kernel", "auto")
+        opts("seg_s", int(kern[3:]))
     else:
-        monkeypatch.setenv("RIFRAF_SCORE_KERNEL", kern)
-    monkeypatch.setenv("RIFRAF_SCORE_MODE", mode)
+        opts("score_kernel", kern)
+    opts("score_mode", mode)
     rng = np.random.default_rng(404)
     templates, seqs, bws = [], [], []
     for L, bw_list, skew in [(320, (100, 60, 9), 40), (250, (45, 120), -35), (90, (70,), 0)]:
@@ -550,12 +549,12 @@ def test_alignment_proposals_device(engine, do_indels):
 
 
 @pytest.mark.parametrize("L,bw,skew", [(700, 9, 0), (400, 40, 30), (300, 120, -40), (260, 9, 60), (90, 3, 0)])
-def test_backtrace_windowed(engine, monkeypatch, L, bw, skew):
+def test_backtrace_windowed(engine, opts, L, bw, skew):
     """k_bt_win (wave per read, LDS windows of kappa rows, re-staged as the
     walk leaves them) against the oracle's backtrace and count_errors, and the
     fused proposal marking against the host moves_to_proposals union, on long
     reads (many windows), wide bands (small windows: P up to 129) and reads
-    longer / shorter than the template; RIFRAF_BT_LEGACY=1 (k_backtrace for
+    longer / shorter than the template; option bt_global=1 (k_backtrace for
     every walk) gives the same moves."""
     from rifraf_amd.align import moves_to_proposals_np
     rng = np.random.default_rng(L + bw)
@@ -575,11 +574,11 @@ def test_backtrace_windowed(engine, monkeypatch, L, bw, skew):
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
-    monkeypatch.delenv("RIFRAF_BT_LEGACY", raising=False)
+    opts("bt_global", 0)
     got, nerr = engine.backtrace(np.arange(n))
-    monkeypatch.setenv("RIFRAF_BT_LEGACY", "1")
+    opts("bt_global", 1)
     legacy, nerr_l = engine.backtrace(np.arange(n))
-    monkeypatch.delenv("RIFRAF_BT_LEGACY")
+    opts("bt_global", 0)
     exp_mask = np.zeros((L + 1, 9), np.uint8)
     for k, s in enumerate(seqs):
         _, mv = oracle.forward(t, s, moves=True, bandwidth=bw)
@@ -590,3 +589,29 @@ def test_backtrace_windowed(engine, monkeypatch, L, bw, skew):
         kk, p, b = moves_to_proposals_np(ref, t, s.seq)
         exp_mask[p, np.where(kk == 0, b, np.where(kk == 2, 4, 5 + b))] = 1
     np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
+
+
+def test_plan_cache_follows_slot_contents(engine):
+    """rf_score_dense reuses its descriptors only while every scored band
+    still describes the same alignment: re-filling the same slots with other
+    (shorter) reads at the same bandwidth -- bands that fit their old
+    regions -- or another bandwidth must rebuild the plan (advisor finding)."""
+    rng = np.random.default_rng(91)
+    t = random_seq(120, rng)
+    long_reads = [make_read(t, rng, 0.03, 9) for _ in range(4)]
+    short_reads = [RifrafSequence(r.seq[:-7], r.error_log_p[:-7], 9, SEQ_SCORES)
+                   for r in (make_read(t, rng, 0.03, 9) for _ in range(4))]
+    sl = np.arange(4)
+    engine.set_templates(0, [t])
+    engine.set_sequences(0, long_reads)
+    engine.set_sequences(4, short_reads)
+    for seqs, ids, bw in ((long_reads, sl, 9), (short_reads, sl + 4, 9), (long_reads, sl, 9),
+                          (long_reads, sl, 12)):
+        engine.realign(sl, ids, 0, [bw] * 4, RF_FWD | RF_BWD)
+        got = engine.score_dense([sl])[0]
+        ref, _ = oracle.cpu_pass(t, [RifrafSequence(s.seq, s.error_log_p, bw, SEQ_SCORES) for s in seqs],
+                                 nthreads=4)
+        mask = np.ones_like(ref, bool)
+        mask[0, :5] = False
+        mask[np.arange(1, len(t) + 1), t.astype(np.int64)] = False
+        np.testing.assert_array_equal(got[mask], ref[mask])

@@ -86,6 +86,7 @@ def summary(res):
             "iters": list(st.stage_iterations), "converged": st.converged,
             "sub": None if res.error_probs is None else res.error_probs.sub.copy(),
             "ins": None if res.error_probs is None else res.error_probs.ins.copy(),
+            "dele": None if res.error_probs is None else res.error_probs.dele.copy(),
             "aln": None if res.aln_error_probs is None else np.asarray(res.aln_error_probs).copy()}
 
 
@@ -117,7 +118,7 @@ def assert_same_run(a, b):
         assert len(x) == len(y)
         for c1, c2 in zip(x, y):
             np.testing.assert_array_equal(c1, c2)
-    for k in ("sub", "ins", "aln"):
+    for k in ("sub", "dele", "ins", "aln"):
         if a[k] is None:
             assert b[k] is None
         else:
@@ -191,3 +192,31 @@ def test_shard_bounds_and_owner():
         assert b[0] == 0 and b[-1] == n and all(x <= y for x, y in zip(b, b[1:]))
         sizes = np.diff(b)
         assert sizes.max() - sizes.min() <= 1
+
+
+def _w_counts(rank, world):
+    from oracle_engine import OracleEngine
+    from rifraf_amd.model import RifrafParams
+    from rifraf_amd.sharded import ShardedEngine
+    out = {}
+    for bs, nreads in [(20, 5000), (0, 5000), (1, 12), (20, 7)]:
+        e = ShardedEngine.for_params(OracleEngine(), nreads, RifrafParams(batch_size=bs))
+        batch = min(nreads, bs) if bs > 1 else nreads
+        out[(bs, nreads)] = (e.nslots, e.slot_counts(np.arange(batch)), e.owner(nreads), e.owner(nreads + 1))
+    return out
+
+
+def test_sharded_slot_balance():
+    """ShardedEngine.for_params partitions the batch slots rifraf() fills
+    (batch_size, or all reads when batch_size <= 1), not the read count, so
+    each rank owns its share of the batch; reference/scratch slots (>= nreads)
+    go to the last rank."""
+    got = _spawn(_w_counts, 2)
+    for r in range(2):
+        c = got[r]
+        assert c[(20, 5000)][:2] == (20, [10, 10])
+        assert c[(0, 5000)][:2] == (5000, [2500, 2500])
+        assert c[(1, 12)][:2] == (12, [6, 6])
+        assert c[(20, 7)][:2] == (7, [3, 4])
+        for v in c.values():
+            assert v[2] == v[3] == 1

@@ -1,0 +1,156 @@
+"""HIP engine vs the CPU oracle at the BASELINE.json workload shapes.
+
+Every other parity test uses small inputs; these run the configs' own shapes
+(SURVEY.md §8(d)):
+
+  c2  sample_sequences(100, 1000; error_rate=0.01), no reference: whole
+      rifraf() runs, default params and the throughput settings with the QV
+      pass (do_score): same consensus after every iteration, same score bits,
+      same accepted proposals, same error_probs / aln_error_probs bits;
+  c3  sample_sequences(1000, 2601; error_rate=0.01, ref_error_rate=0.1,
+      ref_errors=ErrorModel(10,0,0,1,1)) with a one-base frameshift in the
+      reference so that FRAME runs (codon scoring of the reference, penalty
+      increases, seeded indel proposals): same run as the oracle engine;
+  c4  clusters of 50 reads x 1.5 kb (bench.make_workload): rf_score_dense of
+      every STAGE_SCORE proposal vs oracle.cpu_pass, bit-exact;
+  c5  the first 64 reads of the bench's 10 kb / 3 % error cluster
+      (bench.make_read_shard): band doubling (smart_forward_moves!,
+      model.jl:643-672) gives the same bandwidth and A[end,end] per read on
+      both engines; bands at the doubled widths and the dense totals are
+      bit-exact.
+
+The oracle engine is tests/oracle_engine.py (C oracle behind the Engine
+API); tolerance everywhere: bit-exact (north_star allows 1e-9 relative).
+"""
+import copy
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+import oracle
+from rifraf_amd import ErrorModel
+from rifraf_amd.engine import RF_BAND_A, RF_BAND_B, RF_BWD, RF_FWD
+from rifraf_amd.model import RifrafParams, rifraf, smart_forward_moves
+from rifraf_amd.sample import sample_sequences
+
+pytestmark = pytest.mark.gpu
+NTHREADS = min(16, os.cpu_count() or 1)
+
+
+def assert_same_run(a, b):
+    np.testing.assert_array_equal(a.consensus, b.consensus)
+    assert a.state.score == b.state.score
+    assert a.state.stage_iterations == b.state.stage_iterations
+    assert a.state.converged == b.state.converged
+    for sa, sb in zip(a.consensus_stages, b.consensus_stages):
+        assert len(sa) == len(sb)
+        for x, y in zip(sa, sb):
+            np.testing.assert_array_equal(x, y)
+    if a.error_probs is None:
+        assert b.error_probs is None
+    else:
+        for f in ("sub", "dele", "ins"):
+            np.testing.assert_array_equal(getattr(a.error_probs, f), getattr(b.error_probs, f), err_msg=f)
+        np.testing.assert_array_equal(a.aln_error_probs, b.aln_error_probs)
+
+
+def _masked(got, ref, t):
+    mask = np.ones_like(ref, bool)
+    mask[0, :5] = False                       # p = 0 has no sub / del
+    mask[np.arange(1, len(t) + 1), np.asarray(t, np.int64)] = False   # the consensus base is no proposal
+    return got[mask], ref[mask]
+
+
+@pytest.mark.parametrize("variant", ["default", "throughput_qv"])
+def test_c2_run_matches_oracle(engine, variant):
+    from oracle_engine import OracleEngine
+    rng = np.random.default_rng(2)
+    _, template, _, reads, _, phreds, _, _ = sample_sequences(100, 1000, error_rate=0.01, rng=rng)
+    params = (RifrafParams(seed=1) if variant == "default" else
+              RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True))
+    a = rifraf(reads, phreds, params=params, engine=engine)
+    b = rifraf(reads, phreds, params=params, engine=OracleEngine())
+    assert_same_run(a, b)
+    assert a.state.converged and np.array_equal(a.consensus, template)
+
+
+def test_c3_frame_run_matches_oracle(engine):
+    from oracle_engine import OracleEngine
+    rng = np.random.default_rng(3)
+    ref, template, _, reads, _, phreds, _, _ = sample_sequences(
+        1000, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+    # a single-base frameshift in the reference: INIT -> FRAME with codon scoring
+    ref = np.concatenate([ref[:1300], ref[1301:2000], [2], ref[2000:]]).astype(np.uint8)
+    params = RifrafParams(seed=1)
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
+    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    assert_same_run(a, b)
+    assert a.state.stage_iterations[1] >= 2          # FRAME ran (with a penalty increase)
+    assert a.state.n_ref_indel_mults == b.state.n_ref_indel_mults >= 1
+
+
+def test_c3_qv_with_reference_matches_oracle(engine):
+    """QV pass scoring the reference's codon moves too (use_ref_for_qvs,
+    model.jl:617-628, :737-791), 2.6 kb template, 40 reads."""
+    from oracle_engine import OracleEngine
+    rng = np.random.default_rng(33)
+    ref, _, _, reads, _, phreds, _, _ = sample_sequences(
+        40, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+    params = RifrafParams(seed=1, do_score=True, use_ref_for_qvs=True)
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
+    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    assert_same_run(a, b)
+
+
+def test_c4_clusters_dense_bitexact(engine):
+    import bench
+    clusters = bench.make_workload(4, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, 0))
+    reads = [r for _, rs in clusters for r in rs]
+    n = len(reads)
+    engine.set_sequences(0, reads)
+    engine.set_templates(0, [t for t, _ in clusters])
+    tpl = np.repeat(np.arange(len(clusters)), 50)
+    engine.realign(np.arange(n), np.arange(n), tpl, [r.bandwidth for r in reads], RF_FWD | RF_BWD)
+    groups = [np.arange(50 * c, 50 * c + 50) for c in range(len(clusters))]
+    got = engine.score_dense(groups)
+    for c, (t, rs) in enumerate(clusters):
+        ref, _ = oracle.cpu_pass(t, rs, nthreads=NTHREADS)
+        g, e = _masked(got[c], ref, t)
+        np.testing.assert_array_equal(g, e, err_msg=f"cluster {c}")
+
+
+def test_c5_sample_band_doubling_and_scores(engine):
+    import bench
+    from oracle_engine import OracleEngine
+    t, reads = bench.make_read_shard(5000, 10000, 0.03, 9, 2024, 0, 64)
+    m = len(t)
+    # band doubling on both engines (each mutates its own RifrafSequence copies)
+    rh = [copy.copy(r) for r in reads]
+    ro = [copy.copy(r) for r in reads]
+    engine.set_sequences(0, rh)
+    engine.set_templates(0, [t])
+    oe = OracleEngine()
+    oe.set_sequences(0, ro)
+    oe.set_templates(0, [t])
+    jobs = [(k, k) for k in range(len(reads))]
+    sh = smart_forward_moves(SimpleNamespace(e=engine), jobs, rh, m, 0.1)
+    so = smart_forward_moves(SimpleNamespace(e=oe), jobs, ro, m, 0.1)
+    bw_h = [r.bandwidth for r in rh]
+    assert bw_h == [r.bandwidth for r in ro]
+    np.testing.assert_array_equal(sh, so)
+    assert sum(b > 9 for b in bw_h) >= len(reads) // 2      # the config's point: most reads double
+    # bands at the doubled widths, and every STAGE_SCORE total
+    n = len(rh)
+    engine.realign(np.arange(n), np.arange(n), 0, bw_h, RF_FWD | RF_BWD)
+    for k in (0, 1, n - 1):
+        A_exp, _ = oracle.forward(t, rh[k], bandwidth=bw_h[k])
+        B_exp = oracle.backward(t, rh[k], bandwidth=bw_h[k])
+        from test_gpu_parity import assert_band_equal
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(rh[k]) + 1, m + 1, bw_h[k])
+        assert_band_equal(engine.download_band(k, RF_BAND_B), B_exp, len(rh[k]) + 1, m + 1, bw_h[k])
+    got = engine.score_dense([np.arange(n)])[0]
+    ref, _ = oracle.cpu_pass(t, rh, nthreads=NTHREADS)
+    g, e = _masked(got, ref, t)
+    np.testing.assert_array_equal(g, e)
