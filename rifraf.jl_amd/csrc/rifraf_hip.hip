@@ -2250,22 +2250,33 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 
 // ---------------------------------------------------------------------
 // k_bt_win: backtrace + count_errors (align.jl:229-245) for reads (no codon
-// moves, H <= 255), one wave per read, from an LDS window instead of global
-// memory.  k_backtrace's walk is a chain of dependent global loads (band
-// cells, tables and bases at the current cell, ~1 us per move); here the
-// wave stages a window of kappa rows of the A band (contiguous in the
-// kappa-major layout) plus the table rows and bases the walk can reach from
-// it, and every lane walks the same path through LDS (broadcast reads, no
-// divergence).  The walk only moves to lower kappa, so a window is left
-// downwards and re-staged below.  Same move choice as k_backtrace (strict '>'
-// in the reference's order), same count_errors; moves are written in forward
-// order ending at slot n+m-1 of the read's output.  With a mask, the wave
-// also marks the proposals its alignment implies (moves_to_proposals,
-// model.jl:458-480: k_aln_props fused into the walk -- the set union does not
-// depend on the walk direction).
+// moves, H <= 255), one wave per read, from LDS windows.
+//
+// The walk is sequential, so the wave parallelises it across a "box" of the
+// cells it can reach next: from the current cell (ii0, jj0) lane l computes
+// the move of cell (ii0 - di, jj0 - dj), di = l / 3, dj = di - (l % 3 - 1),
+// i.e. the 3 band diagonals around the walk's diagonal for BT_DMAX + 1 steps
+// (63 cells).  Each move is the first strictly-best candidate over the
+// stored A values (align.jl:77-104, the same FP64 sums as the forward fill),
+// so it equals the trace band's move.  The walk then follows the box with
+// one v_readlane per move (the move, the mismatch flag and the read base
+// packed in one dword) until it leaves the box, and a new box is computed
+// at the cell reached.
+//
+// Operands come from LDS: a window of kappa rows [klo, khi] of the A band,
+// restricted to the elements [e0, e0 + wd) around the walk's diagonal
+// (whole rows when P <= BTW_WD), and windows of the table rows and bases.
+// The walk only moves to lower kappa; a window is re-staged below when a
+// box would leave it.  Staging issues every load of a window before the
+// first LDS write (one memory latency per window, not one per element).
+// With a mask, the walk also marks the proposals its alignment implies
+// (moves_to_proposals, model.jl:458-480; k_aln_props fused into the walk --
+// the set union does not depend on the walk direction).
 // ---------------------------------------------------------------------
-constexpr int BTW_A = 4096;    // doubles of A window (32 KB)
-constexpr int BTW_T = 384;     // staged table rows / bases per window
+constexpr int BTW_A = 4096;    // doubles of the A window (32 KB)
+constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
+constexpr int BTW_T = 256;     // staged table rows / template bases per window
+constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
 
 __global__ void __launch_bounds__(64)
 k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
@@ -2284,108 +2295,174 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     const int n = T.n, m = T.m, H = T.H, P = T.P;
     const int c = max(m - n, 0) + T.bw;
     const int K = H + 2 * m;
-    const int W = min(256, BTW_A / P);                 // kappa rows per window
+    const int wd = min(P, BTW_WD);
+    const int W = BTW_A / wd;                          // kappa rows per window (>= 256)
     const bool skew = T.flags & 2, trim = T.flags & 4;
     int8_t *out = moves + T.out;
     uint8_t *mk = mask ? mask + T.mask : nullptr;
-    auto inband = [&](int ii, int jj) {
-        if (ii < 0 || jj < 0 || ii > n || jj > m)
-            return false;
-        const int d = ii - jj + c;
-        return d >= 0 && d < H;
-    };
+    // this lane's box cell offsets
+    const int bdi = lane / 3, bdj = bdi - (lane % 3 - 1);
+    const bool blane = lane < 3 * (BT_DMAX + 1);
     int ii = n, jj = m, cnt = 0, errs = 0;
-    int klo = 0, q0 = 0, r0 = 0;                       // staged: kappa >= klo, table index >= q0, t index >= r0
-    bool staged = false;
-    while (ii > 0 || jj > 0) {
+    int klo = -1, e0 = 0;                              // A window: rows [klo, klo + W), elements [e0, e0 + wd)
+    int q0 = -1, r0 = -1;                              // table rows [q0, q0 + BTW_T), bases [r0, r0 + BTW_T)
+    int failed = 0;
+    while ((ii > 0 || jj > 0) && !failed) {
+        // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
-        if (!staged || (klo > 0 && kap0 - 2 < klo) || max(ii - 1, 0) < q0 || (jj >= 1 && jj - 1 < r0)) {
-            // ---- (re)stage below the current cell: rows [klo, khi], tables [q0, q1], bases
+        const int d0 = ii - jj + c;
+        const int klo_need = max(kap0 - 2 * BT_DMAX - 3, 0);
+        const int elo = max(d0 - 2, 0) >> 1, ehi = min(d0 + 2, H - 1) >> 1;
+        if (klo < 0 || klo_need < klo || elo < e0 || ehi >= e0 + wd) {
             const int khi = min(kap0 - 1, K - 1);
             klo = max(0, khi - W + 1);
-            const int q1 = ii;                         // del index ii; ks = ii - 1
-            q0 = max(0, min((klo + 2 - 2 * c) / 2 - 2, q1 - 1));   // <= max(ii - 1, 0): no re-stage loop
-            q0 = max(q0, q1 - BTW_T + 1);
-            const int r1 = max(jj - 1, 0);
-            r0 = max(0, min((klo + 3 - H) / 2 - 2, r1));
-            r0 = max(r0, r1 - BTW_T + 1);
+            e0 = min(max((d0 >> 1) - wd / 2, 0), P - wd);
+            const int nrow = khi - klo + 1, na = nrow * wd;
             wave_sync();                               // every lane is done with the old window
-            const int na = (khi - klo + 1) * P;
-            const double *ga = A + (size_t)klo * P;
-            for (int e = lane; e < na; e += 64)
-                sA[e] = ga[e];
-            for (int e = lane; e <= q1 - q0; e += 64) {
-                const int q = q0 + e;
-                const int ks = min(q, n - 1);
-                sTm[e] = tb[ks];
-                sTx[e] = tb[n + ks];
-                sTi[e] = tb[2 * (size_t)n + ks];
-                sTd[e] = tb[3 * (size_t)n + q];
-                sS[e] = q < n ? s[q] : 4;
+            // element t = row * wd + col, t = lane + 64 u: incremental row / col
+            const int qr = 64 / wd, rr = 64 % wd;
+            int row = lane / wd, col = lane % wd;
+            for (int u0 = 0; u0 < BTW_A / 64; u0 += 16) {
+                double v[16];
+                int rw = row, cl = col;
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {         // issue all loads of the chunk
+                    const int t = lane + 64 * (u0 + u);
+                    v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
+                    rw += qr;
+                    cl += rr;
+                    if (cl >= wd) {
+                        cl -= wd;
+                        ++rw;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int t = lane + 64 * (u0 + u);
+                    if (t < na)
+                        sA[t] = v[u];
+                }
+                row = rw;
+                col = cl;
+                if (64 * (u0 + 16) >= na)            // lane 0 holds the chunk's lowest t
+                    break;
             }
-            for (int e = lane; e <= r1 - r0; e += 64)
-                sTt[e] = r0 + e < m ? tt[r0 + e] : 4;
             wave_sync();
-            staged = true;
         }
-        // one LDS round trip per move: every operand is read unconditionally
-        // (addresses clamped to the window when a predecessor is out of band),
-        // then the reference's candidate chain is evaluated on registers
-        const bool in1 = inband(ii - 1, jj - 1), in2 = inband(ii - 1, jj), in3 = inband(ii, jj - 1);
-        auto aix = [&](bool in, int i2, int j2) {
-            const int d = i2 - j2 + c;
-            return in ? (d + 2 * j2 - klo) * P + (d >> 1) : 0;
-        };
-        const int ks = max(ii - 1, 0) - q0;
-        const int sbv = sS[ii >= 1 ? ii - 1 - q0 : 0];
-        const int tbv = sTt[jj >= 1 ? jj - 1 - r0 : 0];
-        const double tm = sTm[ks], tx = sTx[ks], ti = sTi[ks], ds = sTd[ii - q0];
-        const double a1 = sA[aix(in1, ii - 1, jj - 1)], a2 = sA[aix(in2, ii - 1, jj)], a3 = sA[aix(in3, ii, jj - 1)];
-        const int sb = ii >= 1 ? sbv : 4;
-        const int tbb = jj >= 1 ? tbv : 4;
-        double ms = (sb == tbb) ? tm : tx;
-        double is = ti;
-        if (skew && sb != tbb)
-            ms *= 0.99;
-        if (trim && (jj == 0 || jj == m))
-            is = 0.0;
-        double best = -RF_INF, x;
-        int mv = 0;
-        x = a1 + ms;
-        if (in1 && x > best) { best = x; mv = 1; }
-        x = a2 + is;
-        if (in2 && x > best) { best = x; mv = 2; }
-        x = a3 + ds;
-        if (in3 && x > best) { best = x; mv = 3; }
-        mv = __builtin_amdgcn_readfirstlane(mv);
-        if (mv == 0 || cnt >= n + m) {
-            if (lane == 0)
-                set_err(err, 2);  // failed to find a move
-            break;
-        }
-        if (lane == 0) {
-            out[n + m - 1 - cnt] = (int8_t)mv;
-            if (mk) {
-                // the forward step of this move ends at (ii, jj) (k_aln_props)
-                if (mv == 1 && sb != tbb)
-                    mk[(size_t)jj * 9 + sb] = 1;
-                else if (mv == 2 && do_indels)
-                    mk[(size_t)jj * 9 + 5 + sb] = 1;
-                else if (mv == 3 && do_indels)
-                    mk[(size_t)jj * 9 + 4] = 1;
+        const int qlo_need = max(ii - BT_DMAX - 1, 0), rlo_need = max(jj - BT_DMAX - 2, 0);
+        if (q0 < 0 || qlo_need < q0 || rlo_need < r0 || ii > q0 + BTW_T - 1 || max(jj - 1, 0) > r0 + BTW_T - 1) {
+            q0 = max(0, ii - BTW_T + 1);               // del index ii .. ; ks = ii - 1 ..
+            r0 = max(0, max(jj - 1, 0) - BTW_T + 1);
+            wave_sync();
+            constexpr int NU = BTW_T / 64;
+            double vm[NU], vx[NU], vi[NU], vd[NU];
+            int vs[NU], vt[NU];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int q = q0 + lane + 64 * u;
+                const int ks = min(q, n - 1);
+                const int qd = min(q, n);
+                vm[u] = tb[ks];
+                vx[u] = tb[n + ks];
+                vi[u] = tb[2 * (size_t)n + ks];
+                vd[u] = tb[3 * (size_t)n + qd];
+                vs[u] = q < n ? s[q] : 4;
+                const int r = r0 + lane + 64 * u;
+                vt[u] = r < m ? tt[r] : 4;
             }
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int e = lane + 64 * u;
+                sTm[e] = vm[u];
+                sTx[e] = vx[u];
+                sTi[e] = vi[u];
+                sTd[e] = vd[u];
+                sS[e] = (uint8_t)vs[u];
+                sTt[e] = (uint8_t)vt[u];
+            }
+            wave_sync();
         }
-        ++cnt;
-        if (mv == 1) {
-            errs += (sb != tbb);
-            --ii;
-            --jj;
-        } else if (mv == 2) {
-            errs += 1;
-            --ii;
-        } else {
-            errs += 1;
-            --jj;
+        // ---- box: the move of cell (ci, cj), packed mv | mismatch << 3 | read base << 4
+        int pack = 0;
+        {
+            const int ci = ii - bdi, cj = jj - bdj;
+            const bool valid = blane && bdj >= 0 && ci >= 0 && cj >= 0 && (ci > 0 || cj > 0) &&
+                               ci - cj + c >= 0 && ci - cj + c < H;
+            auto inb = [&](int i2, int j2) {
+                if (i2 < 0 || j2 < 0)
+                    return false;
+                const int d = i2 - j2 + c;
+                return d >= 0 && d < H;
+            };
+            const bool in1 = valid && inb(ci - 1, cj - 1), in2 = valid && inb(ci - 1, cj),
+                       in3 = valid && inb(ci, cj - 1);
+            auto aix = [&](bool in, int i2, int j2) {
+                const int d = i2 - j2 + c;
+                return in ? (d + 2 * j2 - klo) * wd + (d >> 1) - e0 : 0;
+            };
+            const double a1 = sA[aix(in1, ci - 1, cj - 1)], a2 = sA[aix(in2, ci - 1, cj)],
+                         a3 = sA[aix(in3, ci, cj - 1)];
+            const int ks = valid ? max(ci - 1, 0) - q0 : 0;
+            const int kd = valid ? ci - q0 : 0;
+            const int sb = (valid && ci >= 1) ? sS[ci - 1 - q0] : 4;
+            const int tbb = (valid && cj >= 1) ? sTt[cj - 1 - r0] : 4;
+            double ms = (sb == tbb) ? sTm[ks] : sTx[ks];
+            double is = sTi[ks];
+            const double ds = sTd[kd];
+            if (skew && sb != tbb)
+                ms *= 0.99;
+            if (trim && (cj == 0 || cj == m))
+                is = 0.0;
+            double best = -RF_INF, x;
+            int mv = 0;
+            x = a1 + ms;
+            if (in1 && x > best) { best = x; mv = 1; }
+            x = a2 + is;
+            if (in2 && x > best) { best = x; mv = 2; }
+            x = a3 + ds;
+            if (in3 && x > best) { best = x; mv = 3; }
+            pack = valid ? (mv | ((sb != tbb) ? 8 : 0) | (sb << 4)) : 0;
+        }
+        // ---- walk the box (uniform control flow, one readlane per move)
+        const int bi = ii, bj = jj;
+        while (ii > 0 || jj > 0) {
+            const int di = bi - ii, dj = bj - jj, u = di - dj;
+            if (di > BT_DMAX || u < -1 || u > 1)
+                break;
+            const int pk = __builtin_amdgcn_readlane(pack, di * 3 + u + 1);
+            const int mv = pk & 7;
+            if (mv == 0 || cnt >= n + m) {
+                if (lane == 0)
+                    set_err(err, 2);  // failed to find a move
+                failed = 1;
+                break;
+            }
+            const int sb = pk >> 4;
+            const bool mism = pk & 8;
+            if (lane == 0) {
+                out[n + m - 1 - cnt] = (int8_t)mv;
+                if (mk) {
+                    // the forward step of this move ends at (ii, jj) (k_aln_props)
+                    if (mv == 1 && mism)
+                        mk[(size_t)jj * 9 + sb] = 1;
+                    else if (mv == 2 && do_indels)
+                        mk[(size_t)jj * 9 + 5 + sb] = 1;
+                    else if (mv == 3 && do_indels)
+                        mk[(size_t)jj * 9 + 4] = 1;
+                }
+            }
+            ++cnt;
+            if (mv == 1) {
+                errs += mism;
+                --ii;
+                --jj;
+            } else if (mv == 2) {
+                errs += 1;
+                --ii;
+            } else {
+                errs += 1;
+                --jj;
+            }
         }
     }
     if (lane == 0) {
