@@ -1898,6 +1898,325 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
     }
 }
 
+// ---------------------------------------------------------------------
+// k_score_sdma: k_score_seg's chains with LDS-DMA staging (the default for
+// wide bands).
+//
+// Same per-lane chain, operands, order and FP64 max-plus as lean_chain /
+// k_score_seg (identical results); the difference is how a segment's band
+// slices reach LDS.  For segment D (diagonals [D, D+S)) of work item a0 the
+// chains read kappa rows kb = D + 2 a0 - 1 .. kb + NR - 1 (NR = S + 128) at
+// elements e0 = (D-1) >> 1 .. e0 + W - 1 (W = S/2 + 1).  Each row's piece is
+// fetched as C = (W+1)/2 whole 16-B chunks from its 16-B aligned start
+// (global_load_lds_dwordx4: every lane DMAs one chunk straight into LDS, no
+// VGPR staging, no per-element predicates), so row r sits at LDS doubles
+// [r * 2C, r * 2C + 2C) with its first wanted element at offset
+// ((kb + r) * P + e0) & 1 = (kb + r + e0) & 1 (P odd).  The raw table rows
+// (match / mismatch / ins / del, and the read bases) of the segment come the
+// same way and are turned into {sub A,C,G,T, ins, del} records in LDS.
+// Segments are double-buffered: the DMA of the next segment -- of this read
+// or of the next read of the workgroup -- is in flight while the current
+// one is scored.  In split mode a workgroup takes a chunk of reads and
+// writes each read's partials (k_reduce then folds them in batch order).
+// ---------------------------------------------------------------------
+
+// 16 B per lane, global -> LDS at lds_base + lane * 16 (wave-uniform base)
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_base)
+                 : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int S>
+struct SdmaGeo {
+    static constexpr int W = S / 2 + 1;            // wanted doubles per kappa row
+    static constexpr int C = (W + 1) / 2;          // 16-B chunks per row (with the parity shift)
+    static constexpr int NR = S + 2 * 64;          // kappa rows per segment
+    static constexpr int NI = (NR * C + 63) / 64;  // DMA instructions per band
+    static constexpr int BUF = NI * 128;           // doubles per band buffer
+    static constexpr int NT = S + 65;              // table rows per segment
+    static constexpr int TC = (NT + 2 + 1) / 2;    // 16-B chunks of one raw table (<= 64)
+    static_assert(TC <= 64, "raw table slice must fit one DMA instruction");
+    static_assert((NT + 31) / 16 <= 64, "raw bases must fit one DMA instruction");
+};
+
+template <int S>
+__global__ void __launch_bounds__(64)
+k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+             const double *__restrict__ tabs, const double *__restrict__ bands,
+             double *__restrict__ dense, double *__restrict__ split, int split_mode, int rchunk)
+{
+    using Gm = SdmaGeo<S>;
+    constexpr int C = Gm::C, NI = Gm::NI, BUF = Gm::BUF, NT = Gm::NT, TC = Gm::TC;
+    constexpr int NB = (NT + 31) / 16;   // 16-B chunks of the raw read bases
+    __shared__ __attribute__((aligned(16))) double sBand[2][2][BUF];   // [buffer][A, B]
+    __shared__ __attribute__((aligned(16))) double sRaw[2][4][2 * TC];   // [buffer][match, mism, ins, del]
+    __shared__ __attribute__((aligned(16))) uint8_t sRawB[2][NB * 16];   // [buffer] read bases
+    __shared__ __attribute__((aligned(16))) double sT[NT * 6];         // records of the current segment
+    // XCD-aware over the whole (item, read chunk) grid (see k_score_seg)
+    const int nx = gridDim.x;
+    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
+    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
+    const int cell = x * xq + min(x, xr) + (lin >> 3);
+    const int bx = cell % nx, by = cell / nx;
+    const WorkItem wi = items[bx];
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int lane = threadIdx.x;
+    const int a = a0 + lane;
+    const bool active = a <= m;
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + by * rchunk;
+        if (r0 >= G.r1)
+            return;
+        r1 = min(r0 + rchunk, G.r1);
+    }
+    const bool hasS = a < m;
+    const double smask = hasS ? 0.0 : -RF_INF;
+    const int jn = min(a + 1, m);
+
+    // per-read lane geometry (lean_chain) and the wave's diagonal range
+    struct RG {
+        int dfirst, dlast, dlo, dhi;
+        bool peel;
+    };
+    auto geo = [&](const ScoreRead &R) {
+        RG g;
+        const int i0 = max(0, jn - R.c);
+        const int i1 = min(jn + R.vb, R.n);
+        const int ilast = min(i1, a + R.vb);
+        g.dfirst = i0 - a + R.c;
+        g.dlast = ilast - a + R.c;
+        g.peel = i1 > ilast;
+        int lo = active ? g.dfirst : INT_MAX, hi = active ? g.dlast + (g.peel ? 1 : 0) : -1;
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo = min(lo, __shfl_xor(lo, off));
+            hi = max(hi, __shfl_xor(hi, off));
+        }
+        g.dlo = __builtin_amdgcn_readfirstlane(lo) & ~1;   // even segment starts
+        g.dhi = __builtin_amdgcn_readfirstlane(hi);
+        return g;
+    };
+    // issue the DMA of segment D of read R into buffer `buf`
+    auto issue = [&](const ScoreRead &R, int D, int buf) {
+        const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, P = R.P, K = R.K;
+        const double *gA = bands + R.A;
+        const int64_t dB = R.B - R.A;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const int t = j * 64 + lane;
+            const int rr = t / C, cc = t - (t / C) * C;
+            const int kap = min(max(kb + rr, 0), K - 1);                  // rows outside the band: never read
+            const int64_t g = (((int64_t)kap * P + e0) & ~(int64_t)1) + 2 * cc;
+            glds16(gA + g, lds_addr(&sBand[buf][0][j * 128]));
+            glds16(gA + dB + g, lds_addr(&sBand[buf][1][j * 128]));
+        }
+        // raw tables: rows i in [ib, ib + NT): match / mism / ins at i - 1, del at i
+        const int ib = a0 - R.c + D;
+        const int n = R.n;
+        const int64_t t0[4] = {R.tab + ib - 1, R.tab + n + ib - 1, R.tab + 2 * (int64_t)n + ib - 1,
+                               R.tab + 3 * (int64_t)n + ib};
+        if (lane < TC) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                glds16(tabs + (t0[q] & ~(int64_t)1) + 2 * lane, lds_addr(&sRaw[buf][q][0]));
+        }
+        if (lane < NB) {
+            const int64_t b0 = R.sb + ib - 1;
+            glds16(bases + (b0 & ~(int64_t)15) + 16 * lane, lds_addr(&sRawB[buf][0]));
+        }
+    };
+    // raw tables of buffer `buf` -> records {sub A, C, G, T, ins, del} (align.jl:60-69)
+    auto records = [&](const ScoreRead &R, int D, int buf) {
+        const int ib = a0 - R.c + D;
+        const int n = R.n;
+        const int sm = (int)((R.tab + ib - 1) & 1), sx = (int)((R.tab + n + ib - 1) & 1),
+                  si = (int)((R.tab + 2 * (int64_t)n + ib - 1) & 1), sd = (int)((R.tab + 3 * (int64_t)n + ib) & 1),
+                  sb = (int)((R.sb + ib - 1) & 15);
+        for (int e = lane; e < NT; e += 64) {
+            const int i = min(max(ib + e, 0), n);                          // rows outside [0, n]: never read
+            const int k = min(max(max(i - 1, 0) - (ib - 1), 0), 2 * TC - 2);   // ks = max(i - 1, 0)
+            const int kd = min(max(i - ib, 0), 2 * TC - 2);
+            const int sbse = i >= 1 ? sRawB[buf][min(max(sb + i - ib, 0), NB * 16 - 1)] : 4;
+            lean_row(sT + 6 * e, sbse, sRaw[buf][0][sm + k], sRaw[buf][1][sx + k], sRaw[buf][2][si + k],
+                     sRaw[buf][3][sd + kd]);
+        }
+    };
+
+    double tI[4], tS[4], tD = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] = 0.0;
+        tS[k] = 0.0;
+    }
+    int cur = 0;
+    // invariant: at the top of a segment iteration, that segment's DMA is in
+    // flight into buffer `cur`
+    ScoreRead R = reads[r0];
+    RG g = geo(R);
+    if (g.dlo <= g.dhi)
+        issue(R, g.dlo, cur);
+    for (int r = r0; r < r1; ++r) {
+        bool issued_next = false;   // the next read's first segment is in flight
+        double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            prev[k] = -RF_INF;
+            accI[k] = -RF_INF;
+            accS[k] = -RF_INF;
+        }
+        const int c = R.c;
+        for (int D = g.dlo; D <= g.dhi; D += S) {
+            dma_wait_all();
+            wave_sync();                                   // segment D landed; previous chains done
+            records(R, D, cur);
+            const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, ib = a0 - c + D;
+            // the next segment (this read, or the next read's first) -> other buffer
+            ScoreRead Rn = R;
+            RG gn = g;
+            int Dn = D + S, rn = r;
+            if (Dn > g.dhi) {
+                rn = r + 1;
+                if (rn < r1) {
+                    Rn = reads[rn];
+                    gn = geo(Rn);
+                    Dn = gn.dlo;
+                }
+            }
+            const bool next = rn < r1 && Dn <= gn.dhi;
+            wave_sync();                                   // records visible
+            if (next)
+                issue(Rn, Dn, cur ^ 1);
+            issued_next = next && rn != r;
+            if (active) {
+                const double *sA = &sBand[cur][0][0];
+                const double *sB = &sBand[cur][1][0];
+                const int lo = max(D, g.dfirst), hi = min(D + S - 1, g.dlast);
+                // LDS index of element (kappa, d >> 1): row kappa - kb, shift (kappa + e0) & 1
+                auto at = [&](int kap, int d) { return (kap - kb) * (2 * C) + ((kap + e0) & 1) + (d >> 1) - e0; };
+                auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
+                    const int kap = d + 2 * a;
+                    const int ix = at(kap, d);
+                    ac = sA[ix];
+                    bI = sB[ix];
+                    bS = (hasS ? sB[at(kap + 1, d - 1)] : bI) + smask;
+                    const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
+                    u0 = rec[0];
+                    u1 = rec[1];
+                    u2 = rec[2];
+                };
+                if (lo <= hi) {
+                    double ac, bI, bS;
+                    double2 u0, u1, u2;
+                    ld(lo, ac, bI, bS, u0, u1, u2);
+                    double aprev = (lo >= 1 && a - c + lo >= 1) ? sA[at(lo - 1 + 2 * a, lo - 1)] : -RF_INF;
+                    for (int d = lo; d <= hi; ++d) {
+                        double acn, bIn, bSn;
+                        double2 v0, v1, v2;
+                        ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
+                        const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+                        const double dl = ac + u2.y;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
+                            prev[k] = best;
+                            accI[k] = vmax(accI[k], best + bI);
+                            accS[k] = vmax(accS[k], best + bS);
+                        }
+                        dd = vmax(dd, ac + bS);
+                        aprev = ac;
+                        ac = acn;
+                        bI = bIn;
+                        bS = bSn;
+                        u0 = v0;
+                        u1 = v1;
+                        u2 = v2;
+                    }
+                }
+                const int dp = g.dlast + 1;
+                if (g.peel && dp >= D && dp < D + S) {
+                    // last row of the new column lies below A/B column a's band (a < m)
+                    const int kap = dp + 2 * a;
+                    const double aprev = sA[at(kap - 1, dp - 1)];
+                    const double bSr = sB[at(kap + 1, dp - 1)];
+                    const double2 *rec = (const double2 *)(sT + 6 * (a - c + dp - ib));
+                    const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
+                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+                }
+            }
+            cur ^= 1;
+        }
+        if (active) {
+            const double qnan = __builtin_nan("");
+            if (split_mode & 1) {
+                // this read's partials (k_reduce folds the reads in batch order)
+                double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+                if (a < m) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                    dst[13] = dd;
+                }
+                if (a == 0) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        dst[k] = qnan;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+                    tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+                }
+                tD += dd;
+            }
+        }
+        // the next read; its first segment is in flight unless this read had none
+        if (r + 1 < r1) {
+            R = reads[r + 1];
+            g = geo(R);
+            if (g.dlo <= g.dhi && !issued_next)
+                issue(R, g.dlo, cur);
+        }
+    }
+    dma_wait_all();   // nothing may be left in flight when the wave ends
+    if (!active || (split_mode & 1))
+        return;
+    const double qnan = __builtin_nan("");
+    double *dst = dense + G.dense_off + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[5 + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[9 + k] = tS[k];
+        dst[13] = tD;
+    }
+    if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
 // Read-bandwidth probe over the band arena (calibrates the HBM roofline of
 // the scorer on the same allocation): grid-stride 16-B loads, 8 in flight.
 __global__ void __launch_bounds__(256) k_probe_stream(const dvec2 *__restrict__ src, int64_t n16,
@@ -2552,6 +2871,12 @@ __global__ void k_scatter(const Segment *__restrict__ segs, const uint8_t *__res
 
 namespace {
 
+// Every arena keeps ARENA_GUARD bytes before its first region and after its
+// last: k_score_seg's LDS-DMA staging reads whole 16-B chunks of band rows
+// and table rows, which may start up to one row before a region or end past
+// it (values never used); the guards keep those reads inside the allocation.
+constexpr int64_t ARENA_GUARD = 1 << 16;
+
 struct Region {
     int64_t off = -1;  // bytes
     int64_t cap = 0;
@@ -2614,6 +2939,8 @@ struct Opts {
     int seg_s = 24;         // RF_OPT_SEG_S: k_score_seg diagonals per segment (16, 24, 32)
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
+    int seg_ver = 2;        // RF_OPT_SEG_VER: wide-band scorer 2 = k_score_sdma, 1 = k_score_seg
+    int sdma_s = 8;         // RF_OPT_SDMA_S: k_score_sdma diagonals per segment (8, 12, 16)
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
@@ -2768,7 +3095,7 @@ int arena_grow(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
     for (auto *r : regs)
         if (r != skip)
             live += r->cap;
-    int64_t cap = std::max<int64_t>(live + need, (int64_t)(a.cap * 1.5));
+    int64_t cap = std::max<int64_t>(live + need + 2 * ARENA_GUARD, (int64_t)(a.cap * 1.5));
     cap = align_up(cap + cap / 8 + (1 << 20), 1 << 20);
     char *d = nullptr;
     HIPCHK(ctx, hipMalloc((void **)&d, cap));
@@ -2778,7 +3105,7 @@ int arena_grow(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
     // times would otherwise issue O(N log N) tiny copies
     std::vector<Segment> segs;
     segs.reserve(regs.size());
-    int64_t top = 0;
+    int64_t top = ARENA_GUARD;   // guard bytes before the first region
     for (auto *r : regs) {
         if (r == skip) {
             r->off = -1;
@@ -2812,7 +3139,7 @@ int region_ensure(rf_ctx *ctx, Arena &a, Region &r, int64_t bytes)
     bytes = align_up(std::max<int64_t>(bytes, 16), 256);
     if (r.off >= 0 && r.cap >= bytes)
         return 0;
-    if (a.top + bytes > a.cap)
+    if (a.top + bytes + ARENA_GUARD > a.cap)
         if (int e = arena_grow(ctx, a, bytes, &r))
             return e;
     r.off = a.top;
@@ -2878,6 +3205,8 @@ void load_env_opts(Opts &o)
     o.dp_np8 = env_int("RIFRAF_DP_NO_NP8", 0) ? 0 : 1;
     o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
     o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
+    o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
+    o.sdma_s = env_int("RIFRAF_SDMA_S", o.sdma_s);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -2944,7 +3273,26 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
         sm |= 2;
 #endif
     dim3 grid(nitems, gy);
-    if (pk.seg) {
+    if (pk.seg && ctx->opt.seg_ver >= 2) {
+        // split mode: each workgroup takes a chunk of reads (per-read partials,
+        // k_reduce folds them in batch order); ~16k workgroups in flight
+        int rchunk = 1;
+        if (split) {
+            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 16383) / 16384);
+            grid.y = (gy + rchunk - 1) / rchunk;
+        }
+        const int ss = ctx->opt.sdma_s;
+#define RF_SDMA_LAUNCH(S)                                                                                    \
+    hipLaunchKernelGGL((k_score_sdma<S>), grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,    \
+                       d_tabs, d_bands, dense, split, sm, rchunk)
+        if (ss == 16)
+            RF_SDMA_LAUNCH(16);
+        else if (ss == 12)
+            RF_SDMA_LAUNCH(12);
+        else
+            RF_SDMA_LAUNCH(8);
+#undef RF_SDMA_LAUNCH
+    } else if (pk.seg) {
         // RF_OPT_SEG_S: diagonals per segment (16, 24 or 32)
         const int segs = ctx->opt.seg_s;
         // RF_OPT_SEG_LDS: extra (unused) LDS bytes per workgroup -- caps the
@@ -3090,6 +3438,8 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NP8: return &o.dp_np8;
     case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
     case RF_OPT_DP_STREAMS: return &o.dp_streams;
+    case RF_OPT_SEG_VER: return &o.seg_ver;
+    case RF_OPT_SDMA_S: return &o.sdma_s;
     default: return nullptr;
     }
 }
@@ -3125,7 +3475,7 @@ int rf_reserve(rf_ctx *ctx, int64_t band_bytes)
     if (!ctx || band_bytes < 0)
         return RF_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    if (ctx->band_arena.cap - ctx->band_arena.top >= band_bytes)
+    if (ctx->band_arena.cap - ctx->band_arena.top >= band_bytes + ARENA_GUARD)
         return 0;
     return arena_grow(ctx, ctx->band_arena, band_bytes, nullptr);
 }
@@ -3163,9 +3513,9 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
             if (!(S.bases.off >= 0 && S.bases.cap >= bb)) need_b += bb;
             if (!(S.tabs.off >= 0 && S.tabs.cap >= tb)) need_t += tb;
         }
-        if (ctx->bytes_arena.top + need_b > ctx->bytes_arena.cap)
+        if (ctx->bytes_arena.top + need_b + ARENA_GUARD > ctx->bytes_arena.cap)
             if (int e = arena_grow(ctx, ctx->bytes_arena, need_b, nullptr)) return e;
-        if (ctx->tab_arena.top + need_t > ctx->tab_arena.cap)
+        if (ctx->tab_arena.top + need_t + ARENA_GUARD > ctx->tab_arena.cap)
             if (int e = arena_grow(ctx, ctx->tab_arena, need_t, nullptr)) return e;
     }
     // 1. regions (arena growth may move earlier regions: offsets are read after)

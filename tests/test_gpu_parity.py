@@ -357,8 +357,10 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (score_kernel, lean_nw, lean_lds_kb) engine options
     ("general", None, None),
-    ("seg", None, None),       # row-segment scorer (wide bands) on every shape
-    ("seg16", None, None),     # ... with 16-diagonal segments (seg_s=16)
+    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: k_score_sdma, 8 diagonals
+    ("sdma12", None, None),    # ... k_score_sdma with 12-diagonal segments
+    ("sdma16", None, None),    # ... and 16
+    ("seg16", None, None),     # register-staged k_score_seg with 16-diagonal segments (seg_s=16)
     ("seg32", None, None),     # ... with 32-diagonal segments
     (None, "1", None),
     (None, "2", None),
@@ -383,14 +385,18 @@ def test_score_dense_kernels(engine, opts, kern, nw, lds, mode):
     if lds is not None and lds.startswith("q"):
         parts = lds[1:].split("l")
         wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
-    segs = None
+    segs, ver, sdma = None, 2, 8
     if kern in ("seg16", "seg32"):
-        kern, segs = "seg", kern[3:]
+        kern, segs, ver = "seg", kern[3:], 1
+    elif kern in ("sdma12", "sdma16"):
+        kern, sdma = "seg", int(kern[4:])
     opts("score_kernel", kern or "auto")
     opts("lean_nw", int(nw or 8))
     opts("lean_lds_kb", int(lds or 0))
     opts("ws_q", int(wsq or 256))
     opts("seg_s", int(segs or 24))
+    opts("seg_ver", ver)
+    opts("sdma_s", sdma)
     opts("score_mode", mode)
     rng = np.random.default_rng(77)
     templates, seqs, bws = [], [], []
@@ -459,18 +465,25 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seg16", "seg32", "general"])
+@pytest.mark.parametrize("kern", [None, "sdma12", "sdma16", "seg16", "seg24", "seg32", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    row-segment scorer k_score_seg (default) and the in-place k_score
-    ("general") are both bit-exact against the oracle."""
+    LDS-DMA row-segment scorer k_score_sdma (default; 8, 12, 16 diagonals),
+    the register-staged k_score_seg and the in-place k_score ("general") are
+    all bit-exact against the oracle."""
     opts("seg_s", 24)
+    opts("seg_ver", 2)
+    opts("sdma_s", 8)
     if kern is None:
         opts("score_kernel", "auto")
-    elif kern in ("seg16", "seg32"):
+    elif kern.startswith("seg"):
         opts("score_kernel", "auto")
+        opts("seg_ver", 1)
         opts("seg_s", int(kern[3:]))
+    elif kern.startswith("sdma"):
+        opts("score_kernel", "auto")
+        opts("sdma_s", int(kern[4:]))
     else:
         opts("score_kernel", kern)
     opts("score_mode", mode)
