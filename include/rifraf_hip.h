@@ -96,8 +96,7 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_NP8      11   /* 0: H 128..255 bands in k_dp<64> instead of k_dpr<8> */
 #define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
 #define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
-#define RF_OPT_SEG_VER     14   /* wide-band scorer: 2 k_score_sdma, 1 k_score_seg     */
-#define RF_OPT_SDMA_S      15   /* k_score_sdma diagonals per segment: 8, 12, 16       */
+#define RF_OPT_SEG_VER     14   /* wide-band scorer: 3 k_score_segc, 1 k_score_seg     */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

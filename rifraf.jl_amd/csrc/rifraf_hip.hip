@@ -314,6 +314,15 @@ __device__ __forceinline__ double dpp_f64_any(double x)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+// one {sub A, C, G, T, ins, del} record per read row i (align.jl:60-69)
+__device__ __forceinline__ void lean_row(double *rec, int sbse, double mt, double mm, double ins, double del)
+{
+    double2 *r2 = (double2 *)rec;
+    r2[0] = make_double2(sbse == 0 ? mt : mm, sbse == 1 ? mt : mm);
+    r2[1] = make_double2(sbse == 2 ? mt : mm, sbse == 3 ? mt : mm);
+    r2[2] = make_double2(ins, del);
+}
+
 // Per-row inputs of the recurrence (align.jl:64-76, :87-103): the read base
 // and the score-table entries row ii uses, in forward or reverse indexing.
 struct RowRec {
@@ -1167,14 +1176,6 @@ __device__ __forceinline__ LeanWin lean_win(const ScoreRead &R, int m, int la0, 
     return w;
 }
 
-// one {sub A, C, G, T, ins, del} record per read row i (align.jl:60-69)
-__device__ __forceinline__ void lean_row(double *rec, int sbse, double mt, double mm, double ins, double del)
-{
-    double2 *r2 = (double2 *)rec;
-    r2[0] = make_double2(sbse == 0 ? mt : mm, sbse == 1 ? mt : mm);
-    r2[1] = make_double2(sbse == 2 ? mt : mm, sbse == 3 ? mt : mm);
-    r2[2] = make_double2(ins, del);
-}
 
 // Synchronous staging of a window (bands and tables through VGPRs).
 template <int Q>
@@ -1794,7 +1795,7 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
                     lean_row(sT + 6 * t, tsb[u], tmt[u], tmm[u], tin[u], tdl[u]);
             }
         };
-        if (dlo <= dhi)
+        if (dlo <= dhi && !(split_mode & 4))
             load_seg(dlo);
         for (int D = dlo; D <= dhi; D += SEG_S) {
             const int kb = D + 2 * a0 - 1;          // first staged kappa row
@@ -1803,9 +1804,9 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
             wave_sync();                            // previous segment's chains are done
             store_seg();
             wave_sync();
-            if (D + SEG_S <= dhi)
+            if (D + SEG_S <= dhi && !(split_mode & 4))
                 load_seg(D + SEG_S);
-            if (!active)
+            if (!active || (split_mode & 2))
                 continue;
             const int lo = max(D, dfirst), hi = min(D + SEG_S - 1, dlast);
             // software-pipelined: row d+1's LDS operands are read while row d
@@ -1899,70 +1900,45 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
 }
 
 // ---------------------------------------------------------------------
-// k_score_sdma: k_score_seg's chains with LDS-DMA staging (the default for
-// wide bands).
+// k_score_segc: k_score_seg with whole-chunk staging (the default for wide
+// bands).
 //
-// Same per-lane chain, operands, order and FP64 max-plus as lean_chain /
-// k_score_seg (identical results); the difference is how a segment's band
-// slices reach LDS.  For segment D (diagonals [D, D+S)) of work item a0 the
-// chains read kappa rows kb = D + 2 a0 - 1 .. kb + NR - 1 (NR = S + 128) at
-// elements e0 = (D-1) >> 1 .. e0 + W - 1 (W = S/2 + 1).  Each row's piece is
-// fetched as C = (W+1)/2 whole 16-B chunks from its 16-B aligned start
-// (global_load_lds_dwordx4: every lane DMAs one chunk straight into LDS, no
-// VGPR staging, no per-element predicates), so row r sits at LDS doubles
-// [r * 2C, r * 2C + 2C) with its first wanted element at offset
-// ((kb + r) * P + e0) & 1 = (kb + r + e0) & 1 (P odd).  The raw table rows
-// (match / mismatch / ins / del, and the read bases) of the segment come the
-// same way and are turned into {sub A,C,G,T, ins, del} records in LDS.
-// Segments are double-buffered: the DMA of the next segment -- of this read
-// or of the next read of the workgroup -- is in flight while the current
-// one is scored.  In split mode a workgroup takes a chunk of reads and
-// writes each read's partials (k_reduce then folds them in batch order).
+// Same chains, operands, order and FP64 max-plus as k_score_seg (identical
+// results).  A segment's piece of each kappa row -- W = S/2 + 1 doubles from
+// element e0 = (D-1) >> 1 -- is fetched as C = (W+1)/2 aligned 16-B chunks
+// (global_load_dwordx4, no per-element predicates: rows outside the band
+// are clamped, their values never read, and the arena guards keep chunk
+// over-reads inside the allocation), prefetched into VGPRs while the
+// current segment is scored, then written to LDS with ds_write_b128.  In LDS
+// the rows of even and odd local index live in two regions, so the 64 lanes
+// of a step (kappa rows two apart) read consecutive rows of one region:
+// row stride 2C doubles, a 2-way bank conflict for odd C.  Row r's first
+// wanted element sits at offset (kb + r + e0) & 1 (P odd).
 // ---------------------------------------------------------------------
-
-// 16 B per lane, global -> LDS at lds_base + lane * 16 (wave-uniform base)
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_base)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_base)
-                 : "memory");
-}
-__device__ __forceinline__ uint32_t lds_addr(const void *p)
-{
-    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
-}
-__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 template <int S>
-struct SdmaGeo {
+struct SegcGeo {
     static constexpr int W = S / 2 + 1;            // wanted doubles per kappa row
-    static constexpr int C = (W + 1) / 2;          // 16-B chunks per row (with the parity shift)
-    static constexpr int NR = S + 2 * 64;          // kappa rows per segment
-    static constexpr int NI = (NR * C + 63) / 64;  // DMA instructions per band
-    static constexpr int BUF = NI * 128;           // doubles per band buffer
+    static constexpr int C = (W + 1) / 2;          // 16-B chunks per row (parity shift included)
+    static constexpr int NR = S + 2 * 64;          // kappa rows per segment (even)
+    static constexpr int NH = NR / 2;              // rows per parity region
+    static constexpr int RS = NH * 2 * C;          // doubles per parity region
+    static constexpr int NU = (NR * C + 63) / 64;  // chunks per lane and band
     static constexpr int NT = S + 65;              // table rows per segment
-    static constexpr int TC = (NT + 2 + 1) / 2;    // 16-B chunks of one raw table (<= 64)
-    static_assert(TC <= 64, "raw table slice must fit one DMA instruction");
-    static_assert((NT + 31) / 16 <= 64, "raw bases must fit one DMA instruction");
+    static constexpr int NTL = (NT + 63) / 64;     // table rows per lane
 };
 
 template <int S>
 __global__ void __launch_bounds__(64)
-k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
              const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
              const double *__restrict__ tabs, const double *__restrict__ bands,
              double *__restrict__ dense, double *__restrict__ split, int split_mode, int rchunk)
 {
-    using Gm = SdmaGeo<S>;
-    constexpr int C = Gm::C, NI = Gm::NI, BUF = Gm::BUF, NT = Gm::NT, TC = Gm::TC;
-    constexpr int NB = (NT + 31) / 16;   // 16-B chunks of the raw read bases
-    __shared__ __attribute__((aligned(16))) double sBand[2][2][BUF];   // [buffer][A, B]
-    __shared__ __attribute__((aligned(16))) double sRaw[2][4][2 * TC];   // [buffer][match, mism, ins, del]
-    __shared__ __attribute__((aligned(16))) uint8_t sRawB[2][NB * 16];   // [buffer] read bases
-    __shared__ __attribute__((aligned(16))) double sT[NT * 6];         // records of the current segment
-    // XCD-aware over the whole (item, read chunk) grid (see k_score_seg)
+    using Gm = SegcGeo<S>;
+    constexpr int C = Gm::C, NR = Gm::NR, RS = Gm::RS, NU = Gm::NU, NT = Gm::NT, NTL = Gm::NTL;
+    __shared__ __attribute__((aligned(16))) double sA[2 * RS];
+    __shared__ __attribute__((aligned(16))) double sB[2 * RS];
+    __shared__ __attribute__((aligned(16))) double sT[NT * 6];
     const int nx = gridDim.x;
     const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
     const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
@@ -1972,8 +1948,8 @@ k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     const ScoreGroup G = groups[wi.group];
     const int m = G.m;
     const int a0 = wi.p0;
-    const int lane = threadIdx.x;
-    const int a = a0 + lane;
+    const int tid = threadIdx.x;
+    const int a = a0 + tid;
     const bool active = a <= m;
     int r0 = G.r0, r1 = G.r1;
     if (split_mode & 1) {
@@ -1984,91 +1960,37 @@ k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     }
     const bool hasS = a < m;
     const double smask = hasS ? 0.0 : -RF_INF;
-    const int jn = min(a + 1, m);
-
-    // per-read lane geometry (lean_chain) and the wave's diagonal range
-    struct RG {
-        int dfirst, dlast, dlo, dhi;
-        bool peel;
-    };
-    auto geo = [&](const ScoreRead &R) {
-        RG g;
-        const int i0 = max(0, jn - R.c);
-        const int i1 = min(jn + R.vb, R.n);
-        const int ilast = min(i1, a + R.vb);
-        g.dfirst = i0 - a + R.c;
-        g.dlast = ilast - a + R.c;
-        g.peel = i1 > ilast;
-        int lo = active ? g.dfirst : INT_MAX, hi = active ? g.dlast + (g.peel ? 1 : 0) : -1;
-        for (int off = 32; off >= 1; off >>= 1) {
-            lo = min(lo, __shfl_xor(lo, off));
-            hi = max(hi, __shfl_xor(hi, off));
-        }
-        g.dlo = __builtin_amdgcn_readfirstlane(lo) & ~1;   // even segment starts
-        g.dhi = __builtin_amdgcn_readfirstlane(hi);
-        return g;
-    };
-    // issue the DMA of segment D of read R into buffer `buf`
-    auto issue = [&](const ScoreRead &R, int D, int buf) {
-        const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, P = R.P, K = R.K;
-        const double *gA = bands + R.A;
-        const int64_t dB = R.B - R.A;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-            const int t = j * 64 + lane;
-            const int rr = t / C, cc = t - (t / C) * C;
-            const int kap = min(max(kb + rr, 0), K - 1);                  // rows outside the band: never read
-            const int64_t g = (((int64_t)kap * P + e0) & ~(int64_t)1) + 2 * cc;
-            glds16(gA + g, lds_addr(&sBand[buf][0][j * 128]));
-            glds16(gA + dB + g, lds_addr(&sBand[buf][1][j * 128]));
-        }
-        // raw tables: rows i in [ib, ib + NT): match / mism / ins at i - 1, del at i
-        const int ib = a0 - R.c + D;
-        const int n = R.n;
-        const int64_t t0[4] = {R.tab + ib - 1, R.tab + n + ib - 1, R.tab + 2 * (int64_t)n + ib - 1,
-                               R.tab + 3 * (int64_t)n + ib};
-        if (lane < TC) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                glds16(tabs + (t0[q] & ~(int64_t)1) + 2 * lane, lds_addr(&sRaw[buf][q][0]));
-        }
-        if (lane < NB) {
-            const int64_t b0 = R.sb + ib - 1;
-            glds16(bases + (b0 & ~(int64_t)15) + 16 * lane, lds_addr(&sRawB[buf][0]));
-        }
-    };
-    // raw tables of buffer `buf` -> records {sub A, C, G, T, ins, del} (align.jl:60-69)
-    auto records = [&](const ScoreRead &R, int D, int buf) {
-        const int ib = a0 - R.c + D;
-        const int n = R.n;
-        const int sm = (int)((R.tab + ib - 1) & 1), sx = (int)((R.tab + n + ib - 1) & 1),
-                  si = (int)((R.tab + 2 * (int64_t)n + ib - 1) & 1), sd = (int)((R.tab + 3 * (int64_t)n + ib) & 1),
-                  sb = (int)((R.sb + ib - 1) & 15);
-        for (int e = lane; e < NT; e += 64) {
-            const int i = min(max(ib + e, 0), n);                          // rows outside [0, n]: never read
-            const int k = min(max(max(i - 1, 0) - (ib - 1), 0), 2 * TC - 2);   // ks = max(i - 1, 0)
-            const int kd = min(max(i - ib, 0), 2 * TC - 2);
-            const int sbse = i >= 1 ? sRawB[buf][min(max(sb + i - ib, 0), NB * 16 - 1)] : 4;
-            lean_row(sT + 6 * e, sbse, sRaw[buf][0][sm + k], sRaw[buf][1][sx + k], sRaw[buf][2][si + k],
-                     sRaw[buf][3][sd + kd]);
-        }
-    };
-
     double tI[4], tS[4], tD = 0.0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         tI[k] = 0.0;
         tS[k] = 0.0;
     }
-    int cur = 0;
-    // invariant: at the top of a segment iteration, that segment's DMA is in
-    // flight into buffer `cur`
-    ScoreRead R = reads[r0];
-    RG g = geo(R);
-    if (g.dlo <= g.dhi)
-        issue(R, g.dlo, cur);
+    // LDS slot of chunk t = row r * C + cc of a band slice
+    auto lslot = [&](int t) {
+        const int r = t / C, cc = t - (t / C) * C;
+        return (r & 1) * RS + (r >> 1) * (2 * C) + 2 * cc;
+    };
     for (int r = r0; r < r1; ++r) {
-        bool issued_next = false;   // the next read's first segment is in flight
+        const ScoreRead R = reads[r];
+        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
+        const int jn = min(a + 1, m);
+        const int i0 = max(0, jn - c);
+        const int i1 = min(jn + vb, n);
+        const int ilast = min(i1, a + vb);
+        const int dfirst = i0 - a + c, dlast = ilast - a + c;
+        const bool peel = i1 > ilast;
+        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
+        for (int off = 32; off >= 1; off >>= 1) {
+            dlo = min(dlo, __shfl_xor(dlo, off));
+            dhi = max(dhi, __shfl_xor(dhi, off));
+        }
+        dlo = __builtin_amdgcn_readfirstlane(dlo) & ~1;   // even segment starts
+        dhi = __builtin_amdgcn_readfirstlane(dhi);
+        const double *gA = bands + R.A;
+        const int64_t dB = R.B - R.A;
+        const double *tm = tabs + R.tab;
+        const uint8_t *sq = bases + R.sb;
         double prev[4], accI[4], accS[4], dd = -RF_INF;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -2076,89 +1998,120 @@ k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             accI[k] = -RF_INF;
             accS[k] = -RF_INF;
         }
-        const int c = R.c;
-        for (int D = g.dlo; D <= g.dhi; D += S) {
-            dma_wait_all();
-            wave_sync();                                   // segment D landed; previous chains done
-            records(R, D, cur);
+        dvec2 ra[NU], rb[NU];
+        double tmt[NTL], tmm[NTL], tin[NTL], tdl[NTL];
+        int tsb[NTL];
+        auto load_seg = [&](int D) {
             const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, ib = a0 - c + D;
-            // the next segment (this read, or the next read's first) -> other buffer
-            ScoreRead Rn = R;
-            RG gn = g;
-            int Dn = D + S, rn = r;
-            if (Dn > g.dhi) {
-                rn = r + 1;
-                if (rn < r1) {
-                    Rn = reads[rn];
-                    gn = geo(Rn);
-                    Dn = gn.dlo;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int t = min(tid + 64 * u, NR * C - 1);
+                const int rr = t / C, cc = t - (t / C) * C;
+                const int kap = min(max(kb + rr, 0), K - 1);          // rows outside the band: never read
+                const int64_t g = (((int64_t)kap * P + e0) & ~(int64_t)1) + 2 * cc;
+                ra[u] = *(const dvec2 *)(gA + g);
+                rb[u] = *(const dvec2 *)(gA + dB + g);
+            }
+#pragma unroll
+            for (int u = 0; u < NTL; ++u) {
+                const int i = min(max(ib + tid + 64 * u, 0), n);
+                const int ks = max(i - 1, 0);
+                tsb[u] = i >= 1 ? sq[i - 1] : 4;
+                tmt[u] = tm[ks];
+                tmm[u] = tm[n + ks];
+                tin[u] = tm[2 * (size_t)n + ks];
+                tdl[u] = tm[3 * (size_t)n + i];
+            }
+        };
+        auto store_seg = [&]() {
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int t = tid + 64 * u;
+                if (t < NR * C) {
+                    const int l = lslot(t);
+                    *(dvec2 *)(sA + l) = ra[u];
+                    *(dvec2 *)(sB + l) = rb[u];
                 }
             }
-            const bool next = rn < r1 && Dn <= gn.dhi;
-            wave_sync();                                   // records visible
-            if (next)
-                issue(Rn, Dn, cur ^ 1);
-            issued_next = next && rn != r;
-            if (active) {
-                const double *sA = &sBand[cur][0][0];
-                const double *sB = &sBand[cur][1][0];
-                const int lo = max(D, g.dfirst), hi = min(D + S - 1, g.dlast);
-                // LDS index of element (kappa, d >> 1): row kappa - kb, shift (kappa + e0) & 1
-                auto at = [&](int kap, int d) { return (kap - kb) * (2 * C) + ((kap + e0) & 1) + (d >> 1) - e0; };
-                auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
-                    const int kap = d + 2 * a;
-                    const int ix = at(kap, d);
-                    ac = sA[ix];
-                    bI = sB[ix];
-                    bS = (hasS ? sB[at(kap + 1, d - 1)] : bI) + smask;
-                    const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
-                    u0 = rec[0];
-                    u1 = rec[1];
-                    u2 = rec[2];
-                };
-                if (lo <= hi) {
-                    double ac, bI, bS;
-                    double2 u0, u1, u2;
-                    ld(lo, ac, bI, bS, u0, u1, u2);
-                    double aprev = (lo >= 1 && a - c + lo >= 1) ? sA[at(lo - 1 + 2 * a, lo - 1)] : -RF_INF;
-                    for (int d = lo; d <= hi; ++d) {
-                        double acn, bIn, bSn;
-                        double2 v0, v1, v2;
-                        ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
-                        const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-                        const double dl = ac + u2.y;
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
-                            prev[k] = best;
-                            accI[k] = vmax(accI[k], best + bI);
-                            accS[k] = vmax(accS[k], best + bS);
-                        }
-                        dd = vmax(dd, ac + bS);
-                        aprev = ac;
-                        ac = acn;
-                        bI = bIn;
-                        bS = bSn;
-                        u0 = v0;
-                        u1 = v1;
-                        u2 = v2;
-                    }
-                }
-                const int dp = g.dlast + 1;
-                if (g.peel && dp >= D && dp < D + S) {
-                    // last row of the new column lies below A/B column a's band (a < m)
-                    const int kap = dp + 2 * a;
-                    const double aprev = sA[at(kap - 1, dp - 1)];
-                    const double bSr = sB[at(kap + 1, dp - 1)];
-                    const double2 *rec = (const double2 *)(sT + 6 * (a - c + dp - ib));
-                    const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
+            for (int u = 0; u < NTL; ++u) {
+                const int t = tid + 64 * u;
+                if (t < NT)
+                    lean_row(sT + 6 * t, tsb[u], tmt[u], tmm[u], tin[u], tdl[u]);
+            }
+        };
+        if (dlo <= dhi && !(split_mode & 4))
+            load_seg(dlo);
+        for (int D = dlo; D <= dhi; D += S) {
+            const int kb = D + 2 * a0 - 1;          // first staged kappa row
+            const int e0 = (D - 1) >> 1;            // first wanted element (diagonal D-1)
+            const int ib = a0 - c + D;              // first staged table row
+            wave_sync();                            // previous segment's chains are done
+            store_seg();
+            wave_sync();
+            if (D + S <= dhi && !(split_mode & 4))
+                load_seg(D + S);
+            if (!active || (split_mode & 2))
+                continue;
+            const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
+            // element (kappa, d >> 1): local row r = kappa - kb in region r & 1
+            const int sh0 = (kb + e0) & 1, sh1 = (kb + 1 + e0) & 1;
+            auto at = [&](int kap, int d) {
+                const int rr = kap - kb;
+                return (rr & 1) * RS + (rr >> 1) * (2 * C) + ((rr & 1) ? sh1 : sh0) + (d >> 1) - e0;
+            };
+            auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
+                const int kap = d + 2 * a;
+                const int ix = at(kap, d);
+                ac = sA[ix];
+                bI = sB[ix];
+                bS = (hasS ? sB[at(kap + 1, d - 1)] : bI) + smask;
+                const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
+                u0 = rec[0];
+                u1 = rec[1];
+                u2 = rec[2];
+            };
+            if (lo <= hi) {
+                double ac, bI, bS;
+                double2 u0, u1, u2;
+                ld(lo, ac, bI, bS, u0, u1, u2);
+                double aprev = (lo >= 1 && a - c + lo >= 1) ? sA[at(lo - 1 + 2 * a, lo - 1)] : -RF_INF;
+                for (int d = lo; d <= hi; ++d) {
+                    double acn, bIn, bSn;
+                    double2 v0, v1, v2;
+                    ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
                     const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+                    const double dl = ac + u2.y;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+                    for (int k = 0; k < 4; ++k) {
+                        const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
+                        prev[k] = best;
+                        accI[k] = vmax(accI[k], best + bI);
+                        accS[k] = vmax(accS[k], best + bS);
+                    }
+                    dd = vmax(dd, ac + bS);
+                    aprev = ac;
+                    ac = acn;
+                    bI = bIn;
+                    bS = bSn;
+                    u0 = v0;
+                    u1 = v1;
+                    u2 = v2;
                 }
             }
-            cur ^= 1;
+            const int dp = dlast + 1;
+            if (peel && dp >= D && dp < D + S) {
+                // last row of the new column lies below A/B column a's band (a < m)
+                const int kap = dp + 2 * a;
+                const double aprev = sA[at(kap - 1, dp - 1)];
+                const double bSr = sB[at(kap + 1, dp - 1)];
+                const double2 *rec = (const double2 *)(sT + 6 * (a - c + dp - ib));
+                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
+                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+            }
         }
         if (active) {
             const double qnan = __builtin_nan("");
@@ -2188,15 +2141,7 @@ k_score_sdma(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 tD += dd;
             }
         }
-        // the next read; its first segment is in flight unless this read had none
-        if (r + 1 < r1) {
-            R = reads[r + 1];
-            g = geo(R);
-            if (g.dlo <= g.dhi && !issued_next)
-                issue(R, g.dlo, cur);
-        }
     }
-    dma_wait_all();   // nothing may be left in flight when the wave ends
     if (!active || (split_mode & 1))
         return;
     const double qnan = __builtin_nan("");
@@ -2939,8 +2884,7 @@ struct Opts {
     int seg_s = 24;         // RF_OPT_SEG_S: k_score_seg diagonals per segment (16, 24, 32)
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
-    int seg_ver = 2;        // RF_OPT_SEG_VER: wide-band scorer 2 = k_score_sdma, 1 = k_score_seg
-    int sdma_s = 8;         // RF_OPT_SDMA_S: k_score_sdma diagonals per segment (8, 12, 16)
+    int seg_ver = 3;        // RF_OPT_SEG_VER: wide-band scorer 3 = k_score_segc, 1 = k_score_seg
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
@@ -3206,7 +3150,6 @@ void load_env_opts(Opts &o)
     o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
     o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
     o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
-    o.sdma_s = env_int("RIFRAF_SDMA_S", o.sdma_s);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3269,29 +3212,29 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
 #ifdef RIFRAF_DIAG
     // RIFRAF_LEAN_NOCOMP=1 (diagnostic builds only): the lean scorer stages
     // every window but skips the chains (measures its load pipeline alone)
-    if (ctx->opt.diag_lean_nocomp)
+    if (ctx->opt.diag_lean_nocomp & 1)
         sm |= 2;
+    if (ctx->opt.diag_lean_nocomp & 2)   // k_score_seg: skip the segment loads
+        sm |= 4;
 #endif
     dim3 grid(nitems, gy);
-    if (pk.seg && ctx->opt.seg_ver >= 2) {
-        // split mode: each workgroup takes a chunk of reads (per-read partials,
-        // k_reduce folds them in batch order); ~16k workgroups in flight
+    if (pk.seg && ctx->opt.seg_ver == 3) {
         int rchunk = 1;
         if (split) {
-            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 16383) / 16384);
+            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
-        const int ss = ctx->opt.sdma_s;
-#define RF_SDMA_LAUNCH(S)                                                                                    \
-    hipLaunchKernelGGL((k_score_sdma<S>), grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,    \
+        const int ss = ctx->opt.seg_s;
+#define RF_SEGC_LAUNCH(S)                                                                                    \
+    hipLaunchKernelGGL((k_score_segc<S>), grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,    \
                        d_tabs, d_bands, dense, split, sm, rchunk)
         if (ss == 16)
-            RF_SDMA_LAUNCH(16);
-        else if (ss == 12)
-            RF_SDMA_LAUNCH(12);
+            RF_SEGC_LAUNCH(16);
+        else if (ss == 32)
+            RF_SEGC_LAUNCH(32);
         else
-            RF_SDMA_LAUNCH(8);
-#undef RF_SDMA_LAUNCH
+            RF_SEGC_LAUNCH(24);
+#undef RF_SEGC_LAUNCH
     } else if (pk.seg) {
         // RF_OPT_SEG_S: diagonals per segment (16, 24 or 32)
         const int segs = ctx->opt.seg_s;
@@ -3439,7 +3382,6 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
     case RF_OPT_DP_STREAMS: return &o.dp_streams;
     case RF_OPT_SEG_VER: return &o.seg_ver;
-    case RF_OPT_SDMA_S: return &o.sdma_s;
     default: return nullptr;
     }
 }

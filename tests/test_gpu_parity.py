@@ -357,9 +357,10 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (score_kernel, lean_nw, lean_lds_kb) engine options
     ("general", None, None),
-    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: k_score_sdma, 8 diagonals
-    ("sdma12", None, None),    # ... k_score_sdma with 12-diagonal segments
-    ("sdma16", None, None),    # ... and 16
+    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: default k_score_segc
+    ("segc16", None, None),    # chunk-staged k_score_segc, 16 / 24 / 32 diagonals
+    ("segc24", None, None),
+    ("segc32", None, None),
     ("seg16", None, None),     # register-staged k_score_seg with 16-diagonal segments (seg_s=16)
     ("seg32", None, None),     # ... with 32-diagonal segments
     (None, "1", None),
@@ -385,18 +386,17 @@ def test_score_dense_kernels(engine, opts, kern, nw, lds, mode):
     if lds is not None and lds.startswith("q"):
         parts = lds[1:].split("l")
         wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
-    segs, ver, sdma = None, 2, 8
+    segs, ver = None, 3
     if kern in ("seg16", "seg32"):
         kern, segs, ver = "seg", kern[3:], 1
-    elif kern in ("sdma12", "sdma16"):
-        kern, sdma = "seg", int(kern[4:])
+    elif kern in ("segc16", "segc24", "segc32"):
+        kern, segs, ver = "seg", kern[4:], 3
     opts("score_kernel", kern or "auto")
     opts("lean_nw", int(nw or 8))
     opts("lean_lds_kb", int(lds or 0))
     opts("ws_q", int(wsq or 256))
     opts("seg_s", int(segs or 24))
     opts("seg_ver", ver)
-    opts("sdma_s", sdma)
     opts("score_mode", mode)
     rng = np.random.default_rng(77)
     templates, seqs, bws = [], [], []
@@ -465,25 +465,25 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "sdma12", "sdma16", "seg16", "seg24", "seg32", "general"])
+@pytest.mark.parametrize("kern", [None, "segc16", "segc24", "segc32", "seg16", "seg24", "seg32", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    LDS-DMA row-segment scorer k_score_sdma (default; 8, 12, 16 diagonals),
-    the register-staged k_score_seg and the in-place k_score ("general") are
-    all bit-exact against the oracle."""
+    chunk-staged row-segment scorer k_score_segc (default; 16, 24, 32
+    diagonals), the element-staged k_score_seg and the in-place k_score
+    ("general") are all bit-exact against the oracle."""
     opts("seg_s", 24)
-    opts("seg_ver", 2)
-    opts("sdma_s", 8)
+    opts("seg_ver", 3)
     if kern is None:
         opts("score_kernel", "auto")
+    elif kern.startswith("segc"):
+        opts("score_kernel", "auto")
+        opts("seg_ver", 3)
+        opts("seg_s", int(kern[4:]))
     elif kern.startswith("seg"):
         opts("score_kernel", "auto")
         opts("seg_ver", 1)
         opts("seg_s", int(kern[3:]))
-    elif kern.startswith("sdma"):
-        opts("score_kernel", "auto")
-        opts("sdma_s", int(kern[4:]))
     else:
         opts("score_kernel", kern)
     opts("score_mode", mode)
