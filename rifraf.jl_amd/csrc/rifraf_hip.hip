@@ -2537,11 +2537,11 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 // (moves_to_proposals, model.jl:458-480; k_aln_props fused into the walk --
 // the set union does not depend on the walk direction).
 // ---------------------------------------------------------------------
-constexpr int BTW_A = 4096;    // doubles of the A window (32 KB)
 constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
 
+template <int BTW_A>   // doubles of the A window (4096: 32 KB, 2048: 16 KB)
 __global__ void __launch_bounds__(64)
 k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
          const double *__restrict__ bands, int8_t *__restrict__ moves, int32_t *__restrict__ nmoves,
@@ -2886,6 +2886,7 @@ struct Opts {
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
     int seg_ver = 3;        // RF_OPT_SEG_VER: wide-band scorer 3 = k_score_segc, 1 = k_score_seg
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
+    int bt_win_kb = 32;     // RF_OPT_BT_WIN_KB: k_bt_win A window (32 or 16 KB of LDS)
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
@@ -3150,6 +3151,7 @@ void load_env_opts(Opts &o)
     o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
     o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
     o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
+    o.bt_win_kb = env_int("RIFRAF_BT_WIN_KB", o.bt_win_kb);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3382,6 +3384,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
     case RF_OPT_DP_STREAMS: return &o.dp_streams;
     case RF_OPT_SEG_VER: return &o.seg_ver;
+    case RF_OPT_BT_WIN_KB: return &o.bt_win_kb;
     default: return nullptr;
     }
 }
@@ -3908,7 +3911,8 @@ static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d
     if (!win.empty()) {
         if (int e = upload(ctx, ctx->scratch[16], win))
             return e;
-        hipLaunchKernelGGL(k_bt_win, dim3((unsigned)win.size()), dim3(64), 0, ctx->stream,
+        auto kern = ctx->opt.bt_win_kb == 16 ? k_bt_win<2048> : k_bt_win<4096>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)win.size()), dim3(64), 0, ctx->stream,
                            (const BTTask *)ctx->scratch[16].p, (const uint8_t *)ctx->bytes_arena.d,
                            (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d,
                            (int8_t *)ctx->scratch[3].p, d_cnt, d_cnt + nslots, ctx->d_err, d_mask, do_indels);

@@ -561,8 +561,9 @@ def test_alignment_proposals_device(engine, do_indels):
         np.testing.assert_array_equal(masks[c], exp, err_msg=f"cluster {c}")
 
 
+@pytest.mark.parametrize("win_kb", [32, 16])
 @pytest.mark.parametrize("L,bw,skew", [(700, 9, 0), (400, 40, 30), (300, 120, -40), (260, 9, 60), (90, 3, 0)])
-def test_backtrace_windowed(engine, opts, L, bw, skew):
+def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb):
     """k_bt_win (wave per read, LDS windows of kappa rows, re-staged as the
     walk leaves them) against the oracle's backtrace and count_errors, and the
     fused proposal marking against the host moves_to_proposals union, on long
@@ -587,6 +588,7 @@ def test_backtrace_windowed(engine, opts, L, bw, skew):
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
+    opts("bt_win_kb", win_kb)
     opts("bt_global", 0)
     got, nerr = engine.backtrace(np.arange(n))
     opts("bt_global", 1)
