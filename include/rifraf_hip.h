@@ -97,7 +97,7 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
 #define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
 #define RF_OPT_SEG_VER     14   /* wide-band scorer: 3 k_score_segc, 1 k_score_seg     */
-#define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 32 or 16 KB                  */
+#define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 16 (default) or 32 KB        */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

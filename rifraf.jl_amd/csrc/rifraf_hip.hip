@@ -2886,7 +2886,7 @@ struct Opts {
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
     int seg_ver = 3;        // RF_OPT_SEG_VER: wide-band scorer 3 = k_score_segc, 1 = k_score_seg
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
-    int bt_win_kb = 32;     // RF_OPT_BT_WIN_KB: k_bt_win A window (32 or 16 KB of LDS)
+    int bt_win_kb = 16;     // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS)
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
