@@ -201,7 +201,8 @@ int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms);
 /* Diagnostics: write probes over the band arena (DESTROYS band contents).
  * mode 1 = sequential 16-B stores over `bytes`; mode 2 = the DP fill's store
  * pattern: `nstreams` 16-lane streams each writing its own region in
- * `chunk_bytes` pieces.  Reports ms for one pass. */
+ * `chunk_bytes` pieces; modes 3 and 4 = modes 1 and 2 with nontemporal
+ * stores (the DP fill's).  Reports ms for one pass. */
 int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes,
                    int32_t nstreams, double *ms);
 

@@ -488,6 +488,9 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     }
 }
 
+#ifndef DPL_NO_LDS_OUT
+#define DPL_NO_LDS_OUT 0   // diagnostics only: lean steps skip their LDS band output
+#endif
 // Whole-row DPP rotate of an f64 (no "old" operand: every lane has a source).
 template <int CTRL>
 __device__ __forceinline__ double dpp_rot_f64(double x)
@@ -526,7 +529,7 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
         const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
         nv[r] = raw + lb[r];
-        if (st[r])
+        if (st[r] && !DPL_NO_LDS_OUT)
             o[r * ostep] = nv[r];
     }
 #pragma unroll
@@ -550,6 +553,13 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 // that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
 // several waves per CU
 __host__ __device__ constexpr int dpl_b(int np) { return np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK); }
+#ifndef DPL_SPREAD
+#define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
+#endif
+#define DPL_SPREAD_ON(np) (DPL_SPREAD && (np) == 1)
+#ifndef DPR_WPE1
+#define DPR_WPE1 1   // minimum waves per SIMD requested for the NP = 1 kernels
+#endif
 struct alignas(16) EdgeRec {
     double mt, mm, is, ds;
     int sb, col, pad0, pad1;
@@ -591,7 +601,7 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 // 15, 17), so a c4 task with P = 11 issues 12 stores per lane per block
 // instead of 18.
 template <int NP, bool LEAN, int PM = dpl_pmax(NP)>
-__global__ void __launch_bounds__(64) DPR_ATTR
+__global__ void __launch_bounds__(64) DPR_ATTR __attribute__((amdgpu_waves_per_eu(NP == 1 ? DPR_WPE1 : 1)))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
       double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink)
@@ -703,8 +713,15 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 EdgeRec e;
                 const int kk = kb + 2 * min(q, DPL_B - 1);
                 const int ii = max(1, min(top_c + (kk >> 1), T.n));   // clamped: see dpl_step
+#ifdef DPL_TAB_DIAG   // diagnostics only: every task reads one L2-resident table slice
+                const int ks = (rev ? T.n - ii : ii - 1) & 255;
+                const int kd = rev ? ks : ks + 1;
+                const double *tb = tabs;
+                const uint8_t *sbase = bases;
+#else
                 const int ks = rev ? T.n - ii : ii - 1;
                 const int kd = rev ? ks : ks + 1;
+#endif
                 e.sb = sbase[ks];
                 e.mt = tb[ks];
                 e.mm = tb[T.n + ks];
@@ -718,11 +735,24 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             if (q < DPL_B)
                 ein[q] = pend;
             pend = edge_load(k + 2 * DPL_B);
-            {
+            // spread flush (NP = 1): a block's flush stores are read from LDS
+            // into registers at the block end and issued one per period during
+            // the next block, so the store stream stays steady instead of one
+            // burst per block that stalls the issuing wave behind the memory
+            // pipeline.  Before the first block the pending set is the sink.
+            constexpr int FL = dpl_flush_stores(NP, PM);
+            constexpr int FLS = DPL_SPREAD_ON(NP) ? FL : 1;
+            dvec2 pv[FLS];
+            dvec2 *pg = (dvec2 *)sink;
+            int pnu = 0;
+            bool preal = false;
+#pragma unroll
+            for (int j = 0; j < FLS; ++j)
+                pv[j] = dvec2{0.0, 0.0};
+            if (!DPL_SPREAD_ON(NP)) {
                 // as many stores behind this load as the loop puts behind its
                 // own (to the sink), so that hipcc's wait for `pend` is vmcnt(FL)
                 // on every path into the loop, not vmcnt(0)
-                constexpr int FL = dpl_flush_stores(NP, PM);
                 dvec2 *g = (dvec2 *)sink;
                 const dvec2 z = {0.0, 0.0};
 #pragma unroll
@@ -731,9 +761,23 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             }
             wave_sync();
             for (int b = 0; b < nblk; ++b) {
+                // edge records are LDS broadcasts read one period ahead: a read
+                // issued right before its use exposes the full LDS latency on
+                // every step (the DP chain has nothing else to issue meanwhile)
+                EdgeRec E = ein[0];
 #pragma unroll
                 for (int p = 0; p < DPL_B; ++p) {
-                    const EdgeRec &E = ein[p];   // LDS broadcast within the task
+                    EdgeRec En;
+                    if (p + 1 < DPL_B)
+                        En = ein[p + 1];
+                    if (DPL_SPREAD_ON(NP)) {
+#pragma unroll
+                        for (int j = p; j < FLS; j += DPL_B) {
+                            const int e = preal ? min(q + 16 * j, pnu - 1) : q + 16 * j;
+                            DP_STORE(pg + e, pv[j]);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                     {   // even step: column k/2 enters lane 0
                         const int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
 #pragma unroll
@@ -758,6 +802,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     }
                     const int i1 = rev ? 2 * DPL_B - 2 - 2 * p : 2 * p + 1;
                     dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], ob + i1 * P + sl1, ostep);
+                    if (p + 1 < DPL_B)
+                        E = En;
                 }
                 wave_sync();
                 // next block's edges (loaded one block ago) -> LDS (harmless past
@@ -778,7 +824,6 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 // tasks past ntasks write the sink) keeps hipcc's wait for the next
                 // edge load at vmcnt(FL) instead of draining these stores.
                 {
-                    constexpr int FL = dpl_flush_stores(NP, PM);
                     const ptrdiff_t g0 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
                     const bool last = b + 1 == nblk;
                     ptrdiff_t lo, hi;
@@ -802,10 +847,26 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     const bool real = task_real && nu > 0;
                     dvec2 *g = real ? (dvec2 *)(band + lo2) : (dvec2 *)sink;
                     const dvec2 *o2 = (const dvec2 *)(ob + (lo2 - g0));
+                    if (DPL_SPREAD_ON(NP)) {
 #pragma unroll
-                    for (int j = 0; j < FL; ++j) {
-                        const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
-                        DP_STORE(g + e, real ? o2[e] : o2[0]);
+                        for (int j = 0; j < FLS; ++j)
+                            pv[j] = o2[real ? min(q + 16 * j, nu - 1) : 0];
+                        pg = g;
+                        pnu = nu;
+                        preal = real;
+                        if (last) {   // nothing follows: write the last block now
+#pragma unroll
+                            for (int j = 0; j < FLS; ++j) {
+                                const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
+                                DP_STORE(g + e, pv[j]);
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < FL; ++j) {
+                            const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
+                            DP_STORE(g + e, real ? o2[e] : o2[0]);
+                        }
                     }
                     if (task_real && q == 0 && (lo & 1))
                         band[lo] = ob[lo - g0];
@@ -4536,10 +4597,15 @@ __global__ void __launch_bounds__(64) k_probe_write(dvec2 *__restrict__ dst, int
                                                     int chunk16, int nstreams)
 {
     const dvec2 v = {1.0, 2.0};
-    if (mode == 1) {
+    const bool nt = mode >= 3;   // 3, 4: modes 1, 2 with nontemporal stores
+    if (mode == 1 || mode == 3) {
         const int64_t stride = (int64_t)gridDim.x * 64;
-        for (int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x; e < n16; e += stride)
-            dst[e] = v;
+        for (int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x; e < n16; e += stride) {
+            if (nt)
+                __builtin_nontemporal_store(v, dst + e);
+            else
+                dst[e] = v;
+        }
         return;
     }
     const int sid = blockIdx.x * 4 + (threadIdx.x >> 4);
@@ -4549,8 +4615,12 @@ __global__ void __launch_bounds__(64) k_probe_write(dvec2 *__restrict__ dst, int
     const int64_t per = n16 / nstreams;
     dvec2 *g = dst + (int64_t)sid * per;
     for (int64_t c0 = 0; c0 + chunk16 <= per; c0 += chunk16) {
-        for (int e = q; e < chunk16; e += 16)
-            g[c0 + e] = v;
+        for (int e = q; e < chunk16; e += 16) {
+            if (nt)
+                __builtin_nontemporal_store(v, g + c0 + e);
+            else
+                g[c0 + e] = v;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -4558,12 +4628,12 @@ __global__ void __launch_bounds__(64) k_probe_write(dvec2 *__restrict__ dst, int
 int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes, int32_t nstreams,
                    double *ms)
 {
-    if (!ctx || bytes < 0 || !ms || (mode != 1 && mode != 2) || (mode == 2 && (chunk_bytes < 16 || nstreams < 1)))
+    if (!ctx || bytes < 0 || !ms || mode < 1 || mode > 4 || ((mode & 1) == 0 && (chunk_bytes < 16 || nstreams < 1)))
         return fail(ctx, RF_ERR_ARG, "rf_probe_write: bad arguments");
     (void)hipSetDevice(ctx->device);
     bytes = std::min<int64_t>(bytes, ctx->band_arena.cap) & ~(int64_t)15;
     const int64_t n16 = bytes / 16;
-    const unsigned blocks = mode == 1 ? 256 * 32 : (unsigned)((nstreams + 3) / 4);
+    const unsigned blocks = (mode & 1) ? 256 * 32 : (unsigned)((nstreams + 3) / 4);
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     hipLaunchKernelGGL(k_probe_write, dim3(blocks), dim3(64), 0, ctx->stream, (dvec2 *)ctx->band_arena.d, n16,
                        mode, chunk_bytes / 16, nstreams);
