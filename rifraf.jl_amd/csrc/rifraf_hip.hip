@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rifraf_hip.h"
@@ -89,6 +90,16 @@ struct alignas(16) DPTask {
     int32_t P;      // kappa row stride
     int32_t pad;
 };
+
+// DPTask.flags bit: the read carries row codes (rf_set_sequences) -- one
+// 8-B record per read position i: bits 0-15 the code of (match, mismatch,
+// ins)[i], 16-31 / 32-47 the codes of del[i] / del[i+1], 48-55 the base.
+// Codes index the context's dictionary: RF_CODES entries of 4 doubles
+// {match, mismatch, ins, 0}, then RF_CODES del values.
+constexpr int RF_TASK_CODED = 1024;
+constexpr int RF_CODES = 1 << 16;
+// doubles from a read's table start to its row-code records
+__host__ __device__ inline int64_t row_code_off(int64_t n, int64_t nci, int64_t ncd) { return 4 * n + 1 + nci + ncd; }
 
 // One batch read of a scoring group.
 struct alignas(16) ScoreRead {
@@ -604,7 +615,8 @@ template <int NP, bool LEAN, int PM = dpl_pmax(NP)>
 __global__ void __launch_bounds__(64) DPR_ATTR __attribute__((amdgpu_waves_per_eu(NP == 1 ? DPR_WPE1 : 1)))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
-      double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink)
+      double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink,
+      const double *__restrict__ lut)
 {
     constexpr int DPL_B = dpl_b(NP);
     const int q = threadIdx.x & 15;
@@ -709,32 +721,56 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const int sl1 = rev ? (T.H - 2 - 2 * q * NP) >> 1 : q * NP;
             const int ostep = rev ? -1 : 1;
             const int top_c = 16 * NP - T.c;
-            auto edge_load = [&](int kb) {   // lane q < DPL_B: the period kb + 2q edge row and column
+            // Edge records.  A task whose read has row codes (DPTask flag
+            // RF_TASK_CODED) reads one 8-B code record per row from HBM and the
+            // table values from the context's code dictionary (L2-resident),
+            // instead of 4 table doubles per row; the values are the same
+            // doubles.  The code record of a block is loaded one block before
+            // its dictionary entries, so neither load's wait covers the
+            // block's own band stores.
+            const bool coded = T.flags & RF_TASK_CODED;
+            const uint64_t *codes = (const uint64_t *)(tb + row_code_off(T.n, T.ncins, T.ncdel));
+            auto edge_ks = [&](int kb) {   // lane q < DPL_B: the period kb + 2q edge row (clamped: see dpl_step)
+                const int kk = kb + 2 * min(q, DPL_B - 1);
+                const int ii = max(1, min(top_c + (kk >> 1), T.n));
+                return rev ? T.n - ii : ii - 1;
+            };
+            auto code_load = [&](int kb) -> uint64_t { return coded ? codes[edge_ks(kb)] : 0; };
+            auto edge_load = [&](int kb, uint64_t rec) {
                 EdgeRec e;
                 const int kk = kb + 2 * min(q, DPL_B - 1);
-                const int ii = max(1, min(top_c + (kk >> 1), T.n));   // clamped: see dpl_step
 #ifdef DPL_TAB_DIAG   // diagnostics only: every task reads one L2-resident table slice
-                const int ks = (rev ? T.n - ii : ii - 1) & 255;
-                const int kd = rev ? ks : ks + 1;
+                const int ks = edge_ks(kb) & 255;
                 const double *tb = tabs;
                 const uint8_t *sbase = bases;
 #else
-                const int ks = rev ? T.n - ii : ii - 1;
-                const int kd = rev ? ks : ks + 1;
+                const int ks = edge_ks(kb);
 #endif
-                e.sb = sbase[ks];
-                e.mt = tb[ks];
-                e.mm = tb[T.n + ks];
-                e.is = tb[2 * (size_t)T.n + ks];
-                e.ds = tb[3 * (size_t)T.n + kd];
+                const int kd = rev ? ks : ks + 1;
+                if (coded) {
+                    const double *l3 = lut + 4 * (int)(rec & 0xffff);
+                    const dvec2 mt_mm = *(const dvec2 *)l3;
+                    e.mt = mt_mm.x;
+                    e.mm = mt_mm.y;
+                    e.is = l3[2];
+                    e.ds = lut[4 * RF_CODES + (int)((rec >> (rev ? 16 : 32)) & 0xffff)];
+                    e.sb = (int)(rec >> 48) & 0xff;
+                } else {
+                    e.sb = sbase[ks];
+                    e.mt = tb[ks];
+                    e.mm = tb[T.n + ks];
+                    e.is = tb[2 * (size_t)T.n + ks];
+                    e.ds = tb[3 * (size_t)T.n + kd];
+                }
                 const int jj = max(1, min(kk >> 1, T.m));
                 e.col = tbase[rev ? T.m - jj : jj - 1];
                 return e;
             };
-            EdgeRec pend = edge_load(k);
+            EdgeRec pend = edge_load(k, code_load(k));
             if (q < DPL_B)
                 ein[q] = pend;
-            pend = edge_load(k + 2 * DPL_B);
+            pend = edge_load(k + 2 * DPL_B, code_load(k + 2 * DPL_B));
+            uint64_t pcode = code_load(k + 4 * DPL_B);
             // spread flush (NP = 1): a block's flush stores are read from LDS
             // into registers at the block end and issued one per period during
             // the next block, so the store stream stays steady instead of one
@@ -814,7 +850,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 // is one in-order counter for loads and stores, so a load issued
                 // after the stores could only be waited for by draining them
                 // (clamped rows: past the interior it reads valid, unused rows)
-                pend = edge_load(k + 4 * DPL_B);
+                pend = edge_load(k + 4 * DPL_B, pcode);
+                pcode = code_load(k + 6 * DPL_B);
                 // flush: the block's 2*DPL_B kappa rows are one contiguous run of the
                 // band [g0, g0 + blk).  Only whole 128-B lines are written (a partial
                 // line would leave L2 as a partial HBM write): the part past the last
@@ -2896,6 +2933,7 @@ struct Arena {
 struct SeqObj {
     bool valid = false;
     bool finite = false;   // match / mismatch / ins / del tables hold no -Inf (lean DP eligible)
+    bool coded = false;    // row codes written after the tables (RF_TASK_CODED)
     int32_t n = 0, ncins = 0, ncdel = 0;
     Region bases, tabs;
 };
@@ -2931,6 +2969,102 @@ struct ScorePick {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+};
+
+// Code dictionary of the row codes (RF_TASK_CODED): every distinct
+// (match, mismatch, ins) triple and del value of the context's reads gets a
+// 16-bit code, first come first served, keyed by the exact bit patterns.  A
+// read whose values would need a code past RF_CODES - 1 stays uncoded (its
+// DP reads the tables directly).  Entries are only appended, so codes of
+// earlier reads stay valid; `lut` is the device copy (RF_CODES x 4 triple
+// doubles, then RF_CODES del doubles).
+struct CodeDict {
+    struct K3 {
+        uint64_t a, b, c;
+        bool operator==(const K3 &o) const { return a == o.a && b == o.b && c == o.c; }
+    };
+    struct H3 {
+        size_t operator()(const K3 &k) const
+        {
+            return (size_t)((k.a * 0x9E3779B97F4A7C15ull) ^ (k.b * 0xC2B2AE3D27D4EB4Full) ^ (k.c * 0x165667B19E3779F9ull));
+        }
+    };
+    std::unordered_map<K3, uint32_t, H3> t3;
+    std::unordered_map<uint64_t, uint32_t> d1;
+    std::vector<double> t3v, d1v;   // host copies of the entries
+    size_t up3 = 0, up1 = 0;        // entries already on the device
+    // direct-mapped front caches (few distinct values per read set)
+    struct C3 { K3 k; int32_t code = -1; };
+    struct C1 { uint64_t k; int32_t code = -1; };
+    std::vector<C3> c3 = std::vector<C3>(4096);
+    std::vector<C1> c1 = std::vector<C1>(4096);
+    DevBuf lut;
+
+    static uint64_t bits(double x)
+    {
+        uint64_t u;
+        std::memcpy(&u, &x, 8);
+        return u;
+    }
+    int32_t code3(double mt, double mm, double is)
+    {
+        const K3 k{bits(mt), bits(mm), bits(is)};
+        C3 &c = c3[(H3()(k) >> 20) & 4095];
+        if (c.code >= 0 && c.k == k)
+            return c.code;
+        auto it = t3.find(k);
+        int32_t code;
+        if (it != t3.end()) {
+            code = (int32_t)it->second;
+        } else {
+            if (t3.size() >= (size_t)RF_CODES)
+                return -1;
+            code = (int32_t)t3.size();
+            t3.emplace(k, (uint32_t)code);
+            t3v.insert(t3v.end(), {mt, mm, is, 0.0});
+        }
+        c.k = k;
+        c.code = code;
+        return code;
+    }
+    int32_t code1(double d)
+    {
+        const uint64_t k = bits(d);
+        C1 &c = c1[((k * 0x9E3779B97F4A7C15ull) >> 40) & 4095];
+        if (c.code >= 0 && c.k == k)
+            return c.code;
+        auto it = d1.find(k);
+        int32_t code;
+        if (it != d1.end()) {
+            code = (int32_t)it->second;
+        } else {
+            if (d1.size() >= (size_t)RF_CODES)
+                return -1;
+            code = (int32_t)d1.size();
+            d1.emplace(k, (uint32_t)code);
+            d1v.push_back(d);
+        }
+        c.k = k;
+        c.code = code;
+        return code;
+    }
+    // one read's records (false: the dictionary is full, read stays uncoded)
+    bool encode(int64_t n, const uint8_t *base, const double *mt, const double *mm, const double *is,
+                const double *del, uint64_t *rec)
+    {
+        int32_t dprev = code1(del[0]);
+        if (dprev < 0)
+            return false;
+        for (int64_t i = 0; i < n; ++i) {
+            const int32_t t = code3(mt[i], mm[i], is[i]);
+            const int32_t dn = code1(del[i + 1]);
+            if (t < 0 || dn < 0)
+                return false;
+            rec[i] = (uint64_t)t | ((uint64_t)dprev << 16) | ((uint64_t)dn << 32) | ((uint64_t)base[i] << 48);
+            dprev = dn;
+        }
+        return true;
+    }
 };
 
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
@@ -2970,6 +3104,7 @@ struct rf_ctx {
     Arena bytes_arena;  // sequence + template bases
     Arena tab_arena;    // sequence tables
     Arena band_arena;   // A / B bands
+    CodeDict codes;     // row-code dictionary (RF_TASK_CODED)
     std::vector<SeqObj> seqs;
     std::vector<TplObj> tpls;
     std::vector<Slot> slots;
@@ -3404,6 +3539,8 @@ int rf_destroy(rf_ctx *ctx)
             (void)hipFree(b.p);
     if (ctx->grow_segs.p)
         (void)hipFree(ctx->grow_segs.p);
+    if (ctx->codes.lut.p)
+        (void)hipFree(ctx->codes.lut.p);
     if (ctx->pinned)
         (void)hipHostFree(ctx->pinned);
     if (ctx->d_err)
@@ -3515,7 +3652,7 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
             const int64_t nci = cins_off ? cins_off[k + 1] - cins_off[k] : 0;
             const int64_t ncd = cdel_off ? cdel_off[k + 1] - cdel_off[k] : 0;
             const int64_t bb = align_up(std::max<int64_t>(n, 16), 256);
-            const int64_t tb = align_up(std::max<int64_t>((4 * n + 1 + nci + ncd) * 8, 16), 256);
+            const int64_t tb = align_up(std::max<int64_t>((row_code_off(n, nci, ncd) + n) * 8, 16), 256);
             if (!(S.bases.off >= 0 && S.bases.cap >= bb)) need_b += bb;
             if (!(S.tabs.off >= 0 && S.tabs.cap >= tb)) need_t += tb;
         }
@@ -3538,10 +3675,11 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
         S.ncdel = (int32_t)ncd;
         if (int e = region_ensure(ctx, ctx->bytes_arena, S.bases, n))
             return e;
-        if (int e = region_ensure(ctx, ctx->tab_arena, S.tabs, (4 * n + 1 + nci + ncd) * 8))
+        // tables [match|mismatch|ins|del|cins|cdel], then one row-code record per position
+        if (int e = region_ensure(ctx, ctx->tab_arena, S.tabs, (row_code_off(n, nci, ncd) + n) * 8))
             return e;
         nb += n;
-        nt += 4 * n + 1 + nci + ncd;
+        nt += row_code_off(n, nci, ncd) + n;
     }
     // 2. pack into the pinned staging buffer: tables [match|mismatch|ins|del|
     //    cins|cdel] per sequence, then the bases as given
@@ -3572,16 +3710,31 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
             std::memcpy(h + 4 * n + 1, cins + cins_off[k], nci * 8);
         if (ncd)
             std::memcpy(h + 4 * n + 1 + nci, cdel + cdel_off[k], ncd * 8);
-        const int64_t len = 4 * n + 1 + nci + ncd;
+        const int64_t len = row_code_off(n, nci, ncd) + n;
         bool fin = true;
         for (int64_t e = 0; e < 4 * n + 1; ++e)
             fin = fin && std::isfinite(h[e]);
         ctx->seqs[first + k].finite = fin;
+        ctx->seqs[first + k].coded =
+            ctx->codes.encode(n, bases + off[k], h, h + n, h + 2 * n, h + 3 * n, (uint64_t *)(h + row_code_off(n, nci, ncd)));
         st[k] = {at * 8, S.tabs.off, len * 8, 0};
         sb[k] = {off[k] - off[0], S.bases.off, n, 0};
         at += len;
     }
-    // 3. one H2D copy each + device scatter
+    // 3. new code-dictionary entries, one H2D copy each + device scatter
+    {
+        CodeDict &D = ctx->codes;
+        if (int e = ensure_buf(ctx, D.lut, (size_t)RF_CODES * 5 * 8)) return e;
+        const size_t n3 = D.t3v.size() / 4, n1 = D.d1v.size();
+        if (n3 > D.up3)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * D.up3, D.t3v.data() + 4 * D.up3, (n3 - D.up3) * 32,
+                                       hipMemcpyHostToDevice, ctx->stream));
+        if (n1 > D.up1)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * (size_t)RF_CODES + D.up1, D.d1v.data() + D.up1,
+                                       (n1 - D.up1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        D.up3 = n3;
+        D.up1 = n1;
+    }
     if (int e = ensure_buf(ctx, ctx->scratch[6], (size_t)std::max<int64_t>(nt * 8, 16))) return e;
     if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
     if (nseq > 0) {
@@ -3752,7 +3905,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.ncins = S.ncins;
                 t.ncdel = S.ncdel;
                 t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (flags & RF_SKEW) ? 2 : 0) |
-                          (dir == 0 && (flags & RF_TRIM) ? 4 : 0);
+                          (dir == 0 && (flags & RF_TRIM) ? 4 : 0) | (S.coded ? RF_TASK_CODED : 0);
 #ifdef RIFRAF_DIAG
                 // RIFRAF_DP_SINK=1 (diagnostic builds only): the blocked interior's
                 // band stores all go to one small sink buffer (bands are then invalid)
@@ -3834,6 +3987,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     const uint8_t *d_bases = (const uint8_t *)ctx->bytes_arena.d;
     const double *d_tabs = (const double *)ctx->tab_arena.d;
     double *d_bands = (double *)ctx->band_arena.d;
+    const double *d_lut = (const double *)ctx->codes.lut.p;
 
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     // Each kernel class is its own launch.  The classes are independent (disjoint
@@ -3896,16 +4050,16 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         const int n = (int)L.n;
         if (L.kind < 8) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
-                                 double *);
+                                 double *, const double *);
             const KFn kr[8] = {k_dpr<1, false>, k_dpr<1, true>, k_dpr<2, false>, k_dpr<2, true>,
                                k_dpr<4, false>, k_dpr<4, true>, k_dpr<8, false>, k_dpr<8, true>};
             const int np = 1 << (L.kind >> 1);
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
-                               d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p);
+                               d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 16) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
-                                 double *);
+                                 double *, const double *);
 #define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b)>
             const KFn kp[16] = {KP(0, 0), KP(0, 1), KP(0, 2), KP(0, 3), KP(1, 0), KP(1, 1), KP(1, 2), KP(1, 3),
                                 KP(2, 0), KP(2, 1), KP(2, 2), KP(2, 3), KP(3, 0), KP(3, 1), KP(3, 2), KP(3, 3)};
@@ -3913,7 +4067,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const int c = L.kind - 16, npi = c >> 2, pmi = c & 3;
             hipLaunchKernelGGL(kp[c], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)),
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
-                               (double *)ctx->scratch[7].p);
+                               (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,

@@ -630,3 +630,26 @@ def test_plan_cache_follows_slot_contents(engine):
         mask[0, :5] = False
         mask[np.arange(1, len(t) + 1), t.astype(np.int64)] = False
         np.testing.assert_array_equal(got[mask], ref[mask])
+
+
+def test_row_code_dictionary_overflow():
+    """Reads with all-distinct log error probabilities fill the 65 536-entry
+    row-code dictionary part way through one upload: later reads stay
+    uncoded and their DP reads the tables directly, in the same launches
+    (and waves) as coded reads.  Every band stays bit-exact."""
+    from rifraf_amd.engine import Engine
+    rng = np.random.default_rng(65536)
+    L, bw, nreads = 1000, 9, 80
+    t = random_seq(L, rng)
+    seqs = []
+    for k in range(nreads):
+        r = make_read(t, rng, 0.01, bw)
+        lp = -rng.uniform(0.5, 3.0, len(r.seq))   # continuous: every position its own code
+        if k % 3 == 0:
+            lp = np.round(r.error_log_p, 1)       # phred-like reads interleaved (shared codes)
+        seqs.append(RifrafSequence(r.seq, lp, bw, SEQ_SCORES))
+    e = Engine(0)
+    try:
+        _check_bands(e, t, seqs, [bw] * nreads)
+    finally:
+        e.close()
