@@ -98,6 +98,7 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
 #define RF_OPT_SEG_VER     14   /* wide-band scorer: 3 k_score_segc, 1 k_score_seg     */
 #define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 16 (default) or 32 KB        */
+#define RF_OPT_STAGE_KB    16   /* rf_set_sequences host staging chunk, KB of tables   */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 
@@ -124,6 +125,12 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq,
 /* Templates (consensus sequences, one per cluster): ids [first, first+n). */
 int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl,
                      const uint8_t *bases, const int64_t *off);
+
+/* Templates with arbitrary ids: ids[k] receives bases off[k]..off[k+1]
+ * (rf_set_templates for a sparse set, e.g. the clusters of a batched run
+ * whose consensus changed this iteration). */
+int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids,
+                         const uint8_t *bases, const int64_t *off);
 
 /* Batched DP fill.  Job k aligns sequence seq[k] (rows) against template
  * tpl[k] (columns) with bandwidth bw[k] into slot slot[k].  flags: RF_FWD
@@ -185,6 +192,74 @@ int rf_score_dense(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
  * goes straight into the RCCL all-gather buffer without a host round trip. */
 int rf_score_dense_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
                        const int32_t *slots, double *dev_out);
+
+/* Native batched rifraf() (src/model.jl:1116-1275) for reference-free
+ * clusters: the INIT stage of every cluster runs in lockstep on this context
+ * with one batched engine call per step kind (rifraf_batch.cpp); each
+ * cluster ends exactly as a separate rifraf() call would (consensus, score,
+ * iteration count).  Scope: no reference, deterministic batches
+ * (batch_fixed, or batch_size >= #reads); the caller (rifraf_amd.batch)
+ * uploads the reads and initial consensus first and supplies the host
+ * values that need the Python mirror's transcendental functions.
+ *   read_off[c]..read_off[c+1]: cluster c's reads; read_seq / read_len per
+ *     read: its sequence id and length; threshold per read:
+ *     cquantile(Poisson(est_n_errors), bandwidth_pvalue) (model.jl:661)
+ *   fixed_off / fixed: the fixed batch per cluster (local read indices in
+ *     batch order, sortperm of est_n_errors; required if batch_fixed)
+ *   slot_base[c]: first of the cluster's batch slots; tpl_id[c]: its template
+ *   cons / cons_off: the initial consensus per cluster (already uploaded)
+ * Outputs per cluster: final score, INIT iterations, status (0 = reached
+ * max_iters, 1 = converged, 2 = failed: rf_batch_fetch has the message),
+ * consensus length; out_bw per read = final bandwidth, negated once
+ * bandwidth_fixed.  Results stay in the context until rf_batch_release. */
+typedef struct rf_batch_params {
+    int32_t max_iters;
+    int32_t min_dist;
+    int32_t bandwidth;               /* initial bandwidth of every read */
+    int32_t do_alignment_proposals;
+    int32_t batch_fixed;
+    int32_t batch_size;              /* params.batch_size (<= 1: every read) */
+    double batch_threshold;
+} rf_batch_params;
+int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
+                    const int32_t *read_off, const int32_t *read_seq, const int32_t *read_len,
+                    const double *threshold, const int32_t *fixed_off, const int32_t *fixed,
+                    const int32_t *slot_base, const int32_t *tpl_id, const uint8_t *cons,
+                    const int64_t *cons_off, double *out_score, int32_t *out_iters,
+                    int32_t *out_status, int64_t *out_len, int32_t *out_bw);
+/* Cluster c of the last rf_rifraf_batch: consensus (out_len[c] bytes), the
+ * consensus at each INIT iteration (stage_len[i] bytes each, concatenated
+ * in `stages`), the final batch (local read indices) and the error message
+ * of a failed cluster.  Any output may be NULL. */
+int rf_batch_fetch(rf_ctx *ctx, int32_t cluster, uint8_t *cons, int64_t *stage_len, uint8_t *stages,
+                   int32_t *batch, char *err, int64_t err_cap);
+/* Free the context's stored batch results. */
+void rf_batch_release(rf_ctx *ctx);
+/* alignment_error_probs (model.jl:817-840) before its final normalisation,
+ * for many groups at once: backtraces every slot of group g (slots
+ * slot_off[g]..slot_off[g+1], batch order) and sums base_distribution(read
+ * base, match score) (model.jl:804-809) at each match move, per consensus
+ * column, in batch order: out[(row_g + j) * 4 + b], row_g = sum over h < g
+ * of tlen[h].  bases[k] / match[k] point at slot k's read bases and match
+ * scores (seq_len[k] each, host memory). */
+int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                      const int32_t *tlen, const uint8_t *const *bases, const double *const *match,
+                      const int32_t *seq_len, double *out);
+/* Host sums of segments values[off[k]..off[k+1]): Julia 0.6 sum() order
+ * (pairwise, blocks of 1024; rifrafsequences.jl:74 est_n_errors) and the
+ * plain sequential order (cumsum(...)[end], util.jl:28-38 logsumexp10). */
+int rf_host_julia_sums(int64_t nseg, const double *values, const int64_t *off, double *out);
+int rf_host_seq_sums(int64_t nseg, const double *values, const int64_t *off, double *out);
+/* RifrafSequence tables of many sequences from one byte code per position
+ * (Phred scores): lp_t / p10_t / match_t per code, s_* the Scores terms;
+ * concatenated outputs (del: n+1 per sequence at off[k]+k), est_n_errors. */
+int rf_host_tables_from_codes(int64_t nseg, const uint8_t *codes, const int64_t *off, const double *lp_t,
+                              const double *p10_t, const double *match_t, double s_mis, double s_ins,
+                              double s_del, double *lp, double *match, double *mism, double *ins,
+                              double *del, double *est);
+/* Per segment, the sequential sum of grid[ucode[k] * 256 + codes[i]]. */
+int rf_host_code_seq_sums(int64_t nseg, const uint8_t *codes, const int64_t *off, const int32_t *ucode,
+                          const double *grid, double *out);
 
 /* Geometry of a slot's band: nrows = n+1, ncols = m+1, bandwidth, H. */
 int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,

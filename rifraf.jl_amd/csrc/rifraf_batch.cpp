@@ -1,0 +1,879 @@
+// rifraf_batch.cpp -- native batched rifraf() stage machine (host C++).
+//
+// rf_rifraf_batch runs the INIT stage of rifraf() (src/model.jl:1116-1275)
+// for many reference-free clusters in lockstep over one engine context: each
+// step of the reference's iteration (resample -> realign! / rescore! ->
+// check_score -> get_candidates -> handle_candidates! / finish_stage!) is
+// executed for every live cluster with ONE batched engine call per kind
+// (rf_realign, rf_backtrace, rf_alignment_proposals, rf_score,
+// rf_set_templates_ids).  The per-cluster logic is the reference's, line by
+// line (cited per function), with the same FP64 operations in the same order,
+// so every cluster ends with the consensus, score and iteration count that a
+// separate rifraf() call produces.  Python's batch.py hub does the same with
+// one host thread per cluster; this driver removes that interpreter cost
+// (SURVEY.md §8(f) row 1).
+//
+// Scope: clusters without a reference (the INIT stage converges when no
+// candidate improves the score, model.jl:937-948) whose batches are
+// deterministic -- the fixed lowest-error batch (batch_fixed) or every read.
+// Random resampling (StatsBase.sample) and the reference-guided FRAME stage
+// stay in the Python stage machine.  Host inputs that need transcendental
+// functions (the per-read Poisson thresholds of smart_forward_moves!, the
+// fixed batch order) are computed by the caller with the Python mirror's own
+// code, so no host libm result here can differ from the Python path's.
+
+#include "../../include/rifraf_hip.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <thread>
+#include <vector>
+#include <cstdlib>
+
+namespace {
+
+constexpr double INF = std::numeric_limits<double>::infinity();
+constexpr int SUB = 0, INS = 1, DEL = 2;
+
+struct Prop {
+    int32_t kind, pos, base;
+};
+struct Cand {
+    Prop p;
+    double score;
+};
+
+struct Read {
+    int32_t seq = 0, len = 0, bw = 0;
+    bool fixed = false;
+    double thr = 0.0;   // cquantile(Poisson(est_n_errors), bandwidth_pvalue)
+};
+
+struct Clu {
+    int32_t r0 = 0, nreads = 0;   // reads [r0, r0 + nreads) of the read table
+    int32_t slot0 = 0, tpl = 0;
+    std::vector<uint8_t> cons, old_cons;
+    std::vector<std::vector<uint8_t>> stages;   // consensus at each INIT iteration
+    std::vector<int32_t> batch;                 // batch_seqs (local read indices)
+    int32_t batch_size = 0, base_batch_size = 0;
+    int32_t n_slots = 0;
+    std::vector<double> slot_scores;
+    double score = -INF, old_score = -INF;
+    bool realign_As = true, realign_Bs = true, penalties_increased = false;
+    int32_t iters = 0;
+    bool converged = false, failed = false;
+    std::string err;
+    std::vector<Prop> props;
+    std::vector<Cand> chosen;
+};
+
+struct Driver {
+    rf_ctx *ctx;
+    rf_batch_params P;
+    std::vector<Read> reads;
+    std::vector<Clu> clu;
+    std::vector<int32_t> fixed_off, fixed;   // the caller's fixed batches
+
+    void fail_cluster(int c, const std::string &msg)
+    {
+        clu[c].failed = true;
+        clu[c].err = msg;
+    }
+
+    // Run `fn` on the clusters `cs` in one batched engine call; if the call
+    // fails, run it cluster by cluster so the error reaches exactly the
+    // cluster that raised it (batch.py's attribution).  fn returns 0 or an
+    // rf error code and must not change cluster state unless it succeeds.
+    template <class F>
+    void batched(std::vector<int> &cs, F fn)
+    {
+        if (cs.empty())
+            return;
+        if (fn(cs) == 0)
+            return;
+        std::vector<int> ok;
+        for (int c : cs) {
+            std::vector<int> one{c};
+            if (fn(one) == 0)
+                ok.push_back(c);
+            else
+                fail_cluster(c, rf_last_error(ctx));
+        }
+        cs.swap(ok);
+    }
+
+    // ---------------- resample! (model.jl:1038-1066), deterministic cases
+    void resample(Clu &C, int c)
+    {
+        if (P.batch_fixed) {
+            C.batch.assign(fixed.begin() + fixed_off[c], fixed.begin() + fixed_off[c + 1]);
+        } else {
+            // batch_size >= #reads (the caller guarantees it): every read
+            C.batch.resize(C.nreads);
+            for (int k = 0; k < C.nreads; ++k)
+                C.batch[k] = k;
+        }
+    }
+
+    // ---------------- smart_forward_moves! (model.jl:643-672) over the
+    // batch slots of every cluster in `cs`, then A[end,end] -> slot_scores.
+    int smart_forward(const std::vector<int> &cs)
+    {
+        struct Job {
+            int c, k;
+            int32_t bw, max_bw;
+            int64_t old_err, n_err;
+        };
+        std::vector<Job> jobs;
+        for (int c : cs) {
+            const Clu &C = clu[c];
+            for (int k = 0; k < (int)C.batch.size(); ++k) {
+                const Read &R = reads[C.r0 + C.batch[k]];
+                const int32_t mx = R.fixed ? R.bw
+                                           : std::min<int64_t>(std::min<int64_t>((int64_t)R.bw * 32, (int64_t)C.cons.size()),
+                                                               (int64_t)R.len);
+                jobs.push_back({c, k, R.bw, mx, INT64_MAX, INT64_MAX});
+            }
+        }
+        std::vector<double> score(jobs.size());
+        std::vector<int> pending(jobs.size());
+        for (size_t j = 0; j < jobs.size(); ++j)
+            pending[j] = (int)j;
+        std::vector<int32_t> sl, sq, tp, bw, nerr;
+        std::vector<double> out;
+        while (!pending.empty()) {
+            sl.clear(), sq.clear(), tp.clear(), bw.clear();
+            for (int j : pending) {
+                const Clu &C = clu[jobs[j].c];
+                sl.push_back(C.slot0 + jobs[j].k);
+                sq.push_back(reads[C.r0 + C.batch[jobs[j].k]].seq);
+                tp.push_back(C.tpl);
+                bw.push_back(jobs[j].bw);
+            }
+            out.resize(pending.size());
+            if (int e = rf_realign(ctx, (int32_t)pending.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_FWD,
+                                   out.data()))
+                return e;
+            std::vector<int> check;
+            for (size_t i = 0; i < pending.size(); ++i) {
+                const int j = pending[i];
+                score[j] = out[i];
+                const Read &R = reads[clu[jobs[j].c].r0 + clu[jobs[j].c].batch[jobs[j].k]];
+                if (!(R.fixed || jobs[j].bw >= jobs[j].max_bw))
+                    check.push_back(j);
+            }
+            if (check.empty())
+                break;
+            sl.clear();
+            for (int j : check)
+                sl.push_back(clu[jobs[j].c].slot0 + jobs[j].k);
+            nerr.resize(check.size());
+            if (int e = rf_backtrace(ctx, (int32_t)check.size(), sl.data(), nullptr, nullptr, nullptr, nerr.data()))
+                return e;
+            std::vector<int> nxt;
+            for (size_t i = 0; i < check.size(); ++i) {
+                Job &J = jobs[check[i]];
+                const Read &R = reads[clu[J.c].r0 + clu[J.c].batch[J.k]];
+                J.old_err = J.n_err;
+                J.n_err = nerr[i];
+                if ((double)J.n_err > R.thr && J.n_err < J.old_err) {
+                    J.bw = std::min(J.bw * 2, J.max_bw);
+                    nxt.push_back(check[i]);
+                }
+            }
+            pending.swap(nxt);
+        }
+        // success: commit bandwidths (bandwidth_fixed for every batch read) and scores
+        for (size_t j = 0; j < jobs.size(); ++j) {
+            Clu &C = clu[jobs[j].c];
+            Read &R = reads[C.r0 + C.batch[jobs[j].k]];
+            R.bw = jobs[j].bw;
+            C.slot_scores[jobs[j].k] = score[j];
+        }
+        for (int c : cs)
+            for (int k : clu[c].batch)
+                reads[clu[c].r0 + k].fixed = true;
+        return 0;
+    }
+
+    int realign_B(const std::vector<int> &cs)
+    {
+        std::vector<int32_t> sl, sq, tp, bw;
+        for (int c : cs) {
+            const Clu &C = clu[c];
+            for (int k = 0; k < (int)C.batch.size(); ++k) {
+                const Read &R = reads[C.r0 + C.batch[k]];
+                sl.push_back(C.slot0 + k);
+                sq.push_back(R.seq);
+                tp.push_back(C.tpl);
+                bw.push_back(R.bw);
+            }
+        }
+        return rf_realign(ctx, (int32_t)sl.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_BWD, nullptr);
+    }
+
+    // ---------------- realign! + rescore! (model.jl:630-719), no reference
+    void realign_rescore(std::vector<int> cs)
+    {
+        std::vector<int> a, b;
+        for (int c : cs) {
+            Clu &C = clu[c];
+            while (C.n_slots < (int)C.batch.size()) {   // grow As / Bs (fresh A[end,end] = 0.0)
+                C.slot_scores.push_back(0.0);
+                ++C.n_slots;
+            }
+            if (C.realign_As)
+                a.push_back(c);
+            if (C.realign_Bs)
+                b.push_back(c);
+        }
+        batched(a, [&](const std::vector<int> &s) { return smart_forward(s); });
+        batched(b, [&](const std::vector<int> &s) { return realign_B(s); });
+        for (int c : cs) {
+            Clu &C = clu[c];
+            if (C.failed)
+                continue;
+            double total = C.slot_scores[0];   // left fold over every slot, stale ones included
+            for (int k = 1; k < C.n_slots; ++k)
+                total += C.slot_scores[k];
+            C.score = total;
+        }
+    }
+
+    // ---------------- check_score (model.jl:1074-1114); the clusters that
+    // increase their batch size are realigned by the caller (`redo`)
+    bool check_score(Clu &C, int c, std::vector<int> &redo)
+    {
+        const bool all = C.batch_size == C.nreads;
+        if (!C.penalties_increased && all && C.iters > 1) {
+            if (C.score == C.old_score)
+                return false;
+        }
+        const double rel = (C.score - C.old_score) / C.old_score;   // IEEE: +-Inf / NaN, never a trap
+        if (rel > P.batch_threshold && !C.penalties_increased && C.batch_size < C.nreads && C.iters > 1) {
+            C.batch_size = std::min(C.batch_size + C.base_batch_size, C.nreads);
+            resample(C, c);
+            C.realign_As = true;
+            C.realign_Bs = true;
+            redo.push_back(c);
+        }
+        return true;
+    }
+
+    // ---------------- all_proposals(STAGE_INIT, consensus) without seeds (model.jl:401-456)
+    static void all_proposals_init(const std::vector<uint8_t> &t, std::vector<Prop> &out)
+    {
+        out.clear();
+        for (int b = 0; b < 4; ++b)
+            out.push_back({INS, 0, b});
+        for (int j = 1; j <= (int)t.size(); ++j) {
+            for (int b = 0; b < 4; ++b)
+                if (t[j - 1] != b)
+                    out.push_back({SUB, j, b});
+            out.push_back({DEL, j, 0});
+            for (int b = 0; b < 4; ++b)
+                out.push_back({INS, j, b});
+        }
+    }
+
+    // ---------------- get_candidates (model.jl:499-526) for `cs`; returns the
+    // candidates (score > state.score, in proposal order) per cluster
+    void get_candidates(std::vector<int> cs, std::vector<std::vector<Cand>> &cands)
+    {
+        if (P.do_alignment_proposals) {
+            // alignment_proposals (model.jl:483-497): the device union mask of the batch
+            // backtraces, read out in (pos, kind, base) order
+            batched(cs, [&](const std::vector<int> &s) {
+                std::vector<int32_t> off{0}, sl;
+                int64_t rows = 0;
+                for (int c : s) {
+                    for (int k = 0; k < (int)clu[c].batch.size(); ++k)
+                        sl.push_back(clu[c].slot0 + k);
+                    off.push_back((int32_t)sl.size());
+                    rows += (int64_t)clu[c].cons.size() + 1;
+                }
+                std::vector<uint8_t> mask((size_t)rows * 9);
+                if (int e = rf_alignment_proposals(ctx, (int32_t)s.size(), off.data(), sl.data(), 1, mask.data()))
+                    return e;
+                static const int order[9][3] = {{0, SUB, 0}, {1, SUB, 1}, {2, SUB, 2}, {3, SUB, 3}, {5, INS, 0},
+                                                {6, INS, 1}, {7, INS, 2}, {8, INS, 3}, {4, DEL, 0}};
+                int64_t row = 0;
+                for (int c : s) {
+                    Clu &C = clu[c];
+                    C.props.clear();
+                    const int m = (int)C.cons.size();
+                    for (int p = 0; p <= m; ++p)
+                        for (const auto &o : order)
+                            if (mask[(size_t)(row + p) * 9 + o[0]])
+                                C.props.push_back({o[1], p, o[2]});
+                    row += m + 1;
+                }
+                return 0;
+            });
+        } else {
+            for (int c : cs)
+                all_proposals_init(clu[c].cons, clu[c].props);
+        }
+        // score_proposals (model.jl:385-399): batch fold, no reference
+        std::vector<int> sc;
+        for (int c : cs)
+            if (!clu[c].failed && !clu[c].props.empty())
+                sc.push_back(c);
+        batched(sc, [&](const std::vector<int> &s) {
+            std::vector<int32_t> off{0}, sl, ref, pos;
+            std::vector<int64_t> poff{0};
+            std::vector<uint8_t> kind, base;
+            for (int c : s) {
+                const Clu &C = clu[c];
+                for (int k = 0; k < (int)C.batch.size(); ++k)
+                    sl.push_back(C.slot0 + k);
+                off.push_back((int32_t)sl.size());
+                ref.push_back(-1);
+                for (const Prop &p : C.props) {
+                    kind.push_back((uint8_t)p.kind);
+                    pos.push_back(p.pos);
+                    base.push_back((uint8_t)p.base);
+                }
+                poff.push_back((int64_t)kind.size());
+            }
+            std::vector<double> tot(kind.size());
+            if (int e = rf_score(ctx, (int32_t)s.size(), off.data(), sl.data(), ref.data(), poff.data(), kind.data(),
+                                 pos.data(), base.data(), tot.data(), nullptr))
+                return e;
+            for (size_t g = 0; g < s.size(); ++g) {
+                const Clu &C = clu[s[g]];
+                auto &out = cands[s[g]];
+                out.clear();
+                for (int64_t i = poff[g]; i < poff[g + 1]; ++i)
+                    if (tot[i] > C.score)
+                        out.push_back({C.props[i - poff[g]], tot[i]});
+            }
+            return 0;
+        });
+    }
+
+    // ---------------- choose_candidates (proposals.jl:104-115)
+    std::vector<Cand> choose(std::vector<Cand> cands) const
+    {
+        std::stable_sort(cands.begin(), cands.end(), [](const Cand &x, const Cand &y) { return x.score > y.score; });
+        std::vector<Cand> out;
+        for (const Cand &c : cands) {
+            bool near = false;
+            for (const Cand &o : out)
+                near = near || std::abs(c.p.pos - o.p.pos) < P.min_dist;
+            if (!near)
+                out.push_back(c);
+        }
+        return out;
+    }
+
+    // ---------------- apply_proposals (proposals.jl:41-102); false: ambiguous
+    static bool apply(const std::vector<uint8_t> &seq, std::vector<Cand> ps, std::vector<uint8_t> &out)
+    {
+        std::vector<int> ins, other;
+        for (const Cand &c : ps)
+            (c.p.kind == INS ? ins : other).push_back(c.p.pos);
+        for (auto *v : {&ins, &other}) {
+            std::sort(v->begin(), v->end());
+            if (std::adjacent_find(v->begin(), v->end()) != v->end())
+                return false;
+        }
+        std::stable_sort(ps.begin(), ps.end(), [](const Cand &x, const Cand &y) {
+            const int kx = x.p.kind == DEL ? 0 : 1, ky = y.p.kind == DEL ? 0 : 1;
+            return x.p.pos != y.p.pos ? x.p.pos < y.p.pos : kx < ky;
+        });
+        out.clear();
+        int nxt = 1, last_del = 0;
+        for (const Cand &c : ps) {
+            const Prop &p = c.p;
+            for (int i = nxt - 1; i < std::max(p.pos - 1, 0); ++i)
+                out.push_back(seq[i]);
+            if (p.kind == SUB) {
+                out.push_back((uint8_t)p.base);
+            } else if (p.kind == INS) {
+                if (p.pos > 0 && last_del != p.pos)
+                    out.push_back(seq[p.pos - 1]);
+                out.push_back((uint8_t)p.base);
+            }
+            nxt = p.pos + 1;
+            if (p.kind == DEL)
+                last_del = p.pos;
+        }
+        for (int i = nxt - 1; i < (int)seq.size(); ++i)
+            out.push_back(seq[i]);
+        return true;
+    }
+
+    int upload_templates(const std::vector<int> &cs)
+    {
+        std::vector<int32_t> ids;
+        std::vector<int64_t> off{0};
+        std::vector<uint8_t> bases;
+        for (int c : cs) {
+            ids.push_back(clu[c].tpl);
+            bases.insert(bases.end(), clu[c].cons.begin(), clu[c].cons.end());
+            off.push_back((int64_t)bases.size());
+        }
+        return rf_set_templates_ids(ctx, (int32_t)ids.size(), ids.data(), bases.data(), off.data());
+    }
+
+    // Set the consensus of clusters `cs` (host copy + device template);
+    // a cluster whose upload fails keeps its error.
+    void set_consensus(std::vector<int> &cs)
+    {
+        batched(cs, [&](const std::vector<int> &s) { return upload_templates(s); });
+    }
+
+    // ---------------- handle_candidates! (model.jl:898-935)
+    void handle_candidates(std::vector<int> cs, std::vector<std::vector<Cand>> &cands)
+    {
+        std::vector<int> up;
+        for (int c : cs) {
+            Clu &C = clu[c];
+            C.old_cons = C.cons;
+            C.chosen = choose(cands[c]);
+            std::vector<uint8_t> nc;
+            if (!apply(C.old_cons, C.chosen, nc)) {
+                fail_cluster(c, "AmbiguousProposalsError");
+                continue;
+            }
+            C.cons.swap(nc);
+            up.push_back(c);
+        }
+        set_consensus(up);
+        for (int c : up) {
+            clu[c].realign_As = true;
+            clu[c].realign_Bs = false;
+        }
+        realign_rescore(up);
+        std::vector<int> redo;
+        for (int c : up) {
+            Clu &C = clu[c];
+            if (C.failed)
+                continue;
+            const double best = C.chosen[0].score;
+            const bool close = C.score == best ||
+                               (std::isfinite(C.score) && std::isfinite(best) &&
+                                std::fabs(C.score - best) <= std::sqrt(DBL_EPSILON_) * std::max(std::fabs(C.score), std::fabs(best)));
+            if (C.chosen.size() > 1 && (C.score < best || close)) {
+                // reject multiple candidates in favor of the best
+                C.chosen.resize(1);
+                std::vector<uint8_t> nc;
+                apply(C.old_cons, C.chosen, nc);
+                C.cons.swap(nc);
+                redo.push_back(c);
+            } else {
+                C.realign_As = false;
+            }
+            C.realign_Bs = true;
+        }
+        set_consensus(redo);
+    }
+    static constexpr double DBL_EPSILON_ = std::numeric_limits<double>::epsilon();
+
+    void run()
+    {
+        std::vector<int> live;
+        for (int c = 0; c < (int)clu.size(); ++c)
+            live.push_back(c);
+        std::vector<std::vector<Cand>> cands(clu.size());
+        for (int it = 1; it <= P.max_iters && !live.empty(); ++it) {
+            for (int c : live) {
+                Clu &C = clu[c];
+                C.iters += 1;
+                C.stages.push_back(C.cons);
+                resample(C, c);
+            }
+            realign_rescore(live);
+            std::vector<int> ok, redo, fin;
+            for (int c : live) {
+                if (clu[c].failed)
+                    continue;
+                if (check_score(clu[c], c, redo))
+                    ok.push_back(c);
+                else
+                    fin.push_back(c);
+            }
+            if (!redo.empty())
+                realign_rescore(redo);
+            std::vector<int> gc;
+            for (int c : ok) {
+                Clu &C = clu[c];
+                if (C.failed)
+                    continue;
+                C.old_score = C.score;
+                C.penalties_increased = false;
+                gc.push_back(c);
+            }
+            for (int c : gc)
+                cands[c].clear();
+            get_candidates(gc, cands);
+            std::vector<int> hc;
+            for (int c : gc) {
+                Clu &C = clu[c];
+                if (C.failed)
+                    continue;
+                C.realign_As = true;
+                (cands[c].empty() ? fin : hc).push_back(c);
+            }
+            handle_candidates(hc, cands);
+            // finish_stage! (model.jl:937-948): no reference -> converged
+            for (int c : fin)
+                clu[c].converged = true;
+            std::vector<int> nl;
+            for (int c : live)
+                if (!clu[c].failed && !clu[c].converged)
+                    nl.push_back(c);
+            live.swap(nl);
+        }
+    }
+};
+
+}  // namespace
+
+// result of the last rf_rifraf_batch per context (retrieved by rf_batch_fetch)
+struct BatchResult {
+    std::vector<Clu> clu;
+    std::vector<Read> reads;
+};
+static std::vector<std::pair<const rf_ctx *, BatchResult>> g_results;
+
+static BatchResult &result_of(const rf_ctx *ctx)
+{
+    for (auto &r : g_results)
+        if (r.first == ctx)
+            return r.second;
+    g_results.emplace_back(ctx, BatchResult{});
+    return g_results.back().second;
+}
+
+extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
+                               const int32_t *read_off, const int32_t *read_seq, const int32_t *read_len,
+                               const double *threshold, const int32_t *fixed_off, const int32_t *fixed,
+                               const int32_t *slot_base, const int32_t *tpl_id, const uint8_t *cons,
+                               const int64_t *cons_off, double *out_score, int32_t *out_iters,
+                               int32_t *out_status, int64_t *out_len, int32_t *out_bw)
+{
+    if (!ctx || nclusters < 0 || !params || (nclusters > 0 && (!read_off || !read_seq || !read_len || !threshold ||
+                                                              !slot_base || !tpl_id || !cons || !cons_off)))
+        return RF_ERR_ARG;
+    if (params->batch_fixed && (!fixed_off || !fixed))
+        return RF_ERR_ARG;
+    Driver D{ctx, *params, {}, {}, {}, {}};
+    const int32_t nreads = nclusters > 0 ? read_off[nclusters] : 0;
+    D.reads.resize(nreads);
+    for (int32_t r = 0; r < nreads; ++r)
+        D.reads[r] = {read_seq[r], read_len[r], params->bandwidth, false, threshold[r]};
+    if (params->batch_fixed) {
+        D.fixed_off.assign(fixed_off, fixed_off + nclusters + 1);
+        D.fixed.assign(fixed, fixed + fixed_off[nclusters]);
+    }
+    D.clu.resize(nclusters);
+    for (int32_t c = 0; c < nclusters; ++c) {
+        Clu &C = D.clu[c];
+        C.r0 = read_off[c];
+        C.nreads = read_off[c + 1] - read_off[c];
+        C.slot0 = slot_base[c];
+        C.tpl = tpl_id[c];
+        C.cons.assign(cons + cons_off[c], cons + cons_off[c + 1]);
+        // initial_state (model.jl:564-615)
+        const int32_t bs = params->batch_size > 1 ? std::min(params->batch_size, C.nreads) : C.nreads;
+        C.batch_size = C.base_batch_size = bs;
+        if (C.nreads < 1 || C.cons.empty() || (!params->batch_fixed && bs < C.nreads) ||
+            (params->batch_fixed && fixed_off[c + 1] - fixed_off[c] < 1))
+            return RF_ERR_ARG;   // outside the native driver's scope: the caller checks first
+    }
+    D.run();
+    BatchResult &R = result_of(ctx);
+    R.clu = std::move(D.clu);
+    R.reads = std::move(D.reads);
+    for (int32_t c = 0; c < nclusters; ++c) {
+        const Clu &C = R.clu[c];
+        if (out_score)
+            out_score[c] = C.score;
+        if (out_iters)
+            out_iters[c] = C.iters;
+        if (out_status)
+            out_status[c] = C.failed ? 2 : (C.converged ? 1 : 0);
+        if (out_len)
+            out_len[c] = (int64_t)C.cons.size();
+    }
+    if (out_bw)
+        for (int32_t r = 0; r < nreads; ++r)
+            out_bw[r] = R.reads[r].bw * (R.reads[r].fixed ? -1 : 1);
+    return 0;
+}
+
+extern "C" int rf_batch_fetch(rf_ctx *ctx, int32_t cluster, uint8_t *cons, int64_t *stage_len, uint8_t *stages,
+                              int32_t *batch, char *err, int64_t err_cap)
+{
+    if (!ctx)
+        return RF_ERR_ARG;
+    BatchResult &R = result_of(ctx);
+    if (cluster < 0 || cluster >= (int32_t)R.clu.size())
+        return RF_ERR_ARG;
+    const Clu &C = R.clu[cluster];
+    if (cons)
+        std::memcpy(cons, C.cons.data(), C.cons.size());
+    int64_t at = 0;
+    for (size_t s = 0; s < C.stages.size(); ++s) {
+        if (stage_len)
+            stage_len[s] = (int64_t)C.stages[s].size();
+        if (stages)
+            std::memcpy(stages + at, C.stages[s].data(), C.stages[s].size());
+        at += (int64_t)C.stages[s].size();
+    }
+    if (batch)
+        std::copy(C.batch.begin(), C.batch.end(), batch);
+    if (err && err_cap > 0) {
+        const size_t n = std::min<size_t>(C.err.size(), (size_t)err_cap - 1);
+        std::memcpy(err, C.err.data(), n);
+        err[n] = 0;
+    }
+    return 0;
+}
+
+extern "C" void rf_batch_release(rf_ctx *ctx)
+{
+    for (size_t i = 0; i < g_results.size(); ++i)
+        if (g_results[i].first == ctx) {
+            g_results.erase(g_results.begin() + (ptrdiff_t)i);
+            return;
+        }
+}
+
+// ---------------------------------------------------------------------
+// Host helpers of the batched driver's setup and quality pass.  Only FP64
+// additions and the C library's pow / log10 (the functions Python's float
+// ** and math.log10 call), never a vectorised transcendental, so every
+// value equals the Python mirror's.
+// ---------------------------------------------------------------------
+
+namespace {
+// Julia 0.6 sum(::Vector{Float64}) (base/reduce.jl mapreduce_impl; the mirror
+// is rifrafsequences.julia_sum): sequential below 16 elements, otherwise
+// pairwise halves down to blocks of at most 1024 summed sequentially.
+double julia_sum(const double *a, int64_t lo, int64_t hi)   // inclusive
+{
+    if (lo + 1024 > hi) {
+        double s = a[lo];
+        for (int64_t i = lo + 1; i <= hi; ++i)
+            s += a[i];
+        return s;
+    }
+    const int64_t mid = (lo + hi) >> 1;
+    return julia_sum(a, lo, mid) + julia_sum(a, mid + 1, hi);
+}
+}  // namespace
+
+extern "C" int rf_host_julia_sums(int64_t nseg, const double *values, const int64_t *off, double *out)
+{
+    if (nseg < 0 || (nseg > 0 && (!values || !off || !out)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < nseg; ++k) {
+        const int64_t n = off[k + 1] - off[k];
+        const double *a = values + off[k];
+        if (n == 0) {
+            out[k] = 0.0;
+        } else if (n < 16) {          // cumsum(a)[-1]: sequential
+            double s = a[0];
+            for (int64_t i = 1; i < n; ++i)
+                s += a[i];
+            out[k] = s;
+        } else {
+            out[k] = julia_sum(a, 0, n - 1);
+        }
+    }
+    return 0;
+}
+
+extern "C" int rf_host_seq_sums(int64_t nseg, const double *values, const int64_t *off, double *out)
+{
+    // np.cumsum(a)[-1] per segment: strictly sequential
+    if (nseg < 0 || (nseg > 0 && (!values || !off || !out)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < nseg; ++k) {
+        double s = 0.0;
+        bool first = true;
+        for (int64_t i = off[k]; i < off[k + 1]; ++i) {
+            s = first ? values[i] : s + values[i];
+            first = false;
+        }
+        out[k] = s;
+    }
+    return 0;
+}
+
+// alignment_error_probs (model.jl:817-840) up to its final normalisation:
+// for group g, out[(row_g + j) * 4 + b] = the batch-order sum over the group's
+// reads of base_distribution(read base, match score)[b] at every match move
+// onto consensus column j (0-based); row_g = sum over h < g of m_h.  Moves
+// come from rf_backtrace; base_distribution (model.jl:804-809) is evaluated
+// with pow / log10 exactly as the Python mirror's scalar code.
+extern "C" int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                                 const int32_t *tlen, const uint8_t *const *bases, const double *const *match,
+                                 const int32_t *seq_len, double *out)
+{
+    if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !tlen || !bases || !match || !seq_len || !out)))
+        return RF_ERR_ARG;
+    const int32_t ns = ngroups > 0 ? slot_off[ngroups] : 0;
+    std::vector<int64_t> moff(ns + 1, 0);
+    std::vector<int32_t> glen(ns);
+    for (int32_t g = 0; g < ngroups; ++g)
+        for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k)
+            glen[k] = tlen[g];
+    for (int32_t k = 0; k < ns; ++k)   // capacity n + m per alignment
+        moff[k + 1] = moff[k] + seq_len[k] + glen[k];
+    std::vector<int8_t> moves((size_t)std::max<int64_t>(moff[ns], 1));
+    std::vector<int32_t> nmoves(std::max(ns, 1));
+    if (int e = rf_backtrace(ctx, ns, slots, moves.data(), moff.data(), nmoves.data(), nullptr))
+        return e;
+    const double log3 = std::log10(3.0);
+    // base_distribution rows per distinct match score (math.log10(1.0 - 10.0 ** ilp))
+    std::vector<int64_t> rows(ngroups + 1, 0);
+    for (int32_t g = 0; g < ngroups; ++g)
+        rows[g + 1] = rows[g] + tlen[g];
+    // groups are independent: ranges of groups on host threads (each with its
+    // own base_distribution cache; the values do not depend on the thread)
+    const char *ev = std::getenv("OMP_NUM_THREADS");
+    const int nth = std::max(1, std::min({(ev && *ev) ? std::atoi(ev) : (int)std::thread::hardware_concurrency(), 16,
+                                          std::max(1, (int)(moff[ns] >> 20))}));
+    auto work = [&](int t) {
+    auto cache = std::vector<std::pair<double, double>>(4096, {std::nan(""), 0.0});
+    auto err_lp = [&](double ilp) {
+        uint64_t u;
+        std::memcpy(&u, &ilp, 8);
+        auto &c = cache[(u * 0x9E3779B97F4A7C15ull) >> 52];
+        uint64_t cu;
+        std::memcpy(&cu, &c.first, 8);
+        if (cu == u)
+            return c.second;
+        const double lp = std::log10(1.0 - std::pow(10.0, ilp)) - log3;
+        c = {ilp, lp};
+        return lp;
+    };
+    for (int32_t g = (int32_t)((int64_t)ngroups * t / nth); g < (int32_t)((int64_t)ngroups * (t + 1) / nth); ++g) {
+        const int64_t row = rows[g];
+        double *P = out + row * 4;
+        std::fill(P, P + (size_t)tlen[g] * 4, 0.0);
+        for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
+            const int8_t *mv = moves.data() + moff[k];
+            const uint8_t *b = bases[k];
+            const double *ms = match[k];
+            int64_t i = 0, j = 0;   // read / consensus positions consumed (align.jl OFFSETS)
+            for (int32_t t = 0; t < nmoves[k]; ++t) {
+                switch (mv[t]) {
+                case 1:   // TRACE_MATCH
+                {
+                    const double ilp = ms[i];
+                    const double o = err_lp(ilp);
+                    double *p = P + j * 4;
+                    for (int q = 0; q < 4; ++q)
+                        p[q] += q == b[i] ? ilp : o;
+                    ++i, ++j;
+                    break;
+                }
+                case 2: ++i; break;        // TRACE_INSERT
+                case 3: ++j; break;        // TRACE_DELETE
+                case 4: i += 3; break;     // TRACE_CODON_INSERT
+                case 5: j += 3; break;     // TRACE_CODON_DELETE
+                default: break;
+                }
+            }
+        }
+    }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; ++t)
+        th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th)
+        x.join();
+    return 0;
+}
+
+// RifrafSequence tables (rifrafsequences.jl:19-82) of many sequences whose
+// log error probabilities are lp_t[code] for one byte code per position
+// (Phred scores): per-code values of lp, 10^lp and match (computed by the
+// caller with the Python mirror's numpy expressions) are gathered, and the
+// rest is FP64 addition and max exactly as the constructor writes it:
+//   mismatch = lp + s_mis, ins = lp + s_ins,
+//   del[0] = lp[0] + s_del, del[n] = lp[n-1] + s_del,
+//   del[i] = max(lp[i-1], lp[i]) + s_del,
+//   est_n_errors = Julia-order sum of 10^lp.
+// Outputs are concatenated (del: n + 1 per sequence at off[k] + k).
+extern "C" int rf_host_tables_from_codes(int64_t nseg, const uint8_t *codes, const int64_t *off, const double *lp_t,
+                                         const double *p10_t, const double *match_t, double s_mis, double s_ins,
+                                         double s_del, double *lp, double *match, double *mism, double *ins,
+                                         double *del, double *est)
+{
+    if (nseg < 0 || (nseg > 0 && (!codes || !off || !lp_t || !p10_t || !match_t || !lp || !match || !mism || !ins ||
+                                  !del || !est)))
+        return RF_ERR_ARG;
+    const char *ev = std::getenv("OMP_NUM_THREADS");
+    const int64_t N = nseg > 0 ? off[nseg] : 0;
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)((ev && *ev) ? std::atoi(ev) : (int)std::thread::hardware_concurrency()),
+                                                                16, (N >> 20) + 1}));
+    auto work = [&](int t) {
+        std::vector<double> p10;
+        for (int64_t k = nseg * t / nth; k < nseg * (t + 1) / nth; ++k) {
+            const int64_t a = off[k], n = off[k + 1] - off[k];
+            double *d = del + a + k;
+            p10.resize((size_t)n);
+            for (int64_t i = 0; i < n; ++i) {
+                const uint8_t c = codes[a + i];
+                const double x = lp_t[c];
+                lp[a + i] = x;
+                match[a + i] = match_t[c];
+                mism[a + i] = x + s_mis;
+                ins[a + i] = x + s_ins;
+                p10[(size_t)i] = p10_t[c];
+            }
+            if (n > 0) {
+                d[0] = lp[a] + s_del;
+                d[n] = lp[a + n - 1] + s_del;
+                for (int64_t i = 1; i < n; ++i) {   // Base.max of two finite / -Inf values = std::max here
+                    const double l = lp[a + i - 1], r = lp[a + i];
+                    d[i] = (r > l ? r : l) + s_del;
+                }
+                est[k] = n < 16 ? [&] {
+                    double s = p10[0];
+                    for (int64_t i = 1; i < n; ++i)
+                        s += p10[(size_t)i];
+                    return s;
+                }() : julia_sum(p10.data(), 0, n - 1);
+            } else {
+                est[k] = 0.0;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; ++t)
+        th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th)
+        x.join();
+    return 0;
+}
+
+// logsumexp10 sums of many sequences from the same byte codes: segment k's
+// sequential sum of grid[ucode[k] * 256 + codes[i]] (grid = 10^(x - u) per
+// (u code, x code), evaluated by the caller with numpy).
+extern "C" int rf_host_code_seq_sums(int64_t nseg, const uint8_t *codes, const int64_t *off, const int32_t *ucode,
+                                     const double *grid, double *out)
+{
+    if (nseg < 0 || (nseg > 0 && (!codes || !off || !ucode || !grid || !out)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < nseg; ++k) {
+        const double *g = grid + (size_t)ucode[k] * 256;
+        double s = 0.0;
+        for (int64_t i = off[k]; i < off[k + 1]; ++i)
+            s = i == off[k] ? g[codes[i]] : s + g[codes[i]];
+        out[k] = s;
+    }
+    return 0;
+}

@@ -29,7 +29,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/rifraf_hip.h"
@@ -2971,6 +2973,32 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// Host worker threads: OMP_NUM_THREADS when set (the GPU box's CPU share),
+// else the machine's, at most 16.
+inline int host_threads()
+{
+    static const int n = [] {
+        const char *v = std::getenv("OMP_NUM_THREADS");
+        int t = (v && *v) ? std::atoi(v) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(t, 16));
+    }();
+    return n;
+}
+template <class F>
+void parallel_for(int nth, F fn)
+{
+    if (nth <= 1) {
+        fn(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; ++t)
+        th.emplace_back(fn, t);
+    fn(0);
+    for (auto &x : th)
+        x.join();
+}
+
 // Code dictionary of the row codes (RF_TASK_CODED): every distinct
 // (match, mismatch, ins) triple and del value of the context's reads gets a
 // 16-bit code, first come first served, keyed by the exact bit patterns.  A
@@ -2993,11 +3021,6 @@ struct CodeDict {
     std::unordered_map<uint64_t, uint32_t> d1;
     std::vector<double> t3v, d1v;   // host copies of the entries
     size_t up3 = 0, up1 = 0;        // entries already on the device
-    // direct-mapped front caches (few distinct values per read set)
-    struct C3 { K3 k; int32_t code = -1; };
-    struct C1 { uint64_t k; int32_t code = -1; };
-    std::vector<C3> c3 = std::vector<C3>(4096);
-    std::vector<C1> c1 = std::vector<C1>(4096);
     DevBuf lut;
 
     static uint64_t bits(double x)
@@ -3006,64 +3029,42 @@ struct CodeDict {
         std::memcpy(&u, &x, 8);
         return u;
     }
-    int32_t code3(double mt, double mm, double is)
+    // read-only lookups (safe from several threads while nothing is inserted)
+    int32_t find3(const K3 &k) const
     {
-        const K3 k{bits(mt), bits(mm), bits(is)};
-        C3 &c = c3[(H3()(k) >> 20) & 4095];
-        if (c.code >= 0 && c.k == k)
-            return c.code;
         auto it = t3.find(k);
-        int32_t code;
-        if (it != t3.end()) {
-            code = (int32_t)it->second;
-        } else {
-            if (t3.size() >= (size_t)RF_CODES)
-                return -1;
-            code = (int32_t)t3.size();
-            t3.emplace(k, (uint32_t)code);
-            t3v.insert(t3v.end(), {mt, mm, is, 0.0});
-        }
-        c.k = k;
-        c.code = code;
-        return code;
+        return it == t3.end() ? -1 : (int32_t)it->second;
     }
-    int32_t code1(double d)
+    int32_t find1(uint64_t k) const
     {
-        const uint64_t k = bits(d);
-        C1 &c = c1[((k * 0x9E3779B97F4A7C15ull) >> 40) & 4095];
-        if (c.code >= 0 && c.k == k)
-            return c.code;
         auto it = d1.find(k);
-        int32_t code;
-        if (it != d1.end()) {
-            code = (int32_t)it->second;
-        } else {
-            if (d1.size() >= (size_t)RF_CODES)
-                return -1;
-            code = (int32_t)d1.size();
-            d1.emplace(k, (uint32_t)code);
-            d1v.push_back(d);
-        }
-        c.k = k;
-        c.code = code;
-        return code;
+        return it == d1.end() ? -1 : (int32_t)it->second;
     }
-    // one read's records (false: the dictionary is full, read stays uncoded)
-    bool encode(int64_t n, const uint8_t *base, const double *mt, const double *mm, const double *is,
-                const double *del, uint64_t *rec)
+    // per-thread direct-mapped front cache of the lookups (a read set has few
+    // distinct values; misses fall through to the maps)
+    struct Cache {
+        std::vector<std::pair<K3, int32_t>> c3 = std::vector<std::pair<K3, int32_t>>(1024, {K3{}, -2});
+        std::vector<std::pair<uint64_t, int32_t>> c1 = std::vector<std::pair<uint64_t, int32_t>>(1024, {0, -2});
+    };
+    int32_t find3(const K3 &k, Cache &C) const
     {
-        int32_t dprev = code1(del[0]);
-        if (dprev < 0)
-            return false;
-        for (int64_t i = 0; i < n; ++i) {
-            const int32_t t = code3(mt[i], mm[i], is[i]);
-            const int32_t dn = code1(del[i + 1]);
-            if (t < 0 || dn < 0)
-                return false;
-            rec[i] = (uint64_t)t | ((uint64_t)dprev << 16) | ((uint64_t)dn << 32) | ((uint64_t)base[i] << 48);
-            dprev = dn;
-        }
-        return true;
+        auto &e = C.c3[(H3()(k) >> 32) & 1023];
+        if (e.second != -2 && e.first == k)
+            return e.second;
+        const int32_t v = find3(k);
+        if (v >= 0)
+            e = {k, v};
+        return v;
+    }
+    int32_t find1(uint64_t k, Cache &C) const
+    {
+        auto &e = C.c1[((k * 0x9E3779B97F4A7C15ull) >> 40) & 1023];
+        if (e.second != -2 && e.first == k)
+            return e.second;
+        const int32_t v = find1(k);
+        if (v >= 0)
+            e = {k, v};
+        return v;
     }
 };
 
@@ -3082,6 +3083,7 @@ struct Opts {
     int seg_ver = 3;        // RF_OPT_SEG_VER: wide-band scorer 3 = k_score_segc, 1 = k_score_seg
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
     int bt_win_kb = 16;     // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS)
+    int stage_kb = 262144;  // RF_OPT_STAGE_KB: rf_set_sequences staging chunk (KB of tables)
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
@@ -3583,6 +3585,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_STREAMS: return &o.dp_streams;
     case RF_OPT_SEG_VER: return &o.seg_ver;
     case RF_OPT_BT_WIN_KB: return &o.bt_win_kb;
+    case RF_OPT_STAGE_KB: return &o.stage_kb;
     default: return nullptr;
     }
 }
@@ -3633,6 +3636,158 @@ int64_t rf_device_bytes(const rf_ctx *ctx)
     return t;
 }
 
+// rf_set_sequences's staging of sequences [k0, k1) of one call (their regions
+// exist): host tables + row codes into pinned memory, H2D, device scatter.
+int upload_sequence_chunk(rf_ctx *ctx, int32_t first, int32_t k0, int32_t k1, const uint8_t *bases,
+                          const int64_t *off, const double *match, const double *mismatch, const double *ins,
+                          const double *del, const double *cins, const int64_t *cins_off, const double *cdel,
+                          const int64_t *cdel_off)
+{
+    int64_t nt = 0, nb = 0;
+    for (int32_t k = k0; k < k1; ++k) {
+        const SeqObj &S = ctx->seqs[first + k];
+        nt += row_code_off(S.n, S.ncins, S.ncdel) + S.n;
+        nb += S.n;
+    }
+    const int32_t nseq = k1 - k0;
+    const size_t stage_bytes = (size_t)std::max<int64_t>(nt, 1) * 8 + (size_t)std::max<int64_t>(nb, 1);
+    if (ctx->pinned_bytes < stage_bytes) {
+        if (ctx->pinned)
+            (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        const size_t want = std::max(stage_bytes + stage_bytes / 2, (size_t)1 << 22);
+        if (hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault) != hipSuccess)
+            return fail(ctx, RF_ERR_HIP, "rf_set_sequences: pinned staging allocation failed");
+        ctx->pinned_bytes = want;
+    }
+    double *host_tabs = (double *)ctx->pinned;
+    uint8_t *host_bases = (uint8_t *)ctx->pinned + (size_t)std::max<int64_t>(nt, 1) * 8;
+    std::vector<Segment> sb(nseq), st(nseq);
+    std::vector<int64_t> at(nseq + 1, 0);
+    for (int32_t k = 0; k < nseq; ++k) {
+        const SeqObj &S = ctx->seqs[first + k0 + k];
+        at[k + 1] = at[k] + row_code_off(S.n, S.ncins, S.ncdel) + S.n;
+        st[k] = {at[k] * 8, S.tabs.off, (at[k + 1] - at[k]) * 8, 0};
+        sb[k] = {off[k0 + k] - off[k0], S.bases.off, S.n, 0};
+    }
+    // The host work per position (staging copies, the finiteness test, the
+    // row codes) runs on host threads over ranges of sequences.  Row codes in
+    // three passes so the dictionary is only written by one thread: new keys
+    // per range (read-only lookups), their insertion in range order (= the
+    // serial first-occurrence order), then the records (read-only lookups).
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (nt + (1 << 20) - 1) >> 20));
+    std::vector<int32_t> rng(nth + 1);
+    for (int t = 0; t <= nth; ++t)
+        rng[t] = (int32_t)((int64_t)nseq * t / nth);
+    CodeDict &D = ctx->codes;
+    auto table = [&](int32_t k) { return host_tabs + at[k]; };
+    std::vector<std::vector<CodeDict::K3>> new3(nth);
+    std::vector<std::vector<uint64_t>> new1(nth);
+    parallel_for(nth, [&](int t) {
+        std::unordered_set<CodeDict::K3, CodeDict::H3> s3;
+        std::unordered_set<uint64_t> s1;
+        CodeDict::Cache cache;
+        for (int32_t k = rng[t]; k < rng[t + 1]; ++k) {
+            const SeqObj &S = ctx->seqs[first + k0 + k];
+            const int64_t n = S.n, nci = S.ncins, ncd = S.ncdel;
+            double *h = table(k);
+            const int32_t kg = k0 + k;   // index into the caller's arrays
+            std::memcpy(h, match + off[kg], n * 8);
+            std::memcpy(h + n, mismatch + off[kg], n * 8);
+            std::memcpy(h + 2 * n, ins + off[kg], n * 8);
+            std::memcpy(h + 3 * n, del + off[kg] + kg, (n + 1) * 8);
+            if (nci)
+                std::memcpy(h + 4 * n + 1, cins + cins_off[kg], nci * 8);
+            if (ncd)
+                std::memcpy(h + 4 * n + 1 + nci, cdel + cdel_off[kg], ncd * 8);
+            bool fin = true;
+            for (int64_t e = 0; e < 4 * n + 1; ++e)
+                fin = fin && std::isfinite(h[e]);
+            ctx->seqs[first + k0 + k].finite = fin;
+            for (int64_t i = 0; i < n; ++i) {
+                const CodeDict::K3 key{CodeDict::bits(h[i]), CodeDict::bits(h[n + i]), CodeDict::bits(h[2 * n + i])};
+                if (D.find3(key, cache) < 0 && s3.insert(key).second)
+                    new3[t].push_back(key);
+            }
+            for (int64_t i = 0; i <= n; ++i) {
+                const uint64_t key = CodeDict::bits(h[3 * n + i]);
+                if (D.find1(key, cache) < 0 && s1.insert(key).second)
+                    new1[t].push_back(key);
+            }
+        }
+    });
+    for (int t = 0; t < nth; ++t) {
+        for (const auto &key : new3[t])
+            if (D.find3(key) < 0 && D.t3.size() < (size_t)RF_CODES) {
+                D.t3.emplace(key, (uint32_t)D.t3.size());
+                double v[3];
+                std::memcpy(v, &key.a, 8), std::memcpy(v + 1, &key.b, 8), std::memcpy(v + 2, &key.c, 8);
+                D.t3v.insert(D.t3v.end(), {v[0], v[1], v[2], 0.0});
+            }
+        for (uint64_t key : new1[t])
+            if (D.find1(key) < 0 && D.d1.size() < (size_t)RF_CODES) {
+                D.d1.emplace(key, (uint32_t)D.d1.size());
+                double v;
+                std::memcpy(&v, &key, 8);
+                D.d1v.push_back(v);
+            }
+    }
+    parallel_for(nth, [&](int t) {
+        CodeDict::Cache cache;
+        for (int32_t k = rng[t]; k < rng[t + 1]; ++k) {
+            const SeqObj &S = ctx->seqs[first + k0 + k];
+            const int64_t n = S.n;
+            const double *h = table(k);
+            uint64_t *rec = (uint64_t *)(table(k) + row_code_off(n, S.ncins, S.ncdel));
+            const uint8_t *bs = bases + off[k0 + k];
+            bool ok = true;
+            int32_t dprev = D.find1(CodeDict::bits(h[3 * n]), cache);
+            ok = dprev >= 0;
+            for (int64_t i = 0; i < n && ok; ++i) {
+                const int32_t c3 = D.find3({CodeDict::bits(h[i]), CodeDict::bits(h[n + i]), CodeDict::bits(h[2 * n + i])}, cache);
+                const int32_t dn = D.find1(CodeDict::bits(h[3 * n + i + 1]), cache);
+                ok = c3 >= 0 && dn >= 0;
+                rec[i] = (uint64_t)(uint32_t)c3 | ((uint64_t)(uint32_t)dprev << 16) | ((uint64_t)(uint32_t)dn << 32) |
+                         ((uint64_t)bs[i] << 48);
+                dprev = dn;
+            }
+            ctx->seqs[first + k0 + k].coded = ok;
+        }
+    });
+    // 3. new code-dictionary entries, one H2D copy each + device scatter
+    {
+        CodeDict &D = ctx->codes;
+        if (int e = ensure_buf(ctx, D.lut, (size_t)RF_CODES * 5 * 8)) return e;
+        const size_t n3 = D.t3v.size() / 4, n1 = D.d1v.size();
+        if (n3 > D.up3)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * D.up3, D.t3v.data() + 4 * D.up3, (n3 - D.up3) * 32,
+                                       hipMemcpyHostToDevice, ctx->stream));
+        if (n1 > D.up1)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * (size_t)RF_CODES + D.up1, D.d1v.data() + D.up1,
+                                       (n1 - D.up1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        D.up3 = n3;
+        D.up1 = n1;
+    }
+    if (int e = ensure_buf(ctx, ctx->scratch[6], (size_t)std::max<int64_t>(nt * 8, 16))) return e;
+    if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
+    if (nseq > 0) {
+        std::memcpy(host_bases, bases + off[k0], nb);
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[6].p, host_tabs, nt * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, host_bases, nb, hipMemcpyHostToDevice, ctx->stream));
+        if (int e = upload(ctx, ctx->scratch[5], st)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[6].p, (uint8_t *)ctx->tab_arena.d);
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // scratch[5] is reused below
+        if (int e = upload(ctx, ctx->scratch[5], sb)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
+}
+
 int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases,
                      const int64_t *off, const double *match, const double *mismatch,
                      const double *ins, const double *del, const double *cins,
@@ -3681,75 +3836,28 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
         nb += n;
         nt += row_code_off(n, nci, ncd) + n;
     }
-    // 2. pack into the pinned staging buffer: tables [match|mismatch|ins|del|
-    //    cins|cdel] per sequence, then the bases as given
-    const size_t stage_bytes = (size_t)std::max<int64_t>(nt, 1) * 8 + (size_t)std::max<int64_t>(nb, 1);
-    if (ctx->pinned_bytes < stage_bytes) {
-        if (ctx->pinned)
-            (void)hipHostFree(ctx->pinned);
-        ctx->pinned = nullptr;
-        ctx->pinned_bytes = 0;
-        const size_t want = std::max(stage_bytes + stage_bytes / 2, (size_t)1 << 22);
-        if (hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault) != hipSuccess)
-            return fail(ctx, RF_ERR_HIP, "rf_set_sequences: pinned staging allocation failed");
-        ctx->pinned_bytes = want;
-    }
-    double *host_tabs = (double *)ctx->pinned;
-    uint8_t *host_bases = (uint8_t *)ctx->pinned + (size_t)std::max<int64_t>(nt, 1) * 8;
-    std::vector<Segment> sb(nseq), st(nseq);
-    int64_t at = 0;
-    for (int32_t k = 0; k < nseq; ++k) {
-        const SeqObj &S = ctx->seqs[first + k];
-        const int64_t n = S.n, nci = S.ncins, ncd = S.ncdel;
-        double *h = host_tabs + at;
-        std::memcpy(h, match + off[k], n * 8);
-        std::memcpy(h + n, mismatch + off[k], n * 8);
-        std::memcpy(h + 2 * n, ins + off[k], n * 8);
-        std::memcpy(h + 3 * n, del + off[k] + k, (n + 1) * 8);
-        if (nci)
-            std::memcpy(h + 4 * n + 1, cins + cins_off[k], nci * 8);
-        if (ncd)
-            std::memcpy(h + 4 * n + 1 + nci, cdel + cdel_off[k], ncd * 8);
-        const int64_t len = row_code_off(n, nci, ncd) + n;
-        bool fin = true;
-        for (int64_t e = 0; e < 4 * n + 1; ++e)
-            fin = fin && std::isfinite(h[e]);
-        ctx->seqs[first + k].finite = fin;
-        ctx->seqs[first + k].coded =
-            ctx->codes.encode(n, bases + off[k], h, h + n, h + 2 * n, h + 3 * n, (uint64_t *)(h + row_code_off(n, nci, ncd)));
-        st[k] = {at * 8, S.tabs.off, len * 8, 0};
-        sb[k] = {off[k] - off[0], S.bases.off, n, 0};
-        at += len;
-    }
-    // 3. new code-dictionary entries, one H2D copy each + device scatter
-    {
-        CodeDict &D = ctx->codes;
-        if (int e = ensure_buf(ctx, D.lut, (size_t)RF_CODES * 5 * 8)) return e;
-        const size_t n3 = D.t3v.size() / 4, n1 = D.d1v.size();
-        if (n3 > D.up3)
-            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * D.up3, D.t3v.data() + 4 * D.up3, (n3 - D.up3) * 32,
-                                       hipMemcpyHostToDevice, ctx->stream));
-        if (n1 > D.up1)
-            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * (size_t)RF_CODES + D.up1, D.d1v.data() + D.up1,
-                                       (n1 - D.up1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        D.up3 = n3;
-        D.up1 = n1;
-    }
-    if (int e = ensure_buf(ctx, ctx->scratch[6], (size_t)std::max<int64_t>(nt * 8, 16))) return e;
-    if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
-    if (nseq > 0) {
-        std::memcpy(host_bases, bases + off[0], nb);
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[6].p, host_tabs, nt * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, host_bases, nb, hipMemcpyHostToDevice, ctx->stream));
-        if (int e = upload(ctx, ctx->scratch[5], st)) return e;
-        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
-                           (const uint8_t *)ctx->scratch[6].p, (uint8_t *)ctx->tab_arena.d);
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // scratch[5] is reused below
-        if (int e = upload(ctx, ctx->scratch[5], sb)) return e;
-        hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
-                           (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
-        HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // 2.-3. in chunks of at most RF_OPT_STAGE_KB of tables (a bounded pinned
+    // staging buffer and device scratch, whatever the batch size): pack the
+    // chunk's tables [match|mismatch|ins|del|cins|cdel|row codes] and bases
+    // into pinned memory, then one H2D copy each + a device scatter.
+    (void)nb;
+    (void)nt;
+    int32_t k0 = 0;
+    while (k0 < nseq) {
+        int32_t k1 = k0;
+        int64_t ct = 0;
+        while (k1 < nseq) {
+            const SeqObj &S = ctx->seqs[first + k1];
+            const int64_t len = row_code_off(S.n, S.ncins, S.ncdel) + S.n;
+            if (k1 > k0 && (ct + len) * 8 > (int64_t)std::max(ctx->opt.stage_kb, 1) * 1024)
+                break;
+            ct += len;
+            ++k1;
+        }
+        if (int e = upload_sequence_chunk(ctx, first, k0, k1, bases, off, match, mismatch, ins, del, cins, cins_off,
+                                          cdel, cdel_off))
+            return e;
+        k0 = k1;
     }
     for (int32_t k = 0; k < nseq; ++k)
         ctx->seqs[first + k].valid = true;
@@ -3762,11 +3870,28 @@ int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl, const uint8_t *ba
 {
     if (!ctx || first < 0 || ntpl < 0 || (ntpl > 0 && (!bases || !off)))
         return fail(ctx, RF_ERR_ARG, "rf_set_templates: bad arguments");
+    std::vector<int32_t> ids(ntpl);
+    for (int32_t k = 0; k < ntpl; ++k)
+        ids[k] = first + k;
+    return rf_set_templates_ids(ctx, ntpl, ids.data(), bases, off);
+}
+
+int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids, const uint8_t *bases,
+                         const int64_t *off)
+{
+    if (!ctx || ntpl < 0 || (ntpl > 0 && (!ids || !bases || !off)))
+        return fail(ctx, RF_ERR_ARG, "rf_set_templates: bad arguments");
     (void)hipSetDevice(ctx->device);
-    if ((int64_t)first + ntpl > (int64_t)ctx->tpls.size())
-        ctx->tpls.resize(first + ntpl);
+    int32_t top = 0;
     for (int32_t k = 0; k < ntpl; ++k) {
-        TplObj &T = ctx->tpls[first + k];
+        if (ids[k] < 0)
+            return fail(ctx, RF_ERR_ARG, "rf_set_templates: bad arguments");
+        top = std::max(top, ids[k] + 1);
+    }
+    if ((int64_t)top > (int64_t)ctx->tpls.size())
+        ctx->tpls.resize(top);
+    for (int32_t k = 0; k < ntpl; ++k) {
+        TplObj &T = ctx->tpls[ids[k]];
         const int64_t m = off[k + 1] - off[k];
         if (m < 1)
             return fail(ctx, RF_ERR_ARG, "rf_set_templates: empty template");
@@ -3779,9 +3904,10 @@ int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl, const uint8_t *ba
         T.valid = true;
     }
     if (ntpl > 0) {
+        // offsets are read after every region_ensure (arena growth moves regions)
         std::vector<Segment> sg(ntpl);
         for (int32_t k = 0; k < ntpl; ++k)
-            sg[k] = {off[k] - off[0], ctx->tpls[first + k].bases.off, off[k + 1] - off[k], 0};
+            sg[k] = {off[k] - off[0], ctx->tpls[ids[k]].bases.off, off[k + 1] - off[k], 0};
         const int64_t nb = off[ntpl] - off[0];
         if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(nb, 16))) return e;
         HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, bases + off[0], nb, hipMemcpyHostToDevice, ctx->stream));

@@ -30,6 +30,15 @@ _SIGNATURES = {
     "rf_set_sequences": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_set_templates": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "rf_set_templates_ids": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rf_rifraf_batch": (c_int, [c_void_p, c_int32, c_void_p] + [c_void_p] * 14),
+    "rf_batch_fetch": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
+    "rf_batch_release": (None, [c_void_p]),
+    "rf_aln_error_sums": (c_int, [c_void_p, c_int32] + [c_void_p] * 7),
+    "rf_host_julia_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
+    "rf_host_seq_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
+    "rf_host_tables_from_codes": (c_int, [c_int64] + [c_void_p] * 5 + [c_double] * 3 + [c_void_p] * 6),
+    "rf_host_code_seq_sums": (c_int, [c_int64] + [c_void_p] * 5),
     "rf_realign": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "rf_backtrace": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_score": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -51,10 +60,19 @@ _SIGNATURES = {
 # rf_set_option keys (include/rifraf_hip.h RF_OPT_*)
 OPTIONS = {"score_mode": 1, "score_kernel": 2, "lean_nw": 3, "lean_lds_kb": 4, "ws_q": 5, "seg_s": 6,
            "seg_lds": 7, "seg_wpe": 8, "bt_global": 9, "dp_psplit": 10, "dp_np8": 11, "dp_np8_lean": 12,
-           "dp_streams": 13, "seg_ver": 14, "bt_win_kb": 15}
+           "dp_streams": 13, "seg_ver": 14, "bt_win_kb": 15, "stage_kb": 16}
 # symbolic values of the enum-like options
 OPTION_VALUES = {"score_mode": {"auto": 0, "fused": 1, "split": 2},
                  "score_kernel": {"auto": 0, "general": 1, "seg": 2}}
+
+
+
+class BatchParams(ctypes.Structure):
+    """rf_batch_params (include/rifraf_hip.h)."""
+    _fields_ = [("max_iters", c_int32), ("min_dist", c_int32), ("bandwidth", c_int32),
+                ("do_alignment_proposals", c_int32), ("batch_fixed", c_int32), ("batch_size", c_int32),
+                ("batch_threshold", c_double)]
+
 
 _lib = None
 _load_error = None

@@ -221,17 +221,233 @@ class _Hub:
             at += n
 
 
-STATS = {"launches": 0, "engine_s": 0.0}
+STATS = {"launches": 0, "engine_s": 0.0, "native_s": 0.0, "score_phase_s": 0.0, "setup_native_s": 0.0,
+         "upload_s": 0.0}
 
 
-def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
+def native_eligible(clusters, params) -> bool:
+    """Whether rf_rifraf_batch (rifraf_batch.cpp) can run these clusters: no
+    reference (the INIT stage then ends the run, model.jl:937-948), INIT
+    enabled, and a deterministic batch -- the fixed lowest-error batch or
+    every read (random resampling stays in the Python stage machine)."""
+    if not params.do_init:
+        return False
+    for kw in clusters:
+        ref = kw.get("reference")
+        if ref is not None and len(ref) > 0:
+            return False
+        n = len(kw["dnaseqs"])
+        if n < 1:
+            return False
+        if not params.batch_fixed and 1 < params.batch_size < n:
+            return False
+    return True
+
+
+def _logsumexp10_many(values, off, codes=None, table=None):
+    """model.logsumexp10 of every segment values[off[k]:off[k+1]] (non-empty):
+    the same max, the same numpy power of the shifted values (numpy
+    evaluates each element alike wherever it sits), the same sequential sum
+    (rf_host_seq_sums) and the same math.log10.  With `codes` (values ==
+    table[codes], a 256-entry table), 10 ** (x - u) is evaluated once per
+    (code of x, code of u) pair and gathered -- the same values."""
+    import math
+
+    from . import _lib
+    u = np.maximum.reduceat(values, off[:-1])
+    lens = np.diff(off)
+    p = None
+    if codes is not None:
+        fin = np.isfinite(table)
+        pos = {float(v): c for c, v in enumerate(table.tolist()) if fin[c]}
+        if all(float(x) in pos for x in u.tolist() if math.isfinite(x)):
+            ucode = np.array([pos.get(float(x), 0) for x in u.tolist()], np.int32)
+            with np.errstate(invalid="ignore"):
+                grid = np.ascontiguousarray(np.power(10.0, table[None, :] - table[:, None]))   # [u code, x code]
+            s = np.empty(len(lens))
+            _lib.load().rf_host_code_seq_sums(len(lens), _lib.ptr(np.ascontiguousarray(codes, np.uint8)),
+                                              _lib.ptr(np.ascontiguousarray(off, np.int64)), _lib.ptr(ucode),
+                                              _lib.ptr(grid), _lib.ptr(s))
+            p = True
+    if p is None:
+        sh = values - np.repeat(u, lens)
+        p = np.ascontiguousarray(np.power(10.0, sh))
+        s = np.empty(len(lens))
+        _lib.load().rf_host_seq_sums(len(lens), _lib.ptr(p), _lib.ptr(np.ascontiguousarray(off, np.int64)),
+                                     _lib.ptr(s))
+    out = []
+    for k in range(len(lens)):
+        uk = float(u[k])
+        if abs(uk) == math.inf:
+            seg = values[off[k]:off[k + 1]]
+            out.append(math.nan if np.isnan(seg).any() else uk)
+        else:
+            out.append(math.log10(float(s[k])) + uk)
+    return out
+
+
+def _wave_native(part, params, engine):
+    """One wave through the native stage machine (rf_rifraf_batch), then
+    (do_score) the quality pass of every cluster with three batched engine
+    calls; host setup is vectorised across the wave's reads."""
+    from . import _lib
+    from .engine import RF_BWD, RF_FWD
+    from .errormodel import phred_to_log_p
+    from .model import RifrafResult, Stage, check_params, initial_state, qvs_many
+    from .poisson import cquantile_poisson_many
+    from .proposals import AmbiguousProposalsError
+    from .rifrafsequences import RifrafSequence
+    from .types import DNASeq
+
+    K = len(part)
+    t_setup = time.perf_counter()
+    check_params(params.scores, np.zeros(0, np.uint8), params)
+    all_s, all_lp, nread = [], [], []
+    phred_in = all(kw.get("error_log_ps") is None for kw in part)
+    for kw in part:                                                 # rifraf(), model.jl:1276-1287
+        if phred_in:
+            if any(np.min(p) < 0 for p in kw["phreds"]):
+                raise RifrafError("phred score cannot be negative")
+            all_lp += list(kw["phreds"])
+        else:
+            elp = kw.get("error_log_ps")
+            all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
+        all_s += [DNASeq(x) for x in kw["dnaseqs"]]
+        nread.append(len(kw["dnaseqs"]))
+    lens = np.array([len(x) for x in all_s], np.int64)
+    if (lens == 0).any() or any(len(x) != len(y) for x, y in zip(all_s, all_lp)):
+        raise RifrafError("empty read or length mismatch")
+    soff = np.zeros(len(all_s) + 1, np.int64)
+    np.cumsum(lens, out=soff[1:])
+    # one division / ufunc pass over every read (elementwise: equal to per-read calls)
+    lp = phred_to_log_p(np.concatenate(all_lp)) if phred_in else np.concatenate(
+        [np.asarray(x, np.float64) for x in all_lp])
+    allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
+                                               phreds=np.concatenate(all_lp).astype(np.int8) if phred_in else None)
+    nread = np.array(nread, np.int32)
+    read_off = np.zeros(K + 1, np.int32)
+    np.cumsum(nread, out=read_off[1:])
+    # initial consensus where none is given: the read of max logsumexp10(match scores)
+    need = [k for k, kw in enumerate(part) if kw.get("consensus") is None or len(kw["consensus"]) == 0]
+    first = {}
+    if need:
+        ridx = np.concatenate([np.arange(read_off[k], read_off[k + 1]) for k in need])
+        ms = [allseqs[r].match_scores for r in ridx]
+        moff = np.zeros(len(ms) + 1, np.int64)
+        np.cumsum([len(x) for x in ms], out=moff[1:])
+        if len(need) == K and phred_in:
+            lse = _logsumexp10_many(tabs["match"], moff, codes=tabs["code"], table=tabs["match_table"])
+        else:
+            lse = _logsumexp10_many(np.concatenate(ms), moff)
+        at = 0
+        for k in need:
+            sc = lse[at:at + nread[k]]
+            first[k] = allseqs[read_off[k] + int(np.argmax(sc))].seq.copy()
+            at += nread[k]
+    states = []
+    for k, kw in enumerate(part):
+        cons = first[k] if k in first else DNASeq(kw["consensus"])
+        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], np.zeros(0, np.uint8), params))
+    # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
+    # The bands of every batch read in one arena reservation (growing it in
+    # steps would re-allocate and compact tens of GB several times): A and B
+    # at the initial bandwidth, x1.5 for band doubling
+    nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
+    est_bytes = 0
+    for k, st_ in enumerate(states):
+        m = len(st_.consensus)
+        ln = lens[read_off[k]:read_off[k + 1]]
+        H = 2 * params.bandwidth + np.abs(ln - m) + 1
+        band = (H + 2 * m) * (((H + 1) >> 1) | 1) * 8
+        est_bytes += int(np.sort(band)[::-1][:nb[k]].sum()) * 2
+    engine.reserve(int(est_bytes * 1.5) + (64 << 20))
+    STATS["setup_native_s"] += time.perf_counter() - t_setup
+    allb = np.concatenate(all_s)
+    engine.set_sequences_concat(0, allb, soff, tabs["match"], tabs["mismatch"], tabs["ins"], tabs["del"])
+    engine.set_templates(0, [st_.consensus for st_ in states])
+    STATS["upload_s"] += time.perf_counter() - t_setup
+    read_seq = np.arange(len(all_s), dtype=np.int32)
+    read_len = lens.astype(np.int32)
+    est = np.array([s.est_n_errors for s in allseqs])
+    thr = cquantile_poisson_many(est, params.bandwidth_pvalue)
+    fixed_off = fixed = None
+    if params.batch_fixed:
+        fb = [np.argsort(est[read_off[k]:read_off[k + 1]], kind="stable")[:st_.batch_fixed_size]
+              for k, st_ in enumerate(states)]                      # resample!, model.jl:1045-1049
+        fixed_off = np.zeros(K + 1, np.int32)
+        np.cumsum([len(b) for b in fb], out=fixed_off[1:])
+        fixed = np.concatenate(fb).astype(np.int32)
+    cons = [st_.consensus for st_ in states]
+    cons_off = np.zeros(K + 1, np.int64)
+    np.cumsum([len(c) for c in cons], out=cons_off[1:])
+    bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
+                          int(params.batch_fixed), params.batch_size, params.batch_threshold)
+    t0 = time.perf_counter()
+    res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
+                                         read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons), cons_off)
+    STATS["native_s"] += time.perf_counter() - t0
+    for s, b in zip(allseqs, bw.tolist()):
+        s.bandwidth = abs(b)
+        s.bandwidth_fixed = b < 0
+    results, errors = [], [None] * K
+    for k, (st_, r) in enumerate(zip(states, res)):
+        if r["status"] == 2:
+            errors[k] = AmbiguousProposalsError() if r["error"] == "AmbiguousProposalsError" else RifrafError(r["error"])
+        st_.consensus = DNASeq(r["consensus"])
+        st_.score = r["score"]
+        st_.stage_iterations = [r["iters"], 0, 0, 0]
+        st_.converged = r["status"] == 1
+        st_.batch_seqs = r["batch"]
+        st_.n_slots = len(r["batch"])
+        st_.slot_scores = [0.0] * st_.n_slots
+        st_.stage = Stage.SCORE
+        results.append(RifrafResult(consensus=st_.consensus, params=params, state=st_,
+                                    consensus_stages=[[DNASeq(c) for c in r["stages"]], [], []]))
+    for e in errors:
+        if e is not None:
+            raise e
+    if params.do_score:                                             # model.jl:1262-1270
+        t0 = time.perf_counter()
+        # realign_rescore (every batch read is bandwidth_fixed: one fill each),
+        # estimate_probs over the dense totals, alignment_error_probs's sums
+        groups = [read_off[k] + np.arange(len(st_.batch_seqs), dtype=np.int32) for k, st_ in enumerate(states)]
+        sq = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int32) for k, st_ in enumerate(states)])
+        tp = np.concatenate([np.full(len(g), k, np.int32) for k, g in enumerate(groups)])
+        bws = np.array([st_.sequences[i].bandwidth for st_ in states for i in st_.batch_seqs], np.int32)
+        engine.set_templates(0, [st_.consensus for st_ in states])
+        sc = engine.realign(np.concatenate(groups), sq, tp, bws, RF_FWD | RF_BWD)
+        at = 0
+        for st_ in states:
+            n = len(st_.batch_seqs)
+            st_.slot_scores = [float(v) for v in sc[at:at + n]]
+            total = st_.slot_scores[0]                              # rescore!, model.jl:630-635
+            for v in st_.slot_scores[1:st_.n_slots]:
+                total += v
+            st_.score = total
+            at += n
+        dense = engine.score_dense(groups)
+        ridx = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int64) for k, st_ in enumerate(states)])
+        sums = engine.aln_error_sums_ptr(groups, [len(st_.consensus) for st_ in states],
+                                         allb.ctypes.data + soff[ridx].astype(np.uint64),
+                                         tabs["match"].ctypes.data + 8 * soff[ridx].astype(np.uint64), lens[ridx])
+        for k, (ep, ap) in enumerate(qvs_many(states, dense, sums)):
+            results[k].error_probs = ep
+            results[k].aln_error_probs = ap
+        STATS["score_phase_s"] += time.perf_counter() - t0
+    return results
+
+
+def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None):
     """rifraf() over many independent clusters, batched on one engine.
 
     clusters: sequence of dicts with the keyword arguments of model.rifraf
     (`dnaseqs`, `phreds` or `error_log_ps`, optional `consensus`,
     `reference`).  Returns the list of RifrafResult in input order (an
     exception raised by a cluster is re-raised after the wave finishes).
-    Clusters run in waves of at most `wave` (their bands share the device)."""
+    Clusters run in waves of at most `wave` (their bands share the device).
+    native (default: when eligible, see native_eligible): run the INIT stage
+    machine in the library (rf_rifraf_batch) instead of one host thread per
+    cluster; the results are identical."""
     import os
     from .model import RifrafParams, rifraf
     params = params or RifrafParams()
@@ -239,9 +455,17 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024):
     if engine is None:
         from .align import default_engine
         engine = default_engine()
+    ok = native_eligible(clusters, params) and hasattr(engine, "rifraf_batch_native")
+    if native is None:
+        native = ok
+    elif native and not ok:
+        raise RifrafError("rifraf_batch(native=True): clusters or engine outside the native driver's scope")
     results = [None] * len(clusters)
     for w0 in range(0, len(clusters), wave):
         part = clusters[w0:w0 + wave]
+        if native:
+            results[w0:w0 + len(part)] = _wave_native(part, params, engine)
+            continue
         stride = max(len(c["dnaseqs"]) for c in part) + 2
         hub = _Hub(engine, len(part), stride)
         errors = [None] * len(part)

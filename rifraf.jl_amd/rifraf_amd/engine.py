@@ -103,6 +103,16 @@ class Engine:
             self.ctx, int(first), len(seqs), ptr(bases), ptr(off), ptr(match), ptr(mism), ptr(ins),
             ptr(dele), ptr(cins), ptr(cins_off), ptr(cdel), ptr(cdel_off)))
 
+    def set_sequences_concat(self, first: int, bases, off, match, mismatch, ins, dele):
+        """rf_set_sequences from already concatenated tables (no codon moves):
+        sequence k = bases / tables at off[k]..off[k+1], del at off[k]+k ..
+        off[k+1]+k+1 (the layout RifrafSequence.many_concat returns)."""
+        off = np.ascontiguousarray(off, np.int64)
+        a = [np.ascontiguousarray(x, np.float64) for x in (match, mismatch, ins, dele)]
+        bases = np.ascontiguousarray(bases, np.uint8)
+        self._check(self.lib.rf_set_sequences(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off),
+                                              *[ptr(x) for x in a], None, None, None, None))
+
     def set_templates(self, first: int, tpls):
         if not tpls:
             return
@@ -111,6 +121,76 @@ class Engine:
         np.cumsum(lens, out=off[1:])
         bases = np.ascontiguousarray(np.concatenate([np.asarray(t, np.uint8) for t in tpls]), np.uint8)
         self._check(self.lib.rf_set_templates(self.ctx, int(first), len(tpls), ptr(bases), ptr(off)))
+
+    def rifraf_batch_native(self, bparams, read_off, read_seq, read_len, threshold, fixed_off, fixed,
+                            slot_base, tpl_id, cons, cons_off):
+        """rf_rifraf_batch + rf_batch_fetch: the native lockstep INIT stage of
+        many reference-free clusters (rifraf_batch.cpp).  Returns one dict per
+        cluster: consensus, score, iters, status, stages, batch, error; and
+        the final bandwidth per read (negative once bandwidth_fixed)."""
+        nclu = len(slot_base)
+        c = lambda a, t: np.ascontiguousarray(a, t)   # noqa: E731
+        read_off, read_seq, read_len = c(read_off, np.int32), c(read_seq, np.int32), c(read_len, np.int32)
+        threshold = c(threshold, np.float64)
+        fixed_off = c(fixed_off, np.int32) if fixed_off is not None else None
+        fixed = c(fixed, np.int32) if fixed is not None else None
+        slot_base, tpl_id = c(slot_base, np.int32), c(tpl_id, np.int32)
+        cons, cons_off = c(cons, np.uint8), c(cons_off, np.int64)
+        score = np.empty(max(nclu, 1))
+        iters = np.empty(max(nclu, 1), np.int32)
+        status = np.empty(max(nclu, 1), np.int32)
+        length = np.empty(max(nclu, 1), np.int64)
+        bw = np.empty(max(len(read_seq), 1), np.int32)
+        self._check(self.lib.rf_rifraf_batch(self.ctx, nclu, byref(bparams), ptr(read_off), ptr(read_seq),
+                                             ptr(read_len), ptr(threshold), ptr(fixed_off), ptr(fixed),
+                                             ptr(slot_base), ptr(tpl_id), ptr(cons), ptr(cons_off), ptr(score),
+                                             ptr(iters), ptr(status), ptr(length), ptr(bw)))
+        out = []
+        err = ctypes.create_string_buffer(512)
+        try:
+            for k in range(nclu):
+                cs = np.empty(int(length[k]), np.uint8)
+                slen = np.empty(max(int(iters[k]), 1), np.int64)
+                nb = int(fixed_off[k + 1] - fixed_off[k]) if fixed_off is not None else int(read_off[k + 1] - read_off[k])
+                batch = np.empty(nb, np.int32)
+                self._check(self.lib.rf_batch_fetch(self.ctx, k, ptr(cs), ptr(slen), None, ptr(batch), err, 512))
+                st = np.empty(int(slen[:iters[k]].sum()), np.uint8)
+                self._check(self.lib.rf_batch_fetch(self.ctx, k, None, None, ptr(st), None, None, 0))
+                cut = np.cumsum(slen[:iters[k]])[:-1]
+                out.append({"consensus": cs, "score": float(score[k]), "iters": int(iters[k]),
+                            "status": int(status[k]), "stages": np.split(st, cut) if iters[k] else [],
+                            "batch": batch.tolist(), "error": err.value.decode() if status[k] == 2 else None})
+        finally:
+            self.lib.rf_batch_release(self.ctx)
+        return out, bw[:len(read_seq)]
+
+    def aln_error_sums(self, groups, tlens, seqs):
+        """rf_aln_error_sums: per group (slot list in batch order, consensus
+        length, the slots' RifrafSequences) the (m, 4) base-distribution sums
+        of alignment_error_probs before its normalisation."""
+        keep = [(np.ascontiguousarray(s.seq, np.uint8), np.ascontiguousarray(s.match_scores, np.float64))
+                for gs in seqs for s in gs]
+        bptr = np.array([b.ctypes.data for b, _ in keep], np.uint64)
+        mptr = np.array([m.ctypes.data for _, m in keep], np.uint64)
+        slen = np.array([len(b) for b, _ in keep], np.int32)
+        return self.aln_error_sums_ptr(groups, tlens, bptr, mptr, slen)
+
+    def aln_error_sums_ptr(self, groups, tlens, bptr, mptr, slen):
+        """aln_error_sums with the slots' read bases / match scores given as
+        host addresses (uint64 arrays; the caller keeps the memory alive)."""
+        off = np.zeros(len(groups) + 1, np.int32)
+        np.cumsum([len(g) for g in groups], out=off[1:])
+        slots = np.ascontiguousarray(np.concatenate([np.asarray(g, np.int32) for g in groups])
+                                     if groups else np.zeros(0, np.int32))
+        bptr, mptr = np.ascontiguousarray(bptr, np.uint64), np.ascontiguousarray(mptr, np.uint64)
+        slen = np.ascontiguousarray(slen, np.int32)
+        tl = np.ascontiguousarray(tlens, np.int32)
+        row = np.zeros(len(groups) + 1, np.int64)
+        np.cumsum(tl, out=row[1:])
+        out = np.empty((max(int(row[-1]), 1), 4))
+        self._check(self.lib.rf_aln_error_sums(self.ctx, len(groups), ptr(off), ptr(slots), ptr(tl), ptr(bptr),
+                                               ptr(mptr), ptr(slen), ptr(out)))
+        return [out[row[g]:row[g + 1]] for g in range(len(groups))]
 
     def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
         """Batched forward_moves!/backward! fill; returns A[end,end] (RF_FWD)

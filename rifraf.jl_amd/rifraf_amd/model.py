@@ -605,6 +605,96 @@ def estimate_probs(state: RifrafState, run: _Run, use_ref_for_qvs: bool) -> Esti
     return normalize_log_differences(sub_scores, del_scores, ins_scores, state.score - max_score)
 
 
+def estimate_probs_from_dense(state: RifrafState, dense) -> EstimatedProbs:
+    """estimate_probs (model.jl:737-791) from the cluster's rf_score_dense
+    totals instead of an rf_score proposal list: the dense slots are the same
+    left folds of the same per-read scores (rf_score gathers them from this
+    very table), and every array operation below is estimate_probs's."""
+    m = len(state.consensus)
+    dense = np.asarray(dense)
+    cons = np.asarray(state.consensus, np.int64)
+    sub = dense[1:, 0:4].copy()
+    own = np.zeros((m, 4), bool)
+    own[np.arange(m), cons] = True
+    used = np.concatenate([sub[~own], dense[1:, 4], dense[:, 5:9].ravel()])
+    if np.isnan(used).any():
+        raise RifrafError("failed to compute a valid score")
+    sub_scores = np.zeros((m, 4)) + state.score
+    sub_scores[~own] = sub[~own]
+    del_scores = dense[1:, 4].copy()
+    ins_scores = dense[:, 5:9].copy()
+    max_score = max(sub_scores.max(), del_scores.max(), ins_scores.max())
+    sub_scores = sub_scores - max_score
+    del_scores = del_scores - max_score
+    ins_scores = ins_scores - max_score
+    if sub_scores.max() > 0.0:
+        raise RifrafError("sub scores cannot be positive")
+    if del_scores.max() > 0.0:
+        raise RifrafError("deletion scores cannot be positive")
+    if ins_scores.max() > 0.0:
+        raise RifrafError("insertion scores cannot be positive")
+    return normalize_log_differences(sub_scores, del_scores, ins_scores, state.score - max_score)
+
+
+def qvs_many(states, dense, sums):
+    """estimate_probs_from_dense and aln_error_probs_from_sums for many
+    clusters at once: every cluster's arrays are stacked and each numpy
+    operation runs once over the stack.  The operations are elementwise, per
+    row of a fixed length, or maxima (exact in any order), which numpy
+    evaluates identically wherever a row sits; the per-cluster scalars (the
+    max score, 10.0 ** state_score) are computed per cluster exactly as the
+    single-cluster code does.  Returns [(EstimatedProbs, aln_error_probs)]."""
+    K = len(states)
+    ms = np.array([len(st.consensus) for st in states], np.int64)
+    moff = np.zeros(K + 1, np.int64)
+    np.cumsum(ms, out=moff[1:])
+    roff = moff + np.arange(K + 1)                                      # rows of the dense tables
+    D = np.concatenate([np.asarray(d) for d in dense])                  # (sum(m+1), 9)
+    body = np.ones(len(D), bool)
+    body[roff[:-1]] = False                                              # rows p >= 1
+    Db = D[body]
+    cons = np.concatenate([np.asarray(st.consensus, np.int64) for st in states])
+    rows = np.arange(len(Db))
+    nan = np.isnan(Db[:, 0:5])
+    nan[rows, cons] = False                                              # not a proposal
+    if nan.any() or np.isnan(D[:, 5:9]).any():
+        raise RifrafError("failed to compute a valid score")
+    S = Db[:, 0:4].copy()
+    S[rows, cons] = np.zeros(len(Db)) + np.repeat(np.array([st.score for st in states]), ms)
+    Dl = Db[:, 4].copy()
+    I = D[:, 5:9]
+    mxS = np.maximum.reduceat(S.max(axis=1), moff[:-1])
+    mxD = np.maximum.reduceat(Dl, moff[:-1])
+    mxI = np.maximum.reduceat(I.max(axis=1), roff[:-1])
+    mx = [max(x, y, z) for x, y, z in zip(mxS, mxD, mxI)]              # max(sub.max(), del.max(), ins.max())
+    mxa = np.array(mx, np.float64)
+    for k in np.nonzero((mxS - mxa > 0.0) | (mxD - mxa > 0.0) | (mxI - mxa > 0.0))[0][:1]:
+        raise RifrafError("sub scores cannot be positive" if mxS[k] - mxa[k] > 0.0 else
+                          "deletion scores cannot be positive" if mxD[k] - mxa[k] > 0.0 else
+                          "insertion scores cannot be positive")
+    mrow = np.repeat(mxa, ms)
+    # normalize_log_differences (model.jl:722-735)
+    pos_exp = np.power(10.0, np.hstack([S - mrow[:, None], (Dl - mrow)[:, None]]))
+    pos_probs = pos_exp / pos_exp.sum(axis=1, keepdims=True)
+    ins_exp = np.power(10.0, I - np.repeat(mxa, ms + 1)[:, None])
+    st_pow = np.repeat(np.array([10.0 ** (st.score - mx[k]) for k, st in enumerate(states)]), ms + 1)
+    ins_probs = ins_exp / (st_pow[:, None] + ins_exp.sum(axis=1, keepdims=True))
+    A = np.power(10.0, np.concatenate([np.asarray(x) for x in sums]))   # alignment_error_probs
+    aln = 1.0 - (A / A.sum(axis=1, keepdims=True)).max(axis=1)
+    out = []
+    for k in range(K):
+        a, b, c, d = moff[k], moff[k + 1], roff[k], roff[k + 1]
+        out.append((EstimatedProbs(pos_probs[a:b, :4], pos_probs[a:b, 4], ins_probs[c:d]), aln[a:b]))
+    return out
+
+
+def aln_error_probs_from_sums(sums):
+    """alignment_error_probs's final normalisation (model.jl:835-839) of the
+    per-column base-distribution sums (rf_aln_error_sums)."""
+    probs = np.power(10.0, np.asarray(sums))
+    return 1.0 - (probs / probs.sum(axis=1, keepdims=True)).max(axis=1)
+
+
 def base_distribution(base, ilp):                                  # :804-809
     lp = math.log10(1.0 - 10.0 ** ilp)
     result = np.full(4, lp - math.log10(3))

@@ -54,3 +54,46 @@ def cquantile_poisson(lam: float, p: float) -> float:
         y = y + 1
         if _ppois(y, lam) >= pp:
             return y
+
+
+def cquantile_poisson_many(lams, p: float):
+    """cquantile_poisson over an array of lambdas: the same Cornish-Fisher
+    start and unit-step search, element by element with the same FP64
+    operations (numpy / scipy ufuncs evaluate each element exactly as the
+    scalar calls do), so every threshold equals cquantile_poisson(lam, p)."""
+    import numpy as np
+    lams = np.asarray(lams, np.float64)
+    target = 0.5 - p + 0.5
+    ok = np.isfinite(lams) & (lams > 0)
+    if target in (0.0, 1.0) or target + 1.01 * DBL_EPSILON >= 1.0 or not ok.all():
+        return np.array([cquantile_poisson(float(x), p) for x in lams])
+    mu, sigma = lams, np.sqrt(lams)
+    gamma = 1.0 / sigma
+    z = float(ndtri(target))
+    y = np.maximum(np.rint(mu + sigma * (z + gamma * (z * z - 1) / 6)), 0.0)
+    pp = target * (1 - 64 * DBL_EPSILON)
+    zz = pdtr(y, lams)
+    out = np.empty_like(y)
+    left = zz >= pp
+    # search to the left: the smallest y with ppois(y) >= pp
+    idx = np.nonzero(left)[0]
+    yl = y[idx]
+    while idx.size:
+        at0 = yl == 0
+        out[idx[at0]] = 0.0
+        idx, yl = idx[~at0], yl[~at0]
+        if not idx.size:
+            break
+        zl = pdtr(yl - 1, lams[idx])
+        done = zl < pp
+        out[idx[done]] = yl[done]
+        idx, yl = idx[~done], np.maximum(0.0, yl[~done] - 1)
+    # search to the right
+    idx = np.nonzero(~left)[0]
+    yr = y[idx]
+    while idx.size:
+        yr = yr + 1
+        done = pdtr(yr, lams[idx]) >= pp
+        out[idx[done]] = yr[done]
+        idx, yr = idx[~done], yr[~done]
+    return out

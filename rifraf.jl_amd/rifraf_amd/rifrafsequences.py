@@ -41,6 +41,32 @@ def julia_max(x: float, y: float) -> float:
     return x
 
 
+def self_objects(cls, seqs, lp, match, mism, ins, dele, est, off, bandwidth):
+    """RifrafSequence objects whose tables are views of concatenated arrays
+    (del: n + 1 per sequence at off[k] + k)."""
+    out = []
+    new = object.__new__
+    empty = np.empty(0)
+    offl, estl = np.asarray(off).tolist(), np.asarray(est).tolist()
+    bw = int(bandwidth)
+    for k, sq in enumerate(seqs):
+        a, b = offl[k], offl[k + 1]
+        r = new(cls)
+        r.seq = sq
+        r.error_log_p = lp[a:b]
+        r.match_scores = match[a:b]
+        r.mismatch_scores = mism[a:b]
+        r.ins_scores = ins[a:b]
+        r.del_scores = dele[a + k:b + k + 1]
+        r.codon_ins_scores = empty
+        r.codon_del_scores = empty
+        r.est_n_errors = estl[k]
+        r.bandwidth = bw
+        r.bandwidth_fixed = False
+        out.append(r)
+    return out
+
+
 class RifrafSequence:
     """Mirror of the mutable struct at rifrafsequences.jl:5-17."""
 
@@ -112,6 +138,102 @@ class RifrafSequence:
         self.codon_del_scores = np.zeros(0)
         self.bandwidth = 0
         self.bandwidth_fixed = False
+
+    @classmethod
+    def many(cls, seqs, error_log_ps, bandwidth: int, scores: Scores) -> list:
+        """[RifrafSequence(s, lp, bandwidth, scores) for ...] with every table
+        computed by one numpy call over the concatenated log error
+        probabilities (see many_concat)."""
+        seqs = [DNASeq(sq) for sq in seqs]
+        lps = []
+        for sq, lp in zip(seqs, error_log_ps):
+            lp = np.asarray(lp)
+            if lp.dtype.kind in "iu":
+                lp = phred_to_log_p(lp)
+            lp = np.asarray(lp, dtype=np.float64)
+            if len(sq) != len(lp):
+                raise ValueError("length mismatch")
+            lps.append(lp)
+        if (scores.codon_insertion > -math.inf or scores.codon_deletion > -math.inf or bandwidth < 1
+                or not lps or any(len(x) == 0 for x in lps)):
+            return [cls(sq, lp, bandwidth, scores) for sq, lp in zip(seqs, lps)]
+        off = np.zeros(len(lps) + 1, np.int64)
+        np.cumsum([len(x) for x in lps], out=off[1:])
+        return cls.many_concat(seqs, np.concatenate(lps), off, bandwidth, scores)[0]
+
+    @classmethod
+    def many_concat(cls, seqs, lp, off, bandwidth: int, scores: Scores, phreds=None):
+        """Sequences seqs[k] with log error probabilities lp[off[k]:off[k+1]]
+        (all non-empty, no codon scores).  numpy evaluates each element of a
+        ufunc the same way wherever it sits in an array (checked by
+        tests/test_host_batch.py), so every table is bit-identical to the
+        per-sequence constructor's; est_n_errors is the same Julia-order sum
+        (rf_host_julia_sums; julia_sum without the library).  With `phreds`
+        (the int8 Phred scores lp was divided from) the transcendental tables
+        are evaluated once per distinct score and gathered: the same values,
+        since each element's result depends on its value alone.  Returns the
+        objects (their tables are views) and the concatenated tables for a
+        single rf_set_sequences upload."""
+        lp = np.ascontiguousarray(lp, np.float64)
+        K = len(off) - 1
+        if lp.min() == -math.inf:
+            raise ValueError("a log error probability is negative infinity")
+        if lp.max() > 0.0:
+            raise ValueError(f"a log error probability is > 0: {lp.max()}")
+        if phreds is not None:
+            code = np.ascontiguousarray(np.asarray(phreds, np.int8).view(np.uint8))
+            vals = phred_to_log_p(np.arange(256, dtype=np.uint8).view(np.int8))
+            tp10 = np.power(10.0, vals)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                tmatch = np.log10(1.0 - tp10)
+            extra = {"code": code, "match_table": tmatch}
+            lib = None
+            try:
+                from . import _lib
+                lib = _lib.load()
+            except Exception:  # noqa: BLE001 -- host-only use without the library: numpy below
+                pass
+            if lib is not None:
+                # gathers + FP64 add / max in C++ (rf_host_tables_from_codes): the
+                # same values as the numpy expressions below, without their temporaries
+                N, K = len(code), len(off) - 1
+                off64 = np.ascontiguousarray(off, np.int64)
+                lp2, match, mism, ins = (np.empty(N) for _ in range(4))
+                dele, est = np.empty(N + K), np.empty(K)
+                P = _lib.ptr
+                lib.rf_host_tables_from_codes(K, P(code), P(off64), P(vals), P(tp10), P(tmatch),
+                                              float(scores.mismatch), float(scores.insertion),
+                                              float(scores.deletion), P(lp2), P(match), P(mism), P(ins),
+                                              P(dele), P(est))
+                if not np.array_equal(lp2, lp):
+                    raise ValueError("phreds do not match the log error probabilities")
+                return self_objects(cls, seqs, lp2, match, mism, ins, dele, est, off, bandwidth), \
+                    {"match": match, "mismatch": mism, "ins": ins, "del": dele, **extra}
+            if not np.array_equal(vals[code], lp):
+                raise ValueError("phreds do not match the log error probabilities")
+            p10, match = tp10[code], tmatch[code]
+        else:
+            p10 = np.power(10.0, lp)
+            with np.errstate(divide="ignore"):
+                match = np.log10(1.0 - p10)
+            extra = {}
+        mism = lp + scores.mismatch
+        ins = lp + scores.insertion
+        # del (n + 1 per sequence) = max(left, right) + deletion with left / right the
+        # sequence's lp with its first / last element repeated: the ends are
+        # max(x, x) = x, the inside the neighbour maximum (rifrafsequences.jl:49-53)
+        left = np.insert(lp, off[:-1], lp[off[:-1]])
+        right = np.insert(lp, off[1:], lp[off[1:] - 1])
+        dele = np.maximum(left, right) + scores.deletion
+        est = np.empty(K)
+        try:
+            from . import _lib
+            _lib.load().rf_host_julia_sums(K, _lib.ptr(p10), _lib.ptr(np.ascontiguousarray(off, np.int64)),
+                                           _lib.ptr(est))
+        except Exception:  # noqa: BLE001 -- library absent (host-only use): the Python sum
+            est = np.array([julia_sum(p10[off[k]:off[k + 1]]) for k in range(K)])
+        return self_objects(cls, seqs, lp, match, mism, ins, dele, est, off, bandwidth), \
+            {"match": match, "mismatch": mism, "ins": ins, "del": dele, **extra}
 
     @classmethod
     def rescored(cls, other: "RifrafSequence", scores: Scores) -> "RifrafSequence":

@@ -3,7 +3,7 @@
 stage logic, batch = all 50 reads, quality scores on) over many 50 x 1.5 kb
 clusters, batched on one GPU with rifraf_batch, against the same runs on the
 CPU oracle engine.  Prints one JSON line.
-usage: scripts/e2e_batch.py [CLUSTERS] [CPU_CLUSTERS] [PROCS]
+usage: scripts/e2e_batch.py [CLUSTERS] [CPU_CLUSTERS] [PROCS] [native|hub]
 PROCS > 1: that many worker processes, each with its own engine context on
 GPU 0 and a contiguous share of the clusters (the reference's pmap workers,
 scripts/rifraf.jl:190); the host stage machine is the per-process limit."""
@@ -32,6 +32,7 @@ for k in range(nclu):
 gen_s = time.perf_counter() - t0
 
 nproc = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+native = (sys.argv[4] != "hub") if len(sys.argv) > 4 else None
 
 
 def _shard(args):
@@ -39,7 +40,7 @@ def _shard(args):
     from rifraf_amd.batch import STATS as st
     from rifraf_amd.engine import Engine
     e = Engine(0)
-    out = rifraf_batch(clusters[lo:hi], params=params, engine=e)
+    out = rifraf_batch(clusters[lo:hi], params=params, engine=e, native=native)
     e.close()
     return [(r.consensus, sum(r.state.stage_iterations)) for r in out], st["launches"], st["engine_s"]
 
@@ -48,7 +49,7 @@ if nproc <= 1:
     from rifraf_amd.engine import Engine  # noqa: E402
     eng = Engine(0)
     t0 = time.perf_counter()
-    res = rifraf_batch(clusters, params=params, engine=eng)
+    res = rifraf_batch(clusters, params=params, engine=eng, native=native)
     gpu_s = time.perf_counter() - t0
     cons = [r.consensus for r in res]
     iters = sum(sum(r.state.stage_iterations) for r in res)
@@ -76,4 +77,6 @@ if ncpu > 0:
 print(json.dumps({"workload": "c4-e2e", "clusters": nclu, "procs": nproc, "reads_per_cluster": 50, "template_len": 1500,
                   "gpu_clusters_per_s": nclu / gpu_s, "gpu_seconds": gpu_s, "stage_iterations": iters,
                   "consensus_equals_template": ok,
-                  "engine_calls": STATS["launches"], "engine_s": STATS["engine_s"], "setup_s": gen_s, "cpu_baseline": cpu}))
+                  "engine_calls": STATS["launches"], "engine_s": STATS["engine_s"], "native_s": STATS["native_s"],
+                  "score_phase_s": STATS["score_phase_s"], "setup_native_s": STATS["setup_native_s"], "upload_s": STATS["upload_s"], "driver": "hub" if native is False else "native-if-eligible",
+                  "setup_s": gen_s, "cpu_baseline": cpu}))

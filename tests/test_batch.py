@@ -89,3 +89,71 @@ def test_batch_hip_matches_oracle_runs(engine):
     got = rifraf_batch(clusters, params=params, engine=engine)
     for r, g in zip(ref, got):
         assert_same_run(summary(g), r)
+
+
+def _ref_free_clusters(seed=97):
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    out = []
+    for n, L, err in [(12, 150, 0.02), (20, 300, 0.01), (6, 90, 0.05), (1, 40, 0.02), (9, 220, 0.03),
+                      (30, 120, 0.02), (3, 400, 0.01), (15, 250, 0.04)]:
+        _, _, _, reads, _, phreds, _, _ = sample_sequences(n, L, error_rate=err, rng=rng)
+        out.append(dict(dnaseqs=reads, phreds=phreds))
+    return out
+
+
+NATIVE_PARAMS = {
+    "default": dict(max_iters=60),                                          # fixed batch of 5
+    "all_reads_qv": dict(batch_size=0, batch_fixed=False, do_score=True),
+    "fixed3_noaln": dict(batch_fixed_size=3, do_alignment_proposals=False, do_score=True, max_iters=4),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pset", sorted(NATIVE_PARAMS))
+def test_native_batch_matches_hub(engine, pset):
+    """rf_rifraf_batch (the library's lockstep stage machine) against the
+    Python stage machine over the same engine: identical consensus at every
+    iteration, score, iteration counts, convergence and QVs."""
+    from rifraf_amd import ErrorModel, Scores
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), **NATIVE_PARAMS[pset])
+    clusters = _ref_free_clusters()
+    hub = rifraf_batch(clusters, params=params, engine=engine, native=False)
+    nat = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    for a, b in zip(nat, hub):
+        assert_same_run(summary(a), summary(b))
+
+
+@pytest.mark.gpu
+def test_native_batch_matches_oracle_runs(engine):
+    """Native batched clusters against separate rifraf() runs on the CPU
+    oracle engine (reference-free clusters, quality scores on)."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd import ErrorModel, Scores
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams, rifraf
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), do_score=True, max_iters=60)
+    clusters = _ref_free_clusters(seed=5)[:5]
+    ref = [summary(rifraf(params=params, engine=OracleEngine(), **kw)) for kw in clusters]
+    got = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    for r, g in zip(ref, got):
+        assert_same_run(summary(g), r)
+
+
+def test_native_scope():
+    """Clusters with a reference, random resampling or an engine without the
+    native driver take the Python stage machine."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import native_eligible, rifraf_batch
+    from rifraf_amd.engine import RifrafError
+    from rifraf_amd.model import RifrafParams
+    clusters = _ref_free_clusters()
+    assert native_eligible(clusters, RifrafParams())
+    assert native_eligible(clusters, RifrafParams(batch_size=0, batch_fixed=False))
+    assert not native_eligible(clusters, RifrafParams(batch_size=4, batch_fixed=False))
+    assert not native_eligible(_clusters(), RifrafParams())          # references
+    assert not native_eligible(clusters, RifrafParams(do_init=False))
+    with pytest.raises(RifrafError):
+        rifraf_batch(clusters[:1], params=RifrafParams(max_iters=2), engine=OracleEngine(), native=True)

@@ -653,3 +653,15 @@ def test_row_code_dictionary_overflow():
         _check_bands(e, t, seqs, [bw] * nreads)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("stage_kb", [16, 262144])
+def test_set_sequences_staged_in_chunks(engine, opts, stage_kb):
+    """rf_set_sequences stages its tables in bounded chunks (RF_OPT_STAGE_KB):
+    with 16 KB chunks this upload of 40 reads spans many chunks; every read's
+    bands stay bit-exact (tables and row codes land in the right regions)."""
+    opts("stage_kb", stage_kb)
+    rng = np.random.default_rng(1601)
+    t = random_seq(300, rng)
+    seqs = [make_read(t, rng, 0.02, 9) for _ in range(40)]
+    _check_bands(engine, t, seqs, [9] * len(seqs))

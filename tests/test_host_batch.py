@@ -1,0 +1,125 @@
+"""Host-side batch helpers of the native batched driver (CPU): the vectorised
+RifrafSequence constructor, the library's Julia-order sums and the
+vectorised Poisson thresholds equal the per-sequence Python code bit for bit."""
+import math
+
+import numpy as np
+
+from rifraf_amd import ErrorModel, RifrafSequence, Scores
+from rifraf_amd.poisson import cquantile_poisson, cquantile_poisson_many
+from rifraf_amd.rifrafsequences import julia_sum
+
+
+def _reads(rng, n=300):
+    seqs, lps = [], []
+    for _ in range(n):
+        L = int(rng.choice([1, 2, 3, 15, 16, 17, 100, 1023, 1024, 1025, 1500, 2049, 4100]))
+        seqs.append(rng.integers(0, 4, L).astype(np.uint8))
+        if rng.random() < 0.5:
+            lps.append(rng.integers(0, 41, L).astype(np.int8))          # phreds
+        else:
+            lps.append(-rng.uniform(0.01, 4.0, L))
+    return seqs, lps
+
+
+def test_many_equals_per_sequence_constructor():
+    rng = np.random.default_rng(3)
+    seqs, lps = _reads(rng)
+    sc = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0))
+    got = RifrafSequence.many(seqs, lps, 9, sc)
+    for g, s, lp in zip(got, seqs, lps):
+        e = RifrafSequence(s, lp, 9, sc)
+        for f in ("seq", "error_log_p", "match_scores", "mismatch_scores", "ins_scores", "del_scores",
+                  "codon_ins_scores", "codon_del_scores"):
+            np.testing.assert_array_equal(getattr(g, f), getattr(e, f), err_msg=f)
+        assert g.est_n_errors == e.est_n_errors
+        assert g.bandwidth == e.bandwidth and g.bandwidth_fixed == e.bandwidth_fixed
+
+
+def test_many_concat_phred_tables():
+    """The per-distinct-Phred evaluation + gather equals the direct tables."""
+    from rifraf_amd.errormodel import phred_to_log_p
+    rng = np.random.default_rng(4)
+    ph = [rng.integers(0, 94, int(n)).astype(np.int8) for n in rng.integers(1, 3000, 40)]
+    seqs = [rng.integers(0, 4, len(p)).astype(np.uint8) for p in ph]
+    off = np.zeros(len(ph) + 1, np.int64)
+    np.cumsum([len(p) for p in ph], out=off[1:])
+    sc = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0))
+    cat = np.concatenate(ph)
+    a, ta = RifrafSequence.many_concat(seqs, phred_to_log_p(cat), off, 9, sc, phreds=cat)
+    b, tb = RifrafSequence.many_concat(seqs, phred_to_log_p(cat), off, 9, sc)
+    for k in tb:
+        np.testing.assert_array_equal(ta[k], tb[k])
+    for x, y, s, p in zip(a, b, seqs, ph):
+        e = RifrafSequence(s, p, 9, sc)
+        assert x.est_n_errors == y.est_n_errors == e.est_n_errors
+        np.testing.assert_array_equal(x.match_scores, e.match_scores)
+        np.testing.assert_array_equal(x.del_scores, e.del_scores)
+
+
+def test_host_sums_match_python():
+    from rifraf_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(9)
+    lens = rng.choice([0, 1, 2, 15, 16, 1024, 1025, 3000, 5000], 80)
+    off = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    v = rng.uniform(0, 1, int(off[-1])) ** 7
+    a, b = np.empty(len(lens)), np.empty(len(lens))
+    lib.rf_host_julia_sums(len(lens), _lib.ptr(v), _lib.ptr(off), _lib.ptr(a))
+    lib.rf_host_seq_sums(len(lens), _lib.ptr(v), _lib.ptr(off), _lib.ptr(b))
+    for k in range(len(lens)):
+        seg = v[off[k]:off[k + 1]]
+        assert a[k] == julia_sum(seg)
+        assert b[k] == (float(np.cumsum(seg)[-1]) if len(seg) else 0.0)
+
+
+def test_poisson_thresholds_vectorised():
+    rng = np.random.default_rng(2)
+    lams = np.concatenate([rng.uniform(0.01, 400, 3000), rng.uniform(0.001, 2, 500), np.arange(1, 401.0)])
+    for p in (0.1, 0.01, 0.5):
+        np.testing.assert_array_equal(cquantile_poisson_many(lams, p),
+                                      [cquantile_poisson(float(x), p) for x in lams])
+    assert math.isnan(cquantile_poisson_many(np.array([math.nan]), 0.1)[0])
+
+
+def test_qvs_many_equals_per_cluster():
+    """The stacked QV post-processing equals estimate_probs_from_dense and
+    aln_error_probs_from_sums cluster by cluster, bit for bit."""
+    from types import SimpleNamespace
+
+    from rifraf_amd.model import aln_error_probs_from_sums, estimate_probs_from_dense, qvs_many
+    rng = np.random.default_rng(8)
+    states, dense, sums = [], [], []
+    for m in rng.integers(1, 400, 30):
+        cons = rng.integers(0, 4, m).astype(np.uint8)
+        score = -float(rng.uniform(50, 500))
+        d = score + rng.uniform(-30, 2, (m + 1, 9))
+        d[0, :5] = np.nan
+        states.append(SimpleNamespace(consensus=cons, score=score))
+        dense.append(d)
+        sums.append(-rng.uniform(0, 60, (m, 4)))
+    got = qvs_many(states, dense, sums)
+    for st, d, sm, (ep, ap) in zip(states, dense, sums, got):
+        e = estimate_probs_from_dense(st, d)
+        np.testing.assert_array_equal(ep.sub, e.sub)
+        np.testing.assert_array_equal(ep.dele, e.dele)
+        np.testing.assert_array_equal(ep.ins, e.ins)
+        np.testing.assert_array_equal(ap, aln_error_probs_from_sums(sm))
+
+
+def test_logsumexp10_table_path():
+    from rifraf_amd.batch import _logsumexp10_many
+    from rifraf_amd.errormodel import phred_to_log_p
+    from rifraf_amd.model import logsumexp10
+    rng = np.random.default_rng(6)
+    ph = [rng.integers(0, 60, int(n)).astype(np.int8) for n in rng.integers(1, 2000, 50)]
+    seqs = [rng.integers(0, 4, len(p)).astype(np.uint8) for p in ph]
+    off = np.zeros(len(ph) + 1, np.int64)
+    np.cumsum([len(p) for p in ph], out=off[1:])
+    cat = np.concatenate(ph)
+    objs, tabs = RifrafSequence.many_concat(seqs, phred_to_log_p(cat), off, 9,
+                                            Scores.from_errors(ErrorModel(1.0, 2.0, 2.0)), phreds=cat)
+    a = _logsumexp10_many(tabs["match"], off, codes=tabs["code"], table=tabs["match_table"])
+    b = _logsumexp10_many(tabs["match"], off)
+    assert a == b == [logsumexp10(o.match_scores) for o in objs]
