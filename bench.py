@@ -260,6 +260,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="c4 only: skip the secondary c5 (10 kb, band doubling) workload")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--e2e-clusters", type=int, default=256,
+                    help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     args = ap.parse_args()
@@ -286,6 +288,8 @@ def main():
         result = run_read_sharded(args, rank, world, gpu, dist, torch, coll)
     else:
         result = run_clusters(args, rank, world, gpu, dist, torch, coll)
+        if args.config == "c4" and args.e2e_clusters > 0:
+            result["e2e"] = run_e2e(args, rank, world, gpu, dist, coll)
         if args.config == "c4" and not args.no_secondary:
             # configs[4] beside the headline line: driver-measured 10 kb reads
             # with band doubling, read-sharded over the same ranks
@@ -294,6 +298,50 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_e2e(args, rank, world, gpu, dist, coll):
+    """Whole rifraf() runs on the c4 cluster shape (SURVEY.md §8(d) config 4:
+    every read in each batch, quality scores on) through rifraf_batch on this
+    rank's GPU -- the native lockstep stage machine (rf_rifraf_batch) in one
+    process.  clusters_per_s = all ranks' clusters / the slowest rank's
+    wall time (host setup from reads included, read simulation excluded).
+    Two clusters are re-run through the Python stage machine (the reference
+    restatement) and must match exactly."""
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.engine import Engine
+    from rifraf_amd.model import RifrafParams
+    from rifraf_amd.sample import sample_sequences
+    n = args.e2e_clusters
+    clusters, templates = [], []
+    for k in range(n):
+        _, t, _, reads, _, phreds, _, _ = sample_sequences(
+            50, 1500, error_rate=0.01, rng=np.random.default_rng([args.seed, 77, rank, k]))
+        clusters.append(dict(dnaseqs=reads, phreds=phreds))
+        templates.append(t)
+    params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
+    eng = Engine(gpu)
+    rifraf_batch(clusters[:4], params=params, engine=eng)          # warm-up (kernels, pinned staging)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = rifraf_batch(clusters, params=params, engine=eng)
+    elapsed = time.perf_counter() - t0
+    ref = rifraf_batch(clusters[:2], params=params, engine=eng, native=False)
+    same = all(np.array_equal(a.consensus, b.consensus) and a.state.score == b.state.score and
+               np.array_equal(a.aln_error_probs, b.aln_error_probs) for a, b in zip(res[:2], ref))
+    eng.close()
+    ok = sum(int(np.array_equal(r.consensus, t)) for r, t in zip(res, templates))
+    iters = sum(sum(r.state.stage_iterations) for r in res)
+    tot = [float(n), float(ok), float(iters), 1.0 if same else 0.0]
+    if dist is not None:
+        elapsed, tot = aggregate(elapsed, tot, coll)
+    return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": tot[0] / elapsed,
+            "clusters": int(tot[0]), "seconds": elapsed, "processes_per_gpu": 1,
+            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass",
+            "params": "batch = all 50 reads, do_score (QVs), no reference",
+            "consensus_equals_template": int(tot[1]), "stage_iterations": int(tot[2]),
+            "same_as_python_stage_machine": tot[3] == world}
 
 
 def _sync_fn(torch):

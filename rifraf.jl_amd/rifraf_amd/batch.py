@@ -306,14 +306,14 @@ def _wave_native(part, params, engine):
     phred_in = all(kw.get("error_log_ps") is None for kw in part)
     for kw in part:                                                 # rifraf(), model.jl:1276-1287
         if phred_in:
-            if any(np.min(p) < 0 for p in kw["phreds"]):
-                raise RifrafError("phred score cannot be negative")
             all_lp += list(kw["phreds"])
         else:
             elp = kw.get("error_log_ps")
             all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
         all_s += [DNASeq(x) for x in kw["dnaseqs"]]
         nread.append(len(kw["dnaseqs"]))
+    if phred_in and all_lp and min(int(np.min(p)) for p in all_lp if len(p)) < 0:
+        raise RifrafError("phred score cannot be negative")
     lens = np.array([len(x) for x in all_s], np.int64)
     if (lens == 0).any() or any(len(x) != len(y) for x, y in zip(all_s, all_lp)):
         raise RifrafError("empty read or length mismatch")

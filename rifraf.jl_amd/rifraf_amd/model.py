@@ -636,6 +636,22 @@ def estimate_probs_from_dense(state: RifrafState, dense) -> EstimatedProbs:
     return normalize_log_differences(sub_scores, del_scores, ins_scores, state.score - max_score)
 
 
+def _power10(x):
+    """np.power(10.0, x) over row blocks on host threads (numpy drops the GIL
+    inside a ufunc; each element's value is the same whichever block holds it)."""
+    x = np.ascontiguousarray(x)
+    if x.size < (1 << 20):
+        return np.power(10.0, x)
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.empty_like(x)
+    nth = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    cut = np.linspace(0, len(x), nth + 1).astype(int)
+    with ThreadPoolExecutor(nth) as ex:
+        list(ex.map(lambda t: np.power(10.0, x[cut[t]:cut[t + 1]], out=out[cut[t]:cut[t + 1]]), range(nth)))
+    return out
+
+
 def qvs_many(states, dense, sums):
     """estimate_probs_from_dense and aln_error_probs_from_sums for many
     clusters at once: every cluster's arrays are stacked and each numpy
@@ -674,12 +690,12 @@ def qvs_many(states, dense, sums):
                           "insertion scores cannot be positive")
     mrow = np.repeat(mxa, ms)
     # normalize_log_differences (model.jl:722-735)
-    pos_exp = np.power(10.0, np.hstack([S - mrow[:, None], (Dl - mrow)[:, None]]))
+    pos_exp = _power10(np.hstack([S - mrow[:, None], (Dl - mrow)[:, None]]))
     pos_probs = pos_exp / pos_exp.sum(axis=1, keepdims=True)
-    ins_exp = np.power(10.0, I - np.repeat(mxa, ms + 1)[:, None])
+    ins_exp = _power10(I - np.repeat(mxa, ms + 1)[:, None])
     st_pow = np.repeat(np.array([10.0 ** (st.score - mx[k]) for k, st in enumerate(states)]), ms + 1)
     ins_probs = ins_exp / (st_pow[:, None] + ins_exp.sum(axis=1, keepdims=True))
-    A = np.power(10.0, np.concatenate([np.asarray(x) for x in sums]))   # alignment_error_probs
+    A = _power10(np.concatenate([np.asarray(x) for x in sums]))         # alignment_error_probs
     aln = 1.0 - (A / A.sum(axis=1, keepdims=True)).max(axis=1)
     out = []
     for k in range(K):

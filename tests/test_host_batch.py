@@ -123,3 +123,9 @@ def test_logsumexp10_table_path():
     a = _logsumexp10_many(tabs["match"], off, codes=tabs["code"], table=tabs["match_table"])
     b = _logsumexp10_many(tabs["match"], off)
     assert a == b == [logsumexp10(o.match_scores) for o in objs]
+
+
+def test_threaded_power10_is_elementwise():
+    from rifraf_amd.model import _power10
+    x = -np.random.default_rng(12).uniform(0, 40, (700_001, 3))
+    np.testing.assert_array_equal(_power10(x), np.power(10.0, x))
