@@ -65,10 +65,11 @@ def band_cells(n: int, m: int, bw: int) -> int:
     return int(np.sum(stop - start + 1))
 
 
-def band_bytes(n: int, m: int, bw: int) -> int:
-    """Device bytes of one kappa-major band (rifraf_hip.hip band_K x band_P, 256-B aligned)."""
+def band_bytes(n: int, m: int, bw: int, pad: bool = False) -> int:
+    """Device bytes of one kappa-major band (rifraf_hip.hip band_K x band_stride, 256-B aligned)."""
+    from rifraf_amd.bandedarrays import band_stride
     H = 2 * bw + abs(n - m) + 1
-    P = ((H + 1) >> 1) | 1
+    P = band_stride(H, pad_h=1 if pad else 0)
     return ((H + 2 * m) * P * 8 + 255) // 256 * 256
 
 
@@ -523,7 +524,7 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     # bw and 2*bw; the timed context is then sized exactly for A + B at the
     # final bandwidths (an arena that grows by compaction needs old + new)
     eng = Engine(local)
-    eng.reserve(sum(band_bytes(len(r), length, bw) + band_bytes(len(r), length, 2 * bw) for r in reads)
+    eng.reserve(sum(band_bytes(len(r), length, bw) + band_bytes(len(r), length, 2 * bw, pad=True) for r in reads)
                 + (256 << 20))
     for a in range(0, nloc, 1024):
         eng.set_sequences(a, reads[a:a + 1024])
@@ -541,7 +542,9 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     aln_ms = eng.last_backtrace_ms()
     eng.close()
     eng = Engine(local)
-    eng.reserve(sum(2 * band_bytes(len(r), length, r.bandwidth) for r in reads) + (256 << 20))
+    from rifraf_amd.bandedarrays import BAND_PAD_H
+    pad = max(2 * r.bandwidth + abs(len(r) - length) + 1 for r in reads) >= BAND_PAD_H   # one realign call
+    eng.reserve(sum(2 * band_bytes(len(r), length, r.bandwidth, pad) for r in reads) + (256 << 20))
     for a in range(0, nloc, 1024):
         eng.set_sequences(a, reads[a:a + 1024])
     eng.set_templates(0, [t])

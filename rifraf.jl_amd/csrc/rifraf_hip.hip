@@ -30,6 +30,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -66,6 +67,15 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 #endif
 
 __host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
+// Row stride of a band as allocated: H >= pad_h (> 0) gives rows of a whole
+// number of 128-B lines, so that the wide-band scorer's 32-diagonal segments
+// read exactly one line per kappa row (k_score_segl); else the odd stride.
+// rf_realign pads every band of a call whose widest band has H >=
+// RF_OPT_BAND_PAD (pad_h 1 for the call), none otherwise.
+inline int band_stride(int H, int pad_h)
+{
+    return (pad_h > 0 && H >= pad_h) ? (((H + 1) >> 1) + 15) & ~15 : band_P(H);
+}
 __host__ __device__ inline int64_t band_K(int H, int m) { return (int64_t)H + 2 * (int64_t)m; }
 
 __device__ __forceinline__ size_t bidx(int d, int jj, int P)
@@ -2013,7 +2023,7 @@ k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ g
 // the rows of even and odd local index live in two regions, so the 64 lanes
 // of a step (kappa rows two apart) read consecutive rows of one region:
 // row stride 2C doubles, a 2-way bank conflict for odd C.  Row r's first
-// wanted element sits at offset (kb + r + e0) & 1 (P odd).
+// wanted element sits at offset ((kb + r) * P + e0) & 1.
 // ---------------------------------------------------------------------
 template <int S>
 struct SegcGeo {
@@ -2155,7 +2165,7 @@ k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 continue;
             const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
             // element (kappa, d >> 1): local row r = kappa - kb in region r & 1
-            const int sh0 = (kb + e0) & 1, sh1 = (kb + 1 + e0) & 1;
+            const int sh0 = (kb * (P & 1) + e0) & 1, sh1 = ((kb + 1) * (P & 1) + e0) & 1;
             auto at = [&](int kap, int d) {
                 const int rr = kap - kb;
                 return (rr & 1) * RS + (rr >> 1) * (2 * C) + ((rr & 1) ? sh1 : sh0) + (d >> 1) - e0;
@@ -2217,6 +2227,387 @@ k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             const double qnan = __builtin_nan("");
             if (split_mode & 1) {
                 // this read's partials (k_reduce folds the reads in batch order)
+                double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+                if (a < m) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                    dst[13] = dd;
+                }
+                if (a == 0) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        dst[k] = qnan;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+                    tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+                }
+                tD += dd;
+            }
+        }
+    }
+    if (!active || (split_mode & 1))
+        return;
+    const double qnan = __builtin_nan("");
+    double *dst = dense + G.dense_off + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[5 + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[9 + k] = tS[k];
+        dst[13] = tD;
+    }
+    if (a == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
+// ---------------------------------------------------------------------
+// k_score_segl: the wide-band scorer over line-aligned band rows (default)
+//
+// Same chains, operands, order and FP64 max-plus as k_score_seg / segc
+// (identical results).  Segments are 32 band diagonals [D, D+32) with D a
+// multiple of 32, so a kappa row's piece of a segment is elements
+// [D/2, D/2 + 16): exactly one 128-B line when the band's rows are padded to
+// whole lines (band_stride, P % 16 == 0; band regions are 256-B aligned) --
+// no line is shared by two segments, so each is fetched once.  Bands with the
+// odd stride (H below RF_OPT_BAND_PAD) take 9 pair-aligned 16-B chunks per
+// row instead.  The wave's 65 columns [a0, a0+64] touch kappa rows
+// [D + 2*a0, D + 2*a0 + 160).
+//
+// LDS holds the segment transposed: slot (d - D + 1) * 65 + (a - a0) for
+// d in [D-1, D+32) (row 0 is the previous segment's last diagonal), so lane
+// a's operands at step d -- A(d, a), B(d, a), B(d-1, a+1) -- are one
+// consecutive 512-B run per wave-instruction at an immediate offset, and the
+// table records of read row i = a - c + d (three 16-B arrays) likewise.
+// The next segment's lines are loaded into registers while this one is
+// scored.
+// ---------------------------------------------------------------------
+#ifndef SEGL_UNROLL
+#define SEGL_UNROLL 32
+#endif
+#ifndef SEGL_FENCE_KIND
+#define SEGL_FENCE_KIND 0
+#endif
+#if SEGL_FENCE_KIND == 1
+#define SEGL_FENCE() asm volatile("" ::: "memory")
+#elif SEGL_FENCE_KIND == 2
+#define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0x0006)   // VALU and SALU may cross
+#else
+#define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+struct SeglGeo {
+    static constexpr int S = 32;        // diagonals per segment
+    static constexpr int LS = 65;       // LDS row: columns a0 .. a0+64
+    static constexpr int NRW = S + 1;   // LDS rows: d = D-1 .. D+31
+    static constexpr int NROW = S + 128;   // kappa rows per segment
+    static constexpr int NUA = NROW * 8 / 64;        // 16-B chunks per lane and band, aligned rows
+    static constexpr int NUG = (NROW * 9 + 63) / 64; // odd-stride rows (9 chunks)
+    static constexpr int NT = S + 65;   // table rows: i - ib in [0, 97)
+};
+
+__global__ void __launch_bounds__(64)
+k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+             const double *__restrict__ tabs, const double *__restrict__ bands,
+             double *__restrict__ dense, double *__restrict__ split, int split_mode, int rchunk)
+{
+    using Gm = SeglGeo;
+    constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
+    constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
+    __shared__ __attribute__((aligned(16))) double sA[SL];
+    __shared__ __attribute__((aligned(16))) double sB[SL];
+    __shared__ __attribute__((aligned(16))) dvec2 sT0[NT], sT1[NT], sT2[NT];
+    const int nx = gridDim.x;
+    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
+    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
+    const int cell = x * xq + min(x, xr) + (lin >> 3);
+    const int bx = cell % nx, by = cell / nx;
+    const WorkItem wi = items[bx];
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int tid = threadIdx.x;
+    const int a = a0 + tid;
+    const bool active = a <= m;
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + by * rchunk;
+        if (r0 >= G.r1)
+            return;
+        r1 = min(r0 + rchunk, G.r1);
+    }
+    const bool hasS = a < m;
+    const double smask = hasS ? 0.0 : -RF_INF;
+    const bool wave_s = __all(hasS);   // every lane has a Substitution column
+    double tI[4], tS[4], tD = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tI[k] = 0.0;
+        tS[k] = 0.0;
+    }
+    // aligned-row loader lane roles: row r8 + 8j, 16-B chunk cc of the line
+    const int r8 = tid >> 3, cc8 = tid & 7, p8 = r8 & 1;
+    for (int r = r0; r < r1; ++r) {
+        const ScoreRead R = reads[r];
+        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
+        const int jn = min(a + 1, m);
+        const int i0 = max(0, jn - c);
+        const int i1 = min(jn + vb, n);
+        const int ilast = min(i1, a + vb);
+        const int dfirst = i0 - a + c, dlast = ilast - a + c;
+        const bool peel = i1 > ilast;
+        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
+        int dfmax = active ? dfirst : INT_MAX, dlmin = active ? dlast : -1;
+        for (int off = 32; off >= 1; off >>= 1) {
+            dlo = min(dlo, __shfl_xor(dlo, off));
+            dhi = max(dhi, __shfl_xor(dhi, off));
+            dfmax = max(dfmax, __shfl_xor(dfmax, off));
+            dlmin = min(dlmin, __shfl_xor(dlmin, off));
+        }
+        dlo = __builtin_amdgcn_readfirstlane(dlo);
+        dhi = __builtin_amdgcn_readfirstlane(dhi);
+        dfmax = __builtin_amdgcn_readfirstlane(dfmax);
+        dlmin = __builtin_amdgcn_readfirstlane(dlmin);
+        if (dlo > dhi)
+            continue;
+        const bool aligned = (P & 15) == 0;        // wave-uniform
+        const bool all_act = __all(active) && wave_s;
+        const double *gA = bands + R.A;
+        const int64_t dB = R.B - R.A;
+        const double *tm = tabs + R.tab;
+        const uint8_t *sq = bases + R.sb;
+        double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            prev[k] = -RF_INF;
+            accI[k] = -RF_INF;
+            accS[k] = -RF_INF;
+        }
+        dvec2 ra[NUA], rb[NUA];
+        double tmt[2], tmm[2], tin[2], tdl[2];
+        int tsb[2];
+        auto load_seg = [&](int D) {
+            const int kb = D + 2 * a0, eh = D >> 1;
+            if (aligned) {
+                // prefetched into registers while the current segment is scored
+#pragma unroll
+                for (int j = 0; j < NUA; ++j) {
+                    const int kap = min(kb + r8 + 8 * j, K - 1);
+                    const int64_t g = (int64_t)kap * P + eh + 2 * cc8;
+                    ra[j] = *(const dvec2 *)(gA + g);
+                    rb[j] = *(const dvec2 *)(gA + dB + g);
+                }
+            }
+            const int ib = a0 - c + D;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int i = min(max(ib + tid + 64 * u, 0), n);
+                const int ks = max(i - 1, 0);
+                tsb[u] = sq[ks];   // read row 0 (the gap) is selected at the store
+                tmt[u] = tm[ks];
+                tmm[u] = tm[n + ks];
+                tin[u] = tm[2 * (size_t)n + ks];
+                tdl[u] = tm[3 * (size_t)n + i];
+            }
+        };
+        auto store_seg = [&](int D) {
+            if (aligned) {
+#pragma unroll
+                for (int j = 0; j < NUA; ++j) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
+                        const int col = (r8 + 8 * j - ddl) >> 1;    // a - a0
+                        const double v = h ? ra[j].y : ra[j].x, w = h ? rb[j].y : rb[j].x;
+                        const int l = (ddl + 1) * LS + col;
+                        // rows 32..127 always land in [0, 64]; the parallelogram's
+                        // first / last 32 rows hold cells of the neighbouring items
+                        if ((j >= 4 && j < NUA - 4) || (col >= 0 && col <= 64)) {
+                            sA[l] = v;
+                            sB[l] = w;
+                        }
+                    }
+                }
+            } else {
+                // odd-stride rows (narrow bands in a wide launch): 9 pair-aligned
+                // chunks per row, loaded here in groups of 4 (not prefetched)
+                const int kb = D + 2 * a0, eh = D >> 1;
+#pragma unroll 1
+                for (int j0 = 0; j0 < NUG; j0 += 4) {
+                    dvec2 ga[4], gb[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int t = min(tid + 64 * (j0 + jj), Gm::NROW * 9 - 1);
+                        const int rr = (t * 7282) >> 16, cc = t - 9 * rr;   // t / 9 for t < 1440
+                        const int kap = min(kb + rr, K - 1);
+                        const int g = ((kap * P + eh) & ~1) + 2 * cc;
+                        ga[jj] = *(const dvec2 *)(gA + g);
+                        gb[jj] = *(const dvec2 *)(gA + dB + g);
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int t = tid + 64 * (j0 + jj);
+                        const int rr = (t * 7282) >> 16, cc = t - 9 * rr;
+                        const int sh = (kb + rr + eh) & 1;   // P odd
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int xl = 2 * cc + h - sh;
+                            const int ddl = 2 * xl + (rr & 1);
+                            const int col = (rr - ddl) >> 1;
+                            if (t < Gm::NROW * 9 && xl >= 0 && xl < 16 && col >= 0 && col <= 64) {
+                                const int l = (ddl + 1) * LS + col;
+                                sA[l] = h ? ga[jj].y : ga[jj].x;
+                                sB[l] = h ? gb[jj].y : gb[jj].x;
+                            }
+                        }
+                    }
+                }
+                // nothing of this path stays in flight: hipcc's wait analysis
+                // merges paths, and a load it saw pending here would make it
+                // drain the next segment's prefetch before the chains
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            const int ib = a0 - c + D;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = tid + 64 * u;
+                if (t < NT) {
+                    const int sb = ib + t >= 1 ? tsb[u] : 4;
+                    const double mt = tmt[u], mm = tmm[u];
+                    sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
+                    sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
+                    sT2[t] = dvec2{tin[u], tdl[u]};
+                }
+            }
+        };
+        const int D0 = dlo & ~(S - 1);
+        if (!(split_mode & 4))
+            load_seg(D0);
+        for (int D = D0; D <= dhi; D += S) {
+            wave_sync();   // previous segment's chains are done with LDS
+            // LDS row 0 = diagonal D-1: the previous segment's row 32, or gathered
+            if (D == D0) {
+                if (D > 0) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int t = tid + 64 * u;
+                        if (t <= 64) {
+                            const int kap = min(D - 1 + 2 * (a0 + t), K - 1);
+                            const int64_t g = (int64_t)kap * P + ((D - 1) >> 1);
+                            sA[t] = gA[g];
+                            sB[t] = gA[dB + g];
+                        }
+                    }
+                    __builtin_amdgcn_s_waitcnt(0);   // as after the odd-stride loader
+                }
+            } else {
+                const double va = sA[S * LS + tid], vbv = sB[S * LS + tid];
+                const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
+                sA[tid] = va;
+                sB[tid] = vbv;
+                if (tid == 0) {
+                    sA[64] = va6;
+                    sB[64] = vb6;
+                }
+            }
+            store_seg(D);
+            wave_sync();
+            if (D + S <= dhi && !(split_mode & 4))
+                load_seg(D + S);
+            if (!active || (split_mode & 2))
+                continue;
+            const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
+            const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];   // unconditional read, then select
+            double aprev = (lo <= hi && lo >= 1 && a - c + lo >= 1) ? a0v : -RF_INF;
+            const double *pA = sA + LS + tid;    // row 1 = diagonal D
+            const double *pB = sB + LS + tid;
+            const double *pS = sB + tid + 1;     // B(d-1, a+1): row d - D, column + 1
+            const dvec2 *q0 = sT0 + tid, *q1 = sT1 + tid, *q2 = sT2 + tid;
+            // operands of step s; the next step's are read from LDS while this
+            // one is scored (software pipeline: a read right before its use
+            // exposes the LDS latency on every step at one wave per SIMD)
+            struct Ops {
+                double ac, bI, bs;
+                dvec2 u0, u1, u2;
+            };
+            auto ld = [&](int s) {
+                Ops o;
+                o.ac = pA[s * LS];
+                o.bI = pB[s * LS];
+                o.bs = pS[s * LS];   // in range for every lane
+                o.u0 = q0[s];
+                o.u1 = q1[s];
+                o.u2 = q2[s];
+                return o;
+            };
+            // ALLS: every lane has a Substitution column (hasS; smask = 0)
+            auto step = [&](const Ops &o, auto alls) {
+                const double bS = ((decltype(alls)::value || hasS) ? o.bs : o.bI) + smask;
+                const double sub[4] = {o.u0.x, o.u0.y, o.u1.x, o.u1.y};
+                const double dl = o.ac + o.u2.y;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double best = vmax(vmax(aprev + sub[k], prev[k] + o.u2.x), dl);
+                    prev[k] = best;
+                    accI[k] = vmax(accI[k], best + o.bI);
+                    accS[k] = vmax(accS[k], best + bS);
+                }
+                dd = vmax(dd, o.ac + bS);
+                aprev = o.ac;
+            };
+            if (all_act && dfmax <= D && dlmin >= D + S - 1) {
+                // every lane scores all 32 diagonals (no peel inside: dlast >= D+31);
+                // all_act includes wave_s, so the bS select is the identity
+                Ops cur = ld(0);
+#pragma unroll SEGL_UNROLL
+                for (int s = 0; s < S; ++s) {
+                    const Ops nxt = ld(s + 1 < S ? s + 1 : s);
+                    // keep the reads ahead of this step's chain (hipcc's scheduler
+                    // otherwise sinks them next to their use); the arithmetic may
+                    // still move across (a full sched_barrier costs hazard nops)
+                    SEGL_FENCE();
+                    step(cur, std::true_type{});
+                    cur = nxt;
+                }
+            } else {
+                const int slo = max(lo - D, 0), shi = hi - D;
+                if (slo <= shi) {
+                    Ops cur = ld(slo);
+                    for (int s = slo; s <= shi; ++s) {
+                        const Ops nxt = ld(s < shi ? s + 1 : s);
+                        SEGL_FENCE();
+                        step(cur, std::false_type{});
+                        cur = nxt;
+                    }
+                }
+                const int dp = dlast + 1;
+                if (peel && dp >= D && dp < D + S) {
+                    // last row of the new column lies below A/B column a's band (a < m)
+                    const int sp = dp - D;
+                    const double ap = sA[sp * LS + tid];
+                    const double bSr = sB[sp * LS + tid + 1];
+                    const dvec2 u0 = sT0[tid + sp], u1 = sT1[tid + sp], u2 = sT2[tid + sp];
+                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        accS[k] = vmax(accS[k], vmax(ap + sub[k], prev[k] + u2.x) + bSr);
+                }
+            }
+        }
+        if (active) {
+            const double qnan = __builtin_nan("");
+            if (split_mode & 1) {
                 double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -2950,6 +3341,7 @@ struct TplObj {
 struct Band {
     bool valid = false;
     int32_t seq = -1, tpl = -1, bw = 0, n = 0, m = 0, H = 0, flags = 0;
+    int32_t P = 0;   // kappa row stride (band_stride at the fill)
     uint64_t tplver = 0;
     Region r;
 };
@@ -3080,7 +3472,9 @@ struct Opts {
     int seg_s = 24;         // RF_OPT_SEG_S: k_score_seg diagonals per segment (16, 24, 32)
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
-    int seg_ver = 3;        // RF_OPT_SEG_VER: wide-band scorer 3 = k_score_segc, 1 = k_score_seg
+    int seg_ver = 4;        // RF_OPT_SEG_VER: wide-band scorer 4 = k_score_segl, 3 = k_score_segc, 1 = k_score_seg
+    int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
+                            // 128-B-line rows for all its bands (0: never, 1: always)
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
     int bt_win_kb = 16;     // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS)
     int stage_kb = 262144;  // RF_OPT_STAGE_KB: rf_set_sequences staging chunk (KB of tables)
@@ -3350,6 +3744,7 @@ void load_env_opts(Opts &o)
     o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
     o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
     o.bt_win_kb = env_int("RIFRAF_BT_WIN_KB", o.bt_win_kb);
+    o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3418,7 +3813,15 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
         sm |= 4;
 #endif
     dim3 grid(nitems, gy);
-    if (pk.seg && ctx->opt.seg_ver == 3) {
+    if (pk.seg && ctx->opt.seg_ver == 4) {
+        int rchunk = 1;
+        if (split) {
+            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
+            grid.y = (gy + rchunk - 1) / rchunk;
+        }
+        hipLaunchKernelGGL(k_score_segl, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
+                           d_bands, dense, split, sm, rchunk);
+    } else if (pk.seg && ctx->opt.seg_ver == 3) {
         int rchunk = 1;
         if (split) {
             rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
@@ -3586,6 +3989,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SEG_VER: return &o.seg_ver;
     case RF_OPT_BT_WIN_KB: return &o.bt_win_kb;
     case RF_OPT_STAGE_KB: return &o.stage_kb;
+    case RF_OPT_BAND_PAD: return &o.band_pad_h;
     default: return nullptr;
     }
 }
@@ -3960,6 +4364,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (maxslot >= (int32_t)ctx->slots.size())
             ctx->slots.resize(maxslot + 1);
         bool moved = false;   // a band now describes another alignment
+        // RF_OPT_BAND_PAD: a call whose widest band reaches the threshold lays out
+        // all its bands with line-padded rows (the wide-band scorer reads them a
+        // line per row); narrower calls (c4-like) keep the odd stride, which the
+        // window scorer k_score_ws stages in fewer passes
+        int hmax_call = 0;
+        for (int32_t k = 0; k < njobs; ++k)
+            hmax_call = std::max(hmax_call, band_rows(ctx->seqs[seq[k]].n + 1, ctx->tpls[tpl[k]].m + 1, bw[k]));
+        const bool pad_call = ctx->opt.band_pad_h > 0 && hmax_call >= ctx->opt.band_pad_h;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
                 continue;
@@ -3968,11 +4380,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const TplObj &T = ctx->tpls[tpl[k]];
                 Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
                 const int H = band_rows(S.n + 1, T.m + 1, bw[k]);
-                if (int e = region_ensure(ctx, ctx->band_arena, b.r,
-                                          band_K(H, T.m) * band_P(H) * 8))
+                const int P = band_stride(H, pad_call ? 1 : 0);
+                if (int e = region_ensure(ctx, ctx->band_arena, b.r, band_K(H, T.m) * P * 8))
                     return e;
                 moved = moved || !b.valid || b.seq != seq[k] || b.tpl != tpl[k] || b.bw != bw[k] ||
-                        b.n != S.n || b.m != T.m || b.H != H;
+                        b.n != S.n || b.m != T.m || b.H != H || b.P != P;
+                b.P = P;
                 b.valid = true;
                 b.seq = seq[k];
                 b.tpl = tpl[k];
@@ -4041,7 +4454,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // out_score: forward scores win when both directions run
                 t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
-                t.P = band_P(t.H);
+                t.P = b.P;
                 // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4, 8), lean when
                 // there are no codon moves and no skew / trim; k_dp beyond
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
@@ -4301,7 +4714,7 @@ static int build_bt_tasks(rf_ctx *ctx, int32_t nslots, const int32_t *slot, std:
         t.ncdel = S.ncdel;
         t.flags = (b.flags & RF_SKEW ? 2 : 0) | (b.flags & RF_TRIM ? 4 : 0);
         t.idx = k;
-        t.P = band_P(b.H);
+        t.P = b.P;
         t.mask = 0;
         offs[k] = total;
         total += b.n + b.m;
@@ -4484,7 +4897,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             R.H = A.H;
             R.c = std::max(A.m - A.n, 0) + A.bw;
             R.vb = std::max(A.n - A.m, 0) + A.bw;
-            R.P = band_P(A.H);
+            R.P = A.P;
             R.K = (int32_t)band_K(A.H, A.m);
             reads.push_back(R);
         }
@@ -4545,7 +4958,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                 t.H = A.H;
                 t.ncins = S.ncins;
                 t.ncdel = S.ncdel;
-                t.P = band_P(A.H);
+                t.P = A.P;
                 t.kind = kd;
                 t.pos = ps;
                 t.base = b;
@@ -4745,7 +5158,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
                 R.H = A.H;
                 R.c = std::max(A.m - A.n, 0) + A.bw;
                 R.vb = std::max(A.n - A.m, 0) + A.bw;
-                R.P = band_P(A.H);
+                R.P = A.P;
                 R.K = (int32_t)band_K(A.H, A.m);
                 reads.push_back(R);
             }
@@ -4857,7 +5270,7 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     if (!b.valid)
         return fail(ctx, RF_ERR_STATE, "rf_download_band: band not computed");
     // kappa-major device layout -> the reference's column-major data
-    const int P = band_P(b.H);
+    const int P = b.P;
     const int64_t K = band_K(b.H, b.m);
     std::vector<double> buf((size_t)K * P);
     HIPCHK(ctx, hipMemcpyAsync(buf.data(), ctx->band_arena.d + b.r.off, buf.size() * 8,

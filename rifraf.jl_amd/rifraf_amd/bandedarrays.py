@@ -15,6 +15,20 @@ def ndatarows(nrows: int, ncols: int, bandwidth: int) -> int:   # :101-104
     return 2 * bandwidth + abs(nrows - ncols) + 1
 
 
+BAND_PAD_H = 64   # RF_OPT_BAND_PAD default (rifraf_hip.hip band_stride / rf_realign)
+
+
+def band_stride(H, pad_h: int = BAND_PAD_H):
+    """Row strides (doubles) of the device bands of ONE rf_realign call with
+    band heights H: whole 128-B lines for every band when the call's widest
+    band reaches pad_h (> 0; 1 = always), else the odd stride ceil(H/2) | 1."""
+    H = np.asarray(H)
+    half = (H + 1) >> 1
+    pad = pad_h > 0 and H.size > 0 and int(H.max()) >= pad_h
+    out = (half + 15) & ~15 if pad else half | 1
+    return int(out) if out.ndim == 0 else out
+
+
 def bandlimits(nrows: int, ncols: int, bandwidth: int):          # :44-53
     if ncols > nrows:
         return nrows - ncols - bandwidth, bandwidth

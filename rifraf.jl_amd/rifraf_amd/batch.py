@@ -26,6 +26,7 @@ import time
 
 import numpy as np
 
+from .bandedarrays import band_stride
 from .engine import RifrafError
 from .proposals import to_arrays
 
@@ -358,7 +359,7 @@ def _wave_native(part, params, engine):
         m = len(st_.consensus)
         ln = lens[read_off[k]:read_off[k + 1]]
         H = 2 * params.bandwidth + np.abs(ln - m) + 1
-        band = (H + 2 * m) * (((H + 1) >> 1) | 1) * 8
+        band = (H + 2 * m) * band_stride(H, pad_h=1) * 8   # upper bound: padded rows
         est_bytes += int(np.sort(band)[::-1][:nb[k]].sum()) * 2
     engine.reserve(int(est_bytes * 1.5) + (64 << 20))
     STATS["setup_native_s"] += time.perf_counter() - t_setup

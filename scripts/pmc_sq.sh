@@ -7,7 +7,7 @@ D=gpurun_out/${1:-r02sq}
 mkdir -p $D
 A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS"
 B="SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE"
-for cfg in c5 c4; do
+for cfg in ${CFGS:-c5 c4}; do
   extra=""; [ $cfg = c4 ] && extra="--no-secondary --clusters 400"
   for p in A B; do
     C=${!p}

@@ -2,9 +2,12 @@
 # Round profiles on the GPU box: rocprofv3 --kernel-trace --stats of the c4 and
 # c5 bench commands, then one PMC pass each for FETCH_SIZE and WRITE_SIZE
 # (separate runs, --kernel-trace only; MI355X_MICROARCH.md §HBM).
-# usage: scripts/prof_round.sh TAG        (outputs under gpurun_out/TAG/)
+# usage: scripts/prof_round.sh TAG [CONFIGS] [COUNTERS]   (outputs under gpurun_out/TAG/)
+#   CONFIGS default "c4 c5", COUNTERS default "FETCH_SIZE WRITE_SIZE"
 set -o pipefail
 TAG=${1:-r02}
+CFGS=${2:-"c4 c5"}
+CTRS=${3:-"FETCH_SIZE WRITE_SIZE"}
 D=gpurun_out/$TAG
 export TMPDIR=/tmp
 mkdir -p $D
@@ -15,11 +18,13 @@ run() {   # name, rocprof args..., -- command
   timeout -k 10 300 rocprofv3 "$@" > $D/$name.log 2>&1 || { echo "$name failed"; tail -5 $D/$name.log; exit 1; }
   echo "$name done"
 }
-run stats_c4 --kernel-trace --stats -d $D/stats_c4 -o p --output-format csv -- $C4
-run stats_c5 --kernel-trace --stats -d $D/stats_c5 -o p --output-format csv -- $C5
-for cfg in c4 c5; do
+for cfg in $CFGS; do
   cmd=$C4; [ $cfg = c5 ] && cmd=$C5
-  for ctr in FETCH_SIZE WRITE_SIZE; do
+  run stats_$cfg --kernel-trace --stats -d $D/stats_$cfg -o p --output-format csv -- $cmd
+done
+for cfg in $CFGS; do
+  cmd=$C4; [ $cfg = c5 ] && cmd=$C5
+  for ctr in $CTRS; do
     run pmc_${cfg}_$ctr --kernel-trace --pmc $ctr -d $D/pmc_$cfg/pmc_$ctr -o p --output-format csv -- $cmd
   done
 done

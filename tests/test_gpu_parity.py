@@ -46,8 +46,13 @@ DP_CASES = [
 ]
 
 
+@pytest.mark.parametrize("pad", [64, 1])
 @pytest.mark.parametrize("L,err,bw,jit,codon", DP_CASES)
-def test_dp_bands_bitexact(engine, L, err, bw, jit, codon):
+def test_dp_bands_bitexact(engine, opts, L, err, bw, jit, codon, pad):
+    """Bands, scores, backtraces and error counts vs the oracle, with the
+    default row strides and with every band's rows padded to whole 128-B
+    lines (RF_OPT_BAND_PAD = 1: even strides in every DP class)."""
+    opts("band_pad", pad)
     rng = np.random.default_rng(L * 7 + bw)
     t = random_seq(L, rng)
     seqs = []
@@ -100,11 +105,14 @@ def _check_bands(engine, t, seqs, bws):
         assert scores[k] == A_exp[d_end, L]
 
 
-def test_dp_class_boundaries(engine):
+@pytest.mark.parametrize("pad", [64, 0, 1])
+def test_dp_class_boundaries(engine, opts, pad):
     """H = 2bw + |n-m| + 1 on both sides of every kernel-class edge (31/32,
     63/64, 127/128), reads longer and shorter than the template, mixed in one
     launch so waves hold tasks of different geometry (lean interior bounds are
-    the intersection over a wave's four tasks)."""
+    the intersection over a wave's four tasks); default, odd-only and
+    all-padded row strides."""
+    opts("band_pad", pad)
     rng = np.random.default_rng(77)
     t = random_seq(180, rng)
     seqs, bws = [], []
@@ -357,7 +365,10 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (score_kernel, lean_nw, lean_lds_kb) engine options
     ("general", None, None),
-    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: default k_score_segc
+    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: default k_score_segl
+    ("seglodd", None, None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
+    ("seglpad", None, None),   # k_score_segl with every band line-padded (band_pad 1)
+    ("segcpad", None, None),   # k_score_segc over line-padded (even-stride) rows
     ("segc16", None, None),    # chunk-staged k_score_segc, 16 / 24 / 32 diagonals
     ("segc24", None, None),
     ("segc32", None, None),
@@ -386,11 +397,15 @@ def test_score_dense_kernels(engine, opts, kern, nw, lds, mode):
     if lds is not None and lds.startswith("q"):
         parts = lds[1:].split("l")
         wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
-    segs, ver = None, 3
+    segs, ver, pad = None, 4, 64
     if kern in ("seg16", "seg32"):
         kern, segs, ver = "seg", kern[3:], 1
     elif kern in ("segc16", "segc24", "segc32"):
         kern, segs, ver = "seg", kern[4:], 3
+    elif kern in ("seglodd", "seglpad", "segcpad"):
+        ver, pad = (3 if kern == "segcpad" else 4), (0 if kern == "seglodd" else 1)
+        kern = "seg"
+    opts("band_pad", pad)
     opts("score_kernel", kern or "auto")
     opts("lean_nw", int(nw or 8))
     opts("lean_lds_kb", int(lds or 0))
@@ -465,17 +480,28 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "segc16", "segc24", "segc32", "seg16", "seg24", "seg32", "general"])
+@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "segc16", "segc24", "segc32",
+                                  "segcpad", "seg16", "seg24", "seg32", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    chunk-staged row-segment scorer k_score_segc (default; 16, 24, 32
-    diagonals), the element-staged k_score_seg and the in-place k_score
-    ("general") are all bit-exact against the oracle."""
+    line-aligned row-segment scorer k_score_segl (default; line-padded rows,
+    odd-stride rows, both in one launch), the chunk-staged k_score_segc (16,
+    24, 32 diagonals; odd and even row strides), the element-staged
+    k_score_seg and the in-place k_score ("general") are all bit-exact
+    against the oracle."""
     opts("seg_s", 24)
-    opts("seg_ver", 3)
-    if kern is None:
+    opts("seg_ver", 4)
+    opts("band_pad", 64)
+    if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
+    elif kern in ("seglodd", "seglpad"):
+        opts("score_kernel", "auto")
+        opts("band_pad", 0 if kern == "seglodd" else 1)
+    elif kern == "segcpad":
+        opts("score_kernel", "auto")
+        opts("seg_ver", 3)
+        opts("band_pad", 1)
     elif kern.startswith("segc"):
         opts("score_kernel", "auto")
         opts("seg_ver", 3)
@@ -510,7 +536,16 @@ def test_score_wide_bands(engine, opts, mode, kern):
     engine.set_templates(0, templates)
     tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
     n = len(flat)
-    engine.realign(np.arange(n), np.arange(n), tpl, bws, RF_FWD | RF_BWD)
+    if kern == "seglmix":
+        # line-padded and odd-stride bands in one scoring launch: the even reads
+        # realigned in a padded call, the odd ones in an unpadded one
+        ev, od = np.arange(0, n, 2), np.arange(1, n, 2)
+        opts("band_pad", 1)
+        engine.realign(ev, ev, tpl[ev], np.asarray(bws)[ev], RF_FWD | RF_BWD)
+        opts("band_pad", 0)
+        engine.realign(od, od, tpl[od], np.asarray(bws)[od], RF_FWD | RF_BWD)
+    else:
+        engine.realign(np.arange(n), np.arange(n), tpl, bws, RF_FWD | RF_BWD)
     groups, at = [], 0
     for rs in seqs:
         groups.append(np.arange(at, at + len(rs)))
@@ -561,9 +596,9 @@ def test_alignment_proposals_device(engine, do_indels):
         np.testing.assert_array_equal(masks[c], exp, err_msg=f"cluster {c}")
 
 
-@pytest.mark.parametrize("win_kb", [32, 16])
+@pytest.mark.parametrize("win_kb,pad", [(32, 64), (16, 64), (16, 1)])
 @pytest.mark.parametrize("L,bw,skew", [(700, 9, 0), (400, 40, 30), (300, 120, -40), (260, 9, 60), (90, 3, 0)])
-def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb):
+def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     """k_bt_win (wave per read, LDS windows of kappa rows, re-staged as the
     walk leaves them) against the oracle's backtrace and count_errors, and the
     fused proposal marking against the host moves_to_proposals union, on long
@@ -585,6 +620,7 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb):
             r = RifrafSequence(r.seq[:len(r.seq) - cut], r.error_log_p[:len(r.seq) - cut], bw, SEQ_SCORES)
         seqs.append(r)
     n = len(seqs)
+    opts("band_pad", pad)
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
