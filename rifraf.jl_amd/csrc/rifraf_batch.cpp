@@ -29,6 +29,9 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -540,15 +543,19 @@ struct BatchResult {
     std::vector<Clu> clu;
     std::vector<Read> reads;
 };
-static std::vector<std::pair<const rf_ctx *, BatchResult>> g_results;
+// contexts may run on different host threads (one ctx per thread): the
+// registry is locked, and each result lives in its own heap block so a
+// reference stays valid while other contexts are added or released
+static std::mutex g_results_mu;
+static std::map<const rf_ctx *, std::unique_ptr<BatchResult>> g_results;
 
 static BatchResult &result_of(const rf_ctx *ctx)
 {
-    for (auto &r : g_results)
-        if (r.first == ctx)
-            return r.second;
-    g_results.emplace_back(ctx, BatchResult{});
-    return g_results.back().second;
+    std::lock_guard<std::mutex> lk(g_results_mu);
+    auto &slot = g_results[ctx];
+    if (!slot)
+        slot.reset(new BatchResult{});
+    return *slot;
 }
 
 extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
@@ -639,11 +646,8 @@ extern "C" int rf_batch_fetch(rf_ctx *ctx, int32_t cluster, uint8_t *cons, int64
 
 extern "C" void rf_batch_release(rf_ctx *ctx)
 {
-    for (size_t i = 0; i < g_results.size(); ++i)
-        if (g_results[i].first == ctx) {
-            g_results.erase(g_results.begin() + (ptrdiff_t)i);
-            return;
-        }
+    std::lock_guard<std::mutex> lk(g_results_mu);
+    g_results.erase(ctx);
 }
 
 // ---------------------------------------------------------------------

@@ -2358,175 +2358,220 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     }
     // aligned-row loader lane roles: row r8 + 8j, 16-B chunk cc of the line
     const int r8 = tid >> 3, cc8 = tid & 7, p8 = r8 & 1;
-    for (int r = r0; r < r1; ++r) {
+    // per-read geometry: wave-uniform fields plus the lane's diagonal range
+    struct RG {
+        const double *gA;
+        const double *tm;
+        const uint8_t *sq;
+        int64_t dB;
+        int c, P, K, n;
+        int dfirst, dlast;           // this lane's chain rows as band diagonals
+        bool peel;
+        int dlo, dhi, dfmax, dlmin;  // wave-wide
+    };
+    auto setup = [&](int r, RG &g) {
         const ScoreRead R = reads[r];
-        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
+        g.c = R.c;
+        g.P = R.P;
+        g.K = R.K;
+        g.n = R.n;
+        g.gA = bands + R.A;
+        g.dB = R.B - R.A;
+        g.tm = tabs + R.tab;
+        g.sq = bases + R.sb;
         const int jn = min(a + 1, m);
-        const int i0 = max(0, jn - c);
-        const int i1 = min(jn + vb, n);
-        const int ilast = min(i1, a + vb);
-        const int dfirst = i0 - a + c, dlast = ilast - a + c;
-        const bool peel = i1 > ilast;
-        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
-        int dfmax = active ? dfirst : INT_MAX, dlmin = active ? dlast : -1;
+        const int i0 = max(0, jn - g.c);
+        const int i1 = min(jn + R.vb, g.n);
+        const int ilast = min(i1, a + R.vb);
+        g.dfirst = i0 - a + g.c;
+        g.dlast = ilast - a + g.c;
+        g.peel = i1 > ilast;
+        int dlo = active ? g.dfirst : INT_MAX, dhi = active ? g.dlast + (g.peel ? 1 : 0) : -1;
+        int dfmax = active ? g.dfirst : INT_MAX, dlmin = active ? g.dlast : -1;
         for (int off = 32; off >= 1; off >>= 1) {
             dlo = min(dlo, __shfl_xor(dlo, off));
             dhi = max(dhi, __shfl_xor(dhi, off));
             dfmax = max(dfmax, __shfl_xor(dfmax, off));
             dlmin = min(dlmin, __shfl_xor(dlmin, off));
         }
-        dlo = __builtin_amdgcn_readfirstlane(dlo);
-        dhi = __builtin_amdgcn_readfirstlane(dhi);
-        dfmax = __builtin_amdgcn_readfirstlane(dfmax);
-        dlmin = __builtin_amdgcn_readfirstlane(dlmin);
-        if (dlo > dhi)
-            continue;
-        const bool aligned = (P & 15) == 0;        // wave-uniform
-        const bool all_act = __all(active) && wave_s;
-        const double *gA = bands + R.A;
-        const int64_t dB = R.B - R.A;
-        const double *tm = tabs + R.tab;
-        const uint8_t *sq = bases + R.sb;
-        double prev[4], accI[4], accS[4], dd = -RF_INF;
+        g.dlo = __builtin_amdgcn_readfirstlane(dlo);
+        g.dhi = __builtin_amdgcn_readfirstlane(dhi);
+        g.dfmax = __builtin_amdgcn_readfirstlane(dfmax);
+        g.dlmin = __builtin_amdgcn_readfirstlane(dlmin);
+    };
+    const bool all_act = __all(active) && wave_s;
+    dvec2 ra[NUA], rb[NUA];
+    double tmt[2], tmm[2], tin[2], tdl[2];
+    int tsb[2];
+    double z0a = 0.0, z0b = 0.0, z1a = 0.0, z1b = 0.0;   // LDS row 0 of a read's first segment
+    // loads of segment D of read g (registers only): issued one segment ahead,
+    // and the next read's first segment during the current read's last one
+    auto load_seg = [&](const RG &g, int D, bool first) {
+        const int kb = D + 2 * a0, eh = D >> 1;
+        if ((g.P & 15) == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            prev[k] = -RF_INF;
-            accI[k] = -RF_INF;
-            accS[k] = -RF_INF;
+            for (int j = 0; j < NUA; ++j) {
+                const int kap = min(kb + r8 + 8 * j, g.K - 1);
+                const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
+                ra[j] = *(const dvec2 *)(g.gA + o);
+                rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+            }
         }
-        dvec2 ra[NUA], rb[NUA];
-        double tmt[2], tmm[2], tin[2], tdl[2];
-        int tsb[2];
-        auto load_seg = [&](int D) {
-            const int kb = D + 2 * a0, eh = D >> 1;
-            if (aligned) {
-                // prefetched into registers while the current segment is scored
+        if (first && D > 0) {
+            // diagonal D-1 of columns a0 .. a0+64 (the previous segment's last row)
+            const int kap = min(D - 1 + 2 * a, g.K - 1);
+            const int64_t o = (int64_t)kap * g.P + ((D - 1) >> 1);
+            z0a = g.gA[o];
+            z0b = g.gA[g.dB + o];
+            if (tid == 0) {
+                const int kap1 = min(D - 1 + 2 * (a0 + 64), g.K - 1);
+                const int64_t o1 = (int64_t)kap1 * g.P + ((D - 1) >> 1);
+                z1a = g.gA[o1];
+                z1b = g.gA[g.dB + o1];
+            }
+        }
+        const int ib = a0 - g.c + D;
 #pragma unroll
-                for (int j = 0; j < NUA; ++j) {
-                    const int kap = min(kb + r8 + 8 * j, K - 1);
-                    const int64_t g = (int64_t)kap * P + eh + 2 * cc8;
-                    ra[j] = *(const dvec2 *)(gA + g);
-                    rb[j] = *(const dvec2 *)(gA + dB + g);
+        for (int u = 0; u < 2; ++u) {
+            const int i = min(max(ib + tid + 64 * u, 0), g.n);
+            const int ks = max(i - 1, 0);
+            tsb[u] = g.sq[ks];   // read row 0 (the gap) is selected at the store
+            tmt[u] = g.tm[ks];
+            tmm[u] = g.tm[g.n + ks];
+            tin[u] = g.tm[2 * (size_t)g.n + ks];
+            tdl[u] = g.tm[3 * (size_t)g.n + i];
+        }
+    };
+    auto store_seg = [&](const RG &g, int D) {
+        if ((g.P & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < NUA; ++j) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
+                    const int col = (r8 + 8 * j - ddl) >> 1;    // a - a0
+                    const double v = h ? ra[j].y : ra[j].x, w = h ? rb[j].y : rb[j].x;
+                    const int l = (ddl + 1) * LS + col;
+                    // rows 32..127 always land in [0, 64]; the parallelogram's
+                    // first / last 32 rows hold cells of the neighbouring items
+                    if ((j >= 4 && j < NUA - 4) || (col >= 0 && col <= 64)) {
+                        sA[l] = v;
+                        sB[l] = w;
+                    }
                 }
             }
-            const int ib = a0 - c + D;
+        } else {
+            // odd-stride rows (narrow bands in a wide launch): 9 pair-aligned
+            // chunks per row, loaded here in groups of 4 (not prefetched)
+            const int kb = D + 2 * a0, eh = D >> 1;
+#pragma unroll 1
+            for (int j0 = 0; j0 < NUG; j0 += 4) {
+                dvec2 ga[4], gb[4];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int i = min(max(ib + tid + 64 * u, 0), n);
-                const int ks = max(i - 1, 0);
-                tsb[u] = sq[ks];   // read row 0 (the gap) is selected at the store
-                tmt[u] = tm[ks];
-                tmm[u] = tm[n + ks];
-                tin[u] = tm[2 * (size_t)n + ks];
-                tdl[u] = tm[3 * (size_t)n + i];
-            }
-        };
-        auto store_seg = [&](int D) {
-            if (aligned) {
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int t = min(tid + 64 * (j0 + jj), Gm::NROW * 9 - 1);
+                    const int rr = (t * 7282) >> 16, cc = t - 9 * rr;   // t / 9 for t < 1440
+                    const int kap = min(kb + rr, g.K - 1);
+                    const int o = ((kap * g.P + eh) & ~1) + 2 * cc;
+                    ga[jj] = *(const dvec2 *)(g.gA + o);
+                    gb[jj] = *(const dvec2 *)(g.gA + g.dB + o);
+                }
 #pragma unroll
-                for (int j = 0; j < NUA; ++j) {
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int t = tid + 64 * (j0 + jj);
+                    const int rr = (t * 7282) >> 16, cc = t - 9 * rr;
+                    const int sh = (kb + rr + eh) & 1;   // P odd
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
-                        const int col = (r8 + 8 * j - ddl) >> 1;    // a - a0
-                        const double v = h ? ra[j].y : ra[j].x, w = h ? rb[j].y : rb[j].x;
-                        const int l = (ddl + 1) * LS + col;
-                        // rows 32..127 always land in [0, 64]; the parallelogram's
-                        // first / last 32 rows hold cells of the neighbouring items
-                        if ((j >= 4 && j < NUA - 4) || (col >= 0 && col <= 64)) {
-                            sA[l] = v;
-                            sB[l] = w;
+                        const int xl = 2 * cc + h - sh;
+                        const int ddl = 2 * xl + (rr & 1);
+                        const int col = (rr - ddl) >> 1;
+                        if (t < Gm::NROW * 9 && xl >= 0 && xl < 16 && col >= 0 && col <= 64) {
+                            const int l = (ddl + 1) * LS + col;
+                            sA[l] = h ? ga[jj].y : ga[jj].x;
+                            sB[l] = h ? gb[jj].y : gb[jj].x;
                         }
                     }
-                }
-            } else {
-                // odd-stride rows (narrow bands in a wide launch): 9 pair-aligned
-                // chunks per row, loaded here in groups of 4 (not prefetched)
-                const int kb = D + 2 * a0, eh = D >> 1;
-#pragma unroll 1
-                for (int j0 = 0; j0 < NUG; j0 += 4) {
-                    dvec2 ga[4], gb[4];
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int t = min(tid + 64 * (j0 + jj), Gm::NROW * 9 - 1);
-                        const int rr = (t * 7282) >> 16, cc = t - 9 * rr;   // t / 9 for t < 1440
-                        const int kap = min(kb + rr, K - 1);
-                        const int g = ((kap * P + eh) & ~1) + 2 * cc;
-                        ga[jj] = *(const dvec2 *)(gA + g);
-                        gb[jj] = *(const dvec2 *)(gA + dB + g);
-                    }
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int t = tid + 64 * (j0 + jj);
-                        const int rr = (t * 7282) >> 16, cc = t - 9 * rr;
-                        const int sh = (kb + rr + eh) & 1;   // P odd
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int xl = 2 * cc + h - sh;
-                            const int ddl = 2 * xl + (rr & 1);
-                            const int col = (rr - ddl) >> 1;
-                            if (t < Gm::NROW * 9 && xl >= 0 && xl < 16 && col >= 0 && col <= 64) {
-                                const int l = (ddl + 1) * LS + col;
-                                sA[l] = h ? ga[jj].y : ga[jj].x;
-                                sB[l] = h ? gb[jj].y : gb[jj].x;
-                            }
-                        }
-                    }
-                }
-                // nothing of this path stays in flight: hipcc's wait analysis
-                // merges paths, and a load it saw pending here would make it
-                // drain the next segment's prefetch before the chains
-                __builtin_amdgcn_s_waitcnt(0);
-            }
-            const int ib = a0 - c + D;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int t = tid + 64 * u;
-                if (t < NT) {
-                    const int sb = ib + t >= 1 ? tsb[u] : 4;
-                    const double mt = tmt[u], mm = tmm[u];
-                    sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
-                    sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
-                    sT2[t] = dvec2{tin[u], tdl[u]};
                 }
             }
-        };
-        const int D0 = dlo & ~(S - 1);
-        if (!(split_mode & 4))
-            load_seg(D0);
-        for (int D = D0; D <= dhi; D += S) {
-            wave_sync();   // previous segment's chains are done with LDS
-            // LDS row 0 = diagonal D-1: the previous segment's row 32, or gathered
-            if (D == D0) {
-                if (D > 0) {
+            // nothing of this path stays in flight: hipcc's wait analysis
+            // merges paths, and a load it saw pending here would make it
+            // drain the next segment's prefetch before the chains
+            __builtin_amdgcn_s_waitcnt(0);
+        }
+        const int ib = a0 - g.c + D;
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int t = tid + 64 * u;
-                        if (t <= 64) {
-                            const int kap = min(D - 1 + 2 * (a0 + t), K - 1);
-                            const int64_t g = (int64_t)kap * P + ((D - 1) >> 1);
-                            sA[t] = gA[g];
-                            sB[t] = gA[dB + g];
-                        }
-                    }
-                    __builtin_amdgcn_s_waitcnt(0);   // as after the odd-stride loader
-                }
-            } else {
-                const double va = sA[S * LS + tid], vbv = sB[S * LS + tid];
-                const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
-                sA[tid] = va;
-                sB[tid] = vbv;
+        for (int u = 0; u < 2; ++u) {
+            const int t = tid + 64 * u;
+            if (t < NT) {
+                const int sb = ib + t >= 1 ? tsb[u] : 4;
+                const double mt = tmt[u], mm = tmm[u];
+                sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
+                sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
+                sT2[t] = dvec2{tin[u], tdl[u]};
+            }
+        }
+    };
+    const bool do_load = !(split_mode & 4);
+    // a wave with no column (every a > m) writes nothing; any other wave has
+    // rows in every read (each band column holds at least one row)
+    if (!__any(active))
+        return;
+    // reads and their segments as one stream: the register prefetch always
+    // holds the next segment -- this read's next, or the next read's first --
+    // so no read starts on an exposed load
+    RG g, gn;
+    int r = r0;
+    if (r < r1) {
+        setup(r, g);
+        gn = g;
+    }
+    int D0 = g.dlo & ~(S - 1), D = D0;
+    if (r < r1 && do_load)
+        load_seg(g, D, true);
+    double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        prev[k] = -RF_INF;
+        accI[k] = -RF_INF;
+        accS[k] = -RF_INF;
+    }
+    while (r < r1) {
+        const bool more = r + 1 < r1;
+        const int c = g.c, dfirst = g.dfirst, dlast = g.dlast, dhi = g.dhi;
+        const int dfmax = g.dfmax, dlmin = g.dlmin;
+        const bool peel = g.peel;
+        wave_sync();   // previous segment's chains are done with LDS
+        // LDS row 0 = diagonal D-1: the previous segment's row 32, or prefetched
+        if (D == D0) {
+            if (D > 0) {
+                sA[tid] = z0a;
+                sB[tid] = z0b;
                 if (tid == 0) {
-                    sA[64] = va6;
-                    sB[64] = vb6;
+                    sA[64] = z1a;
+                    sB[64] = z1b;
                 }
             }
-            store_seg(D);
-            wave_sync();
-            if (D + S <= dhi && !(split_mode & 4))
-                load_seg(D + S);
-            if (!active || (split_mode & 2))
-                continue;
+        } else {
+            const double va = sA[S * LS + tid], vbv = sB[S * LS + tid];
+            const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
+            sA[tid] = va;
+            sB[tid] = vbv;
+            if (tid == 0) {
+                sA[64] = va6;
+                sB[64] = vb6;
+            }
+        }
+        store_seg(g, D);
+        wave_sync();
+        const bool last = D + S > dhi;
+        if (last && more)
+            setup(r + 1, gn);
+        if (do_load && (!last || more)) {
+            const RG gl = last ? gn : g;
+            load_seg(gl, last ? (gn.dlo & ~(S - 1)) : D + S, last);
+        }
+        if (active && !(split_mode & 2)) {
             const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
             const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];   // unconditional read, then select
             double aprev = (lo <= hi && lo >= 1 && a - c + lo >= 1) ? a0v : -RF_INF;
@@ -2605,32 +2650,47 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 }
             }
         }
-        if (active) {
-            const double qnan = __builtin_nan("");
-            if (split_mode & 1) {
-                double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
-                if (a < m) {
+        if (last) {
+            if (active) {
+                const double qnan = __builtin_nan("");
+                if (split_mode & 1) {
+                    double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
-                    dst[13] = dd;
-                }
-                if (a == 0) {
+                        dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+                    if (a < m) {
 #pragma unroll
-                    for (int k = 0; k < 5; ++k)
-                        dst[k] = qnan;
-                }
-            } else {
+                        for (int k = 0; k < 4; ++k)
+                            dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                        dst[13] = dd;
+                    }
+                    if (a == 0) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
-                    tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+                        for (int k = 0; k < 5; ++k)
+                            dst[k] = qnan;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+                        tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+                    }
+                    tD += dd;
                 }
-                tD += dd;
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                prev[k] = -RF_INF;
+                accI[k] = -RF_INF;
+                accS[k] = -RF_INF;
+            }
+            dd = -RF_INF;
+            g = gn;
+            ++r;
+            D0 = g.dlo & ~(S - 1);
+            D = D0;
+        } else {
+            D += S;
         }
     }
     if (!active || (split_mode & 1))
@@ -4380,7 +4440,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const TplObj &T = ctx->tpls[tpl[k]];
                 Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
                 const int H = band_rows(S.n + 1, T.m + 1, bw[k]);
-                const int P = band_stride(H, pad_call ? 1 : 0);
+                // A and B of one alignment share a row stride: every scorer reads
+                // both bands with one P, and the two are often filled by different
+                // calls (forward_moves with band doubling, then backward!) that
+                // may differ in pad_call
+                const Band &o = dir == 0 ? ctx->slots[slot[k]].b : ctx->slots[slot[k]].a;
+                const bool partner = o.valid && o.seq == seq[k] && o.tpl == tpl[k] && o.bw == bw[k] &&
+                                     o.n == S.n && o.m == T.m && o.H == H && o.tplver == T.version;
+                const int P = partner ? o.P : band_stride(H, pad_call ? 1 : 0);
                 if (int e = region_ensure(ctx, ctx->band_arena, b.r, band_K(H, T.m) * P * 8))
                     return e;
                 moved = moved || !b.valid || b.seq != seq[k] || b.tpl != tpl[k] || b.bw != bw[k] ||
@@ -4855,6 +4922,10 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             why = "A and B bands were computed for different alignments";
             return false;
         }
+        if (S.a.P != S.b.P) {
+            why = "A and B bands have different row strides";
+            return false;
+        }
         if (ctx->tpls[S.a.tpl].version != S.a.tplver) {
             why = "template changed since the bands were computed";
             return false;
@@ -5113,6 +5184,8 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             if (!S.a.valid || !S.b.valid || S.a.seq != S.b.seq || S.a.tpl != S.b.tpl ||
                 S.a.bw != S.b.bw || S.a.tplver != S.b.tplver || S.a.m != S.b.m)
                 return fail(ctx, RF_ERR_STATE, "rf_score_dense: A and B bands were computed for different alignments");
+            if (S.a.P != S.b.P)
+                return fail(ctx, RF_ERR_STATE, "rf_score_dense: A and B bands have different row strides");
             if (ctx->tpls[S.a.tpl].version != S.a.tplver)
                 return fail(ctx, RF_ERR_STATE, "rf_score_dense: template changed since the bands were computed");
             const SeqObj &Q = ctx->seqs[S.a.seq];

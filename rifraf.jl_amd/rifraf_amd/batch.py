@@ -438,8 +438,14 @@ def _wave_native(part, params, engine):
     return results
 
 
-def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None):
+def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None, engines=None):
     """rifraf() over many independent clusters, batched on one engine.
+
+    engines: several engines (contexts, each with its own HIP stream, e.g.
+    on one GPU) -- the clusters are split into contiguous shards, one per
+    engine, and each shard runs on its own host thread, so one shard's host
+    work (table setup, quality pass) overlaps another's kernels.  Clusters
+    are independent, so the results equal one engine's.
 
     clusters: sequence of dicts with the keyword arguments of model.rifraf
     (`dnaseqs`, `phreds` or `error_log_ps`, optional `consensus`,
@@ -452,6 +458,29 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
     import os
     from .model import RifrafParams, rifraf
     params = params or RifrafParams()
+    if engines is not None and len(engines) > 1:
+        E = len(engines)
+        cut = [k * len(clusters) // E for k in range(E + 1)]
+        out = [None] * E
+        errs = [None] * E
+
+        def shard(i):
+            try:
+                out[i] = rifraf_batch(clusters[cut[i]:cut[i + 1]], params=params, engine=engines[i], wave=wave,
+                                      native=native)
+            except BaseException as e:  # noqa: BLE001 -- re-raised below in shard order
+                errs[i] = e
+        ts = [threading.Thread(target=shard, args=(i,), daemon=True) for i in range(E)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e
+        return [r for part in out for r in part]
+    if engines is not None and engine is None:
+        engine = engines[0]
     profile_dir = os.environ.get("RIFRAF_BATCH_PROFILE")
     if engine is None:
         from .align import default_engine

@@ -70,6 +70,20 @@ def test_batch_waves_and_errors():
         rifraf_batch(bad, params=params, engine=OracleEngine())
 
 
+def test_batch_engine_shards_oracle():
+    """rifraf_batch(engines=[...]): contiguous cluster shards on their own
+    host threads and engines give the single-engine results, in input order."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    clusters = _clusters()
+    params = _params()
+    one = rifraf_batch(clusters, params=params, engine=OracleEngine())
+    three = rifraf_batch(clusters, params=params, engines=[OracleEngine() for _ in range(3)])
+    assert len(three) == len(one)
+    for x, y in zip(three, one):
+        assert_same_run(summary(x), summary(y))
+
+
 @pytest.mark.gpu
 def test_batch_matches_separate_runs_hip(engine):
     _check(lambda: engine)
@@ -157,3 +171,61 @@ def test_native_scope():
     assert not native_eligible(clusters, RifrafParams(do_init=False))
     with pytest.raises(RifrafError):
         rifraf_batch(clusters[:1], params=RifrafParams(max_iters=2), engine=OracleEngine(), native=True)
+
+
+def _doubling_clusters(seed=12):
+    """Reference-free clusters in which one read per cluster carries a run of
+    deletions: its band doubles (smart_forward_moves!) to H >= 64, so the
+    driver's forward, refill and backward calls differ in row padding."""
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    out = []
+    for n, L, cut in [(10, 400, 30), (8, 300, 26), (12, 350, 0)]:
+        _, _, _, reads, _, phreds, _, _ = sample_sequences(n, L, error_rate=0.01, rng=rng)
+        reads, phreds = list(reads), list(phreds)
+        if cut:
+            k = int(rng.integers(0, n))
+            at = int(rng.integers(50, L - 50 - cut))
+            reads[k] = np.concatenate([reads[k][:at], reads[k][at + cut:]])
+            phreds[k] = np.concatenate([phreds[k][:at], phreds[k][at + cut:]])
+        out.append(dict(dnaseqs=reads, phreds=phreds))
+    return out
+
+
+@pytest.mark.gpu
+def test_native_batch_band_doubling_vs_oracle(engine):
+    """Native batched driver with band doubling into line-padded layouts (the
+    c4 e2e shape's failure mode: A and B of one read filled by calls that
+    differ in padding) against separate oracle-engine rifraf() runs, QVs on."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams, rifraf
+    params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True, max_iters=20)
+    clusters = _doubling_clusters()
+    got = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    # bw >= 18 with |n - m| ~ 30: H = 2 bw + |n - m| + 1 >= 64 (a padded call)
+    assert max(s.bandwidth for r in got for s in r.state.sequences) >= 18
+    ref = [summary(rifraf(params=params, engine=OracleEngine(), **kw)) for kw in clusters]
+    for r, g in zip(ref, got):
+        assert_same_run(summary(g), r)
+
+
+@pytest.mark.gpu
+def test_native_batch_engines_one_gpu(engine):
+    """Three contexts on one GPU, one host thread each (rifraf_batch(engines=)),
+    equal the single-engine native run."""
+    from rifraf_amd import ErrorModel, Scores
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.engine import Engine
+    from rifraf_amd.model import RifrafParams
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), **NATIVE_PARAMS["all_reads_qv"])
+    clusters = _ref_free_clusters() + _ref_free_clusters(seed=3)
+    one = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    engs = [Engine(0) for _ in range(3)]
+    try:
+        many = rifraf_batch(clusters, params=params, engines=engs, native=True)
+    finally:
+        for e in engs:
+            e.close()
+    for a, b in zip(many, one):
+        assert_same_run(summary(a), summary(b))

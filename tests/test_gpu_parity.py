@@ -561,6 +561,46 @@ def test_score_wide_bands(engine, opts, mode, kern):
         np.testing.assert_array_equal(got[c][mask], ref_tot[mask], err_msg=f"cluster {c}")
 
 
+@pytest.mark.parametrize("order", ["fwd_then_bwd", "bwd_then_fwd"])
+def test_split_direction_calls_share_stride(engine, opts, order):
+    """smart_forward_moves! + backward! as separate calls: the forward bands of
+    narrow reads come from an unpadded call, the band-doubling refill of one
+    read makes a line-padded call, and the backward bands of every read come
+    from another padded call (its widest band has H >= RF_OPT_BAND_PAD).  A
+    and B of one alignment must keep one row stride (the scorers read both
+    with one P); dense and proposal-list totals equal the oracle."""
+    opts("band_pad", 64)
+    rng = np.random.default_rng(515)
+    t = random_seq(400, rng)
+    reads = [make_read(t, rng, 0.02, 9) for _ in range(6)]
+    wide = make_read(t, rng, 0.05, 40)
+    seqs = reads + [wide]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    n = len(seqs)
+    sl = np.arange(n)
+    bws = np.array([9] * (n - 1) + [40])
+    if order == "fwd_then_bwd":
+        engine.realign(sl, sl, 0, [9] * n, RF_FWD)                   # unpadded (H < 64)
+        engine.realign(sl[-1:], sl[-1:], 0, bws[-1:], RF_FWD)       # padded refill
+        engine.realign(sl, sl, 0, bws, RF_BWD)                      # padded call
+    else:
+        engine.realign(sl[:-1], sl[:-1], 0, bws[:-1], RF_BWD)       # unpadded
+        engine.realign(sl, sl, 0, bws, RF_FWD)                      # padded call
+        engine.realign(sl[-1:], sl[-1:], 0, bws[-1:], RF_BWD)
+    got = engine.score_dense([sl])[0]
+    ref_tot, _ = oracle.cpu_pass(t, seqs, nthreads=4)
+    mask = np.ones_like(ref_tot, bool)
+    mask[0, :5] = False
+    for j in range(1, len(t) + 1):
+        mask[j, t[j - 1]] = False
+    np.testing.assert_array_equal(got[mask], ref_tot[mask])
+    kinds, poss, bases = all_proposals_arrays(t)
+    tot = engine.score([(sl, -1, (kinds, poss, bases))])[0]
+    slot = np.where(kinds == 0, bases, np.where(kinds == 2, 4, 5 + bases))
+    np.testing.assert_array_equal(tot, ref_tot[poss, slot])
+
+
 @pytest.mark.parametrize("do_indels", [True, False])
 def test_alignment_proposals_device(engine, do_indels):
     """rf_alignment_proposals (device moves_to_proposals + Set union) equals the

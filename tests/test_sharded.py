@@ -25,11 +25,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _spawn(fn, world, *args):
+def _spawn(fn, world, *args, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q) + args) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q, backend) + args) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=300) for _ in procs]
@@ -41,11 +41,14 @@ def _spawn(fn, world, *args):
     return dict((r, v) for r, _, v in got)
 
 
-def _entry(fn, rank, world, port, q, *args):
+def _entry(fn, rank, world, port, q, backend, *args):
     import traceback
+    import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(rank)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         q.put((rank, "ok", fn(rank, world, *args)))
     except Exception:

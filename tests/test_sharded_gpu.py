@@ -65,3 +65,49 @@ def test_score_dense_dev_matches_host(engine):
     dev = buf.cpu().numpy()
     np.testing.assert_array_equal(dev[:121 * 9].reshape(121, 9), host[0])
     np.testing.assert_array_equal(dev[121 * 9:].reshape(76, 9), host[1])
+
+
+def _w_rccl_dense(rank, world):
+    """One RCCL rank (backend "nccl" on cuda:0): ShardedEngine.realign (object
+    all-gather over RCCL) and score_dense (rf_score_dense_dev straight into a
+    CUDA tensor, all_gather_into_tensor, device rank-order sum)."""
+    import torch
+    import torch.distributed as dist
+    from _util import make_read
+    from rifraf_amd.engine import RF_BWD, RF_FWD, Engine
+    from rifraf_amd.sample import random_seq
+    from rifraf_amd.sharded import ShardedEngine, allgather_fold
+    assert dist.get_backend() == "nccl"
+    rng = np.random.default_rng(21)
+    tpls = [random_seq(300, rng), random_seq(180, rng)]
+    reads = [[make_read(t, rng, 0.03, 9) for _ in range(6)] for t in tpls]
+    flat = [r for rs in reads for r in rs]
+    n = len(flat)
+    groups = [np.arange(0, 6), np.arange(6, 12)]
+    plain = Engine(0)
+    plain.set_sequences(0, flat)
+    plain.set_templates(0, tpls)
+    v0 = plain.realign(np.arange(n), np.arange(n), np.repeat([0, 1], 6), [9] * n, RF_FWD | RF_BWD)
+    want = plain.score_dense(groups)
+    plain.close()
+    sh = ShardedEngine(Engine(0), n)
+    assert sh.dev.type == "cuda"
+    sh.set_sequences(0, flat)
+    sh.set_templates(0, tpls)
+    v1 = sh.realign(np.arange(n), np.arange(n), np.repeat([0, 1], 6), [9] * n, RF_FWD | RF_BWD)
+    got = sh.score_dense(groups)
+    assert sh.last_dense.is_cuda
+    x = torch.arange(10, dtype=torch.float64, device="cuda:0")
+    y = allgather_fold(x, dist)
+    sh.close()
+    return {"v0": v0, "v1": v1, "want": want, "got": got, "fold": y.cpu().numpy()}
+
+
+def test_rccl_world1_dense_exchange():
+    """The RCCL branch of the read-sharded exchange (sharded.py allgather_fold
+    on CUDA tensors) executes and, at world size 1, equals the plain engine."""
+    got = _spawn(_w_rccl_dense, 1, backend="nccl")[0]
+    np.testing.assert_array_equal(got["v0"], got["v1"])
+    for a, b in zip(got["want"], got["got"]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(got["fold"], np.arange(10, dtype=np.float64))
