@@ -263,6 +263,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--e2e-clusters", type=int, default=256,
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
+    ap.add_argument("--e2e-engines", type=int, default=2,
+                    help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     args = ap.parse_args()
@@ -321,17 +323,20 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         clusters.append(dict(dnaseqs=reads, phreds=phreds))
         templates.append(t)
     params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
-    eng = Engine(gpu)
-    rifraf_batch(clusters[:4], params=params, engine=eng)          # warm-up (kernels, pinned staging)
+    ne = max(1, args.e2e_engines)
+    engs = [Engine(gpu) for _ in range(ne)]
+    for e in engs:
+        rifraf_batch(clusters[:4], params=params, engine=e)        # warm-up (kernels, pinned staging)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    res = rifraf_batch(clusters, params=params, engine=eng)
+    res = rifraf_batch(clusters, params=params, engines=engs)
     elapsed = time.perf_counter() - t0
-    ref = rifraf_batch(clusters[:2], params=params, engine=eng, native=False)
+    ref = rifraf_batch(clusters[:2], params=params, engine=engs[0], native=False)
     same = all(np.array_equal(a.consensus, b.consensus) and a.state.score == b.state.score and
                np.array_equal(a.aln_error_probs, b.aln_error_probs) for a, b in zip(res[:2], ref))
-    eng.close()
+    for e in engs:
+        e.close()
     ok = sum(int(np.array_equal(r.consensus, t)) for r, t in zip(res, templates))
     iters = sum(sum(r.state.stage_iterations) for r in res)
     tot = [float(n), float(ok), float(iters), 1.0 if same else 0.0]
@@ -339,7 +344,9 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         elapsed, tot = aggregate(elapsed, tot, coll)
     return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": tot[0] / elapsed,
             "clusters": int(tot[0]), "seconds": elapsed, "processes_per_gpu": 1,
-            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass",
+            "engines_per_gpu": ne,
+            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; clusters sharded "
+                      "over engines_per_gpu contexts (own HIP stream, own host thread) in one process",
             "params": "batch = all 50 reads, do_score (QVs), no reference",
             "consensus_equals_template": int(tot[1]), "stage_iterations": int(tot[2]),
             "same_as_python_stage_machine": tot[3] == world}

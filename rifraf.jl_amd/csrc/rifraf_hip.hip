@@ -320,6 +320,16 @@ __device__ __forceinline__ double dpp_f64(double x)
 #define DPP_FROM_L2 0x112   // row_shr:2 -> lane q-2
 #define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
 #define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
+// Lanes per DP task: 16 (one DPP row, 4 tasks per wave) or 64 (the whole
+// wave, wave_shr / wave_shl / wave_ror / wave_rol: the same moves across rows).
+template <int LPT>
+struct TaskLanes {
+    static_assert(LPT == 16 || LPT == 64, "tasks are one DPP row or one wave");
+    static constexpr int FROM_L1 = LPT == 64 ? 0x138 : 0x111;   // lane q-1 (edge lane 0 reads `old`)
+    static constexpr int FROM_R1 = LPT == 64 ? 0x130 : 0x101;   // lane q+1 (edge lane LPT-1 reads `old`)
+    static constexpr int ROT_L1 = LPT == 64 ? 0x13C : 0x121;    // lane (q-1) mod LPT
+    static constexpr int ROT_R1 = LPT == 64 ? 0x134 : 0x12F;    // lane (q+1) mod LPT
+};
 
 // Shift an int / double across the 16-lane DPP row (lanes outside the row
 // read `bound`).
@@ -386,15 +396,18 @@ __device__ __forceinline__ int load_col(const DPTask &T, bool rev, const uint8_t
     return (jj >= 1 && jj <= T.m) ? tbase[rev ? T.m - jj : jj - 1] : 4;
 }
 
-// Row record of the lane above (row_shl:1); lane 15 receives `edge`.
+// Row record of the lane above (row_shl:1 / wave_shl:1); lane LPT-1 receives `edge`.
+template <int LPT = 16>
 __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &edge, bool codon)
 {
+    constexpr int C = TaskLanes<LPT>::FROM_R1;
     RowRec r;
-    r.sb = __builtin_amdgcn_update_dpp(edge.sb, x.sb, DPP_FROM_R1, 0xF, 0xF, false);
+    r.sb = __builtin_amdgcn_update_dpp(edge.sb, x.sb, C, 0xF, 0xF, false);
     auto sh = [](double v, double e) {
+        constexpr int C = TaskLanes<LPT>::FROM_R1;
         const long long b = __double_as_longlong(v), eb = __double_as_longlong(e);
-        const int lo = __builtin_amdgcn_update_dpp((int)eb, (int)b, DPP_FROM_R1, 0xF, 0xF, false);
-        const int hi = __builtin_amdgcn_update_dpp((int)(eb >> 32), (int)(b >> 32), DPP_FROM_R1, 0xF, 0xF, false);
+        const int lo = __builtin_amdgcn_update_dpp((int)eb, (int)b, C, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_update_dpp((int)(eb >> 32), (int)(b >> 32), C, 0xF, 0xF, false);
         return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
     };
     r.mt = sh(x.mt, edge.mt);
@@ -432,7 +445,7 @@ __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &
 // with the strict order.
 // ---------------------------------------------------------------------
 
-template <int NP, int PAR>
+template <int NP, int PAR, int LPT = 16>
 __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool codon, bool rev,
                                          bool skew, bool trim, double (&v1)[NP], double (&v2)[NP],
                                          double (&v3)[NP], const RowRec (&row)[NP],
@@ -442,11 +455,11 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     // block-edge neighbours at kappa-1 (every lane shifts: uniform control flow)
     double E1;
     if (PAR == 0)
-        E1 = dpp_f64<DPP_FROM_L1>(v1[NP - 1]);   // (d-1) of pair 0 = lane q-1's last pair
+        E1 = dpp_f64<TaskLanes<LPT>::FROM_L1>(v1[NP - 1]);   // (d-1) of pair 0 = lane q-1's last pair
     else
-        E1 = dpp_f64<DPP_FROM_R1>(v1[0]);        // (d+1) of the last pair = lane q+1's pair 0
+        E1 = dpp_f64<TaskLanes<LPT>::FROM_R1>(v1[0]);        // (d+1) of the last pair = lane q+1's pair 0
     double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
-    if (codon) {
+    if (LPT == 16 && codon) {   // codon tasks are never lean, so never 64-lane
         if (NP == 1) {
             L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
             L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
@@ -537,12 +550,41 @@ __device__ __forceinline__ double dpp_rot_f64(double x)
 // finite match/mismatch/ins/del tables, so every in-band cell is finite (each
 // has an in-band predecessor chain to the origin) and the "new score is
 // invalid" check (align.jl:105-107) cannot fire here; the general steps keep it.
-template <int NP, int PAR>
+// LDS band-output swizzle of the lean blocks (NP >= 4).  Lane q writes the
+// cells of its pairs q*NP + r at one slot per r, i.e. 16 lanes at a stride of
+// NP doubles: with NP = 4 / 8 lanes q, q+8 (q+4, q+8, q+12) hit the same LDS
+// banks (2- / 4-way conflicts on every cell store).  Slot u is stored at
+// u ^ ((u >> 4) & 7): a permutation inside each aligned group of 8 slots
+// whose key differs between slots 32 apart, so the 16 lanes of a task land on
+// 16 distinct bank pairs; the flush reads 16-B pairs (u even, u + 1), which
+// stay one aligned pair (swapped when the key is odd).  Measured at c5
+// (DP-only, bw 18, profiles/r02_exp_dp_swz.json): bit-exact but slower
+// (30.2 -> 32.0 ms: the address arithmetic and registers cost more than the
+// conflicts), so it is off; the LDS output itself costs ~5 ms there
+// (DPL_NO_LDS_OUT diagnostic build: 30.2 -> 25.5 ms).
+#ifndef DPL_SWZ
+#define DPL_SWZ 0
+#endif
+template <int NP>
+__device__ __forceinline__ int dpl_swz(int u)
+{
+    return (DPL_SWZ && NP >= 4) ? (u ^ ((u >> 4) & 7)) : u;
+}
+template <int NP>
+__device__ __forceinline__ dvec2 dpl_rd2(const double *R, int u)   // u even
+{
+    const int U = dpl_swz<NP>(u);
+    const dvec2 v = *(const dvec2 *)(R + (U & ~1));
+    return (U & 1) ? dvec2{v.y, v.x} : v;
+}
+
+template <int NP, int PAR, int LPT = 16>
 __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], const double (&lb)[NP],
-                                         const bool (&st)[NP], double *o, int ostep)
+                                         const bool (&st)[NP], double *Rb, int u0, int ostep)
 {
-    const double E1 = PAR == 0 ? dpp_rot_f64<DPP_ROT_L1>(v1[NP - 1]) : dpp_rot_f64<DPP_ROT_R1>(v1[0]);
+    const double E1 = PAR == 0 ? dpp_rot_f64<TaskLanes<LPT>::ROT_L1>(v1[NP - 1])
+                               : dpp_rot_f64<TaskLanes<LPT>::ROT_R1>(v1[0]);
     double nv[NP];
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
@@ -553,7 +595,7 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
         nv[r] = raw + lb[r];
         if (st[r] && !DPL_NO_LDS_OUT)
-            o[r * ostep] = nv[r];
+            Rb[dpl_swz<NP>(u0 + r * ostep)] = nv[r];
     }
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
@@ -575,11 +617,17 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 // takes 4 (measured: NP = 2/4 at 16 need 280/430 VGPRs -> one wave per SIMD), so
 // that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
 // several waves per CU
-__host__ __device__ constexpr int dpl_b(int np) { return np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK); }
+#ifndef DPL_B64
+#define DPL_B64 8   // periods per block of the 64-lane tasks
+#endif
+__host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
+{
+    return lpt == 64 ? DPL_B64 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK));
+}
 #ifndef DPL_SPREAD
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
 #endif
-#define DPL_SPREAD_ON(np) (DPL_SPREAD && (np) == 1)
+#define DPL_SPREAD_ON(np, lpt) (DPL_SPREAD && (np) == 1 && (lpt) == 16)
 #ifndef DPR_WPE1
 #define DPR_WPE1 1   // minimum waves per SIMD requested for the NP = 1 kernels
 #endif
@@ -587,19 +635,19 @@ struct alignas(16) EdgeRec {
     double mt, mm, is, ds;
     int sb, col, pad0, pad1;
 };
-__host__ __device__ constexpr int dpl_pmax(int np) { return (16 * np) | 1; }   // band_P(32*NP-1)
+__host__ __device__ constexpr int dpl_pmax(int np, int lpt = 16) { return (lpt * np) | 1; }   // band_P(2*LPT*NP-1)
 // carry slots on either side of a task's band-output rows: a flush writes
 // whole 128-B lines only and carries the partial line into the next block
 constexpr int DPL_CARRY = 16;
-__host__ __device__ constexpr int dpl_task_bytes(int np, int pm)
+__host__ __device__ constexpr int dpl_task_bytes(int np, int pm, int lpt = 16)
 {
-    return (int)(dpl_b(np) * sizeof(EdgeRec)) + (2 * dpl_b(np) * pm + 2 * DPL_CARRY) * 8;
+    return (int)(dpl_b(np, lpt) * sizeof(EdgeRec)) + (2 * dpl_b(np, lpt) * pm + 2 * DPL_CARRY + 8) * 8;
 }
 __host__ __device__ constexpr int dpl_task_bytes(int np) { return dpl_task_bytes(np, dpl_pmax(np)); }
 // 16-B stores per lane of one flush: at most 2*DPL_B*P + DPL_CARRY doubles
-__host__ __device__ constexpr int dpl_flush_stores(int np, int pm)
+__host__ __device__ constexpr int dpl_flush_stores(int np, int pm, int lpt = 16)
 {
-    return (dpl_b(np) * pm + DPL_CARRY / 2 + 15) / 16;
+    return (dpl_b(np, lpt) * pm + DPL_CARRY / 2 + lpt - 1) / lpt;
 }
 // stride classes of the lean DP launches: k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
 // takes the lean tasks of NP class npi with P <= dpr_pm (the largest is the
@@ -623,16 +671,20 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 // its last pair.  For NP = 1 the host splits the lean class by P (11, 13,
 // 15, 17), so a c4 task with P = 11 issues 12 stores per lane per block
 // instead of 18.
-template <int NP, bool LEAN, int PM = dpl_pmax(NP)>
-__global__ void __launch_bounds__(64) DPR_ATTR __attribute__((amdgpu_waves_per_eu(NP == 1 ? DPR_WPE1 : 1)))
+#ifndef DPR_WPE64
+#define DPR_WPE64 2   // minimum waves per SIMD requested for the 64-lane kernels
+#endif
+template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16>
+__global__ void __launch_bounds__(64) DPR_ATTR
+__attribute__((amdgpu_waves_per_eu(LPT == 64 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
       double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink,
       const double *__restrict__ lut)
 {
-    constexpr int DPL_B = dpl_b(NP);
-    const int q = threadIdx.x & 15;
-    const int tid = blockIdx.x * 4 + (threadIdx.x >> 4);
+    constexpr int DPL_B = dpl_b(NP, LPT);
+    const int q = threadIdx.x & (LPT - 1);
+    const int tid = blockIdx.x * (64 / LPT) + threadIdx.x / LPT;
     DPTask T = {};
     if (tid < ntasks)
         T = tasks[tid];
@@ -661,7 +713,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         row[r] = load_row(T, rev, sbase, tb, pp - T.c, codon);   // kappa = 0
         col[r] = load_col(T, rev, tbase, -pp);
     }
-    const int top = 16 * NP - 1;
+    const int top = LPT * NP - 1;
     RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);   // enters at kappa = 1
 
     // Lean interior [klo, khi]: the kappa range in which every cell of every
@@ -714,8 +766,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // ---- blocked lean interior: DPL_B periods (2*DPL_B anti-diagonals)
             // per block, inputs and outputs staged in this task's LDS slice
             const int P = T.P;
-            const int t = threadIdx.x >> 4;
-            EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP, PM));
+            const int t = threadIdx.x / LPT;
+            EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP, PM, LPT));
             // line-aligned flushes: `fl` is the band position (doubles from the
             // band start, which is 256-B aligned) up to which (forward) or down
             // from which (reverse) the interior has been written.  A block's
@@ -725,14 +777,16 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const int blk = 2 * DPL_B * P;
             const ptrdiff_t g00 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
             ptrdiff_t fl = g00 + (rev ? blk : 0);
-            double *ob = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP, PM) + DPL_B * sizeof(EdgeRec)) +
-                         DPL_CARRY + (int)(g00 & 1);
+            // rows region R; slot u of R holds the band value at position
+            // g0 + (u - ub) of the block (dpl_swz: the physical LDS slot)
+            double *R = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP, PM, LPT) + DPL_B * sizeof(EdgeRec));
+            const int ub = DPL_CARRY + (int)(g00 & 1);
             // this lane's LDS slot per parity; a block's 2*DPL_B rows are the
             // contiguous global chunk (reverse: flipped rows)
             const int sl0 = rev ? (T.H - 1 - 2 * q * NP) >> 1 : q * NP;
             const int sl1 = rev ? (T.H - 2 - 2 * q * NP) >> 1 : q * NP;
             const int ostep = rev ? -1 : 1;
-            const int top_c = 16 * NP - T.c;
+            const int top_c = LPT * NP - T.c;
             // Edge records.  A task whose read has row codes (DPTask flag
             // RF_TASK_CODED) reads one 8-B code record per row from HBM and the
             // table values from the context's code dictionary (L2-resident),
@@ -788,8 +842,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // the next block, so the store stream stays steady instead of one
             // burst per block that stalls the issuing wave behind the memory
             // pipeline.  Before the first block the pending set is the sink.
-            constexpr int FL = dpl_flush_stores(NP, PM);
-            constexpr int FLS = DPL_SPREAD_ON(NP) ? FL : 1;
+            constexpr int FL = dpl_flush_stores(NP, PM, LPT);
+            constexpr int FLS = DPL_SPREAD_ON(NP, LPT) ? FL : 1;
             dvec2 pv[FLS];
             dvec2 *pg = (dvec2 *)sink;
             int pnu = 0;
@@ -797,7 +851,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 #pragma unroll
             for (int j = 0; j < FLS; ++j)
                 pv[j] = dvec2{0.0, 0.0};
-            if (!DPL_SPREAD_ON(NP)) {
+            if (!DPL_SPREAD_ON(NP, LPT)) {
                 // as many stores behind this load as the loop puts behind its
                 // own (to the sink), so that hipcc's wait for `pend` is vmcnt(FL)
                 // on every path into the loop, not vmcnt(0)
@@ -805,7 +859,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 const dvec2 z = {0.0, 0.0};
 #pragma unroll
                 for (int j = 0; j < FL; ++j)
-                    g[q + 16 * j] = z;
+                    g[q + LPT * j] = z;
             }
             wave_sync();
             for (int b = 0; b < nblk; ++b) {
@@ -818,23 +872,23 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     EdgeRec En;
                     if (p + 1 < DPL_B)
                         En = ein[p + 1];
-                    if (DPL_SPREAD_ON(NP)) {
+                    if (DPL_SPREAD_ON(NP, LPT)) {
 #pragma unroll
                         for (int j = p; j < FLS; j += DPL_B) {
-                            const int e = preal ? min(q + 16 * j, pnu - 1) : q + 16 * j;
+                            const int e = preal ? min(q + LPT * j, pnu - 1) : q + LPT * j;
                             DP_STORE(pg + e, pv[j]);
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     {   // even step: column k/2 enters lane 0
-                        const int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
+                        const int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
 #pragma unroll
                         for (int r = NP - 1; r > 0; --r)
                             col[r] = col[r - 1];
                         col[0] = from;
                     }
                     const int i0 = rev ? 2 * DPL_B - 1 - 2 * p : 2 * p;
-                    dpl_step<NP, 0>(v1, v2, row, col, lb[0], st[0], ob + i0 * P + sl0, ostep);
+                    dpl_step<NP, 0, LPT>(v1, v2, row, col, lb[0], st[0], R, ub + i0 * P + sl0, ostep);
                     {   // odd step: rows advance; lane 15 receives the edge row
                         RowRec e;
                         e.sb = E.sb;
@@ -842,14 +896,14 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                         e.mm = E.mm;
                         e.is = E.is;
                         e.ds = E.ds;
-                        const RowRec up = row_from_above(row[0], e, false);
+                        const RowRec up = row_from_above<LPT>(row[0], e, false);
 #pragma unroll
                         for (int r = 0; r < NP - 1; ++r)
                             row[r] = row[r + 1];
                         row[NP - 1] = up;
                     }
                     const int i1 = rev ? 2 * DPL_B - 2 - 2 * p : 2 * p + 1;
-                    dpl_step<NP, 1>(v1, v2, row, col, lb[1], st[1], ob + i1 * P + sl1, ostep);
+                    dpl_step<NP, 1, LPT>(v1, v2, row, col, lb[1], st[1], R, ub + i1 * P + sl1, ostep);
                     if (p + 1 < DPL_B)
                         E = En;
                 }
@@ -895,41 +949,41 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     const bool task_real = tid < ntasks && !(T.flags & 512);
                     const bool real = task_real && nu > 0;
                     dvec2 *g = real ? (dvec2 *)(band + lo2) : (dvec2 *)sink;
-                    const dvec2 *o2 = (const dvec2 *)(ob + (lo2 - g0));
-                    if (DPL_SPREAD_ON(NP)) {
+                    const int u2 = ub + (int)(lo2 - g0);   // even
+                    if (DPL_SPREAD_ON(NP, LPT)) {
 #pragma unroll
                         for (int j = 0; j < FLS; ++j)
-                            pv[j] = o2[real ? min(q + 16 * j, nu - 1) : 0];
+                            pv[j] = dpl_rd2<NP>(R, u2 + 2 * (real ? min(q + LPT * j, nu - 1) : 0));
                         pg = g;
                         pnu = nu;
                         preal = real;
                         if (last) {   // nothing follows: write the last block now
 #pragma unroll
                             for (int j = 0; j < FLS; ++j) {
-                                const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
+                                const int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
                                 DP_STORE(g + e, pv[j]);
                             }
                         }
                     } else {
 #pragma unroll
                         for (int j = 0; j < FL; ++j) {
-                            const int e = real ? min(q + 16 * j, nu - 1) : q + 16 * j;
-                            DP_STORE(g + e, real ? o2[e] : o2[0]);
+                            const int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
+                            DP_STORE(g + e, dpl_rd2<NP>(R, u2 + 2 * (real ? e : 0)));
                         }
                     }
                     if (task_real && q == 0 && (lo & 1))
-                        band[lo] = ob[lo - g0];
+                        band[lo] = R[dpl_swz<NP>(ub + (int)(lo - g0))];
                     if (task_real && q == 1 && (hi & 1))
-                        band[hi - 1] = ob[hi - 1 - g0];
+                        band[hi - 1] = R[dpl_swz<NP>(ub + (int)(hi - 1 - g0))];
                     // carry the unwritten partial line next to the next block's rows
                     if (!rev) {
                         const int c = (int)(g0 + blk - fl), src = (int)(fl - g0);
                         if (q < c)
-                            ob[src - blk + q] = ob[src + q];
+                            R[dpl_swz<NP>(ub + src - blk + q)] = R[dpl_swz<NP>(ub + src + q)];
                     } else {
                         const int c = (int)(fl - g0);
                         if (q < c)
-                            ob[blk + q] = ob[q];
+                            R[dpl_swz<NP>(ub + blk + q)] = R[dpl_swz<NP>(ub + q)];
                     }
                 }
                 wave_sync();
@@ -943,22 +997,22 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         if (k > 0) {
             // even step: columns advance; lane 0 receives column k/2
             const int edge = load_col(T, rev, tbase, k / 2);
-            const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], DPP_FROM_L1, 0xF, 0xF, false);
+            const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
 #pragma unroll
             for (int r = NP - 1; r > 0; --r)
                 col[r] = col[r - 1];
             col[0] = from;
         }
-        dpr_step<NP, 0>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err);
+        dpr_step<NP, 0, LPT>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err);
         if (k + 1 < kmax) {
             // odd step: rows advance; lane 15 receives the prefetched row
-            const RowRec up = row_from_above(row[0], nxt, codon);
+            const RowRec up = row_from_above<LPT>(row[0], nxt, codon);
 #pragma unroll
             for (int r = 0; r < NP - 1; ++r)
                 row[r] = row[r + 1];
             row[NP - 1] = up;
             nxt = load_row(T, rev, sbase, tb, top + (k + 2) / 2 + 1 - T.c, codon);
-            dpr_step<NP, 1>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
+            dpr_step<NP, 1, LPT>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
                             out_score, err);
         }
     }
@@ -1212,9 +1266,23 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
     const ScoreGroup G = groups[lo];
     const int64_t local = e - gstart[lo];
     const int64_t stride = (int64_t)(G.m + 1) * 9;
+    const double *src = split + G.split_off + local;
+    const int nr = G.r1 - G.r0;
+    // the left fold in read order (model.jl:389-393); 16 partials are loaded
+    // before they are added, so each lane keeps 16 streaming loads in flight
     double acc = 0.0;
-    for (int r = 0; r < G.r1 - G.r0; ++r)
-        acc += split[G.split_off + r * stride + local];
+    int r = 0;
+    for (; r + 16 <= nr; r += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            v[u] = __builtin_nontemporal_load(src + (int64_t)(r + u) * stride);
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            acc += v[u];
+    }
+    for (; r < nr; ++r)
+        acc += __builtin_nontemporal_load(src + (int64_t)r * stride);
     dense[G.dense_off + local] = acc;
 }
 
@@ -3533,6 +3601,7 @@ struct Opts {
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
     int seg_ver = 4;        // RF_OPT_SEG_VER: wide-band scorer 4 = k_score_segl, 3 = k_score_segc, 1 = k_score_seg
+    int dp_wide = 1;        // RF_OPT_DP_WIDE: lean bands in 64-lane tasks (bit 0: H 128..255, bit 1: H 64..127)
     int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
                             // 128-B-line rows for all its bands (0: never, 1: always)
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
@@ -3586,6 +3655,7 @@ struct rf_ctx {
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
+        size_t nw[2] = {};     // lean whole-wave tasks (RF_OPT_DP_WIDE)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -3805,6 +3875,7 @@ void load_env_opts(Opts &o)
     o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
     o.bt_win_kb = env_int("RIFRAF_BT_WIN_KB", o.bt_win_kb);
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
+    o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4050,6 +4121,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_BT_WIN_KB: return &o.bt_win_kb;
     case RF_OPT_STAGE_KB: return &o.stage_kb;
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
+    case RF_OPT_DP_WIDE: return &o.dp_wide;
     default: return nullptr;
     }
 }
@@ -4470,7 +4542,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4];
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2];
         int hmax64 = 0, hmaxg = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
@@ -4527,7 +4599,13 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
                 const int npi = t.H <= 31 ? 0 : t.H <= 63 ? 1 : t.H <= 127 ? 2 : 3;
                 const bool np8 = npi < 3 || (t.H <= 255 && ctx->opt.dp_np8 && ctx->opt.dp_np8_lean);
-                if (lean && ((psplit >> npi) & 1) && np8) {
+                // whole-wave tasks (k_dpr<NP, true, 64 NP | 1, 64>) for the wide lean
+                // bands: 1 task per wave at 2-4 waves per SIMD instead of 4 tasks per
+                // wave at one (the 16-lane NP = 4 / 8 kernels need > 256 registers)
+                const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
+                if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
+                    cw[wide].push_back(t);
+                } else if (lean && ((psplit >> npi) & 1) && np8) {
                     int pmi = 0;
                     while (pmi < 3 && t.P > dpr_pm(npi, pmi))
                         ++pmi;
@@ -4562,6 +4640,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 std::stable_sort(c.begin(), c.end(), by_len);
                 all.insert(all.end(), c.begin(), c.end());
             }
+        for (auto &c : cw) {
+            std::stable_sort(c.begin(), c.end(), by_len);
+            all.insert(all.end(), c.begin(), c.end());
+        }
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
@@ -4581,6 +4663,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 4; ++b)
                 P.nrp[a][b] = cp[a][b].size();
+        P.nw[0] = cw[0].size();
+        P.nw[1] = cw[1].size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -4619,6 +4703,11 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     launches.push_back({16 + 4 * a + b, at, P.nrp[a][b]});
                     at += P.nrp[a][b];
                 }
+        for (int a = 0; a < 2; ++a)
+            if (P.nw[a]) {
+                launches.push_back({32 + a, at, P.nw[a]});
+                at += P.nw[a];
+            }
         if (P.n64) {
             launches.push_back({8, at, P.n64});
             at += P.n64;
@@ -4663,7 +4752,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
-        } else if (L.kind >= 16) {
+        } else if (L.kind >= 16 && L.kind < 32) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
 #define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b)>
@@ -4673,6 +4762,15 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const int c = L.kind - 16, npi = c >> 2, pmi = c & 3;
             hipLaunchKernelGGL(kp[c], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)),
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
+                               (double *)ctx->scratch[7].p, d_lut);
+        } else if (L.kind >= 32) {
+            // whole-wave tasks: 32 = NP 2 (H <= 255), 33 = NP 1 (H <= 127)
+            using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
+                                 double *, const double *);
+            const KFn kw[2] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<1, true, dpl_pmax(1, 64), 64>};
+            const int a = L.kind - 32, np = a == 0 ? 2 : 1;
+            hipLaunchKernelGGL(kw[a], dim3(n), dim3(64), (size_t)dpl_task_bytes(np, dpl_pmax(np, 64), 64), st,
+                               d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;

@@ -12,7 +12,7 @@ bw = int(sys.argv[1]) if len(sys.argv) > 1 else 18
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
 t, reads = bench.make_read_shard(n, 10000, 0.03, bw, 2024, 0, n)
 e = Engine(0)
-e.reserve(sum(2 * bench.band_bytes(len(r), 10000, bw) for r in reads) + (256 << 20))
+e.reserve(sum(2 * bench.band_bytes(len(r), 10000, bw, pad=True) for r in reads) + (256 << 20))
 e.set_sequences(0, reads)
 e.set_templates(0, [t])
 sl = np.arange(n, dtype=np.int32)
