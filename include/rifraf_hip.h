@@ -103,9 +103,9 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_BAND_PAD    17   /* an rf_realign call whose widest band has H >= value
                                     lays out all its bands with kappa rows of whole
                                     128-B lines (default 64; 1 always, 0 never)       */
-#define RF_OPT_DP_WIDE     18   /* lean DP bands in whole-wave (64-lane) tasks: bit 0
-                                    H 128..255 (k_dpr<2,..,64>), bit 1 H 64..127
-                                    (k_dpr<1,..,64>); 0 = 16-lane tasks only         */
+#define RF_OPT_DP_WIDE     18   /* lean DP bands in wide tasks: bit 0 H 128..255 as
+                                    64-lane tasks (k_dpr<2,..,64>), bit 1 H 64..127 as
+                                    32-lane tasks (k_dpr<2,..,32>); 0 = 16-lane only */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

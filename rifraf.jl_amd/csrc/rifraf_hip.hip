@@ -320,15 +320,22 @@ __device__ __forceinline__ double dpp_f64(double x)
 #define DPP_FROM_L2 0x112   // row_shr:2 -> lane q-2
 #define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
 #define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
-// Lanes per DP task: 16 (one DPP row, 4 tasks per wave) or 64 (the whole
-// wave, wave_shr / wave_shl / wave_ror / wave_rol: the same moves across rows).
+// Lanes per DP task: 16 (one DPP row, 4 tasks per wave), 32 (two tasks per
+// wave) or 64 (the whole wave).  32 and 64 use wave_shr / wave_shl /
+// wave_ror / wave_rol, the same moves across DPP rows.  With 32 lanes the
+// wave shifts also cross the two tasks: lane 32 (31) would read lane 31's
+// (32's) value where it should read its task's edge, so those lanes select
+// the edge after the move (EDGE_FIX).  The rotations need no fix: the lanes
+// they wrap between hold a task's top pairs, whose diagonals are >= H (the
+// host's class bound), i.e. -Inf or masked, exactly as within a DPP row.
 template <int LPT>
 struct TaskLanes {
-    static_assert(LPT == 16 || LPT == 64, "tasks are one DPP row or one wave");
-    static constexpr int FROM_L1 = LPT == 64 ? 0x138 : 0x111;   // lane q-1 (edge lane 0 reads `old`)
-    static constexpr int FROM_R1 = LPT == 64 ? 0x130 : 0x101;   // lane q+1 (edge lane LPT-1 reads `old`)
-    static constexpr int ROT_L1 = LPT == 64 ? 0x13C : 0x121;    // lane (q-1) mod LPT
-    static constexpr int ROT_R1 = LPT == 64 ? 0x134 : 0x12F;    // lane (q+1) mod LPT
+    static_assert(LPT == 16 || LPT == 32 || LPT == 64, "tasks are 16, 32 or 64 lanes");
+    static constexpr int FROM_L1 = LPT >= 32 ? 0x138 : 0x111;   // lane q-1 (edge lane 0 reads `old`)
+    static constexpr int FROM_R1 = LPT >= 32 ? 0x130 : 0x101;   // lane q+1 (edge lane LPT-1 reads `old`)
+    static constexpr int ROT_L1 = LPT >= 32 ? 0x13C : 0x121;    // lane (q-1) mod LPT (or mod 64)
+    static constexpr int ROT_R1 = LPT >= 32 ? 0x134 : 0x12F;    // lane (q+1) mod LPT (or mod 64)
+    static constexpr bool EDGE_FIX = LPT == 32;
 };
 
 // Shift an int / double across the 16-lane DPP row (lanes outside the row
@@ -414,6 +421,13 @@ __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &
     r.mm = sh(x.mm, edge.mm);
     r.is = sh(x.is, edge.is);
     r.ds = sh(x.ds, edge.ds);
+    if (TaskLanes<LPT>::EDGE_FIX && (threadIdx.x & (LPT - 1)) == LPT - 1) {
+        r.sb = edge.sb;
+        r.mt = edge.mt;
+        r.mm = edge.mm;
+        r.is = edge.is;
+        r.ds = edge.ds;
+    }
     if (codon) {
         r.ci = sh(x.ci, edge.ci);
         r.cd = sh(x.cd, edge.cd);
@@ -622,7 +636,7 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 #endif
 __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 {
-    return lpt == 64 ? DPL_B64 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK));
+    return lpt >= 32 ? DPL_B64 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK));
 }
 #ifndef DPL_SPREAD
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
@@ -676,7 +690,7 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 #endif
 template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16>
 __global__ void __launch_bounds__(64) DPR_ATTR
-__attribute__((amdgpu_waves_per_eu(LPT == 64 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
+__attribute__((amdgpu_waves_per_eu(LPT >= 32 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
       double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink,
@@ -881,7 +895,9 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     {   // even step: column k/2 enters lane 0
-                        const int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
+                        int from = __builtin_amdgcn_update_dpp(E.col, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
+                        if (TaskLanes<LPT>::EDGE_FIX && q == 0)
+                            from = E.col;
 #pragma unroll
                         for (int r = NP - 1; r > 0; --r)
                             col[r] = col[r - 1];
@@ -997,7 +1013,9 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         if (k > 0) {
             // even step: columns advance; lane 0 receives column k/2
             const int edge = load_col(T, rev, tbase, k / 2);
-            const int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
+            int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
+            if (TaskLanes<LPT>::EDGE_FIX && q == 0)
+                from = edge;
 #pragma unroll
             for (int r = NP - 1; r > 0; --r)
                 col[r] = col[r - 1];
@@ -3591,6 +3609,9 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
+#ifndef DP_WIDE_DEFAULT
+#define DP_WIDE_DEFAULT 3
+#endif
 struct Opts {
     int score_mode = 0;     // RF_OPT_SCORE_MODE: 0 auto, 1 fused, 2 split
     int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg
@@ -3601,7 +3622,8 @@ struct Opts {
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
     int seg_ver = 4;        // RF_OPT_SEG_VER: wide-band scorer 4 = k_score_segl, 3 = k_score_segc, 1 = k_score_seg
-    int dp_wide = 1;        // RF_OPT_DP_WIDE: lean bands in 64-lane tasks (bit 0: H 128..255, bit 1: H 64..127)
+    int dp_wide = DP_WIDE_DEFAULT;   // RF_OPT_DP_WIDE: wide lean tasks (bit 0: H 128..255 in 64 lanes,
+                                     // bit 1: H 64..127 in 32 lanes)
     int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
                             // 128-B-line rows for all its bands (0: never, 1: always)
     int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
@@ -4599,9 +4621,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const int lean = (S.ncins == 0 && S.ncdel == 0 && S.finite && !(t.flags & 6)) ? 1 : 0;
                 const int npi = t.H <= 31 ? 0 : t.H <= 63 ? 1 : t.H <= 127 ? 2 : 3;
                 const bool np8 = npi < 3 || (t.H <= 255 && ctx->opt.dp_np8 && ctx->opt.dp_np8_lean);
-                // whole-wave tasks (k_dpr<NP, true, 64 NP | 1, 64>) for the wide lean
-                // bands: 1 task per wave at 2-4 waves per SIMD instead of 4 tasks per
-                // wave at one (the 16-lane NP = 4 / 8 kernels need > 256 registers)
+                // wide tasks for the wide lean bands: H 128..255 as one 64-lane
+                // task per wave, H 64..127 as two 32-lane tasks per wave, both NP = 2
+                // (the 16-lane NP = 4 / 8 kernels need > 256 registers: one wave
+                // per SIMD)
                 const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
                 if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
@@ -4764,14 +4787,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 32) {
-            // whole-wave tasks: 32 = NP 2 (H <= 255), 33 = NP 1 (H <= 127)
+            // wide-task classes: 32 = 64 lanes NP 2 (H <= 255), 33 = 32 lanes NP 2 (H <= 127)
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
-            const KFn kw[2] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<1, true, dpl_pmax(1, 64), 64>};
-            const int a = L.kind - 32, np = a == 0 ? 2 : 1;
-            hipLaunchKernelGGL(kw[a], dim3(n), dim3(64), (size_t)dpl_task_bytes(np, dpl_pmax(np, 64), 64), st,
-                               d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
-                               (double *)ctx->scratch[7].p, d_lut);
+            const KFn kw[2] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<2, true, dpl_pmax(2, 32), 32>};
+            const int a = L.kind - 32, lpt = a == 0 ? 64 : 32, tpw = 64 / lpt;
+            hipLaunchKernelGGL(kw[a], dim3((n + tpw - 1) / tpw), dim3(64),
+                               (size_t)tpw * dpl_task_bytes(2, dpl_pmax(2, lpt), lpt), st, d_tasks + L.at, n,
+                               d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 8) {
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
