@@ -263,7 +263,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--e2e-clusters", type=int, default=256,
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
-    ap.add_argument("--e2e-engines", type=int, default=2,
+    ap.add_argument("--e2e-engines", type=int, default=1,
                     help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")

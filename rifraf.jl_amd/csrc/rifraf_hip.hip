@@ -2392,24 +2392,37 @@ k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
 #else
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
+// S = 32: a kappa row's piece of a segment is one 128-B line; S = 16: half a
+// line (64 B, 64-B aligned), with fewer registers and 55 % of the LDS of
+// S = 32, so that two waves fit per SIMD.
+template <int S_>
 struct SeglGeo {
-    static constexpr int S = 32;        // diagonals per segment
+    static_assert(S_ == 16 || S_ == 32, "segments of 16 or 32 diagonals");
+    static constexpr int S = S_;        // diagonals per segment
     static constexpr int LS = 65;       // LDS row: columns a0 .. a0+64
-    static constexpr int NRW = S + 1;   // LDS rows: d = D-1 .. D+31
+    static constexpr int NRW = S + 1;   // LDS rows: d = D-1 .. D+S-1
     static constexpr int NROW = S + 128;   // kappa rows per segment
-    static constexpr int NUA = NROW * 8 / 64;        // 16-B chunks per lane and band, aligned rows
-    static constexpr int NUG = (NROW * 9 + 63) / 64; // odd-stride rows (9 chunks)
-    static constexpr int NT = S + 65;   // table rows: i - ib in [0, 97)
+    static constexpr int CPR = S / 4;      // 16-B chunks of a row piece (S/2 doubles), aligned rows
+    static constexpr int RPI = 64 / CPR;   // rows per wave-wide load
+    static constexpr int NUA = NROW * CPR / 64;          // chunks per lane and band, aligned rows
+    static constexpr int NC = CPR + 1;                   // pair-aligned chunks per row, odd stride
+    static constexpr int NUG = (NROW * NC + 63) / 64;
+    static constexpr int NT = S + 65;   // table rows: i - ib in [0, S + 65)
 };
+#ifndef SEGL_WPE16
+#define SEGL_WPE16 2   // waves per SIMD requested for S = 16
+#endif
 
-__global__ void __launch_bounds__(64)
+template <int SEGS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SEGS == 16 ? SEGL_WPE16 : 1)))
 k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
              const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
              const double *__restrict__ tabs, const double *__restrict__ bands,
              double *__restrict__ dense, double *__restrict__ split, int split_mode, int rchunk)
 {
-    using Gm = SeglGeo;
+    using Gm = SeglGeo<SEGS>;
     constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
+    constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
     constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
     __shared__ __attribute__((aligned(16))) double sA[SL];
     __shared__ __attribute__((aligned(16))) double sB[SL];
@@ -2442,8 +2455,8 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         tI[k] = 0.0;
         tS[k] = 0.0;
     }
-    // aligned-row loader lane roles: row r8 + 8j, 16-B chunk cc of the line
-    const int r8 = tid >> 3, cc8 = tid & 7, p8 = r8 & 1;
+    // aligned-row loader lane roles: row r8 + RPI j, 16-B chunk cc8 of the row piece
+    const int r8 = tid / CPR, cc8 = tid % CPR, p8 = r8 & 1;
     // per-read geometry: wave-uniform fields plus the lane's diagonal range
     struct RG {
         const double *gA;
@@ -2497,7 +2510,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         if ((g.P & 15) == 0) {
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
-                const int kap = min(kb + r8 + 8 * j, g.K - 1);
+                const int kap = min(kb + r8 + RPI * j, g.K - 1);
                 const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
                 ra[j] = *(const dvec2 *)(g.gA + o);
                 rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
@@ -2535,19 +2548,19 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
-                    const int col = (r8 + 8 * j - ddl) >> 1;    // a - a0
+                    const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0
                     const double v = h ? ra[j].y : ra[j].x, w = h ? rb[j].y : rb[j].x;
                     const int l = (ddl + 1) * LS + col;
-                    // rows 32..127 always land in [0, 64]; the parallelogram's
-                    // first / last 32 rows hold cells of the neighbouring items
-                    if ((j >= 4 && j < NUA - 4) || (col >= 0 && col <= 64)) {
+                    // rows S..127 always land in [0, 64]; the parallelogram's
+                    // first / last S rows hold cells of the neighbouring items
+                    if ((j * RPI >= S && (j + 1) * RPI <= 128) || (col >= 0 && col <= 64)) {
                         sA[l] = v;
                         sB[l] = w;
                     }
                 }
             }
         } else {
-            // odd-stride rows (narrow bands in a wide launch): 9 pair-aligned
+            // odd-stride rows (narrow bands in a wide launch): NC pair-aligned
             // chunks per row, loaded here in groups of 4 (not prefetched)
             const int kb = D + 2 * a0, eh = D >> 1;
 #pragma unroll 1
@@ -2555,8 +2568,8 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 dvec2 ga[4], gb[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
-                    const int t = min(tid + 64 * (j0 + jj), Gm::NROW * 9 - 1);
-                    const int rr = (t * 7282) >> 16, cc = t - 9 * rr;   // t / 9 for t < 1440
+                    const int t = min(tid + 64 * (j0 + jj), Gm::NROW * NC - 1);
+                    const int rr = t / NC, cc = t - NC * rr;
                     const int kap = min(kb + rr, g.K - 1);
                     const int o = ((kap * g.P + eh) & ~1) + 2 * cc;
                     ga[jj] = *(const dvec2 *)(g.gA + o);
@@ -2565,14 +2578,14 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int t = tid + 64 * (j0 + jj);
-                    const int rr = (t * 7282) >> 16, cc = t - 9 * rr;
+                    const int rr = t / NC, cc = t - NC * rr;
                     const int sh = (kb + rr + eh) & 1;   // P odd
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int xl = 2 * cc + h - sh;
                         const int ddl = 2 * xl + (rr & 1);
                         const int col = (rr - ddl) >> 1;
-                        if (t < Gm::NROW * 9 && xl >= 0 && xl < 16 && col >= 0 && col <= 64) {
+                        if (t < Gm::NROW * NC && xl >= 0 && xl < S / 2 && col >= 0 && col <= 64) {
                             const int l = (ddl + 1) * LS + col;
                             sA[l] = h ? ga[jj].y : ga[jj].x;
                             sB[l] = h ? gb[jj].y : gb[jj].x;
@@ -3609,6 +3622,9 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
+#ifndef SEG_S_DEFAULT
+#define SEG_S_DEFAULT 24
+#endif
 #ifndef DP_WIDE_DEFAULT
 #define DP_WIDE_DEFAULT 3
 #endif
@@ -3618,7 +3634,7 @@ struct Opts {
     int lean_nw = 8;        // RF_OPT_LEAN_NW: 8 = k_score_ws, 1/2/4 = k_score_lean waves
     int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: 0 = default budget
     int ws_q = 256;         // RF_OPT_WS_Q: k_score_ws chain lanes (256 or 128)
-    int seg_s = 24;         // RF_OPT_SEG_S: k_score_seg diagonals per segment (16, 24, 32)
+    int seg_s = SEG_S_DEFAULT;   // RF_OPT_SEG_S: diagonals per segment (k_score_segl: 16 or 32; seg/segc: 16, 24, 32)
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
     int seg_ver = 4;        // RF_OPT_SEG_VER: wide-band scorer 4 = k_score_segl, 3 = k_score_segc, 1 = k_score_seg
@@ -3972,8 +3988,13 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
             rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
-        hipLaunchKernelGGL(k_score_segl, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
-                           d_bands, dense, split, sm, rchunk);
+        // RF_OPT_SEG_S 16: half-line segments (two waves per SIMD), else 32
+        if (ctx->opt.seg_s == 16)
+            hipLaunchKernelGGL(k_score_segl<16>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm, rchunk);
+        else
+            hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm, rchunk);
     } else if (pk.seg && ctx->opt.seg_ver == 3) {
         int rchunk = 1;
         if (split) {
