@@ -480,8 +480,8 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "segc16", "segc24", "segc32",
-                                  "segcpad", "seg16", "seg24", "seg32", "general"])
+@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "segl16", "segl16odd", "segl16pad",
+                                  "segc16", "segc24", "segc32", "segcpad", "seg16", "seg24", "seg32", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
@@ -495,6 +495,11 @@ def test_score_wide_bands(engine, opts, mode, kern):
     opts("band_pad", 64)
     if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
+    elif kern.startswith("segl16"):
+        # k_score_segl<16>: half-line segments; default, odd-only, all-padded strides
+        opts("score_kernel", "auto")
+        opts("seg_s", 16)
+        opts("band_pad", {"segl16": 64, "segl16odd": 0, "segl16pad": 1}[kern])
     elif kern in ("seglodd", "seglpad"):
         opts("score_kernel", "auto")
         opts("band_pad", 0 if kern == "seglodd" else 1)
