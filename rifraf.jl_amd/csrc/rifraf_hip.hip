@@ -1353,6 +1353,53 @@ __device__ __forceinline__ double vmax(double a, double b)
 }
 
 
+// One row of the four new-column chains of a lane (score_nocodon's update
+// over MATCH / INSERT / DELETE, model.jl:262-270, then summax's running max
+// against B, util.jl:40-48): best_k = max(aprev + sub_k, prev_k + ins, dl),
+// accI_k = max(accI_k, best_k + bI), accS_k = max(accS_k, best_k + bS).
+// Issued phase by phase across the four chains, so that no FP64 op waits on
+// the op issued right before it (CHAIN_PHASED 0: chain by chain, the same
+// values).
+#ifndef CHAIN_PHASED
+#define CHAIN_PHASED 1
+#endif
+__device__ __forceinline__ void chain_row(double aprev, const double (&sub)[4], double ins, double dl, double bI,
+                                          double bS, double (&prev)[4], double (&accI)[4], double (&accS)[4])
+{
+#if CHAIN_PHASED
+    double x[4], y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        x[k] = aprev + sub[k];
+        y[k] = prev[k] + ins;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        x[k] = vmax(x[k], y[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        prev[k] = vmax(x[k], dl);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        x[k] = prev[k] + bI;
+        y[k] = prev[k] + bS;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        accI[k] = vmax(accI[k], x[k]);
+        accS[k] = vmax(accS[k], y[k]);
+    }
+#else
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double best = vmax(vmax(aprev + sub[k], prev[k] + ins), dl);
+        prev[k] = best;
+        accI[k] = vmax(accI[k], best + bI);
+        accS[k] = vmax(accS[k], best + bS);
+    }
+#endif
+}
+
 // Geometry of one staged (read, lanes [la0, la1]) window.
 struct LeanWin {
     int kw0, shift, n16, win;   // kappa rows from kw0, 16-B chunks per band, doubles per band slot
@@ -1456,14 +1503,9 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         const double bS = bSr + smask;
         const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
         const double dl = ac + u2.y;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
-            prev[k] = best;
-            accI[k] = vmax(accI[k], best + bI);
-            accS[k] = vmax(accS[k], best + bS);
-        }
-        dd = vmax(dd, ac + bS);
+        const double dsum = ac + bS;
+        chain_row(aprev, sub, u2.x, dl, bI, bS, prev, accI, accS);
+        dd = vmax(dd, dsum);
         aprev = ac;
         ac = acn;
         bI = bIn;
@@ -2409,6 +2451,9 @@ struct SeglGeo {
     static constexpr int NUG = (NROW * NC + 63) / 64;
     static constexpr int NT = S + 65;   // table rows: i - ib in [0, S + 65)
 };
+#ifndef SEGL_PF16
+#define SEGL_PF16 1    // S = 16: register prefetch of the next segment (0: load at its store)
+#endif
 #ifndef SEGL_WPE16
 #define SEGL_WPE16 2   // waves per SIMD requested for S = 16
 #endif
@@ -2423,6 +2468,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     using Gm = SeglGeo<SEGS>;
     constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
     constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
+    constexpr bool PF = SEGS == 32 || SEGL_PF16;   // next segment prefetched into registers
     constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
     __shared__ __attribute__((aligned(16))) double sA[SL];
     __shared__ __attribute__((aligned(16))) double sB[SL];
@@ -2626,7 +2672,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         gn = g;
     }
     int D0 = g.dlo & ~(S - 1), D = D0;
-    if (r < r1 && do_load)
+    if (PF && r < r1 && do_load)
         load_seg(g, D, true);
     double prev[4], accI[4], accS[4], dd = -RF_INF;
 #pragma unroll
@@ -2641,6 +2687,8 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         const int dfmax = g.dfmax, dlmin = g.dlmin;
         const bool peel = g.peel;
         wave_sync();   // previous segment's chains are done with LDS
+        if (!PF && do_load)
+            load_seg(g, D, D == D0);   // no register prefetch: the other waves hide the latency
         // LDS row 0 = diagonal D-1: the previous segment's row 32, or prefetched
         if (D == D0) {
             if (D > 0) {
@@ -2666,7 +2714,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         const bool last = D + S > dhi;
         if (last && more)
             setup(r + 1, gn);
-        if (do_load && (!last || more)) {
+        if (PF && do_load && (!last || more)) {
             const RG gl = last ? gn : g;
             load_seg(gl, last ? (gn.dlo & ~(S - 1)) : D + S, last);
         }
@@ -2700,14 +2748,9 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 const double bS = ((decltype(alls)::value || hasS) ? o.bs : o.bI) + smask;
                 const double sub[4] = {o.u0.x, o.u0.y, o.u1.x, o.u1.y};
                 const double dl = o.ac + o.u2.y;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const double best = vmax(vmax(aprev + sub[k], prev[k] + o.u2.x), dl);
-                    prev[k] = best;
-                    accI[k] = vmax(accI[k], best + o.bI);
-                    accS[k] = vmax(accS[k], best + bS);
-                }
-                dd = vmax(dd, o.ac + bS);
+                const double dsum = o.ac + bS;
+                chain_row(aprev, sub, o.u2.x, dl, o.bI, bS, prev, accI, accS);
+                dd = vmax(dd, dsum);
                 aprev = o.ac;
             };
             if (all_act && dfmax <= D && dlmin >= D + S - 1) {

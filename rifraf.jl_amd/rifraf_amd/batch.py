@@ -313,7 +313,8 @@ def _wave_native(part, params, engine):
             all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
         all_s += [DNASeq(x) for x in kw["dnaseqs"]]
         nread.append(len(kw["dnaseqs"]))
-    if phred_in and all_lp and min(int(np.min(p)) for p in all_lp if len(p)) < 0:
+    cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
+    if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
         raise RifrafError("phred score cannot be negative")
     lens = np.array([len(x) for x in all_s], np.int64)
     if (lens == 0).any() or any(len(x) != len(y) for x, y in zip(all_s, all_lp)):
@@ -321,10 +322,10 @@ def _wave_native(part, params, engine):
     soff = np.zeros(len(all_s) + 1, np.int64)
     np.cumsum(lens, out=soff[1:])
     # one division / ufunc pass over every read (elementwise: equal to per-read calls)
-    lp = phred_to_log_p(np.concatenate(all_lp)) if phred_in else np.concatenate(
+    lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
         [np.asarray(x, np.float64) for x in all_lp])
     allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
-                                               phreds=np.concatenate(all_lp).astype(np.int8) if phred_in else None)
+                                               phreds=cat_lp.astype(np.int8) if phred_in else None)
     nread = np.array(nread, np.int32)
     read_off = np.zeros(K + 1, np.int32)
     np.cumsum(nread, out=read_off[1:])

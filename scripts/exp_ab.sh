@@ -1,15 +1,16 @@
 #!/bin/bash
-# Same-box A/B of the c4 bench under environment settings, alternating:
-# exp_ab.sh DIR ROUNDS "tagA=VAR=val,..." "tagB=VAR=val,..." ...
+# A/B of library builds on the c4 step and the c5 secondary line (no CPU
+# baseline, no e2e): exp_ab.sh DIR lib1 lib2 ... (rifraf.jl_amd/librifraf_<lib>.so),
+# alternated twice.  Prints dp / score ms and GCUPS per run.
 set -o pipefail
-D=gpurun_out/${1:-r02ab}; R=${2:-2}; shift 2
+D=gpurun_out/${1:-ab}; shift
 mkdir -p $D
-for r in $(seq 1 $R); do
-  for spec in "$@"; do
-    tag=${spec%%=*}; vars=${spec#*=}
-    f=$D/${tag}_$r
-    env $(echo $vars | tr ',' ' ') timeout -k 10 200 python bench.py --no-cpu --no-secondary --e2e-clusters 0 --steps 10 --warmup 3 > $f.json 2> $f.err \
-      || { echo "bench $tag failed"; tail -20 $f.err; exit 1; }
-    python -c "import json; d=json.load(open('$f.json')); print('$tag', $r, 'value', round(d['value'],1), 'dp_ms', round(d['dp_ms'],2), 'score_ms', round(d['score_ms'],2))"
+for rep in 1 2; do
+  for v in "$@"; do
+    RIFRAF_HIP_LIB=$PWD/rifraf.jl_amd/librifraf_$v.so timeout -k 10 300 python bench.py --no-cpu --e2e-clusters 0 --steps 5 --warmup 2 \
+      > $D/${v}_$rep.json 2> $D/${v}_$rep.err || { echo "bench $v failed"; tail -20 $D/${v}_$rep.err; exit 1; }
+    python -c "
+import json; d=json.load(open('$D/${v}_$rep.json')); s=d['secondary']
+print('$v', $rep, 'c4 dp %.2f score %.2f gcups %.1f %s | c5 dp %.2f score %.2f gcups %.1f %s' % (d['dp_ms'], d['score_ms'], d['value'], d['parity']['bitexact'], s['dp_ms'], s['score_ms'], s['value'], s['parity']['bitexact']))"
   done
 done
