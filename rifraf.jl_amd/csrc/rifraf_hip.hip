@@ -1360,6 +1360,9 @@ __device__ __forceinline__ double vmax(double a, double b)
 // Issued phase by phase across the four chains, so that no FP64 op waits on
 // the op issued right before it (CHAIN_PHASED 0: chain by chain, the same
 // values).
+#ifndef CHAIN_LA
+#define CHAIN_LA 1   // k_score_ws / k_score_lean chains: rows of operands read ahead (1 or 2)
+#endif
 #ifndef CHAIN_PHASED
 #define CHAIN_PHASED 1
 #endif
@@ -1490,6 +1493,47 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         accI[k] = -RF_INF;
         accS[k] = -RF_INF;
     }
+#if CHAIN_LA == 2
+    // operands two rows ahead (LDS latency under four chain waves exceeds
+    // one row's arithmetic); the reads past row ilast + 1 stay inside the
+    // workgroup's LDS and are never used
+    struct RowOps {
+        double ac, bI, bS;
+        double2 u0, u1, u2;
+    };
+    auto ldrow = [&](int ix, int dx, const double *t) {
+        RowOps o;
+        o.ac = sA[ix];
+        o.bI = sB[ix];
+        o.bS = sB[ix + sofs + (sodd & dx)];
+        o.u0 = ((const double2 *)t)[0];
+        o.u1 = ((const double2 *)t)[1];
+        o.u2 = ((const double2 *)t)[2];
+        return o;
+    };
+    RowOps c0 = ldrow(idx, d, tr);
+    idx += P + (d & 1);
+    ++d;
+    tr += 6;
+    RowOps c1 = ldrow(idx, d, tr);
+    for (int i = i0; i <= ilast; ++i) {
+        idx += P + (d & 1);
+        ++d;
+        tr += 6;
+        const RowOps c2 = ldrow(idx, d, tr);
+        const double bS = c0.bS + smask;
+        const double sub[4] = {c0.u0.x, c0.u0.y, c0.u1.x, c0.u1.y};
+        const double dl = c0.ac + c0.u2.y;
+        const double dsum = c0.ac + bS;
+        chain_row(aprev, sub, c0.u2.x, dl, c0.bI, bS, prev, accI, accS);
+        dd = vmax(dd, dsum);
+        aprev = c0.ac;
+        c0 = c1;
+        c1 = c2;
+    }
+    const double bSr = c0.bS;
+    const double2 u0 = c0.u0, u1 = c0.u1, u2 = c0.u2;
+#else
     double ac = sA[idx], bI = sB[idx], bSr = sB[idx + sofs + (sodd & d)];
     double2 u0 = ((const double2 *)tr)[0], u1 = ((const double2 *)tr)[1], u2 = ((const double2 *)tr)[2];
     for (int i = i0; i <= ilast; ++i) {
@@ -1514,6 +1558,7 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         u1 = v1;
         u2 = v2;
     }
+#endif
     if (i1 > ilast) {
         // last row of the new column lies below A/B column a's band (a < m)
         const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
@@ -1708,7 +1753,7 @@ __device__ __forceinline__ void wg_barrier()
 #define WS_NPF128 20
 #endif
 #ifndef WS_NPF
-#define WS_NPF 22
+#define WS_NPF 19
 #endif
 
 template <int NPF, int Q>
