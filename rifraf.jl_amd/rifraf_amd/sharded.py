@@ -30,11 +30,11 @@ Ownership:
 Exchange and exactness:
   - realign / backtrace results are per job; they are gathered verbatim, so
     `rescore!`'s host fold is bit-identical to one GPU;
-  - `score` (proposal lists: get_candidates, estimate_probs) continues ONE
-    left fold along the ranks: rank 0 starts at 0.0, adds its reads' scores
-    in batch order and hands the running P-vector to rank 1, and so on; the
-    reference is added last.  This is the reference's own summation order,
-    so totals are bit-identical to one GPU (and to model.jl:389-397);
+  - `score` (proposal lists: get_candidates, estimate_probs): each rank
+    scores its own reads, one tensor all-gather collects every read's score
+    column, and every rank folds them in batch order starting at 0.0, the
+    reference last.  This is the reference's own summation order, so totals
+    are bit-identical to one GPU (and to model.jl:389-397);
   - `score_dense` (all proposals of a cluster, the throughput path) has every
     rank fold its own reads on the device (rf_score_dense_dev), all-gathers
     the partial vectors over RCCL and sums them in rank order on the device.
@@ -114,21 +114,6 @@ class ShardedEngine:
         for e in errs:
             if e is not None:
                 raise RifrafError(e)
-
-    def _send(self, vec: np.ndarray, dst: int):
-        self.dist.send(self.torch.from_numpy(np.ascontiguousarray(vec)).to(self.dev),
-                       dst=self._global(dst), group=self.group)
-
-    def _recv(self, n: int, src: int) -> np.ndarray:
-        t = self.torch.empty(n, dtype=self.torch.float64, device=self.dev)
-        self.dist.recv(t, src=self._global(src), group=self.group)
-        return t.cpu().numpy()
-
-    def _bcast(self, vec, src: int, n: int) -> np.ndarray:
-        t = (self.torch.from_numpy(np.ascontiguousarray(vec)).to(self.dev) if self.rank == src
-             else self.torch.empty(n, dtype=self.torch.float64, device=self.dev))
-        self.dist.broadcast(t, src=self._global(src), group=self.group)
-        return t.cpu().numpy()
 
     def _global(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
@@ -229,56 +214,71 @@ class ShardedEngine:
         return obj[0]
 
     # ------------------------------------------------------------------
+    def owned_by(self, rank: int, slots) -> np.ndarray:
+        """Mask of the slots `rank` owns (the same rule as owned())."""
+        slots = np.asarray(slots, np.int64)
+        lo, hi = self.bounds[rank], self.bounds[rank + 1]
+        mine = (slots >= lo) & (slots < hi)
+        if rank == self.world - 1:
+            mine |= slots >= self.nslots
+        return mine
+
     def score(self, groups, per_seq: bool = False):
-        """Proposal-list scoring with the reference's exact left fold carried
-        from rank to rank (see the module docstring)."""
-        totals, mats = [], []
+        """Proposal-list scoring (get_candidates, estimate_probs): every rank
+        scores its own reads (and the reference when it owns the reference
+        slot) against every proposal; ONE tensor all-gather (RCCL / gloo) of
+        the padded per-read score matrices of all groups; every rank then
+        folds the columns in batch order, 0.0 + s_1 + ... + s_R, and adds the
+        reference last -- the reference's own order (model.jl:389-397), so the
+        totals are bit-identical to one GPU.  Three collectives per call
+        (errors, lengths, scores), whatever the world size and group count."""
+        torch = self.torch
+        arrs, local, err = [], [], None
         for bslots, ref, props in groups:
             k, p, b = props if isinstance(props, tuple) else to_arrays(props)
             P = len(k)
             bslots = np.asarray(bslots, np.int32)
             own = self.owned(bslots)
             mine_ref = ref >= 0 and self.owner(ref) == self.rank
-            err, per = None, np.zeros((P, int(own.sum()) + (1 if mine_ref else 0)))
-            if (own.any() or mine_ref) and P > 0:
+            per = np.zeros((P, int(own.sum()) + (1 if mine_ref else 0)))
+            if (own.any() or mine_ref) and P > 0 and err is None:
                 try:
                     _, m = self.e.score([(bslots[own], ref if mine_ref else -1, (k, p, b))], per_seq=True)
-                    per = m[0]
+                    per = np.asarray(m[0], np.float64).reshape(P, -1)
                 except RifrafError as e:
                     err = str(e)
-            self._raise_any(err)
-            n_own = int(own.sum())
-            owners = [self.owner(s) for s in bslots]
-            chain = all(a <= c for a, c in zip(owners, owners[1:]))
-            if per_seq or not chain or P == 0:
-                # gather every column and fold in batch order on every rank
-                parts = self._gather((np.flatnonzero(own), per))
-                full = np.empty((P, len(bslots) + (1 if ref >= 0 else 0)))
-                for idx, m in parts:
-                    full[:, idx] = m[:, :len(idx)]
-                    if m.shape[1] > len(idx):
-                        full[:, -1] = m[:, -1]
-                acc = np.zeros(P)
-                for j in range(full.shape[1]):
-                    acc = acc + full[:, j]
-                totals.append(acc)
-                mats.append(full)
-                continue
-            # chain: ranks in order continue one left fold; the reference is last
-            acc = np.zeros(P) if self.rank == 0 else self._recv(P, self.rank - 1)
-            for j in range(n_own):
-                acc = acc + per[:, j]
-            last = self.world - 1
-            ref_owner = self.owner(ref) if ref >= 0 else last
-            if self.rank < last:
-                self._send(acc, self.rank + 1)
-            elif ref_owner != last:
-                self._send(acc, ref_owner)
-            if ref >= 0 and self.rank == ref_owner:
-                if ref_owner != last:
-                    acc = self._recv(P, last)
-                acc = acc + per[:, -1]
-            totals.append(self._bcast(acc, ref_owner, P))
+            arrs.append((P, bslots, ref))
+            local.append(per)
+        self._raise_any(err)
+        flat = np.concatenate([x.reshape(-1) for x in local]) if local else np.zeros(0)
+        n = torch.tensor([flat.size], dtype=torch.int64, device=self.dev)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        ns = [int(x.item()) for x in ns]
+        buf = torch.zeros(max(max(ns), 1), dtype=torch.float64, device=self.dev)
+        buf[:flat.size] = torch.from_numpy(flat).to(self.dev)
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(parts, buf, group=self.group)
+        parts = [x.cpu().numpy() for x in parts]
+        at = [0] * self.world
+        totals, mats = [], []
+        for P, bslots, ref in arrs:
+            R = len(bslots)
+            full = np.empty((P, R + (1 if ref >= 0 else 0)))
+            ref_owner = self.owner(ref) if ref >= 0 else -1
+            for r in range(self.world):
+                idx = np.flatnonzero(self.owned_by(r, bslots))
+                cols = len(idx) + (1 if r == ref_owner else 0)
+                m = parts[r][at[r]:at[r] + P * cols].reshape(P, cols)
+                at[r] += P * cols
+                full[:, idx] = m[:, :len(idx)]
+                if r == ref_owner:
+                    full[:, -1] = m[:, -1]
+            acc = np.zeros(P)
+            for j in range(full.shape[1]):
+                acc = acc + full[:, j]
+            totals.append(acc)
+            mats.append(full)
         return (totals, mats) if per_seq else totals
 
     # ------------------------------------------------------------------

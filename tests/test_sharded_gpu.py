@@ -97,10 +97,20 @@ def _w_rccl_dense(rank, world):
     v1 = sh.realign(np.arange(n), np.arange(n), np.repeat([0, 1], 6), [9] * n, RF_FWD | RF_BWD)
     got = sh.score_dense(groups)
     assert sh.last_dense.is_cuda
+    from _util import all_proposals_arrays
+    props = all_proposals_arrays(tpls[0])
+    plain2 = Engine(0)
+    plain2.set_sequences(0, flat)
+    plain2.set_templates(0, tpls)
+    plain2.realign(np.arange(n), np.arange(n), np.repeat([0, 1], 6), [9] * n, RF_FWD | RF_BWD)
+    want_list = plain2.score([(groups[0], -1, props)])[0]
+    plain2.close()
+    got_list = sh.score([(groups[0], -1, props)])[0]
     x = torch.arange(10, dtype=torch.float64, device="cuda:0")
     y = allgather_fold(x, dist)
     sh.close()
-    return {"v0": v0, "v1": v1, "want": want, "got": got, "fold": y.cpu().numpy()}
+    return {"v0": v0, "v1": v1, "want": want, "got": got, "fold": y.cpu().numpy(),
+            "want_list": want_list, "got_list": got_list}
 
 
 def test_rccl_world1_dense_exchange():
@@ -111,3 +121,4 @@ def test_rccl_world1_dense_exchange():
     for a, b in zip(got["want"], got["got"]):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(got["fold"], np.arange(10, dtype=np.float64))
+    np.testing.assert_array_equal(got["want_list"], got["got_list"])
