@@ -103,9 +103,10 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_BAND_PAD    17   /* an rf_realign call whose widest band has H >= value
                                     lays out all its bands with kappa rows of whole
                                     128-B lines (default 64; 1 always, 0 never)       */
-#define RF_OPT_DP_WIDE     18   /* lean DP bands in wide tasks: bit 0 H 128..255 as
-                                    64-lane tasks (k_dpr<2,..,64>), bit 1 H 64..127 as
-                                    32-lane tasks (k_dpr<2,..,32>); 0 = 16-lane only */
+#define RF_OPT_DP_WIDE     18   /* lean DP task widths: bit 0 H 128..255 as 64-lane
+                                    tasks (k_dpr<2,..,64>), bit 1 H 64..127 as 32-lane
+                                    tasks (k_dpr<2,..,32>), bit 2 H <= 31 as 8-lane
+                                    tasks (k_dpr<2,..,8>); 0 = 16-lane tasks only   */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

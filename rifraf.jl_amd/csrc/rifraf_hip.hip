@@ -320,8 +320,8 @@ __device__ __forceinline__ double dpp_f64(double x)
 #define DPP_FROM_L2 0x112   // row_shr:2 -> lane q-2
 #define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
 #define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
-// Lanes per DP task: 16 (one DPP row, 4 tasks per wave), 32 (two tasks per
-// wave) or 64 (the whole wave).  32 and 64 use wave_shr / wave_shl /
+// Lanes per DP task: 8 (half a DPP row, 8 tasks per wave), 16 (one DPP
+// row, 4 tasks per wave), 32 (two tasks per wave) or 64 (the whole wave).  32 and 64 use wave_shr / wave_shl /
 // wave_ror / wave_rol, the same moves across DPP rows.  With 32 lanes the
 // wave shifts also cross the two tasks: lane 32 (31) would read lane 31's
 // (32's) value where it should read its task's edge, so those lanes select
@@ -330,12 +330,14 @@ __device__ __forceinline__ double dpp_f64(double x)
 // host's class bound), i.e. -Inf or masked, exactly as within a DPP row.
 template <int LPT>
 struct TaskLanes {
-    static_assert(LPT == 16 || LPT == 32 || LPT == 64, "tasks are 16, 32 or 64 lanes");
+    static_assert(LPT == 8 || LPT == 16 || LPT == 32 || LPT == 64, "tasks are 8, 16, 32 or 64 lanes");
     static constexpr int FROM_L1 = LPT >= 32 ? 0x138 : 0x111;   // lane q-1 (edge lane 0 reads `old`)
     static constexpr int FROM_R1 = LPT >= 32 ? 0x130 : 0x101;   // lane q+1 (edge lane LPT-1 reads `old`)
     static constexpr int ROT_L1 = LPT >= 32 ? 0x13C : 0x121;    // lane (q-1) mod LPT (or mod 64)
     static constexpr int ROT_R1 = LPT >= 32 ? 0x134 : 0x12F;    // lane (q+1) mod LPT (or mod 64)
-    static constexpr bool EDGE_FIX = LPT == 32;
+    // 8-lane tasks (two per DPP row) use the row moves; like 32-lane tasks
+    // their shifts cross into the neighbouring task
+    static constexpr bool EDGE_FIX = LPT == 32 || LPT == 8;
 };
 
 // Shift an int / double across the 16-lane DPP row (lanes outside the row
@@ -631,12 +633,15 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 // takes 4 (measured: NP = 2/4 at 16 need 280/430 VGPRs -> one wave per SIMD), so
 // that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
 // several waves per CU
+#ifndef DPL_B8
+#define DPL_B8 4    // periods per block of the 8-lane tasks (8 tasks' LDS slices per wave)
+#endif
 #ifndef DPL_B64
 #define DPL_B64 8   // periods per block of the 64-lane tasks
 #endif
 __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 {
-    return lpt >= 32 ? DPL_B64 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK));
+    return lpt >= 32 ? DPL_B64 : (lpt == 8 ? DPL_B8 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK)));
 }
 #ifndef DPL_SPREAD
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
@@ -992,14 +997,19 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     if (task_real && q == 1 && (hi & 1))
                         band[hi - 1] = R[dpl_swz<NP>(ub + (int)(hi - 1 - g0))];
                     // carry the unwritten partial line next to the next block's rows
+                    // (fewer than 16 doubles: one pass of a 16-lane task, two of an 8-lane one)
                     if (!rev) {
                         const int c = (int)(g0 + blk - fl), src = (int)(fl - g0);
-                        if (q < c)
-                            R[dpl_swz<NP>(ub + src - blk + q)] = R[dpl_swz<NP>(ub + src + q)];
+#pragma unroll
+                        for (int x = q; x < (LPT < 16 ? 16 : LPT); x += LPT)
+                            if (x < c)
+                                R[dpl_swz<NP>(ub + src - blk + x)] = R[dpl_swz<NP>(ub + src + x)];
                     } else {
                         const int c = (int)(fl - g0);
-                        if (q < c)
-                            R[dpl_swz<NP>(ub + blk + q)] = R[dpl_swz<NP>(ub + q)];
+#pragma unroll
+                        for (int x = q; x < (LPT < 16 ? 16 : LPT); x += LPT)
+                            if (x < c)
+                                R[dpl_swz<NP>(ub + blk + x)] = R[dpl_swz<NP>(ub + x)];
                     }
                 }
                 wave_sync();
@@ -3781,7 +3791,7 @@ struct rf_ctx {
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
-        size_t nw[2] = {};     // lean whole-wave tasks (RF_OPT_DP_WIDE)
+        size_t nw[3] = {};     // lean wide / narrow-task classes (RF_OPT_DP_WIDE)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -4673,7 +4683,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2];
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[3];
         int hmax64 = 0, hmaxg = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
@@ -4734,7 +4744,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // task per wave, H 64..127 as two 32-lane tasks per wave, both NP = 2
                 // (the 16-lane NP = 4 / 8 kernels need > 256 registers: one wave
                 // per SIMD)
-                const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
+                const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : (npi == 0 ? 2 : -1));
                 if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
                 } else if (lean && ((psplit >> npi) & 1) && np8) {
@@ -4795,8 +4805,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 4; ++b)
                 P.nrp[a][b] = cp[a][b].size();
-        P.nw[0] = cw[0].size();
-        P.nw[1] = cw[1].size();
+        for (int a = 0; a < 3; ++a)
+            P.nw[a] = cw[a].size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -4835,7 +4845,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     launches.push_back({16 + 4 * a + b, at, P.nrp[a][b]});
                     at += P.nrp[a][b];
                 }
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 3; ++a)
             if (P.nw[a]) {
                 launches.push_back({32 + a, at, P.nw[a]});
                 at += P.nw[a];
@@ -4896,11 +4906,13 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 32) {
-            // wide-task classes: 32 = 64 lanes NP 2 (H <= 255), 33 = 32 lanes NP 2 (H <= 127)
+            // task-width classes, all NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
+            // (H <= 127), 34 = 8 lanes (H <= 31)
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
-            const KFn kw[2] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<2, true, dpl_pmax(2, 32), 32>};
-            const int a = L.kind - 32, lpt = a == 0 ? 64 : 32, tpw = 64 / lpt;
+            const KFn kw[3] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<2, true, dpl_pmax(2, 32), 32>,
+                               k_dpr<2, true, dpl_pmax(2, 8), 8>};
+            const int a = L.kind - 32, lpt = a == 0 ? 64 : (a == 1 ? 32 : 8), tpw = 64 / lpt;
             hipLaunchKernelGGL(kw[a], dim3((n + tpw - 1) / tpw), dim3(64),
                                (size_t)tpw * dpl_task_bytes(2, dpl_pmax(2, lpt), lpt), st, d_tasks + L.at, n,
                                d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
