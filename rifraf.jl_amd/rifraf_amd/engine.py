@@ -22,6 +22,29 @@ class RifrafError(Exception):
     """A reference `error(...)` raised on the engine path (same message text)."""
 
 
+class PackedGroups:
+    """Batch-slot groups packed for rf_score_dense: slot_off (G+1, int32) and
+    the concatenated slots (int32)."""
+    __slots__ = ("n", "slot_off", "slots")
+
+    def __init__(self, slot_off, slots):
+        self.slot_off = np.ascontiguousarray(slot_off, np.int32)
+        self.slots = np.ascontiguousarray(slots, np.int32)
+        self.n = len(self.slot_off) - 1
+
+
+def pack_groups(groups) -> PackedGroups:
+    """Pack a list of batch-slot arrays (one per cluster) once."""
+    G = len(groups)
+    slot_off = np.zeros(G + 1, np.int32)
+    if G:
+        np.cumsum([len(s) for s in groups], out=slot_off[1:])
+        slots = np.concatenate(groups).astype(np.int32, copy=False)
+    else:
+        slots = np.zeros(0, np.int32)
+    return PackedGroups(slot_off, slots)
+
+
 class Engine:
     """One device context.  Sequence ids, template ids and slot ids are small
     integers chosen by the caller (see model.py for the RIFRAF mapping)."""
@@ -292,18 +315,18 @@ class Engine:
 
     def score_dense(self, groups, to_host: bool = True, rows=None):
         """Dense all-proposals scoring (rf_score_dense).  groups: list of
-        batch-slot arrays (one per cluster).  Returns a list of (m_g+1, 9)
-        arrays (or None when to_host is False: totals stay in HBM)."""
-        G = len(groups)
-        slot_off = np.zeros(G + 1, np.int32)
-        for g, sl in enumerate(groups):
-            slot_off[g + 1] = slot_off[g] + len(sl)
-        slots = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in groups]), np.int32)
+        batch-slot arrays (one per cluster), or the PackedGroups of
+        pack_groups(list) when the same groups are scored repeatedly.
+        Returns a list of (m_g+1, 9) arrays (or None when to_host is False:
+        totals stay in HBM)."""
+        pg = groups if isinstance(groups, PackedGroups) else pack_groups(groups)
+        G, slot_off, slots = pg.n, pg.slot_off, pg.slots
+        groups = pg
         if not to_host:
             self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), None))
             return None
         if rows is None:
-            rows = [self.geometry(int(sl[0]), RF_BAND_A)[1] for sl in groups]
+            rows = [self.geometry(int(slots[slot_off[g]]), RF_BAND_A)[1] for g in range(G)]
         out = np.empty((int(sum(rows)), 9))
         self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), ptr(out)))
         res, at = [], 0
@@ -315,11 +338,8 @@ class Engine:
     def score_dense_dev(self, groups, dev_ptr: int):
         """rf_score_dense_dev: dense totals written to device memory at
         dev_ptr (sum_g (m_g+1)*9 doubles on this engine's device)."""
-        G = len(groups)
-        slot_off = np.zeros(G + 1, np.int32)
-        for g, sl in enumerate(groups):
-            slot_off[g + 1] = slot_off[g] + len(sl)
-        slots = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int32) for s in groups]), np.int32)
+        pg = groups if isinstance(groups, PackedGroups) else pack_groups(groups)
+        G, slot_off, slots = pg.n, pg.slot_off, pg.slots
         self._check(self.lib.rf_score_dense_dev(self.ctx, G, ptr(slot_off), ptr(slots), c_void_p(int(dev_ptr))))
 
     def geometry(self, slot: int, which: int = RF_BAND_A):
