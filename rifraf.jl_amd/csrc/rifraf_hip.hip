@@ -3771,11 +3771,19 @@ struct rf_ctx {
     std::vector<Slot> slots;
     uint64_t tpl_counter = 0;
     uint64_t layout_gen = 1;   // bumped whenever a device offset / length may change
+    // bumped by every call that changes sequences, templates or band metadata:
+    // a plan validated at the current epoch with the same job / slot list
+    // needs no per-slot validation again
+    uint64_t state_epoch = 1;
     DevBuf scratch[17];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
+    // pinned landing zone for small per-call results (rf_realign's scores and
+    // the error flag): one D2H + one synchronize per call
+    void *hout = nullptr;
+    size_t hout_bytes = 0;
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
@@ -3787,6 +3795,7 @@ struct rf_ctx {
     struct {
         bool valid = false;
         uint64_t gen = 0;
+        uint64_t val_epoch = 0;   // state_epoch at which the job list was last validated
         int32_t flags = 0;
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
@@ -3799,6 +3808,7 @@ struct rf_ctx {
     struct {
         bool valid = false;
         uint64_t gen = 0;
+        uint64_t val_epoch = 0;   // state_epoch at which the slot list was last validated
         std::vector<int32_t> slot_off, slots;
         size_t nitems = 0;
         int max_reads = 0, ngroups = 0;
@@ -3949,6 +3959,36 @@ int region_ensure(rf_ctx *ctx, Arena &a, Region &r, int64_t bytes)
     r.cap = bytes;
     a.top += bytes;
     ++ctx->layout_gen;
+    return 0;
+}
+
+// The error flag and `bytes` of results land in ctx->hout (pinned, 16-B
+// error slot first); returns the results' host address.
+int ensure_hout(rf_ctx *ctx, size_t bytes)
+{
+    const size_t want = 16 + bytes;
+    if (ctx->hout_bytes >= want)
+        return 0;
+    if (ctx->hout)
+        (void)hipHostFree(ctx->hout);
+    ctx->hout = nullptr;
+    ctx->hout_bytes = 0;
+    const size_t sz = std::max<size_t>(want, 1 << 20);
+    if (hipHostMalloc(&ctx->hout, sz, hipHostMallocDefault) != hipSuccess)
+        return fail(ctx, RF_ERR_HIP, "pinned result buffer allocation failed");
+    ctx->hout_bytes = sz;
+    return 0;
+}
+
+// After the stream was synchronized with the error flag copied to hout.
+int check_err_landed(rf_ctx *ctx)
+{
+    const int h = *(const int *)ctx->hout;
+    if (h) {
+        int z = 0;
+        HIPCHK(ctx, hipMemcpy(ctx->d_err, &z, sizeof(int), hipMemcpyHostToDevice));
+        return fail(ctx, RF_ERR_NUMERIC, numeric_message(h));
+    }
     return 0;
 }
 
@@ -4220,6 +4260,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipFree(ctx->codes.lut.p);
     if (ctx->pinned)
         (void)hipHostFree(ctx->pinned);
+    if (ctx->hout)
+        (void)hipHostFree(ctx->hout);
     if (ctx->d_err)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
@@ -4298,6 +4340,7 @@ int rf_reserve(rf_ctx *ctx, int64_t band_bytes)
     if (!ctx || band_bytes < 0)
         return RF_ERR_ARG;
     (void)hipSetDevice(ctx->device);
+    ++ctx->state_epoch;
     if (ctx->band_arena.cap - ctx->band_arena.top >= band_bytes + ARENA_GUARD)
         return 0;
     return arena_grow(ctx, ctx->band_arena, band_bytes, nullptr);
@@ -4473,6 +4516,7 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     if (!ctx || first < 0 || nseq < 0 || (nseq > 0 && (!bases || !off || !match || !mismatch || !ins || !del)))
         return fail(ctx, RF_ERR_ARG, "rf_set_sequences: bad arguments");
     (void)hipSetDevice(ctx->device);
+    ++ctx->state_epoch;
     if ((int64_t)first + nseq > (int64_t)ctx->seqs.size())
         ctx->seqs.resize(first + nseq);
     // 0. grow each arena at most once for the whole batch
@@ -4559,6 +4603,7 @@ int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids, const ui
     if (!ctx || ntpl < 0 || (ntpl > 0 && (!ids || !bases || !off)))
         return fail(ctx, RF_ERR_ARG, "rf_set_templates: bad arguments");
     (void)hipSetDevice(ctx->device);
+    ++ctx->state_epoch;
     int32_t top = 0;
     for (int32_t k = 0; k < ntpl; ++k) {
         if (ids[k] < 0)
@@ -4605,32 +4650,45 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     if (!(flags & (RF_FWD | RF_BWD)))
         return fail(ctx, RF_ERR_ARG, "rf_realign: need RF_FWD and/or RF_BWD");
     (void)hipSetDevice(ctx->device);
-    for (int32_t k = 0; k < njobs; ++k) {
-        if (slot[k] < 0 || seq[k] < 0 || seq[k] >= (int32_t)ctx->seqs.size() || !ctx->seqs[seq[k]].valid ||
-            tpl[k] < 0 || tpl[k] >= (int32_t)ctx->tpls.size() || !ctx->tpls[tpl[k]].valid)
-            return fail(ctx, RF_ERR_ARG, "rf_realign: unknown slot / sequence / template");
-        if (bw[k] < 1)
-            return fail(ctx, RF_ERR_ARG, "bandwidth must be positive");
-    }
     auto &P = ctx->rplan;
     const size_t nb = sizeof(int32_t) * (size_t)njobs;
     const bool same = P.valid && P.gen == ctx->layout_gen && P.flags == flags &&
                       P.slot.size() == (size_t)njobs && (njobs == 0 ||
                       (!std::memcmp(P.slot.data(), slot, nb) && !std::memcmp(P.seq.data(), seq, nb) &&
                        !std::memcmp(P.tpl.data(), tpl, nb) && !std::memcmp(P.bw.data(), bw, nb)));
+    // the same job list, validated with nothing changed since: its checks and
+    // its band bookkeeping would come out the same
+    const bool fresh = same && P.val_epoch == ctx->state_epoch;
+    if (!fresh)
+        for (int32_t k = 0; k < njobs; ++k) {
+            if (slot[k] < 0 || seq[k] < 0 || seq[k] >= (int32_t)ctx->seqs.size() || !ctx->seqs[seq[k]].valid ||
+                tpl[k] < 0 || tpl[k] >= (int32_t)ctx->tpls.size() || !ctx->tpls[tpl[k]].valid)
+                return fail(ctx, RF_ERR_ARG, "rf_realign: unknown slot / sequence / template");
+            if (bw[k] < 1)
+                return fail(ctx, RF_ERR_ARG, "bandwidth must be positive");
+        }
     if (same) {
         // identical job list on an unchanged layout: descriptors on the device
         // are still exact; only the band bookkeeping (template version) moves
-        for (int dir = 0; dir < 2; ++dir) {
-            if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                continue;
-            for (int32_t k = 0; k < njobs; ++k) {
-                Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
-                b.tplver = ctx->tpls[tpl[k]].version;
+        if (!fresh) {
+            bool changed = false;
+            for (int dir = 0; dir < 2; ++dir) {
+                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
+                    continue;
+                for (int32_t k = 0; k < njobs; ++k) {
+                    Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
+                    const uint64_t v = ctx->tpls[tpl[k]].version;
+                    changed = changed || b.tplver != v;
+                    b.tplver = v;
+                }
             }
+            if (changed)
+                ++ctx->state_epoch;
+            P.val_epoch = ctx->state_epoch;
         }
     } else {
         P.valid = false;
+        ++ctx->state_epoch;   // band metadata changes below
         int32_t maxslot = -1;
         for (int32_t k = 0; k < njobs; ++k)
             maxslot = std::max(maxslot, slot[k]);
@@ -4794,6 +4852,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             return e;
         P.valid = true;
         P.gen = ctx->layout_gen;
+        P.val_epoch = ctx->state_epoch;
         P.flags = flags;
         P.slot.assign(slot, slot + njobs);
         P.seq.assign(seq, seq + njobs);
@@ -4932,14 +4991,20 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-    if (out_score && njobs > 0)
-        HIPCHK(ctx, hipMemcpyAsync(out_score, d_out, sizeof(double) * njobs, hipMemcpyDeviceToHost,
-                                   ctx->stream));
+    // scores and the error flag into pinned memory, one synchronize
+    const size_t ob = (out_score && njobs > 0) ? sizeof(double) * njobs : 0;
+    if (int e = ensure_hout(ctx, ob))
+        return e;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->hout, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (ob)
+        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->hout + 16, d_out, ob, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ob)
+        std::memcpy(out_score, (const char *)ctx->hout + 16, ob);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
     ctx->dp_ms = ms;
-    return check_err(ctx);
+    return check_err_landed(ctx);
 }
 
 // k_bt_win takes reads (no codon tables) with H <= 255; the rest (the
@@ -5413,7 +5478,14 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         return fail(ctx, RF_ERR_ARG, "rf_score_dense: bad arguments");
     (void)hipSetDevice(ctx->device);
     const int32_t nslots = ngroups > 0 ? slot_off[ngroups] : 0;
-    // per-call validation of the bands (cheap; versions may have moved)
+    auto &P = ctx->dplan;
+    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
+                      P.slots.size() == (size_t)nslots &&
+                      !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
+                      (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
+    // per-call validation of the bands, unless this very slot list was
+    // validated and nothing (sequences, templates, bands) changed since
+    if (!(same && P.val_epoch == ctx->state_epoch))
     for (int32_t g = 0; g < ngroups; ++g) {
         if (slot_off[g + 1] <= slot_off[g])
             return fail(ctx, RF_ERR_ARG, "rf_score_dense: empty group");
@@ -5438,11 +5510,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             tpl = S.a.tpl;
         }
     }
-    auto &P = ctx->dplan;
-    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
-                      P.slots.size() == (size_t)nslots &&
-                      !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
-                      (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
+    P.val_epoch = ctx->state_epoch;
     if (!same) {
         P.valid = false;
         std::vector<ScoreGroup> &groups = P.groups;

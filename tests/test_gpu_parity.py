@@ -687,6 +687,34 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
 
 
+def test_validation_skip_follows_state(engine):
+    """rf_realign / rf_score_dense skip their per-job checks only for the same
+    job / slot list with nothing changed since it was validated: a template
+    change must still be refused by a repeated rf_score_dense (stale bands),
+    and a re-realign must make it valid again."""
+    rng = np.random.default_rng(303)
+    t1 = random_seq(100, rng)
+    t2 = t1.copy()
+    t2[50:53] = (t2[50:53] + 2) % 4
+    seqs = [make_read(t1, rng, 0.03, 9) for _ in range(5)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t1])
+    sl = np.arange(5)
+    for _ in range(3):                                   # plan built, then reused twice
+        engine.realign(sl, sl, 0, [9] * 5, RF_FWD | RF_BWD)
+        d1 = engine.score_dense([sl])[0]
+    engine.set_templates(0, [t2])
+    with pytest.raises(RifrafError):
+        engine.score_dense([sl])
+    engine.realign(sl, sl, 0, [9] * 5, RF_FWD | RF_BWD)
+    d2 = engine.score_dense([sl])[0]
+    d2b = engine.score_dense([sl])[0]
+    ref2, _ = oracle.cpu_pass(t2, seqs, nthreads=2)
+    np.testing.assert_array_equal(d2[1:, 5:], ref2[1:, 5:])
+    np.testing.assert_array_equal(d2, d2b)
+    assert not np.array_equal(d1[1:, 5:], d2[1:, 5:])
+
+
 def test_plan_cache_follows_slot_contents(engine):
     """rf_score_dense reuses its descriptors only while every scored band
     still describes the same alignment: re-filling the same slots with other
