@@ -3720,6 +3720,9 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
+#ifndef WS_Q_DEFAULT
+#define WS_Q_DEFAULT 256
+#endif
 #ifndef SEG_S_DEFAULT
 #define SEG_S_DEFAULT 24
 #endif
@@ -3731,7 +3734,7 @@ struct Opts {
     int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg
     int lean_nw = 8;        // RF_OPT_LEAN_NW: 8 = k_score_ws, 1/2/4 = k_score_lean waves
     int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: 0 = default budget
-    int ws_q = 256;         // RF_OPT_WS_Q: k_score_ws chain lanes (256 or 128)
+    int ws_q = WS_Q_DEFAULT;   // RF_OPT_WS_Q: k_score_ws chain lanes (256 or 128)
     int seg_s = SEG_S_DEFAULT;   // RF_OPT_SEG_S: diagonals per segment (k_score_segl: 16 or 32; seg/segc: 16, 24, 32)
     int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
     int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
