@@ -18,6 +18,13 @@ on the data path (clusters are independent); the only cross-rank traffic is
 the timing barrier / max.  "c2" / "c3" select configs[1] / configs[2]
 (single cluster; replicas under --gpus N).
 
+Ranks: `bench.py --gpus N` (N > 1) with no RANK / WORLD_SIZE in the
+environment starts N child ranks itself, one per GPU, before anything touches
+the GPU; under an external launcher (torch.distributed.run) it checks that
+WORLD_SIZE == N.  Each rank needs a GPU of its own (`--shared-gpu` rehearses
+several ranks on one GPU); `n_gpus` counts distinct devices (PCI ids), `ranks`
+the processes.
+
 Prints ONE JSON line on rank 0 (contract in the task statement); metric
 value = GCUPS = in-band DP cells (forward + backward) per second over the
 whole step; proposals/s and (proposal x read) pairs/s are reported beside it.
@@ -53,6 +60,61 @@ def dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return rank, world, local
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nranks: int, argv) -> int:
+    """`bench.py --gpus N` without an external launcher: start N child ranks,
+    one per GPU (LOCAL_RANK = RANK = 0..N-1, WORLD_SIZE = N, rendezvous on
+    127.0.0.1), wait for all of them and return the worst exit code.  Runs
+    before anything in this process touches HIP or torch.cuda (the children
+    are fresh interpreters, not an exec of this one).  A rank that fails ends
+    the others, so a dead peer cannot leave the rest waiting in a collective."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for o in live:
+                    o.terminate()
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
+def device_identity(torch, gpu):
+    """Physical identity of this rank's device (PCI domain:bus:device), so
+    that n_gpus counts distinct GPUs, not ranks."""
+    if torch is not None and torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(gpu)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return f"cpu-rank-device-{gpu}"   # --dry-run on a host without GPUs: the assignment itself
+
+
+def distinct_devices(dist, ident: str) -> int:
+    if dist is None:
+        return 1
+    ids = [None] * dist.get_world_size()
+    dist.all_gather_object(ids, ident)
+    return len(set(ids))
 
 
 def band_cells(n: int, m: int, bw: int) -> int:
@@ -267,9 +329,21 @@ def main():
                     help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal only: allow several ranks on one GPU (n_gpus then counts distinct devices)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch, rendezvous, workload and device assignment only (no engine): checks the "
+                         "multi-rank plumbing on a host without GPUs")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+        # no external launcher: one child process per GPU, started before this
+        # process touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
     rank, world, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     dist = torch = coll = None
     gpu = local
     if world > 1:
@@ -281,13 +355,19 @@ def main():
         if backend == "auto":
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         ndev = torch.cuda.device_count()
-        gpu = local % ndev if ndev else local      # gloo rehearsals: several ranks per GPU
+        if ndev and local >= ndev and not args.shared_gpu:
+            raise SystemExit(f"bench.py: rank {rank} (local {local}) has no GPU of its own: {ndev} visible "
+                             f"for {world} ranks (--shared-gpu rehearses several ranks per GPU)")
+        gpu = local % ndev if ndev else local      # --shared-gpu rehearsals: several ranks per GPU
         if backend == "nccl":
             torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
         coll = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
+    n_dev = distinct_devices(dist, device_identity(torch, gpu)) if world > 1 else 1
 
-    if args.config == "c5":
+    if args.dry_run:
+        result = run_dry(args, rank, world, gpu, dist, coll, n_dev)
+    elif args.config == "c5":
         result = run_read_sharded(args, rank, world, gpu, dist, torch, coll)
     else:
         result = run_clusters(args, rank, world, gpu, dist, torch, coll)
@@ -297,10 +377,44 @@ def main():
             # configs[4] beside the headline line: driver-measured 10 kb reads
             # with band doubling, read-sharded over the same ranks
             result["secondary"] = run_read_sharded(args, rank, world, gpu, dist, torch, coll)
+    # n_gpus: distinct physical devices the ranks ran on (a rehearsal with
+    # several ranks per GPU reports fewer GPUs than ranks)
+    result["n_gpus"] = n_dev
+    result["ranks"] = world
+    if isinstance(result.get("secondary"), dict):
+        result["secondary"]["n_gpus"] = n_dev
+        result["secondary"]["ranks"] = world
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_dry(args, rank, world, gpu, dist, coll, n_dev):
+    """--dry-run: every step of a run except the engine -- launch, rendezvous,
+    device assignment, this rank's workload and its cell count, the whole-job
+    reduction -- so the multi-rank plumbing is testable on a host without
+    GPUs.  Reports no throughput."""
+    nclu, nreads, length, err, bw, label = CONFIGS[args.config]
+    if args.clusters is not None:
+        nclu = args.clusters
+    if args.config == "c5":
+        from rifraf_amd.sharded import shard_bounds
+        lo, hi = shard_bounds(nreads, world)[rank:rank + 2]
+        t, reads = make_read_shard(nreads, length, err, bw, args.seed, lo, hi)
+        clusters = [(t, reads)]
+    else:
+        clusters = make_workload(nclu, nreads, length, err, bw, seed=shard_seed(args.seed, rank))
+    cells = sum(2 * band_cells(len(r), len(t), r.bandwidth) for t, rs in clusters for r in rs)
+    units = [float(cells), float(sum(len(rs) for _, rs in clusters))]
+    elapsed = 0.0
+    if dist is not None:
+        elapsed, units = aggregate(elapsed, units, coll)
+    return {"metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
+            "value": None, "unit": "GCUPS", "dry_run": True, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "scaling": "strong" if args.config == "c5" else "weak",
+            "config": {"workload": args.config, "description": label},
+            "cells_per_step_all_ranks": int(units[0]), "reads_all_ranks": int(units[1])}
 
 
 def run_e2e(args, rank, world, gpu, dist, coll):

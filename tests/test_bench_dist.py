@@ -51,6 +51,42 @@ def test_aggregate_two_ranks():
         assert units == [30.0, 6.0, 11.0]      # whole-job units
 
 
+def _bench(args, env=None, timeout=300):
+    import json
+    import subprocess
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=e, cwd=REPO,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, [json.loads(ln) for ln in lines]
+
+
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself: one JSON
+    line (rank 0) whose reduction covers both ranks' shards."""
+    p, lines = _bench(["--gpus", "2", "--backend", "gloo", "--config", "c4", "--clusters", "2",
+                       "--no-cpu", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1
+    out = lines[0]
+    assert out["ranks"] == 2 and out["n_gpus"] == 2
+    assert out["reads_all_ranks"] == 2 * 2 * 50
+    cells = sum(2 * bench.band_cells(len(r), len(t), r.bandwidth)
+                for rank in range(2)
+                for t, rs in bench.make_workload(2, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, rank))
+                for r in rs)
+    assert out["cells_per_step_all_ranks"] == cells
+
+
+def test_bench_rejects_world_mismatch():
+    """Under an external launcher the world size must equal --gpus."""
+    p, lines = _bench(["--gpus", "2", "--dry-run", "--config", "c4", "--clusters", "1"],
+                      env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and not lines
+    assert "WORLD_SIZE=1" in p.stderr
+
+
 def test_shards_are_independent():
     a = bench.make_workload(2, 3, 60, 0.01, 9, seed=bench.shard_seed(7, 0))
     b = bench.make_workload(2, 3, 60, 0.01, 9, seed=bench.shard_seed(7, 1))

@@ -136,6 +136,45 @@ def test_dp_class_boundaries(engine, opts, pad):
     _check_bands(engine, t, seqs, bws)
 
 
+@pytest.mark.parametrize("dp_wide", [3, 1, 2, 0])
+def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide):
+    """Regression for the round-2 64/32-lane DP task work (RF_OPT_DP_WIDE):
+    one rf_realign whose lean tasks straddle every task-width class edge
+    (H 62..66 -> 16 / 32 lanes, 125..131 -> 32 / 64 lanes, 250..257 -> 64
+    lanes / k_dp<64>) at lengths where the blocked lean interior runs many
+    blocks (m = 2400), odd task counts per class (partial waves: padding tasks
+    write the sink), reads longer and shorter than the template, both
+    directions, padded and unpadded strides in the same context.  Bands and
+    A[end,end] bit-exact vs oracle.forward / oracle.backward."""
+    opts("dp_wide", dp_wide)
+    rng = np.random.default_rng(4242 + dp_wide)
+    t = random_seq(2400, rng)
+    seqs, bws = [], []
+    for H, delta in ((62, 1), (63, 0), (64, -2), (65, 3), (66, 0), (125, 0), (127, 2), (128, -1),
+                     (129, 0), (131, 4), (250, 1), (254, 0), (255, 2), (256, -5), (257, 0),
+                     (29, 0), (31, 1), (129, -2), (191, 0)):
+        bw = (H - 1 - abs(delta)) // 2
+        r = make_read(t, rng, 0.02, bw)
+        s, lp = r.seq, r.error_log_p
+        want = len(t) + delta
+        if len(s) > want:
+            s, lp = s[:want], lp[:want]
+        else:
+            extra = random_seq(want - len(s), rng)
+            s = np.concatenate([s, extra])
+            lp = np.concatenate([lp, np.full(len(extra), -1.2)])
+        seqs.append(RifrafSequence(s, lp, bw, SEQ_SCORES))
+        bws.append(bw)
+    _check_bands(engine, t, seqs, bws)
+    # the same jobs split over two calls (forward alone, then backward alone)
+    n = len(seqs)
+    engine.realign(np.arange(n), np.arange(n), 0, bws, RF_FWD)
+    engine.realign(np.arange(n), np.arange(n), 0, bws, RF_BWD)
+    for k in (0, 7, 12, n - 1):
+        A_exp, _ = oracle.forward(t, seqs[k], bandwidth=bws[k])
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(seqs[k]) + 1, len(t) + 1, bws[k])
+
+
 @pytest.mark.parametrize("m,n,bw", [(3, 40, 9), (8, 8, 9), (1, 1, 1), (2, 30, 2), (40, 3, 9), (25, 60, 6)])
 def test_dp_short_and_skewed_shapes(engine, m, n, bw):
     """Templates shorter than the bandwidth (c > m: no lean interior) and very
