@@ -84,20 +84,13 @@ const char *rf_last_error(const rf_ctx *ctx);
  * are read once from the RIFRAF_* environment at rf_create.  No reference
  * counterpart (the reference has one code path). */
 #define RF_OPT_SCORE_MODE   1   /* 0 auto, 1 fused in-kernel fold, 2 split + k_reduce  */
-#define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_seg            */
-#define RF_OPT_LEAN_NW      3   /* 8 = k_score_ws; 1, 2, 4 = k_score_lean waves         */
-#define RF_OPT_LEAN_LDS_KB  4   /* lean scorer LDS budget (0 = default)                */
-#define RF_OPT_WS_Q         5   /* k_score_ws chain lanes: 256 or 128                  */
-#define RF_OPT_SEG_S        6   /* k_score_seg diagonals per segment: 16, 24, 32       */
-#define RF_OPT_SEG_LDS      7   /* k_score_seg extra LDS bytes per workgroup           */
-#define RF_OPT_SEG_WPE      8   /* k_score_seg waves-per-EU register cap: 1, 2         */
+#define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_segl           */
+#define RF_OPT_LEAN_LDS_KB  4   /* k_score_ws LDS budget in KB (0 = default 160)       */
 #define RF_OPT_BT_GLOBAL    9   /* 1: every backtrace walk in k_backtrace              */
 #define RF_OPT_DP_PSPLIT   10   /* lean DP stride-class split mask (-1 auto)           */
 #define RF_OPT_DP_NP8      11   /* 0: H 128..255 bands in k_dp<64> instead of k_dpr<8> */
 #define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
 #define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
-#define RF_OPT_SEG_VER     14   /* wide-band scorer: 4 k_score_segl (default),
-                                    3 k_score_segc, 1 k_score_seg                        */
 #define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 16 (default) or 32 KB        */
 #define RF_OPT_STAGE_KB    16   /* rf_set_sequences host staging chunk, KB of tables   */
 #define RF_OPT_BAND_PAD    17   /* an rf_realign call whose widest band has H >= value
@@ -105,8 +98,10 @@ const char *rf_last_error(const rf_ctx *ctx);
                                     128-B lines (default 64; 1 always, 0 never)       */
 #define RF_OPT_DP_WIDE     18   /* lean DP task widths: bit 0 H 128..255 as 64-lane
                                     tasks (k_dpr<2,..,64>), bit 1 H 64..127 as 32-lane
-                                    tasks (k_dpr<2,..,32>), bit 2 H <= 31 as 8-lane
-                                    tasks (k_dpr<2,..,8>); 0 = 16-lane tasks only   */
+                                    tasks (k_dpr<2,..,32>); 0 = 16-lane tasks only   */
+/* Keys 3, 5-8 and 14 selected scorer variants measured slower and removed in
+   round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg / k_score_segc,
+   16-diagonal k_score_segl); rf_set_option rejects them. */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 
@@ -114,6 +109,13 @@ int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 int rf_reserve(rf_ctx *ctx, int64_t band_bytes);
 /* Bytes currently allocated on the device by this context. */
 int64_t rf_device_bytes(const rf_ctx *ctx);
+/* Row-code dictionary of the context (the lean DP's 8-B per-row records):
+   distinct (match, mismatch, ins) triples and del values held, reads left
+   uncoded because the 65,536-entry dictionary was full (their DP reads the
+   tables: slower, same values), and fresh starts (an upload that replaces
+   every coded sequence resets it).  Engine-internal; no reference analog. */
+int rf_code_stats(const rf_ctx *ctx, int64_t *entries3, int64_t *entries1, int64_t *uncoded_reads,
+                  int64_t *resets);
 
 /* Sequences (reads or a reference): ids [first, first+nseq).  Replaces any
  * previous content of those ids.  Per sequence k (n_k = off[k+1]-off[k]):

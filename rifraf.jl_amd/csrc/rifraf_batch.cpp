@@ -37,6 +37,9 @@
 #include <vector>
 #include <cstdlib>
 
+// rf_last_error text (rifraf_hip.hip)
+int rf_internal_fail(rf_ctx *ctx, int code, const char *msg);
+
 namespace {
 
 constexpr double INF = std::numeric_limits<double>::infinity();
@@ -565,11 +568,13 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
                                const int64_t *cons_off, double *out_score, int32_t *out_iters,
                                int32_t *out_status, int64_t *out_len, int32_t *out_bw)
 {
-    if (!ctx || nclusters < 0 || !params || (nclusters > 0 && (!read_off || !read_seq || !read_len || !threshold ||
-                                                              !slot_base || !tpl_id || !cons || !cons_off)))
+    if (!ctx)
         return RF_ERR_ARG;
+    if (nclusters < 0 || !params || (nclusters > 0 && (!read_off || !read_seq || !read_len || !threshold ||
+                                                       !slot_base || !tpl_id || !cons || !cons_off)))
+        return rf_internal_fail(ctx, RF_ERR_ARG, "rf_rifraf_batch: bad arguments");
     if (params->batch_fixed && (!fixed_off || !fixed))
-        return RF_ERR_ARG;
+        return rf_internal_fail(ctx, RF_ERR_ARG, "rf_rifraf_batch: batch_fixed needs fixed_off and fixed");
     Driver D{ctx, *params, {}, {}, {}, {}};
     const int32_t nreads = nclusters > 0 ? read_off[nclusters] : 0;
     D.reads.resize(nreads);
@@ -590,9 +595,16 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
         // initial_state (model.jl:564-615)
         const int32_t bs = params->batch_size > 1 ? std::min(params->batch_size, C.nreads) : C.nreads;
         C.batch_size = C.base_batch_size = bs;
-        if (C.nreads < 1 || C.cons.empty() || (!params->batch_fixed && bs < C.nreads) ||
-            (params->batch_fixed && fixed_off[c + 1] - fixed_off[c] < 1))
-            return RF_ERR_ARG;   // outside the native driver's scope: the caller checks first
+        // outside the native driver's scope (the caller checks first)
+        const char *why = C.nreads < 1 ? "no reads"
+                          : C.cons.empty() ? "empty consensus"
+                          : (!params->batch_fixed && bs < C.nreads) ? "a random batch smaller than the read count"
+                          : (params->batch_fixed && fixed_off[c + 1] - fixed_off[c] < 1) ? "an empty fixed batch"
+                          : nullptr;
+        if (why)
+            return rf_internal_fail(ctx, RF_ERR_ARG,
+                                    ("rf_rifraf_batch: cluster " + std::to_string(c) +
+                                     " is outside the native driver's scope (" + why + ")").c_str());
     }
     D.run();
     BatchResult &R = result_of(ctx);

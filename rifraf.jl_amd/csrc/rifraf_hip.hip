@@ -320,8 +320,8 @@ __device__ __forceinline__ double dpp_f64(double x)
 #define DPP_FROM_L2 0x112   // row_shr:2 -> lane q-2
 #define DPP_FROM_R1 0x101   // row_shl:1 -> lane q+1
 #define DPP_FROM_R2 0x102   // row_shl:2 -> lane q+2
-// Lanes per DP task: 8 (half a DPP row, 8 tasks per wave), 16 (one DPP
-// row, 4 tasks per wave), 32 (two tasks per wave) or 64 (the whole wave).  32 and 64 use wave_shr / wave_shl /
+// Lanes per DP task: 16 (one DPP row, 4 tasks per wave), 32 (two tasks per
+// wave) or 64 (the whole wave).  32 and 64 use wave_shr / wave_shl /
 // wave_ror / wave_rol, the same moves across DPP rows.  With 32 lanes the
 // wave shifts also cross the two tasks: lane 32 (31) would read lane 31's
 // (32's) value where it should read its task's edge, so those lanes select
@@ -330,14 +330,12 @@ __device__ __forceinline__ double dpp_f64(double x)
 // host's class bound), i.e. -Inf or masked, exactly as within a DPP row.
 template <int LPT>
 struct TaskLanes {
-    static_assert(LPT == 8 || LPT == 16 || LPT == 32 || LPT == 64, "tasks are 8, 16, 32 or 64 lanes");
+    static_assert(LPT == 16 || LPT == 32 || LPT == 64, "tasks are 16, 32 or 64 lanes");
     static constexpr int FROM_L1 = LPT >= 32 ? 0x138 : 0x111;   // lane q-1 (edge lane 0 reads `old`)
     static constexpr int FROM_R1 = LPT >= 32 ? 0x130 : 0x101;   // lane q+1 (edge lane LPT-1 reads `old`)
     static constexpr int ROT_L1 = LPT >= 32 ? 0x13C : 0x121;    // lane (q-1) mod LPT (or mod 64)
     static constexpr int ROT_R1 = LPT >= 32 ? 0x134 : 0x12F;    // lane (q+1) mod LPT (or mod 64)
-    // 8-lane tasks (two per DPP row) use the row moves; like 32-lane tasks
-    // their shifts cross into the neighbouring task
-    static constexpr bool EDGE_FIX = LPT == 32 || LPT == 8;
+    static constexpr bool EDGE_FIX = LPT == 32;
 };
 
 // Shift an int / double across the 16-lane DPP row (lanes outside the row
@@ -540,8 +538,10 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     }
 }
 
-#ifndef DPL_NO_LDS_OUT
-#define DPL_NO_LDS_OUT 0   // diagnostics only: lean steps skip their LDS band output
+#if defined(RIFRAF_DIAG) && defined(DPL_NO_LDS_OUT_DIAG)
+#define DPL_NO_LDS_OUT 1   // diagnostic builds only: lean steps skip their LDS band output
+#else
+#define DPL_NO_LDS_OUT 0
 #endif
 // Whole-row DPP rotate of an f64 (no "old" operand: every lane has a source).
 template <int CTRL>
@@ -566,32 +566,13 @@ __device__ __forceinline__ double dpp_rot_f64(double x)
 // finite match/mismatch/ins/del tables, so every in-band cell is finite (each
 // has an in-band predecessor chain to the origin) and the "new score is
 // invalid" check (align.jl:105-107) cannot fire here; the general steps keep it.
-// LDS band-output swizzle of the lean blocks (NP >= 4).  Lane q writes the
-// cells of its pairs q*NP + r at one slot per r, i.e. 16 lanes at a stride of
-// NP doubles: with NP = 4 / 8 lanes q, q+8 (q+4, q+8, q+12) hit the same LDS
-// banks (2- / 4-way conflicts on every cell store).  Slot u is stored at
-// u ^ ((u >> 4) & 7): a permutation inside each aligned group of 8 slots
-// whose key differs between slots 32 apart, so the 16 lanes of a task land on
-// 16 distinct bank pairs; the flush reads 16-B pairs (u even, u + 1), which
-// stay one aligned pair (swapped when the key is odd).  Measured at c5
-// (DP-only, bw 18, profiles/r02_exp_dp_swz.json): bit-exact but slower
-// (30.2 -> 32.0 ms: the address arithmetic and registers cost more than the
-// conflicts), so it is off; the LDS output itself costs ~5 ms there
-// (DPL_NO_LDS_OUT diagnostic build: 30.2 -> 25.5 ms).
-#ifndef DPL_SWZ
-#define DPL_SWZ 0
-#endif
-template <int NP>
-__device__ __forceinline__ int dpl_swz(int u)
-{
-    return (DPL_SWZ && NP >= 4) ? (u ^ ((u >> 4) & 7)) : u;
-}
+// (An XOR swizzle of the lean blocks' LDS band rows, removing the 4-way bank
+// conflicts of the NP = 8 cell stores, was bit-exact but slower at c5:
+// 30.2 -> 32.0 ms DP-only, profiles/r02_exp_dp_swz.json.)
 template <int NP>
 __device__ __forceinline__ dvec2 dpl_rd2(const double *R, int u)   // u even
 {
-    const int U = dpl_swz<NP>(u);
-    const dvec2 v = *(const dvec2 *)(R + (U & ~1));
-    return (U & 1) ? dvec2{v.y, v.x} : v;
+    return *(const dvec2 *)(R + u);
 }
 
 template <int NP, int PAR, int LPT = 16>
@@ -611,7 +592,7 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
         nv[r] = raw + lb[r];
         if (st[r] && !DPL_NO_LDS_OUT)
-            Rb[dpl_swz<NP>(u0 + r * ostep)] = nv[r];
+            Rb[u0 + r * ostep] = nv[r];
     }
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
@@ -626,22 +607,16 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
 #ifndef DPL_BLOCK
 #define DPL_BLOCK 16
 #endif
-#ifndef DP_STAGGER
-#define DP_STAGGER 0   // measured: no gain (flush convoys are not the limiter)
-#endif
 // periods per block (<= 16: one edge record per lane); NP = 2, 4 take 8 and NP = 8
 // takes 4 (measured: NP = 2/4 at 16 need 280/430 VGPRs -> one wave per SIMD), so
 // that a 4-task workgroup's LDS slices (rows of up to 129 doubles) leave
 // several waves per CU
-#ifndef DPL_B8
-#define DPL_B8 4    // periods per block of the 8-lane tasks (8 tasks' LDS slices per wave)
-#endif
 #ifndef DPL_B64
 #define DPL_B64 8   // periods per block of the 64-lane tasks
 #endif
 __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 {
-    return lpt >= 32 ? DPL_B64 : (lpt == 8 ? DPL_B8 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK)));
+    return lpt >= 32 ? DPL_B64 : (np >= 8 ? 4 : (np >= 2 ? 8 : DPL_BLOCK));
 }
 #ifndef DPL_SPREAD
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
@@ -769,11 +744,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             hi = min(hi, __shfl_xor(hi, off));
         }
         if (__all(ok)) {
-            // stagger: waves of one CU (blocks b, b+8, b+16, ... share an XCD) enter
-            // the blocked interior a quarter block apart, so that their band
-            // flushes do not all hit the store path at once (RIFRAF_DP_STAGGER)
-            const int stag = ((blockIdx.x >> 3) & 3) * (DPL_B / 2) * DP_STAGGER;
-            klo = __builtin_amdgcn_readfirstlane(((lo + 1) & ~1) + stag);   // wave-uniform: scalar loop
+            klo = __builtin_amdgcn_readfirstlane((lo + 1) & ~1);   // wave-uniform: scalar loop
             khi = __builtin_amdgcn_readfirstlane(hi);
         }
     }
@@ -797,7 +768,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const ptrdiff_t g00 = (ptrdiff_t)(rev ? T.klen - 2 * DPL_B - k : k) * P;
             ptrdiff_t fl = g00 + (rev ? blk : 0);
             // rows region R; slot u of R holds the band value at position
-            // g0 + (u - ub) of the block (dpl_swz: the physical LDS slot)
+            // g0 + (u - ub) of the block
             double *R = reinterpret_cast<double *>(dpl_smem + t * dpl_task_bytes(NP, PM, LPT) + DPL_B * sizeof(EdgeRec));
             const int ub = DPL_CARRY + (int)(g00 & 1);
             // this lane's LDS slot per parity; a block's 2*DPL_B rows are the
@@ -824,7 +795,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             auto edge_load = [&](int kb, uint64_t rec) {
                 EdgeRec e;
                 const int kk = kb + 2 * min(q, DPL_B - 1);
-#ifdef DPL_TAB_DIAG   // diagnostics only: every task reads one L2-resident table slice
+#if defined(RIFRAF_DIAG) && defined(DPL_TAB_DIAG)   // diagnostic builds only: one L2-resident table slice
                 const int ks = edge_ks(kb) & 255;
                 const double *tb = tabs;
                 const uint8_t *sbase = bases;
@@ -993,23 +964,19 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                         }
                     }
                     if (task_real && q == 0 && (lo & 1))
-                        band[lo] = R[dpl_swz<NP>(ub + (int)(lo - g0))];
+                        band[lo] = R[ub + (int)(lo - g0)];
                     if (task_real && q == 1 && (hi & 1))
-                        band[hi - 1] = R[dpl_swz<NP>(ub + (int)(hi - 1 - g0))];
-                    // carry the unwritten partial line next to the next block's rows
-                    // (fewer than 16 doubles: one pass of a 16-lane task, two of an 8-lane one)
+                        band[hi - 1] = R[ub + (int)(hi - 1 - g0)];
+                    // carry the unwritten partial line (fewer than 16 doubles: one
+                    // pass of the task's lanes) next to the next block's rows
                     if (!rev) {
                         const int c = (int)(g0 + blk - fl), src = (int)(fl - g0);
-#pragma unroll
-                        for (int x = q; x < (LPT < 16 ? 16 : LPT); x += LPT)
-                            if (x < c)
-                                R[dpl_swz<NP>(ub + src - blk + x)] = R[dpl_swz<NP>(ub + src + x)];
+                        if (q < c)
+                            R[ub + src - blk + q] = R[ub + src + q];
                     } else {
                         const int c = (int)(fl - g0);
-#pragma unroll
-                        for (int x = q; x < (LPT < 16 ? 16 : LPT); x += LPT)
-                            if (x < c)
-                                R[dpl_swz<NP>(ub + blk + x)] = R[dpl_swz<NP>(ub + x)];
+                        if (q < c)
+                            R[ub + blk + q] = R[ub + q];
                     }
                 }
                 wave_sync();
@@ -1315,7 +1282,7 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
 }
 
 // ---------------------------------------------------------------------
-// k_score_lean: the same dense scoring, one new-column chain per lane
+// Lean dense scoring (k_score_ws, k_score_segl): one new-column chain per lane
 //
 // A new column built from A column a (0-based) with base b over the rows of
 // column min(a+1, m) serves two proposals (model.jl:250-270):
@@ -1341,9 +1308,6 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
 // ---------------------------------------------------------------------
 
 // doubles of LDS a sub-pass over L lanes needs for a read of band height H
-#ifndef LEAN_NPF
-#define LEAN_NPF 12
-#endif
 
 __host__ __device__ inline int lean_need(int L, int H, int P)
 {
@@ -1368,18 +1332,11 @@ __device__ __forceinline__ double vmax(double a, double b)
 // against B, util.jl:40-48): best_k = max(aprev + sub_k, prev_k + ins, dl),
 // accI_k = max(accI_k, best_k + bI), accS_k = max(accS_k, best_k + bS).
 // Issued phase by phase across the four chains, so that no FP64 op waits on
-// the op issued right before it (CHAIN_PHASED 0: chain by chain, the same
-// values).
-#ifndef CHAIN_LA
-#define CHAIN_LA 1   // k_score_ws / k_score_lean chains: rows of operands read ahead (1 or 2)
-#endif
-#ifndef CHAIN_PHASED
-#define CHAIN_PHASED 1
-#endif
+// the op issued right before it (measured: about 1 % faster than chain by
+// chain at c5, the same values).
 __device__ __forceinline__ void chain_row(double aprev, const double (&sub)[4], double ins, double dl, double bI,
                                           double bS, double (&prev)[4], double (&accI)[4], double (&accS)[4])
 {
-#if CHAIN_PHASED
     double x[4], y[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1402,15 +1359,6 @@ __device__ __forceinline__ void chain_row(double aprev, const double (&sub)[4], 
         accI[k] = vmax(accI[k], x[k]);
         accS[k] = vmax(accS[k], y[k]);
     }
-#else
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double best = vmax(vmax(aprev + sub[k], prev[k] + ins), dl);
-        prev[k] = best;
-        accI[k] = vmax(accI[k], best + bI);
-        accS[k] = vmax(accS[k], best + bS);
-    }
-#endif
 }
 
 // Geometry of one staged (read, lanes [la0, la1]) window.
@@ -1503,47 +1451,6 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         accI[k] = -RF_INF;
         accS[k] = -RF_INF;
     }
-#if CHAIN_LA == 2
-    // operands two rows ahead (LDS latency under four chain waves exceeds
-    // one row's arithmetic); the reads past row ilast + 1 stay inside the
-    // workgroup's LDS and are never used
-    struct RowOps {
-        double ac, bI, bS;
-        double2 u0, u1, u2;
-    };
-    auto ldrow = [&](int ix, int dx, const double *t) {
-        RowOps o;
-        o.ac = sA[ix];
-        o.bI = sB[ix];
-        o.bS = sB[ix + sofs + (sodd & dx)];
-        o.u0 = ((const double2 *)t)[0];
-        o.u1 = ((const double2 *)t)[1];
-        o.u2 = ((const double2 *)t)[2];
-        return o;
-    };
-    RowOps c0 = ldrow(idx, d, tr);
-    idx += P + (d & 1);
-    ++d;
-    tr += 6;
-    RowOps c1 = ldrow(idx, d, tr);
-    for (int i = i0; i <= ilast; ++i) {
-        idx += P + (d & 1);
-        ++d;
-        tr += 6;
-        const RowOps c2 = ldrow(idx, d, tr);
-        const double bS = c0.bS + smask;
-        const double sub[4] = {c0.u0.x, c0.u0.y, c0.u1.x, c0.u1.y};
-        const double dl = c0.ac + c0.u2.y;
-        const double dsum = c0.ac + bS;
-        chain_row(aprev, sub, c0.u2.x, dl, c0.bI, bS, prev, accI, accS);
-        dd = vmax(dd, dsum);
-        aprev = c0.ac;
-        c0 = c1;
-        c1 = c2;
-    }
-    const double bSr = c0.bS;
-    const double2 u0 = c0.u0, u1 = c0.u1, u2 = c0.u2;
-#else
     double ac = sA[idx], bI = sB[idx], bSr = sB[idx + sofs + (sodd & d)];
     double2 u0 = ((const double2 *)tr)[0], u1 = ((const double2 *)tr)[1], u2 = ((const double2 *)tr)[2];
     for (int i = i0; i <= ilast; ++i) {
@@ -1568,7 +1475,6 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         u1 = v1;
         u2 = v2;
     }
-#endif
     if (i1 > ilast) {
         // last row of the new column lies below A/B column a's band (a < m)
         const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
@@ -1583,160 +1489,6 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
         tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
     }
     tD += dd;
-}
-
-template <int NW>
-__device__ __forceinline__ void lean_barrier()
-{
-    if (NW > 1)
-        __syncthreads();
-    else
-        wave_sync();
-}
-
-// NPF: 16-byte chunks per band and lane the cross-read register prefetch
-// holds; a read whose full window needs more (or does not fit the LDS
-// budget) is staged synchronously, in sub-passes if needed.
-template <int NW, int NPF>
-__global__ void __launch_bounds__(64 * NW)
-k_score_lean(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
-             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
-             const double *__restrict__ tabs, const double *__restrict__ bands,
-             double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
-{
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int Q = 64 * NW;
-    // XCD-aware remap (blocks are dealt round-robin over the 8 XCDs)
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int xq = nb >> 3, xr = nb & 7, x = b & 7;
-    const int item = x * xq + min(x, xr) + (b >> 3);
-    const WorkItem wi = items[item];
-    const ScoreGroup G = groups[wi.group];
-    const int tid = threadIdx.x;
-    const int m = G.m;
-    const int a0 = wi.p0;
-    const int a = a0 + tid;
-    const int la1f = min(a0 + Q - 1, m);
-    int r0 = G.r0, r1 = G.r1;
-    if (split_mode & 1) {
-        r0 = G.r0 + blockIdx.y;
-        if (r0 >= G.r1)
-            return;
-        r1 = r0 + 1;
-    }
-    double tI[4], tS[4], tD = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        tI[k] = 0.0;
-        tS[k] = 0.0;
-    }
-    // a read takes the prefetch path when its full window fits both budgets
-    auto fast = [&](const ScoreRead &R, const LeanWin &w) {
-        return lean_need(Q, R.H, R.P) <= lds_elems && w.n16 <= NPF * Q && w.t1 - w.t0 < 2 * Q;
-    };
-    dvec2 pa[NPF], pb[NPF];
-    double pm[2], px[2], pn[2], pd[2];
-    int ps[2];
-    // Issue read rr's full window + table rows into registers (no wait).
-    auto issue = [&](int rr) -> bool {
-        const ScoreRead R2 = reads[rr];
-        const LeanWin w2 = lean_win(R2, m, a0, la1f);
-        if (!fast(R2, w2))
-            return false;
-        const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
-        const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
-#pragma unroll
-        for (int u = 0; u < NPF; ++u) {
-            const int e = min(u * Q + tid, w2.n16 - 1);
-            pa[u] = ga[e];
-            pb[u] = gb[e];
-        }
-        const double *tm = tabs + R2.tab;
-        const int n2 = R2.n;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int i = min(w2.t0 + tid + k * Q, w2.t1);
-            const int ks = max(i - 1, 0);
-            pm[k] = tm[ks];
-            px[k] = tm[n2 + ks];
-            pn[k] = tm[2 * (size_t)n2 + ks];
-            pd[k] = tm[3 * (size_t)n2 + i];
-            ps[k] = bases[R2.sb + ks];
-        }
-        // keep the loads here (a memory clobber: no sinking into the commit)
-        asm volatile("" ::: "memory");
-        return true;
-    };
-    bool pf = r0 < r1 ? issue(r0) : false;
-    for (int r = r0; r < r1; ++r) {
-        const ScoreRead R = reads[r];
-        const LeanWin wf = lean_win(R, m, a0, la1f);
-        if (pf) {
-            // ---- commit the prefetched window, start the next read's, score this one
-            {
-                dvec2 *sA = (dvec2 *)smem;
-                dvec2 *sB = (dvec2 *)(smem + wf.win);
-                double *sT = smem + 2 * wf.win;
-#pragma unroll
-                for (int u = 0; u < NPF; ++u) {
-                    const int e = u * Q + tid;
-                    if (e < wf.n16) {
-                        sA[e] = pa[u];
-                        sB[e] = pb[u];
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int e = tid + k * Q;
-                    const int i = wf.t0 + e;
-                    if (i <= wf.t1)
-                        lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
-                }
-            }
-            lean_barrier<NW>();
-            pf = r + 1 < r1 ? issue(r + 1) : false;
-            if (a <= m && !(split_mode & 2))
-                lean_chain(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
-            lean_barrier<NW>();
-        } else {
-            // ---- wide read: synchronous sub-passes over L lanes
-            int L = Q;
-            while (L > 1 && lean_need(L, R.H, R.P) > lds_elems)
-                L >>= 1;
-            for (int s0 = 0; s0 < Q; s0 += L) {
-                const int la0 = a0 + s0;
-                if (la0 > m)
-                    break;
-                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
-                lean_stage<Q>(R, w, tid, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
-                lean_barrier<NW>();
-                if (tid >= s0 && tid < s0 + L && a <= m)
-                    lean_chain(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
-                lean_barrier<NW>();
-            }
-            pf = r + 1 < r1 ? issue(r + 1) : false;
-        }
-    }
-    if (a > m)
-        return;
-    const double qnan = __builtin_nan("");
-    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
-                                    : dense + G.dense_off;
-    double *dst = base + (size_t)a * 9;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        dst[5 + k] = tI[k];
-    if (a < m) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dst[9 + k] = tS[k];
-        dst[13] = tD;
-    }
-    if (a == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            dst[k] = qnan;
-    }
 }
 
 // ---------------------------------------------------------------------
@@ -1759,9 +1511,6 @@ __device__ __forceinline__ void wg_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-#ifndef WS_NPF128
-#define WS_NPF128 20
-#endif
 #ifndef WS_NPF
 #define WS_NPF 19
 #endif
@@ -1810,11 +1559,6 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
             const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
 #pragma unroll
             for (int u = 0; u < NPF; ++u) {
-#ifdef WS_CLAMP_LOADS
-                const int e = min(u * Q + lt, w2.n16 - 1);
-                pa[u] = ga[e];
-                pb[u] = gb[e];
-#else
                 // predicated: chunks past the window are neither loaded nor
                 // committed (the commit's `e < n16` test)
                 const int e = u * Q + lt;
@@ -1822,7 +1566,6 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                     pa[u] = ga[e];
                     pb[u] = gb[e];
                 }
-#endif
             }
             const double *tm = tabs + R2.tab;
             const int n2 = R2.n;
@@ -1943,522 +1686,9 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 }
 
 // ---------------------------------------------------------------------
-// k_score_seg: the lean chains for bands too wide for k_score_ws's window
-//
-// Same per-lane chain as lean_chain (one new column per lane a: Sub(a+1, b),
-// Ins(a, b), Del(a+1); identical operands, order and FP64 max-plus, so
-// identical results), but the rows are walked in segments of SEG_S band
-// diagonals.  In column a's frame a row is d = i - a + c, and every interior
-// lane walks the same d range [1, H], so one segment [D, D+SEG_S) of all
-// SEG_L lanes touches kappa rows [D + 2*a0 - 1, D + SEG_S + 2*(a0+SEG_L) - 2]
-// and, in each, only the SEG_S/2 + 1 elements of diagonals [D-1, D+SEG_S).
-// That (SEG_S + 2*SEG_L) x (SEG_S/2 + 1) slice per band is staged in LDS --
-// independent of H, unlike the full kappa-row window (2L + H) x H/2 -- and
-// each band element is loaded about once per work item.
-// ---------------------------------------------------------------------
-// Fetch efficiency: a kappa row is P doubles at an arbitrary 8-B alignment,
-// so a segment's SEG_S/2 + 1 doubles of it span 1-2 128-B lines, and the
-// neighbouring segments of one row are too far apart in time to hit in L2:
-// HBM bytes are ~3x the useful bytes at SEG_S = 16, ~2.3x at 24, ~2x at 32.
-// Measured at c5 (PMC FETCH_SIZE, one GPU): S = 16 48.9 ms (328 GB),
-// S = 24 45.7 ms (264 GB), S = 32 62.2 ms (214 GB: 48 KB of LDS and 256
-// VGPRs with spills leave 3 workgroups per CU, latency-bound).  Default 24.
-constexpr int SEG_L = 64;                       // lanes (columns) per work item
-
-template <int SEG_S, int SEG_WPE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SEG_WPE)))
-k_score_seg(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
-            const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
-            const double *__restrict__ tabs, const double *__restrict__ bands,
-            double *__restrict__ dense, double *__restrict__ split, int split_mode)
-{
-    constexpr int SEG_W = SEG_S / 2 + 1;            // staged doubles per kappa row (odd)
-    constexpr int SEG_NR = SEG_S + 2 * SEG_L;       // staged kappa rows per band
-    constexpr int SEG_NT = SEG_S + SEG_L + 1;       // staged table rows
-    __shared__ double sA[SEG_NR * SEG_W];
-    __shared__ double sB[SEG_NR * SEG_W];
-    __shared__ __attribute__((aligned(16))) double sT[SEG_NT * 6];
-    // XCD-aware over the whole (item, read) grid: workgroups are dealt
-    // round-robin to the 8 XCDs in linear order, so linear id `lin` runs on XCD
-    // lin & 7; give each XCD a contiguous run of (item-fastest) grid cells, so
-    // the neighbouring items of one read, which share S kappa rows per segment,
-    // run at the same time under the same L2 (in split mode the grid is
-    // items x reads and gridDim.x is rarely a multiple of 8)
-    const int nx = gridDim.x;
-    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
-    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
-    const int cell = x * xq + min(x, xr) + (lin >> 3);
-    const int bx = cell % nx, by = cell / nx;
-    const WorkItem wi = items[bx];
-    const ScoreGroup G = groups[wi.group];
-    const int m = G.m;
-    const int a0 = wi.p0;
-    const int tid = threadIdx.x;
-    const int a = a0 + tid;
-    const bool active = a <= m;
-    int r0 = G.r0, r1 = G.r1;
-    if (split_mode & 1) {
-        r0 = G.r0 + by;
-        if (r0 >= G.r1)
-            return;
-        r1 = r0 + 1;
-    }
-    const bool hasS = a < m;
-    const double smask = hasS ? 0.0 : -RF_INF;
-    double tI[4], tS[4], tD = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        tI[k] = 0.0;
-        tS[k] = 0.0;
-    }
-    for (int r = r0; r < r1; ++r) {
-        const ScoreRead R = reads[r];
-        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
-        // this lane's rows (lean_chain): [i0, ilast] in the loop, i1 = ilast + 1 peeled
-        const int jn = min(a + 1, m);
-        const int i0 = max(0, jn - c);
-        const int i1 = min(jn + vb, n);
-        const int ilast = min(i1, a + vb);
-        const int dfirst = i0 - a + c, dlast = ilast - a + c;
-        const bool peel = i1 > ilast;
-        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
-        for (int off = 32; off >= 1; off >>= 1) {
-            dlo = min(dlo, __shfl_xor(dlo, off));
-            dhi = max(dhi, __shfl_xor(dhi, off));
-        }
-        dlo = __builtin_amdgcn_readfirstlane(dlo) & ~1;   // even segment starts
-        dhi = __builtin_amdgcn_readfirstlane(dhi);
-        const double *gA = bands + R.A;
-        const double *gB = bands + R.B;
-        const double *tm = tabs + R.tab;
-        const uint8_t *sq = bases + R.sb;
-        double prev[4], accI[4], accS[4], dd = -RF_INF;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            prev[k] = -RF_INF;
-            accI[k] = -RF_INF;
-            accS[k] = -RF_INF;
-        }
-        // segment staging, software-pipelined: the next segment's band slices
-        // and table rows are loaded into registers while this one is scored
-        constexpr int NL = (SEG_NR * SEG_W + 63) / 64;   // band elements per lane
-        constexpr int NTL = (SEG_NT + 63) / 64;           // table rows per lane
-        double ra[NL], rb[NL], tmt[NTL], tmm[NTL], tin[NTL], tdl[NTL];
-        int tsb[NTL];
-        auto load_seg = [&](int D) {
-            const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, ib = a0 - c + D;
-#pragma unroll
-            for (int u = 0; u < NL; ++u) {
-                const int t = tid + 64 * u;
-                const int row = t / SEG_W, col = t - row * SEG_W;
-                const int kap = kb + row, e = e0 + col;
-                const bool ok = t < SEG_NR * SEG_W && kap >= 0 && kap < K && e >= 0 && e < P;
-                const size_t g = ok ? (size_t)kap * P + e : 0;
-                ra[u] = gA[g];
-                rb[u] = gB[g];
-                if (!ok) {
-                    ra[u] = -RF_INF;
-                    rb[u] = -RF_INF;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < NTL; ++u) {
-                const int i = min(max(ib + tid + 64 * u, 0), n);
-                const int ks = max(i - 1, 0);
-                tsb[u] = i >= 1 ? sq[i - 1] : 4;
-                tmt[u] = tm[ks];
-                tmm[u] = tm[n + ks];
-                tin[u] = tm[2 * (size_t)n + ks];
-                tdl[u] = tm[3 * (size_t)n + i];
-            }
-        };
-        auto store_seg = [&]() {
-#pragma unroll
-            for (int u = 0; u < NL; ++u) {
-                const int t = tid + 64 * u;
-                if (t < SEG_NR * SEG_W) {
-                    sA[t] = ra[u];
-                    sB[t] = rb[u];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < NTL; ++u) {
-                const int t = tid + 64 * u;
-                if (t < SEG_NT)
-                    lean_row(sT + 6 * t, tsb[u], tmt[u], tmm[u], tin[u], tdl[u]);
-            }
-        };
-        if (dlo <= dhi && !(split_mode & 4))
-            load_seg(dlo);
-        for (int D = dlo; D <= dhi; D += SEG_S) {
-            const int kb = D + 2 * a0 - 1;          // first staged kappa row
-            const int e0 = (D - 1) >> 1;            // first staged element (diagonal D-1)
-            const int ib = a0 - c + D;              // first staged table row
-            wave_sync();                            // previous segment's chains are done
-            store_seg();
-            wave_sync();
-            if (D + SEG_S <= dhi && !(split_mode & 4))
-                load_seg(D + SEG_S);
-            if (!active || (split_mode & 2))
-                continue;
-            const int lo = max(D, dfirst), hi = min(D + SEG_S - 1, dlast);
-            // software-pipelined: row d+1's LDS operands are read while row d
-            // is scored; A(d-1, a) of row d+1 is row d's A(d, a)
-            auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
-                const int kr = d + 2 * a - kb;                       // staged row of (d, a)
-                const int ec = (d >> 1) - e0, ep = ((d - 1) >> 1) - e0;
-                ac = sA[kr * SEG_W + ec];
-                bI = sB[kr * SEG_W + ec];
-                bS = (hasS ? sB[(kr + 1) * SEG_W + ep] : bI) + smask;
-                const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
-                u0 = rec[0];
-                u1 = rec[1];
-                u2 = rec[2];
-            };
-            if (lo <= hi) {
-                double ac, bI, bS;
-                double2 u0, u1, u2;
-                ld(lo, ac, bI, bS, u0, u1, u2);
-                double aprev = (lo >= 1 && a - c + lo >= 1)
-                                   ? sA[(lo - 1 + 2 * a - kb) * SEG_W + ((lo - 1) >> 1) - e0] : -RF_INF;
-                for (int d = lo; d <= hi; ++d) {
-                    double acn, bIn, bSn;
-                    double2 v0, v1, v2;
-                    ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
-                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-                    const double dl = ac + u2.y;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
-                        prev[k] = best;
-                        accI[k] = vmax(accI[k], best + bI);
-                        accS[k] = vmax(accS[k], best + bS);
-                    }
-                    dd = vmax(dd, ac + bS);
-                    aprev = ac;
-                    ac = acn;
-                    bI = bIn;
-                    bS = bSn;
-                    u0 = v0;
-                    u1 = v1;
-                    u2 = v2;
-                }
-            }
-            const int dp = dlast + 1;
-            if (peel && dp >= D && dp < D + SEG_S) {
-                // last row of the new column lies below A/B column a's band (a < m)
-                const int kr = dp + 2 * a - kb;
-                const int ep = ((dp - 1) >> 1) - e0;
-                const int i = a - c + dp;
-                const double aprev = sA[(kr - 1) * SEG_W + ep];
-                const double bSr = sB[(kr + 1) * SEG_W + ep];
-                const double2 *rec = (const double2 *)(sT + 6 * (i - ib));
-                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
-                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
-            }
-        }
-        if (active) {
-            const double qnan = __builtin_nan("");
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
-                tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
-            }
-            tD += dd;
-        }
-    }
-    if (!active)
-        return;
-    const double qnan = __builtin_nan("");
-    double *base = (split_mode & 1) ? split + G.split_off + (size_t)by * (m + 1) * 9
-                                    : dense + G.dense_off;
-    double *dst = base + (size_t)a * 9;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        dst[5 + k] = tI[k];
-    if (a < m) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dst[9 + k] = tS[k];
-        dst[13] = tD;
-    }
-    if (a == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            dst[k] = qnan;
-    }
-}
-
-// ---------------------------------------------------------------------
-// k_score_segc: k_score_seg with whole-chunk staging (the default for wide
-// bands).
-//
-// Same chains, operands, order and FP64 max-plus as k_score_seg (identical
-// results).  A segment's piece of each kappa row -- W = S/2 + 1 doubles from
-// element e0 = (D-1) >> 1 -- is fetched as C = (W+1)/2 aligned 16-B chunks
-// (global_load_dwordx4, no per-element predicates: rows outside the band
-// are clamped, their values never read, and the arena guards keep chunk
-// over-reads inside the allocation), prefetched into VGPRs while the
-// current segment is scored, then written to LDS with ds_write_b128.  In LDS
-// the rows of even and odd local index live in two regions, so the 64 lanes
-// of a step (kappa rows two apart) read consecutive rows of one region:
-// row stride 2C doubles, a 2-way bank conflict for odd C.  Row r's first
-// wanted element sits at offset ((kb + r) * P + e0) & 1.
-// ---------------------------------------------------------------------
-template <int S>
-struct SegcGeo {
-    static constexpr int W = S / 2 + 1;            // wanted doubles per kappa row
-    static constexpr int C = (W + 1) / 2;          // 16-B chunks per row (parity shift included)
-    static constexpr int NR = S + 2 * 64;          // kappa rows per segment (even)
-    static constexpr int NH = NR / 2;              // rows per parity region
-    static constexpr int RS = NH * 2 * C;          // doubles per parity region
-    static constexpr int NU = (NR * C + 63) / 64;  // chunks per lane and band
-    static constexpr int NT = S + 65;              // table rows per segment
-    static constexpr int NTL = (NT + 63) / 64;     // table rows per lane
-};
-
-template <int S>
-__global__ void __launch_bounds__(64)
-k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
-             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
-             const double *__restrict__ tabs, const double *__restrict__ bands,
-             double *__restrict__ dense, double *__restrict__ split, int split_mode, int rchunk)
-{
-    using Gm = SegcGeo<S>;
-    constexpr int C = Gm::C, NR = Gm::NR, RS = Gm::RS, NU = Gm::NU, NT = Gm::NT, NTL = Gm::NTL;
-    __shared__ __attribute__((aligned(16))) double sA[2 * RS];
-    __shared__ __attribute__((aligned(16))) double sB[2 * RS];
-    __shared__ __attribute__((aligned(16))) double sT[NT * 6];
-    const int nx = gridDim.x;
-    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
-    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
-    const int cell = x * xq + min(x, xr) + (lin >> 3);
-    const int bx = cell % nx, by = cell / nx;
-    const WorkItem wi = items[bx];
-    const ScoreGroup G = groups[wi.group];
-    const int m = G.m;
-    const int a0 = wi.p0;
-    const int tid = threadIdx.x;
-    const int a = a0 + tid;
-    const bool active = a <= m;
-    int r0 = G.r0, r1 = G.r1;
-    if (split_mode & 1) {
-        r0 = G.r0 + by * rchunk;
-        if (r0 >= G.r1)
-            return;
-        r1 = min(r0 + rchunk, G.r1);
-    }
-    const bool hasS = a < m;
-    const double smask = hasS ? 0.0 : -RF_INF;
-    double tI[4], tS[4], tD = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        tI[k] = 0.0;
-        tS[k] = 0.0;
-    }
-    // LDS slot of chunk t = row r * C + cc of a band slice
-    auto lslot = [&](int t) {
-        const int r = t / C, cc = t - (t / C) * C;
-        return (r & 1) * RS + (r >> 1) * (2 * C) + 2 * cc;
-    };
-    for (int r = r0; r < r1; ++r) {
-        const ScoreRead R = reads[r];
-        const int c = R.c, vb = R.vb, P = R.P, K = R.K, n = R.n;
-        const int jn = min(a + 1, m);
-        const int i0 = max(0, jn - c);
-        const int i1 = min(jn + vb, n);
-        const int ilast = min(i1, a + vb);
-        const int dfirst = i0 - a + c, dlast = ilast - a + c;
-        const bool peel = i1 > ilast;
-        int dlo = active ? dfirst : INT_MAX, dhi = active ? dlast + (peel ? 1 : 0) : -1;
-        for (int off = 32; off >= 1; off >>= 1) {
-            dlo = min(dlo, __shfl_xor(dlo, off));
-            dhi = max(dhi, __shfl_xor(dhi, off));
-        }
-        dlo = __builtin_amdgcn_readfirstlane(dlo) & ~1;   // even segment starts
-        dhi = __builtin_amdgcn_readfirstlane(dhi);
-        const double *gA = bands + R.A;
-        const int64_t dB = R.B - R.A;
-        const double *tm = tabs + R.tab;
-        const uint8_t *sq = bases + R.sb;
-        double prev[4], accI[4], accS[4], dd = -RF_INF;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            prev[k] = -RF_INF;
-            accI[k] = -RF_INF;
-            accS[k] = -RF_INF;
-        }
-        dvec2 ra[NU], rb[NU];
-        double tmt[NTL], tmm[NTL], tin[NTL], tdl[NTL];
-        int tsb[NTL];
-        auto load_seg = [&](int D) {
-            const int kb = D + 2 * a0 - 1, e0 = (D - 1) >> 1, ib = a0 - c + D;
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const int t = min(tid + 64 * u, NR * C - 1);
-                const int rr = t / C, cc = t - (t / C) * C;
-                const int kap = min(max(kb + rr, 0), K - 1);          // rows outside the band: never read
-                const int64_t g = (((int64_t)kap * P + e0) & ~(int64_t)1) + 2 * cc;
-                ra[u] = *(const dvec2 *)(gA + g);
-                rb[u] = *(const dvec2 *)(gA + dB + g);
-            }
-#pragma unroll
-            for (int u = 0; u < NTL; ++u) {
-                const int i = min(max(ib + tid + 64 * u, 0), n);
-                const int ks = max(i - 1, 0);
-                tsb[u] = i >= 1 ? sq[i - 1] : 4;
-                tmt[u] = tm[ks];
-                tmm[u] = tm[n + ks];
-                tin[u] = tm[2 * (size_t)n + ks];
-                tdl[u] = tm[3 * (size_t)n + i];
-            }
-        };
-        auto store_seg = [&]() {
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const int t = tid + 64 * u;
-                if (t < NR * C) {
-                    const int l = lslot(t);
-                    *(dvec2 *)(sA + l) = ra[u];
-                    *(dvec2 *)(sB + l) = rb[u];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < NTL; ++u) {
-                const int t = tid + 64 * u;
-                if (t < NT)
-                    lean_row(sT + 6 * t, tsb[u], tmt[u], tmm[u], tin[u], tdl[u]);
-            }
-        };
-        if (dlo <= dhi && !(split_mode & 4))
-            load_seg(dlo);
-        for (int D = dlo; D <= dhi; D += S) {
-            const int kb = D + 2 * a0 - 1;          // first staged kappa row
-            const int e0 = (D - 1) >> 1;            // first wanted element (diagonal D-1)
-            const int ib = a0 - c + D;              // first staged table row
-            wave_sync();                            // previous segment's chains are done
-            store_seg();
-            wave_sync();
-            if (D + S <= dhi && !(split_mode & 4))
-                load_seg(D + S);
-            if (!active || (split_mode & 2))
-                continue;
-            const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
-            // element (kappa, d >> 1): local row r = kappa - kb in region r & 1
-            const int sh0 = (kb * (P & 1) + e0) & 1, sh1 = ((kb + 1) * (P & 1) + e0) & 1;
-            auto at = [&](int kap, int d) {
-                const int rr = kap - kb;
-                return (rr & 1) * RS + (rr >> 1) * (2 * C) + ((rr & 1) ? sh1 : sh0) + (d >> 1) - e0;
-            };
-            auto ld = [&](int d, double &ac, double &bI, double &bS, double2 &u0, double2 &u1, double2 &u2) {
-                const int kap = d + 2 * a;
-                const int ix = at(kap, d);
-                ac = sA[ix];
-                bI = sB[ix];
-                bS = (hasS ? sB[at(kap + 1, d - 1)] : bI) + smask;
-                const double2 *rec = (const double2 *)(sT + 6 * (a - c + d - ib));
-                u0 = rec[0];
-                u1 = rec[1];
-                u2 = rec[2];
-            };
-            if (lo <= hi) {
-                double ac, bI, bS;
-                double2 u0, u1, u2;
-                ld(lo, ac, bI, bS, u0, u1, u2);
-                double aprev = (lo >= 1 && a - c + lo >= 1) ? sA[at(lo - 1 + 2 * a, lo - 1)] : -RF_INF;
-                for (int d = lo; d <= hi; ++d) {
-                    double acn, bIn, bSn;
-                    double2 v0, v1, v2;
-                    ld(min(d + 1, hi), acn, bIn, bSn, v0, v1, v2);
-                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-                    const double dl = ac + u2.y;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const double best = vmax(vmax(aprev + sub[k], prev[k] + u2.x), dl);
-                        prev[k] = best;
-                        accI[k] = vmax(accI[k], best + bI);
-                        accS[k] = vmax(accS[k], best + bS);
-                    }
-                    dd = vmax(dd, ac + bS);
-                    aprev = ac;
-                    ac = acn;
-                    bI = bIn;
-                    bS = bSn;
-                    u0 = v0;
-                    u1 = v1;
-                    u2 = v2;
-                }
-            }
-            const int dp = dlast + 1;
-            if (peel && dp >= D && dp < D + S) {
-                // last row of the new column lies below A/B column a's band (a < m)
-                const int kap = dp + 2 * a;
-                const double aprev = sA[at(kap - 1, dp - 1)];
-                const double bSr = sB[at(kap + 1, dp - 1)];
-                const double2 *rec = (const double2 *)(sT + 6 * (a - c + dp - ib));
-                const double2 u0 = rec[0], u1 = rec[1], u2 = rec[2];
-                const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
-            }
-        }
-        if (active) {
-            const double qnan = __builtin_nan("");
-            if (split_mode & 1) {
-                // this read's partials (k_reduce folds the reads in batch order)
-                double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
-                if (a < m) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
-                    dst[13] = dd;
-                }
-                if (a == 0) {
-#pragma unroll
-                    for (int k = 0; k < 5; ++k)
-                        dst[k] = qnan;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
-                    tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
-                }
-                tD += dd;
-            }
-        }
-    }
-    if (!active || (split_mode & 1))
-        return;
-    const double qnan = __builtin_nan("");
-    double *dst = dense + G.dense_off + (size_t)a * 9;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        dst[5 + k] = tI[k];
-    if (a < m) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dst[9 + k] = tS[k];
-        dst[13] = tD;
-    }
-    if (a == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            dst[k] = qnan;
-    }
-}
-
-// ---------------------------------------------------------------------
 // k_score_segl: the wide-band scorer over line-aligned band rows (default)
 //
-// Same chains, operands, order and FP64 max-plus as k_score_seg / segc
+// Same chains, operands, order and FP64 max-plus as k_score_ws's lean_chain
 // (identical results).  Segments are 32 band diagonals [D, D+32) with D a
 // multiple of 32, so a kappa row's piece of a segment is elements
 // [D/2, D/2 + 16): exactly one 128-B line when the band's rows are padded to
@@ -2479,22 +1709,14 @@ k_score_segc(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
 #ifndef SEGL_UNROLL
 #define SEGL_UNROLL 32
 #endif
-#ifndef SEGL_FENCE_KIND
-#define SEGL_FENCE_KIND 0
-#endif
-#if SEGL_FENCE_KIND == 1
-#define SEGL_FENCE() asm volatile("" ::: "memory")
-#elif SEGL_FENCE_KIND == 2
-#define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0x0006)   // VALU and SALU may cross
-#else
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
-// S = 32: a kappa row's piece of a segment is one 128-B line; S = 16: half a
-// line (64 B, 64-B aligned), with fewer registers and 55 % of the LDS of
-// S = 32, so that two waves fit per SIMD.
+// A kappa row's piece of a segment is one 128-B line.  (Half-line segments
+// of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
+// slower at c5: 30.6 ms at one wave per SIMD, 40.6 ms at two with spills,
+// against 27.9 ms; profiles/r02_exp_segl16.json.)
 template <int S_>
 struct SeglGeo {
-    static_assert(S_ == 16 || S_ == 32, "segments of 16 or 32 diagonals");
+    static_assert(S_ == 32, "segments of 32 diagonals");
     static constexpr int S = S_;        // diagonals per segment
     static constexpr int LS = 65;       // LDS row: columns a0 .. a0+64
     static constexpr int NRW = S + 1;   // LDS rows: d = D-1 .. D+S-1
@@ -2506,15 +1728,9 @@ struct SeglGeo {
     static constexpr int NUG = (NROW * NC + 63) / 64;
     static constexpr int NT = S + 65;   // table rows: i - ib in [0, S + 65)
 };
-#ifndef SEGL_PF16
-#define SEGL_PF16 1    // S = 16: register prefetch of the next segment (0: load at its store)
-#endif
-#ifndef SEGL_WPE16
-#define SEGL_WPE16 2   // waves per SIMD requested for S = 16
-#endif
 
 template <int SEGS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SEGS == 16 ? SEGL_WPE16 : 1)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
              const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
              const double *__restrict__ tabs, const double *__restrict__ bands,
@@ -2523,7 +1739,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     using Gm = SeglGeo<SEGS>;
     constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
     constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
-    constexpr bool PF = SEGS == 32 || SEGL_PF16;   // next segment prefetched into registers
+    constexpr bool PF = true;   // next segment prefetched into registers
     constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
     __shared__ __attribute__((aligned(16))) double sA[SL];
     __shared__ __attribute__((aligned(16))) double sB[SL];
@@ -3610,11 +2826,9 @@ struct Slot {
 // Choice of dense scorer for one launch.
 struct ScorePick {
     bool lean = false;
-    bool seg = false;   // k_score_seg: wide bands (window too large for LDS), finite tables
-    int nw = 1;     // lean: waves per workgroup (64 * nw chain columns per work item)
+    bool seg = false;   // k_score_segl: wide bands (window too large for LDS), finite tables
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
-    int wsq = 256;  // ws: chain lanes per workgroup (256: 1 workgroup per CU; 128: 2)
-    int q() const { return nw == 8 ? wsq : 64 * nw; }   // chain columns per work item
+    int q() const { return 256; }   // k_score_ws chain columns per work item
 };
 
 struct DevBuf {
@@ -3652,9 +2866,12 @@ void parallel_for(int nth, F fn)
 // (match, mismatch, ins) triple and del value of the context's reads gets a
 // 16-bit code, first come first served, keyed by the exact bit patterns.  A
 // read whose values would need a code past RF_CODES - 1 stays uncoded (its
-// DP reads the tables directly).  Entries are only appended, so codes of
-// earlier reads stay valid; `lut` is the device copy (RF_CODES x 4 triple
-// doubles, then RF_CODES del doubles).
+// DP reads the tables directly; counted in `uncoded_reads`, rf_code_stats).
+// Entries are only appended while any coded sequence outside an upload is
+// still valid, so codes of earlier reads stay valid; an upload that replaces
+// every coded sequence of the context starts a fresh dictionary, so a
+// long-lived context refilled batch after batch does not fill it up.  `lut`
+// is the device copy (RF_CODES x 4 triple doubles, then RF_CODES del doubles).
 struct CodeDict {
     struct K3 {
         uint64_t a, b, c;
@@ -3670,7 +2887,19 @@ struct CodeDict {
     std::unordered_map<uint64_t, uint32_t> d1;
     std::vector<double> t3v, d1v;   // host copies of the entries
     size_t up3 = 0, up1 = 0;        // entries already on the device
+    int64_t uncoded_reads = 0;      // reads left uncoded because the dictionary was full
+    int64_t resets = 0;
     DevBuf lut;
+
+    void reset()
+    {
+        t3.clear();
+        d1.clear();
+        t3v.clear();
+        d1v.clear();
+        up3 = up1 = 0;
+        ++resets;
+    }
 
     static uint64_t bits(double x)
     {
@@ -3720,25 +2949,13 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
-#ifndef WS_Q_DEFAULT
-#define WS_Q_DEFAULT 256
-#endif
-#ifndef SEG_S_DEFAULT
-#define SEG_S_DEFAULT 24
-#endif
 #ifndef DP_WIDE_DEFAULT
 #define DP_WIDE_DEFAULT 3
 #endif
 struct Opts {
     int score_mode = 0;     // RF_OPT_SCORE_MODE: 0 auto, 1 fused, 2 split
     int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg
-    int lean_nw = 8;        // RF_OPT_LEAN_NW: 8 = k_score_ws, 1/2/4 = k_score_lean waves
-    int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: 0 = default budget
-    int ws_q = WS_Q_DEFAULT;   // RF_OPT_WS_Q: k_score_ws chain lanes (256 or 128)
-    int seg_s = SEG_S_DEFAULT;   // RF_OPT_SEG_S: diagonals per segment (k_score_segl: 16 or 32; seg/segc: 16, 24, 32)
-    int seg_lds = 0;        // RF_OPT_SEG_LDS: extra LDS bytes per k_score_seg workgroup
-    int seg_wpe = 1;        // RF_OPT_SEG_WPE: k_score_seg waves-per-EU register cap (1, 2)
-    int seg_ver = 4;        // RF_OPT_SEG_VER: wide-band scorer 4 = k_score_segl, 3 = k_score_segc, 1 = k_score_seg
+    int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: k_score_ws LDS budget (0 = default 160 KB)
     int dp_wide = DP_WIDE_DEFAULT;   // RF_OPT_DP_WIDE: wide lean tasks (bit 0: H 128..255 in 64 lanes,
                                      // bit 1: H 64..127 in 32 lanes)
     int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
@@ -3803,7 +3020,7 @@ struct rf_ctx {
         std::vector<int32_t> slot, seq, tpl, bw;
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
-        size_t nw[3] = {};     // lean wide / narrow-task classes (RF_OPT_DP_WIDE)
+        size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -4040,18 +3257,12 @@ void load_env_opts(Opts &o)
         o.score_kernel = !std::strcmp(k, "general") ? 1 : !std::strcmp(k, "seg") ? 2 : 0;
     if (const char *m = std::getenv("RIFRAF_SCORE_MODE"))
         o.score_mode = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "split") ? 2 : 0;
-    o.lean_nw = env_int("RIFRAF_LEAN_NW", o.lean_nw);
     o.lean_lds_kb = env_int("RIFRAF_LEAN_LDS_KB", o.lean_lds_kb);
-    o.ws_q = env_int("RIFRAF_WS_Q", o.ws_q);
-    o.seg_s = env_int("RIFRAF_SEG_S", o.seg_s);
-    o.seg_lds = env_int("RIFRAF_SEG_LDS", o.seg_lds);
-    o.seg_wpe = env_int("RIFRAF_SEG_WPE", o.seg_wpe);
     o.bt_global = env_int("RIFRAF_BT_GLOBAL", o.bt_global);
     o.dp_psplit = env_int("RIFRAF_DP_PSPLIT", o.dp_psplit);
     o.dp_np8 = env_int("RIFRAF_DP_NO_NP8", 0) ? 0 : 1;
     o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
     o.dp_streams = env_int("RIFRAF_DP_STREAMS", o.dp_streams);
-    o.seg_ver = env_int("RIFRAF_SEG_VER", o.seg_ver);
     o.bt_win_kb = env_int("RIFRAF_BT_WIN_KB", o.bt_win_kb);
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
@@ -4070,19 +3281,12 @@ ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool a
         int need1 = 0;
         for (const auto &R : reads)
             need1 = std::max(need1, lean_need(1, R.H, R.P));
-        // 8 = wave-specialized k_score_ws (256 chain lanes + 256 loader lanes)
-        int nw = o.lean_nw;
-        nw = nw >= 8 ? 8 : (nw >= 4 ? 4 : (nw >= 2 ? 2 : 1));
-        // k_score_ws with 128 chain lanes: two workgroups (two windows in
-        // flight) per CU, each with half the LDS
-        // (measured at c4: 128 -> +14 %, 320 / 384 chain lanes -> +50 % scoring time)
-        const int wsq = (nw == 8 && o.ws_q == 128) ? 128 : 256;
-        const int dflt_kb = nw >= 4 ? (wsq == 128 ? 80 : 160) : 40 * nw;
-        const int lds = std::max((o.lean_lds_kb > 0 ? o.lean_lds_kb : dflt_kb) * 1024 / 8, need1);
+        // k_score_ws: 256 chain lanes + 256 loader lanes, one workgroup per CU
+        // (measured at c4: 128 chain lanes (two workgroups per CU) +14 %,
+        // 320 / 384 chain lanes +50 % scoring time)
+        const int lds = std::max((o.lean_lds_kb > 0 ? o.lean_lds_kb : 160) * 1024 / 8, need1);
         if (lds <= 160 * 1024 / 8) {
             p.lean = true;
-            p.nw = nw;
-            p.wsq = wsq;
             p.lds = lds;
             return p;
         }
@@ -4119,86 +3323,35 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     // every window but skips the chains (measures its load pipeline alone)
     if (ctx->opt.diag_lean_nocomp & 1)
         sm |= 2;
-    if (ctx->opt.diag_lean_nocomp & 2)   // k_score_seg: skip the segment loads
+    if (ctx->opt.diag_lean_nocomp & 2)   // k_score_segl: skip the segment loads
         sm |= 4;
 #endif
     dim3 grid(nitems, gy);
-    if (pk.seg && ctx->opt.seg_ver == 4) {
+    if (pk.seg) {
         int rchunk = 1;
         if (split) {
             rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
-        // RF_OPT_SEG_S 16: half-line segments (two waves per SIMD), else 32
-        if (ctx->opt.seg_s == 16)
-            hipLaunchKernelGGL(k_score_segl<16>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm, rchunk);
-        else
-            hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm, rchunk);
-    } else if (pk.seg && ctx->opt.seg_ver == 3) {
-        int rchunk = 1;
-        if (split) {
-            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
-            grid.y = (gy + rchunk - 1) / rchunk;
-        }
-        const int ss = ctx->opt.seg_s;
-#define RF_SEGC_LAUNCH(S)                                                                                    \
-    hipLaunchKernelGGL((k_score_segc<S>), grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,    \
-                       d_tabs, d_bands, dense, split, sm, rchunk)
-        if (ss == 16)
-            RF_SEGC_LAUNCH(16);
-        else if (ss == 32)
-            RF_SEGC_LAUNCH(32);
-        else
-            RF_SEGC_LAUNCH(24);
-#undef RF_SEGC_LAUNCH
-    } else if (pk.seg) {
-        // RF_OPT_SEG_S: diagonals per segment (16, 24 or 32)
-        const int segs = ctx->opt.seg_s;
-        // RF_OPT_SEG_LDS: extra (unused) LDS bytes per workgroup -- caps the
-        // workgroups per CU, i.e. the L2 footprint between a kappa row's reuses
-        const size_t pad = (size_t)std::max(ctx->opt.seg_lds, 0);
-        // RF_OPT_SEG_WPE: minimum waves per SIMD the register allocation is
-        // capped for (1: no cap; 2: <= 256 VGPRs)
-        const int wpe = ctx->opt.seg_wpe;
-#define RF_SEG_LAUNCH(S, W)                                                                                  \
-    hipLaunchKernelGGL((k_score_seg<S, W>), grid, dim3(64), pad, ctx->stream, items, groups, reads, d_bases, \
-                       d_tabs, d_bands, dense, split, sm)
-        if (segs == 16 && wpe == 2)
-            RF_SEG_LAUNCH(16, 2);
-        else if (segs == 16)
-            RF_SEG_LAUNCH(16, 1);
-        else if (segs == 24)
-            RF_SEG_LAUNCH(24, 1);
-        else
-            RF_SEG_LAUNCH(32, 1);
-#undef RF_SEG_LAUNCH
-    }
-    else if (!pk.lean)
+        hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                           d_tabs, d_bands, dense, split, sm, rchunk);
+    } else if (!pk.lean) {
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
-    else if (pk.nw == 8)
-    {
-        if (pk.wsq == 128)
-            hipLaunchKernelGGL((k_score_ws<WS_NPF128, 128>), grid, dim3(256), pk.lds * 8, ctx->stream, items,
-                               groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
-        else
-            hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
-                               groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    } else {
+        hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
+                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     }
-    else if (pk.nw == 1)
-        hipLaunchKernelGGL((k_score_lean<1, LEAN_NPF>), grid, dim3(64), pk.lds * 8, ctx->stream, items,
-                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
-    else if (pk.nw == 2)
-        hipLaunchKernelGGL((k_score_lean<2, LEAN_NPF>), grid, dim3(128), pk.lds * 8, ctx->stream, items,
-                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
-    else
-        hipLaunchKernelGGL((k_score_lean<4, LEAN_NPF>), grid, dim3(256), pk.lds * 8, ctx->stream, items,
-                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
 }
 
 }  // namespace
+
+// rf_last_error text for the host stage machine in rifraf_batch.cpp (same
+// library, C++ linkage, not part of the C-ABI)
+int rf_internal_fail(rf_ctx *ctx, int code, const char *msg)
+{
+    return fail(ctx, code, msg ? msg : "");
+}
 
 extern "C" {
 
@@ -4231,14 +3384,6 @@ int rf_create(int device, rf_ctx **out)
         (void)hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
     }
     // the lean scorer may use up to the whole 160 KiB LDS of a CU
-    (void)hipFuncSetAttribute((const void *)k_score_lean<1, LEAN_NPF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_score_lean<2, LEAN_NPF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_score_lean<4, LEAN_NPF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF128, 128>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
@@ -4292,18 +3437,12 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     switch (key) {
     case RF_OPT_SCORE_MODE: return &o.score_mode;
     case RF_OPT_SCORE_KERNEL: return &o.score_kernel;
-    case RF_OPT_LEAN_NW: return &o.lean_nw;
     case RF_OPT_LEAN_LDS_KB: return &o.lean_lds_kb;
-    case RF_OPT_WS_Q: return &o.ws_q;
-    case RF_OPT_SEG_S: return &o.seg_s;
-    case RF_OPT_SEG_LDS: return &o.seg_lds;
-    case RF_OPT_SEG_WPE: return &o.seg_wpe;
     case RF_OPT_BT_GLOBAL: return &o.bt_global;
     case RF_OPT_DP_PSPLIT: return &o.dp_psplit;
     case RF_OPT_DP_NP8: return &o.dp_np8;
     case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
     case RF_OPT_DP_STREAMS: return &o.dp_streams;
-    case RF_OPT_SEG_VER: return &o.seg_ver;
     case RF_OPT_BT_WIN_KB: return &o.bt_win_kb;
     case RF_OPT_STAGE_KB: return &o.stage_kb;
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
@@ -4343,10 +3482,26 @@ int rf_reserve(rf_ctx *ctx, int64_t band_bytes)
     if (!ctx || band_bytes < 0)
         return RF_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    ++ctx->state_epoch;
     if (ctx->band_arena.cap - ctx->band_arena.top >= band_bytes + ARENA_GUARD)
-        return 0;
+        return 0;   // room already: nothing moves, cached plans stay valid
+    ++ctx->state_epoch;   // regions move (arena_grow also bumps layout_gen)
     return arena_grow(ctx, ctx->band_arena, band_bytes, nullptr);
+}
+
+int rf_code_stats(const rf_ctx *ctx, int64_t *entries3, int64_t *entries1, int64_t *uncoded_reads,
+                  int64_t *resets)
+{
+    if (!ctx)
+        return RF_ERR_ARG;
+    if (entries3)
+        *entries3 = (int64_t)ctx->codes.t3.size();
+    if (entries1)
+        *entries1 = (int64_t)ctx->codes.d1.size();
+    if (uncoded_reads)
+        *uncoded_reads = ctx->codes.uncoded_reads;
+    if (resets)
+        *resets = ctx->codes.resets;
+    return 0;
 }
 
 int64_t rf_device_bytes(const rf_ctx *ctx)
@@ -4478,6 +3633,8 @@ int upload_sequence_chunk(rf_ctx *ctx, int32_t first, int32_t k0, int32_t k1, co
             ctx->seqs[first + k0 + k].coded = ok;
         }
     });
+    for (int32_t k = 0; k < nseq; ++k)
+        D.uncoded_reads += ctx->seqs[first + k0 + k].coded ? 0 : 1;
     // 3. new code-dictionary entries, one H2D copy each + device scatter
     {
         CodeDict &D = ctx->codes;
@@ -4522,6 +3679,16 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     ++ctx->state_epoch;
     if ((int64_t)first + nseq > (int64_t)ctx->seqs.size())
         ctx->seqs.resize(first + nseq);
+    // a fresh code dictionary when no coded sequence outside this upload is
+    // still valid (nothing references the old codes)
+    {
+        bool others = false;
+        for (size_t k = 0; k < ctx->seqs.size() && !others; ++k)
+            others = ((int64_t)k < first || (int64_t)k >= (int64_t)first + nseq) && ctx->seqs[k].valid &&
+                     ctx->seqs[k].coded;
+        if (!others && !(ctx->codes.t3.empty() && ctx->codes.d1.empty()))
+            ctx->codes.reset();
+    }
     // 0. grow each arena at most once for the whole batch
     {
         int64_t need_b = 0, need_t = 0;
@@ -4744,7 +3911,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[3];
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2];
         int hmax64 = 0, hmaxg = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
@@ -4805,7 +3972,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // task per wave, H 64..127 as two 32-lane tasks per wave, both NP = 2
                 // (the 16-lane NP = 4 / 8 kernels need > 256 registers: one wave
                 // per SIMD)
-                const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : (npi == 0 ? 2 : -1));
+                const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
                 if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
                 } else if (lean && ((psplit >> npi) & 1) && np8) {
@@ -4867,7 +4034,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 4; ++a)
             for (int b = 0; b < 4; ++b)
                 P.nrp[a][b] = cp[a][b].size();
-        for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 2; ++a)
             P.nw[a] = cw[a].size();
         P.n64 = c64.size();
         P.ng = cg.size();
@@ -4907,7 +4074,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     launches.push_back({16 + 4 * a + b, at, P.nrp[a][b]});
                     at += P.nrp[a][b];
                 }
-        for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 2; ++a)
             if (P.nw[a]) {
                 launches.push_back({32 + a, at, P.nw[a]});
                 at += P.nw[a];
@@ -4968,13 +4135,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 32) {
-            // task-width classes, all NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
-            // (H <= 127), 34 = 8 lanes (H <= 31)
+            // task-width classes, both NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
+            // (H <= 127)
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
-            const KFn kw[3] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<2, true, dpl_pmax(2, 32), 32>,
-                               k_dpr<2, true, dpl_pmax(2, 8), 8>};
-            const int a = L.kind - 32, lpt = a == 0 ? 64 : (a == 1 ? 32 : 8), tpw = 64 / lpt;
+            const KFn kw[2] = {k_dpr<2, true, dpl_pmax(2, 64), 64>, k_dpr<2, true, dpl_pmax(2, 32), 32>};
+            const int a = L.kind - 32, lpt = a == 0 ? 64 : 32, tpw = 64 / lpt;
             hipLaunchKernelGGL(kw[a], dim3((n + tpw - 1) / tpw), dim3(64),
                                (size_t)tpw * dpl_task_bytes(2, dpl_pmax(2, lpt), lpt), st, d_tasks + L.at, n,
                                d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);

@@ -27,6 +27,7 @@ _SIGNATURES = {
     "rf_last_error": (c_char_p, [c_void_p]),
     "rf_reserve": (c_int, [c_void_p, c_int64]),
     "rf_device_bytes": (c_int64, [c_void_p]),
+    "rf_code_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "rf_set_sequences": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_set_templates": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
@@ -58,9 +59,8 @@ _SIGNATURES = {
 }
 
 # rf_set_option keys (include/rifraf_hip.h RF_OPT_*)
-OPTIONS = {"score_mode": 1, "score_kernel": 2, "lean_nw": 3, "lean_lds_kb": 4, "ws_q": 5, "seg_s": 6,
-           "seg_lds": 7, "seg_wpe": 8, "bt_global": 9, "dp_psplit": 10, "dp_np8": 11, "dp_np8_lean": 12,
-           "dp_streams": 13, "seg_ver": 14, "bt_win_kb": 15, "stage_kb": 16,
+OPTIONS = {"score_mode": 1, "score_kernel": 2, "lean_lds_kb": 4, "bt_global": 9, "dp_psplit": 10,
+           "dp_np8": 11, "dp_np8_lean": 12, "dp_streams": 13, "bt_win_kb": 15, "stage_kb": 16,
            "band_pad": 17, "dp_wide": 18}
 # symbolic values of the enum-like options
 OPTION_VALUES = {"score_mode": {"auto": 0, "fused": 1, "split": 2},

@@ -242,6 +242,18 @@ def native_eligible(clusters, params) -> bool:
             return False
         if not params.batch_fixed and 1 < params.batch_size < n:
             return False
+        # an empty read or a per-base vector of the wrong length keeps the
+        # cluster on the Python stage machine, whose RifrafSequence
+        # constructor (rifrafsequences.jl:19-35) gives the reference's
+        # behaviour for it (empty sequence / ValueError)
+        quals = kw.get("error_log_ps")
+        if quals is None:
+            quals = kw.get("phreds")
+        if quals is None or len(quals) != n:
+            return False
+        for s, q in zip(kw["dnaseqs"], quals):
+            if len(s) == 0 or len(q) != len(s):
+                return False
     return True
 
 

@@ -8,7 +8,7 @@ GPU raises EngineUnavailable.
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_double, c_int32, c_void_p
+from ctypes import c_int64, byref, c_double, c_int32, c_void_p
 
 import numpy as np
 
@@ -96,6 +96,13 @@ class Engine:
 
     def device_bytes(self) -> int:
         return int(self.lib.rf_device_bytes(self.ctx))
+
+    def code_stats(self) -> dict:
+        """rf_code_stats: the row-code dictionary's size, the reads left
+        uncoded because it was full, and its fresh starts."""
+        v = [c_int64() for _ in range(4)]
+        self._check(self.lib.rf_code_stats(self.ctx, *[byref(x) for x in v]))
+        return dict(zip(("entries3", "entries1", "uncoded_reads", "resets"), (x.value for x in v)))
 
     def set_sequences(self, first: int, seqs):
         """Upload RifrafSequence tables for ids [first, first+len(seqs))."""

@@ -13,19 +13,16 @@ call on the same inputs, and every method below is collective.
 
 Ownership:
   - sequence tables and templates are replicated (uploaded on every rank);
-  - batch slots [0, nslots) are split into contiguous blocks, one per rank
-    (rank r owns [r*nslots//W, (r+1)*nslots//W)); the A/B bands of a slot
-    live only on its owner, so band memory is sharded;
-  - slots >= nslots (the reference and scratch slots of model._Run) belong
+  - read batch slots [0, nreads) are dealt round-robin: rank r owns the
+    slots s with s % W == r, so the A/B bands of a slot live only on its
+    owner and band memory is sharded;
+  - slots >= nreads (the reference and scratch slots of model._Run) belong
     to the last rank.
-  - `nslots` must be the batch size the run actually uses (rifraf() fills
-    batch slots 0..batch_size-1, model.jl:569-573 / :1038-1066), not the
-    read count: `ShardedEngine.for_params` derives it from RifrafParams.  A
-    block partition over the read count would put every batch slot of a
-    20-read batch on rank 0.  The work is then balanced whenever the batch
-    holds >= W reads (REFINE / SCORE, and every stage with batch_size <= 1,
-    the throughput setting of configs 2-5); the fixed 5-read INIT/FRAME
-    batch (batch_fixed_size) is spread over min(W, 5)-ish ranks only.
+  - rifraf() fills batch slots 0..B-1 (model.jl:569-573, :1038-1066) and
+    check_score! can grow B by base_batch_size up to the read count
+    (model.jl:1094-1112).  A round-robin deal is balanced for every prefix
+    [0, B), so the work stays balanced (within one read per rank) as the
+    batch grows, and no rank holds more than ceil(nreads / W) reads' bands.
 
 Exchange and exactness:
   - realign / backtrace results are per job; they are gathered verbatim, so
@@ -50,11 +47,11 @@ from .proposals import to_arrays
 
 
 class ShardedEngine:
-    def __init__(self, local, nslots: int, group=None):
+    def __init__(self, local, nreads: int, group=None):
         import torch
         import torch.distributed as dist
         self.e = local
-        self.nslots = int(nslots)
+        self.nreads = int(nreads)
         self.group = group
         self.dist = dist
         self.torch = torch
@@ -63,16 +60,15 @@ class ShardedEngine:
         backend = dist.get_backend(group)
         self.dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
                     else torch.device("cpu"))
-        self.bounds = [r * self.nslots // self.world for r in range(self.world + 1)]
         self.last_dense = None
 
     @classmethod
     def for_params(cls, local, nreads: int, params=None, group=None):
-        """ShardedEngine sized for the batch rifraf() will use: batch_size
-        (all reads when batch_size <= 1, model.jl:569-573), capped at nreads."""
-        bs = getattr(params, "batch_size", 0) if params is not None else 0
-        nslots = nreads if bs <= 1 else min(bs, nreads)
-        return cls(local, nslots, group)
+        """ShardedEngine for a rifraf() run over `nreads` reads.  Every batch
+        size the run may reach (batch_size, grown by check_score! up to all
+        reads) is balanced by the round-robin deal, so only the read count
+        matters; `params` is accepted for call-site symmetry."""
+        return cls(local, nreads, group)
 
     def slot_counts(self, slots) -> list:
         """Number of the given slots each rank owns (load-balance diagnostics)."""
@@ -87,19 +83,12 @@ class ShardedEngine:
         slot = int(slot)
         if slot < 0:
             raise ValueError("negative slot")
-        if slot >= self.nslots:
+        if slot >= self.nreads:
             return self.world - 1
-        return int(np.searchsorted(self.bounds, slot, side="right")) - 1
+        return slot % self.world
 
     def owned(self, slots) -> np.ndarray:
-        slots = np.asarray(slots, np.int64)
-        if slots.size == 0:
-            return np.zeros(0, bool)
-        lo, hi = self.bounds[self.rank], self.bounds[self.rank + 1]
-        mine = (slots >= lo) & (slots < hi)
-        if self.rank == self.world - 1:
-            mine |= slots >= self.nslots
-        return mine
+        return self.owned_by(self.rank, slots)
 
     # ------------------------------------------------------------------
     # collectives
@@ -217,10 +206,12 @@ class ShardedEngine:
     def owned_by(self, rank: int, slots) -> np.ndarray:
         """Mask of the slots `rank` owns (the same rule as owned())."""
         slots = np.asarray(slots, np.int64)
-        lo, hi = self.bounds[rank], self.bounds[rank + 1]
-        mine = (slots >= lo) & (slots < hi)
+        if slots.size == 0:
+            return np.zeros(0, bool)
+        reads = slots < self.nreads
+        mine = reads & (slots % self.world == rank)
         if rank == self.world - 1:
-            mine |= slots >= self.nslots
+            mine |= ~reads
         return mine
 
     def score(self, groups, per_seq: bool = False):

@@ -5,6 +5,8 @@ run end to end on CPU, and gives GPU-vs-oracle whole-run comparisons.  Same
 method signatures and semantics as Engine (slots own A/B bands, forward
 flags, left-fold scoring)."""
 import copy
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -12,6 +14,11 @@ import oracle
 from rifraf_amd.bandedarrays import BandedArray
 from rifraf_amd.engine import RF_BAND_A, RF_BWD, RF_FWD, RF_SKEW, RF_TRIM, RifrafError
 from rifraf_amd.proposals import to_arrays
+
+
+# host threads for the oracle's C calls (ctypes releases the GIL): the GPU
+# box grants 16 cores of a much larger machine
+NTHREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))))
 
 
 class OracleEngine:
@@ -39,42 +46,62 @@ class OracleEngine:
         bws = np.broadcast_to(bws, (n,))
         out = np.empty(n)
         for k in range(n):
+            if int(bws[k]) < 1:
+                raise RifrafError("bandwidth must be positive")
+
+        def one(k):
             s = self.seqs[int(seqs[k])]
             t, ver = self.tpls[int(tpls[k])]
             bw = int(bws[k])
-            if bw < 1:
-                raise RifrafError("bandwidth must be positive")
-            ent = self.slots.setdefault(int(slots[k]), {})
             key = (int(seqs[k]), int(tpls[k]), ver, bw)
+            A = B = None
             try:
                 if flags & RF_FWD:
-                    A, mv = oracle.forward(t, s, moves=True, skew=bool(flags & RF_SKEW),
-                                           trim=bool(flags & RF_TRIM), bandwidth=bw)
-                    ent["A"] = (A, mv, key, len(s), len(t))
+                    A = oracle.forward(t, s, moves=True, skew=bool(flags & RF_SKEW),
+                                       trim=bool(flags & RF_TRIM), bandwidth=bw)
                 if flags & RF_BWD:
                     B = oracle.backward(t, s, bandwidth=bw)
-                    ent["B"] = (B, None, key, len(s), len(t))
             except oracle.OracleError as e:
-                raise RifrafError(str(e))
-            band = ent["A"] if flags & RF_FWD else ent["B"]
-            data = band[0]
-            H = data.shape[0]
+                return RifrafError(str(e))
+            return key, len(s), len(t), A, B
+
+        if n >= 32 and NTHREADS > 1:
+            with ThreadPoolExecutor(NTHREADS) as ex:
+                res = list(ex.map(one, range(n)))
+        else:
+            res = [one(k) for k in range(n)]
+        for k, r in enumerate(res):     # in job order: the first error wins, as in a serial loop
+            if isinstance(r, RifrafError):
+                raise r
+            key, ns, nt, A, B = r
+            ent = self.slots.setdefault(int(slots[k]), {})
+            if A is not None:
+                ent["A"] = (A[0], A[1], key, ns, nt)
+            if B is not None:
+                ent["B"] = (B, None, key, ns, nt)
+            bw = key[3]
+            data = ent["A"][0] if flags & RF_FWD else ent["B"][0]
             if flags & RF_FWD:
-                d = len(s) - len(t) + max(len(t) - len(s), 0) + bw
-                out[k] = data[d, len(t)]
+                out[k] = data[ns - nt + max(nt - ns, 0) + bw, nt]
             else:
-                out[k] = data[max(len(t) - len(s), 0) + bw, 0]
+                out[k] = data[max(nt - ns, 0) + bw, 0]
         return out
 
     def backtrace(self, slots, want_moves=True):
-        mvs, errs = [], []
-        for sl in np.atleast_1d(slots):
+        def one(sl):
             A, mv, key, n, m = self.slots[int(sl)]["A"]
             moves = oracle.backtrace(mv, n + 1, m + 1, key[3])
             t = self.tpls[key[1]][0]
             s = self.seqs[key[0]]
-            mvs.append(moves)
-            errs.append(oracle.count_errors(moves, t, s.seq))
+            return moves, oracle.count_errors(moves, t, s.seq)
+        sl = np.atleast_1d(slots)
+        if len(sl) >= 32 and NTHREADS > 1:
+            with ThreadPoolExecutor(NTHREADS) as ex:
+                res = list(ex.map(one, sl))
+        else:
+            res = [one(x) for x in sl]
+        mvs = [r[0] for r in res]
+        errs = [r[1] for r in res]
         return (mvs if want_moves else None), np.array(errs, np.int32)
 
     def _check_slot(self, sl):
@@ -103,7 +130,7 @@ class OracleEngine:
                 continue
             try:
                 tot, mat = oracle.score_list((k, p, b), [e["A"][0] for e in ents], [e["B"][0] for e in ents],
-                                             [s for s, _ in reads], t, per_seq=True, nthreads=8, **kw)
+                                             [s for s, _ in reads], t, per_seq=True, nthreads=NTHREADS, **kw)
             except oracle.OracleError as e:
                 raise RifrafError(str(e))
             totals.append(tot)
@@ -137,7 +164,7 @@ class OracleEngine:
         res = []
         for sl in groups:
             sb = [self._seq_bw(self._check_slot(s)) for s in sl]
-            tot, _ = oracle.cpu_pass(sb[0][1], [s for s, _ in sb], nthreads=2)
+            tot, _ = oracle.cpu_pass(sb[0][1], [s for s, _ in sb], nthreads=NTHREADS)
             res.append(tot)
         return res if to_host else None
 

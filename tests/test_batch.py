@@ -169,8 +169,54 @@ def test_native_scope():
     assert not native_eligible(clusters, RifrafParams(batch_size=4, batch_fixed=False))
     assert not native_eligible(_clusters(), RifrafParams())          # references
     assert not native_eligible(clusters, RifrafParams(do_init=False))
+    # an empty read or a quality vector of another length: the Python stage
+    # machine (RifrafSequence's own handling), never a whole-wave native error
+    empty = [dict(c) for c in clusters[:2]]
+    empty[1]["dnaseqs"] = list(empty[1]["dnaseqs"][:-1]) + [np.zeros(0, np.int8)]
+    empty[1]["phreds"] = list(empty[1]["phreds"][:-1]) + [np.zeros(0, np.int8)]
+    assert not native_eligible(empty, RifrafParams())
+    short = [dict(c) for c in clusters[:2]]
+    short[0]["phreds"] = [p[:-1] if k == 0 else p for k, p in enumerate(short[0]["phreds"])]
+    assert not native_eligible(short, RifrafParams())
     with pytest.raises(RifrafError):
         rifraf_batch(clusters[:1], params=RifrafParams(max_iters=2), engine=OracleEngine(), native=True)
+
+
+@pytest.mark.gpu
+def test_native_auto_with_empty_read(engine):
+    """rifraf_batch's automatic driver choice (native=None) with an empty read
+    in one cluster gives what the Python stage machine gives (native=False):
+    the same results, or the same error."""
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    clusters = [dict(c) for c in _ref_free_clusters()[:3]]
+    clusters[1]["dnaseqs"] = list(clusters[1]["dnaseqs"]) + [np.zeros(0, np.int8)]
+    clusters[1]["phreds"] = list(clusters[1]["phreds"]) + [np.zeros(0, np.int8)]
+    params = RifrafParams(batch_size=0, batch_fixed=False, max_iters=10)
+
+    def run(native):
+        try:
+            return [summary(r) for r in rifraf_batch(clusters, params=params, engine=engine, native=native)]
+        except Exception as e:   # noqa: BLE001 - the error itself is compared
+            return (type(e).__name__, str(e))
+    a, b = run(None), run(False)
+    if isinstance(b, tuple):
+        assert a == b
+    else:
+        for x, y in zip(a, b):
+            assert_same_run(x, y)
+
+
+@pytest.mark.gpu
+def test_native_scope_error_message(engine):
+    """rf_rifraf_batch refuses a cluster outside its scope with its own
+    rf_last_error text, not a stale message of an earlier call."""
+    from rifraf_amd import _lib
+    from rifraf_amd.engine import RifrafError
+    bp = _lib.BatchParams(10, 15, 9, 1, 0, 0, 0.1)
+    with pytest.raises(RifrafError, match="cluster 1 is outside the native driver's scope .no reads."):
+        engine.rifraf_batch_native(bp, [0, 1, 1], [0], [10], [1.0], None, None, [0, 1], [0, 1],
+                                   np.zeros(20, np.uint8), [0, 10, 20])
 
 
 def _doubling_clusters(seed=12):

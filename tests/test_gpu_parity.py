@@ -402,55 +402,32 @@ def test_plan_cache_follows_template_content(engine):
 
 
 SCORER_CONFIGS = [
-    # (score_kernel, lean_nw, lean_lds_kb) engine options
-    ("general", None, None),
-    ("seg", None, None),       # row-segment scorer (wide bands) on every shape: default k_score_segl
-    ("seglodd", None, None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
-    ("seglpad", None, None),   # k_score_segl with every band line-padded (band_pad 1)
-    ("segcpad", None, None),   # k_score_segc over line-padded (even-stride) rows
-    ("segc16", None, None),    # chunk-staged k_score_segc, 16 / 24 / 32 diagonals
-    ("segc24", None, None),
-    ("segc32", None, None),
-    ("seg16", None, None),     # register-staged k_score_seg with 16-diagonal segments (seg_s=16)
-    ("seg32", None, None),     # ... with 32-diagonal segments
-    (None, "1", None),
-    (None, "2", None),
-    (None, "1", "8"),      # windows exceed the budget: sub-passes over fewer lanes
-    (None, "2", "12"),
-    (None, "4", None),
-    (None, "4", "24"),
-    (None, "8", None),
-    (None, "8", "40"),
-    (None, "8", "60"),
-    (None, "8", "q128"),     # k_score_ws with 128 chain lanes (ws_q=128), 80 KB LDS
-    (None, "8", "q128l40"),  # ... with windows beyond the budget: sub-passes
+    # (score_kernel, lean_lds_kb) engine options
+    ("general", None),
+    ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segl
+    ("seglodd", None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
+    ("seglpad", None),   # k_score_segl with every band line-padded (band_pad 1)
+    (None, None),        # k_score_ws (the default for these shapes)
+    (None, "8"),         # windows exceed the budget: sub-passes over fewer lanes
+    (None, "12"),
+    (None, "24"),
+    (None, "40"),
+    (None, "60"),
 ]
 
 
-@pytest.mark.parametrize("kern,nw,lds", SCORER_CONFIGS)
+@pytest.mark.parametrize("kern,lds", SCORER_CONFIGS)
 @pytest.mark.parametrize("mode", ["fused", "split"])
-def test_score_dense_kernels(engine, opts, kern, nw, lds, mode):
-    """Both dense scorers (general and lean chain-per-column) over ragged
+def test_score_dense_kernels(engine, opts, kern, lds, mode):
+    """The dense scorers (general, k_score_ws, k_score_segl) over ragged
     clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the oracle."""
-    wsq = None
-    if lds is not None and lds.startswith("q"):
-        parts = lds[1:].split("l")
-        wsq, lds = parts[0], (parts[1] if len(parts) > 1 else None)
-    segs, ver, pad = None, 4, 64
-    if kern in ("seg16", "seg32"):
-        kern, segs, ver = "seg", kern[3:], 1
-    elif kern in ("segc16", "segc24", "segc32"):
-        kern, segs, ver = "seg", kern[4:], 3
-    elif kern in ("seglodd", "seglpad", "segcpad"):
-        ver, pad = (3 if kern == "segcpad" else 4), (0 if kern == "seglodd" else 1)
+    pad = 64
+    if kern in ("seglodd", "seglpad"):
+        pad = 0 if kern == "seglodd" else 1
         kern = "seg"
     opts("band_pad", pad)
     opts("score_kernel", kern or "auto")
-    opts("lean_nw", int(nw or 8))
     opts("lean_lds_kb", int(lds or 0))
-    opts("ws_q", int(wsq or 256))
-    opts("seg_s", int(segs or 24))
-    opts("seg_ver", ver)
     opts("score_mode", mode)
     rng = np.random.default_rng(77)
     templates, seqs, bws = [], [], []
@@ -519,41 +496,19 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "segl16", "segl16odd", "segl16pad",
-                                  "segc16", "segc24", "segc32", "segcpad", "seg16", "seg24", "seg32", "general"])
+@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
     line-aligned row-segment scorer k_score_segl (default; line-padded rows,
-    odd-stride rows, both in one launch), the chunk-staged k_score_segc (16,
-    24, 32 diagonals; odd and even row strides), the element-staged
-    k_score_seg and the in-place k_score ("general") are all bit-exact
-    against the oracle."""
-    opts("seg_s", 24)
-    opts("seg_ver", 4)
+    odd-stride rows, both in one launch) and the in-place k_score ("general")
+    are bit-exact against the oracle."""
     opts("band_pad", 64)
     if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
-    elif kern.startswith("segl16"):
-        # k_score_segl<16>: half-line segments; default, odd-only, all-padded strides
-        opts("score_kernel", "auto")
-        opts("seg_s", 16)
-        opts("band_pad", {"segl16": 64, "segl16odd": 0, "segl16pad": 1}[kern])
     elif kern in ("seglodd", "seglpad"):
         opts("score_kernel", "auto")
         opts("band_pad", 0 if kern == "seglodd" else 1)
-    elif kern == "segcpad":
-        opts("score_kernel", "auto")
-        opts("seg_ver", 3)
-        opts("band_pad", 1)
-    elif kern.startswith("segc"):
-        opts("score_kernel", "auto")
-        opts("seg_ver", 3)
-        opts("seg_s", int(kern[4:]))
-    elif kern.startswith("seg"):
-        opts("score_kernel", "auto")
-        opts("seg_ver", 1)
-        opts("seg_s", int(kern[3:]))
     else:
         opts("score_kernel", kern)
     opts("score_mode", mode)
@@ -784,10 +739,12 @@ def test_row_code_dictionary_overflow():
     """Reads with all-distinct log error probabilities fill the 65 536-entry
     row-code dictionary part way through one upload: later reads stay
     uncoded and their DP reads the tables directly, in the same launches
-    (and waves) as coded reads.  Every band stays bit-exact."""
+    (and waves) as coded reads.  Every band stays bit-exact; the overflow is
+    counted (rf_code_stats) and a refill of every slot starts a fresh
+    dictionary."""
     from rifraf_amd.engine import Engine
     rng = np.random.default_rng(65536)
-    L, bw, nreads = 1000, 9, 80
+    L, bw, nreads = 1000, 9, 120   # ~80 continuous reads x 1000 distinct triples > 65 536
     t = random_seq(L, rng)
     seqs = []
     for k in range(nreads):
@@ -799,6 +756,16 @@ def test_row_code_dictionary_overflow():
     e = Engine(0)
     try:
         _check_bands(e, t, seqs, [bw] * nreads)
+        st = e.code_stats()
+        assert st["entries3"] == 65536 and st["uncoded_reads"] > 0
+        # a refill of every slot: nothing references the old codes, so the
+        # dictionary starts afresh and phred-like reads are coded again
+        # (the counter keeps its history)
+        fresh = [make_read(t, rng, 0.01, bw) for _ in range(nreads)]
+        _check_bands(e, t, fresh, [bw] * nreads)
+        st2 = e.code_stats()
+        assert st2["resets"] >= 1 and st2["entries3"] < 65536
+        assert st2["uncoded_reads"] == st["uncoded_reads"]
     finally:
         e.close()
 
@@ -813,3 +780,15 @@ def test_set_sequences_staged_in_chunks(engine, opts, stage_kb):
     t = random_seq(300, rng)
     seqs = [make_read(t, rng, 0.02, 9) for _ in range(40)]
     _check_bands(engine, t, seqs, [9] * len(seqs))
+
+
+def test_removed_option_keys_rejected(engine):
+    """Scorer-variant keys removed in round 3 (include/rifraf_hip.h) are
+    refused with an error, not silently accepted."""
+    from rifraf_amd.engine import RifrafError
+    for key in (3, 5, 6, 7, 8, 14):
+        assert engine.lib.rf_set_option(engine.ctx, key, 1) != 0
+        assert "unknown option" in engine.lib.rf_last_error(engine.ctx).decode()
+    with pytest.raises(KeyError):
+        engine.set_option("seg_ver", 4)
+    assert RifrafError is not None

@@ -82,6 +82,24 @@ def _sampled(engine_factory, seed):
     return summary(res)
 
 
+def _grown(engine_factory, seed, out=None):
+    """A run whose batch grows (check_score!, model.jl:1094-1112): batch_size 3
+    of 12 reads, batch_threshold 0 (any score drop grows the batch), a fixed seed for
+    resample!'s weighted draws (seed 1 grows it to all 12 reads)."""
+    from rifraf_amd.model import RifrafParams, rifraf
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    _, _, _, reads, _, phreds, _, _ = sample_sequences(12, 60, error_rate=0.05, rng=rng)
+    params = RifrafParams(batch_size=3, batch_fixed=False, batch_threshold=0.0, max_iters=30, seed=11)
+    eng = engine_factory(len(reads))
+    res = rifraf(reads, phreds, params=params, engine=eng)
+    s = summary(res)
+    s["batch_size"] = res.state.batch_size
+    if hasattr(eng, "slot_counts"):
+        s["counts"] = eng.slot_counts(np.arange(res.state.batch_size))
+    return s
+
+
 def summary(res):
     st = res.state
     return {"consensus": np.asarray(res.consensus).copy(), "score": st.score,
@@ -139,6 +157,26 @@ def test_sharded_config1_with_reference(world):
     got = _spawn(_w_config1, world, f, refid)
     for r in range(world):
         assert_same_run(got[r], single)
+
+
+def _w_grown(rank, world, seed):
+    return _grown(_sharded_factory, seed)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batch_growth(world):
+    """check_score! grows the batch from 3 reads towards all 12: the sharded
+    run equals one engine bit for bit, and the grown batch's bands stay
+    spread over the ranks (round-robin slots, at most one read apart)."""
+    single = _grown(_plain_factory, 1)
+    assert single["batch_size"] > 3
+    got = _spawn(_w_grown, world, 1)
+    for r in range(world):
+        g = dict(got[r])
+        counts = g.pop("counts")
+        assert g.pop("batch_size") == single["batch_size"]
+        assert_same_run(g, {k: v for k, v in single.items() if k != "batch_size"})
+        assert sum(counts) == single["batch_size"] and max(counts) - min(counts) <= 1
 
 
 def test_sharded_sampled_cluster():
@@ -205,21 +243,22 @@ def _w_counts(rank, world):
     for bs, nreads in [(20, 5000), (0, 5000), (1, 12), (20, 7)]:
         e = ShardedEngine.for_params(OracleEngine(), nreads, RifrafParams(batch_size=bs))
         batch = min(nreads, bs) if bs > 1 else nreads
-        out[(bs, nreads)] = (e.nslots, e.slot_counts(np.arange(batch)), e.owner(nreads), e.owner(nreads + 1))
+        out[(bs, nreads)] = (e.slot_counts(np.arange(batch)), e.slot_counts(np.arange(nreads)),
+                             e.owner(nreads), e.owner(nreads + 1))
     return out
 
 
 def test_sharded_slot_balance():
-    """ShardedEngine.for_params partitions the batch slots rifraf() fills
-    (batch_size, or all reads when batch_size <= 1), not the read count, so
-    each rank owns its share of the batch; reference/scratch slots (>= nreads)
-    go to the last rank."""
+    """ShardedEngine deals the read slots round-robin, so every batch prefix
+    rifraf() fills (batch_size, and the larger batches check_score! grows it
+    to) is balanced within one read; reference/scratch slots (>= nreads) go
+    to the last rank."""
     got = _spawn(_w_counts, 2)
     for r in range(2):
         c = got[r]
-        assert c[(20, 5000)][:2] == (20, [10, 10])
-        assert c[(0, 5000)][:2] == (5000, [2500, 2500])
-        assert c[(1, 12)][:2] == (12, [6, 6])
-        assert c[(20, 7)][:2] == (7, [3, 4])
+        assert c[(20, 5000)][:2] == ([10, 10], [2500, 2500])
+        assert c[(0, 5000)][:2] == ([2500, 2500], [2500, 2500])
+        assert c[(1, 12)][:2] == ([6, 6], [6, 6])
+        assert c[(20, 7)][:2] == ([4, 3], [4, 3])
         for v in c.values():
             assert v[2] == v[3] == 1

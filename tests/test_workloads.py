@@ -10,10 +10,13 @@ Every other parity test uses small inputs; these run the configs' own shapes
   c3  sample_sequences(1000, 2601; error_rate=0.01, ref_error_rate=0.1,
       ref_errors=ErrorModel(10,0,0,1,1)) with a one-base frameshift in the
       reference so that FRAME runs (codon scoring of the reference, penalty
-      increases, seeded indel proposals): same run as the oracle engine;
+      increases, seeded indel proposals): same run as the oracle engine,
+      default params and the throughput settings (all 1000 reads, QVs);
   c4  clusters of 50 reads x 1.5 kb (bench.make_workload): rf_score_dense of
-      every STAGE_SCORE proposal vs oracle.cpu_pass, bit-exact;
-  c5  the first 64 reads of the bench's 10 kb / 3 % error cluster
+      every STAGE_SCORE proposal vs oracle.cpu_pass, bit-exact; and two
+      whole runs at the throughput settings (all reads, QVs) on the Python
+      stage machine and the native driver;
+  c5  the first 64 / 256 reads of the bench's 10 kb / 3 % error cluster
       (bench.make_read_shard): band doubling (smart_forward_moves!,
       model.jl:643-672) gives the same bandwidth and A[end,end] per read on
       both engines; bands at the doubled widths and the dense totals are
@@ -91,6 +94,26 @@ def test_c3_frame_run_matches_oracle(engine):
     assert a.state.n_ref_indel_mults == b.state.n_ref_indel_mults >= 1
 
 
+def test_c3_throughput_frame_run_matches_oracle(engine):
+    """Config 3 at the throughput settings (SURVEY §8(d) "Parity runs"):
+    every one of the 1000 reads in every batch (batch_size 0, batch_fixed
+    false, model.jl:569-573) through INIT, FRAME (frameshifted reference:
+    codon scoring, seeded indel proposals, penalty increases) and REFINE,
+    with the QV pass: the same run as the oracle engine, bit for bit."""
+    from oracle_engine import OracleEngine
+    rng = np.random.default_rng(3)
+    ref, template, _, reads, _, phreds, _, _ = sample_sequences(
+        1000, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+    ref = np.concatenate([ref[:1300], ref[1301:2000], [2], ref[2000:]]).astype(np.uint8)
+    params = RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True)
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
+    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    assert_same_run(a, b)
+    assert a.state.batch_size == 1000
+    assert a.state.stage_iterations[1] >= 2 and a.state.n_ref_indel_mults >= 1
+    assert np.array_equal(a.consensus, template)
+
+
 def test_c3_qv_with_reference_matches_oracle(engine):
     """QV pass scoring the reference's codon moves too (use_ref_for_qvs,
     model.jl:617-628, :737-791), 2.6 kb template, 40 reads."""
@@ -102,6 +125,34 @@ def test_c3_qv_with_reference_matches_oracle(engine):
     a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
     b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
     assert_same_run(a, b)
+
+
+def _c4_clusters(n, seed=77):
+    """c4 cluster shape from the e2e bench leg: sample_sequences(50, 1500)."""
+    out = []
+    for k in range(n):
+        _, t, _, reads, _, phreds, _, _ = sample_sequences(50, 1500, error_rate=0.01,
+                                                           rng=np.random.default_rng([seed, k]))
+        out.append((t, dict(dnaseqs=reads, phreds=phreds)))
+    return out
+
+
+def test_c4_throughput_runs_match_oracle(engine):
+    """SURVEY §8(d) config 4 at its throughput settings (batch = all 50
+    reads, QV pass on), two clusters as whole rifraf() runs: the HIP engine
+    through the Python stage machine, through rf_rifraf_batch (the native
+    lockstep driver), and the oracle engine agree run for run."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
+    clusters = _c4_clusters(2)
+    nat = rifraf_batch([kw for _, kw in clusters], params=params, engine=engine, native=True)
+    for (t, kw), n in zip(clusters, nat):
+        a = rifraf(params=params, engine=engine, **kw)
+        b = rifraf(params=params, engine=OracleEngine(), **kw)
+        assert_same_run(a, b)
+        assert_same_run(n, b)
+        assert b.error_probs is not None
 
 
 def test_c4_clusters_dense_bitexact(engine):
@@ -121,10 +172,11 @@ def test_c4_clusters_dense_bitexact(engine):
         np.testing.assert_array_equal(g, e, err_msg=f"cluster {c}")
 
 
-def test_c5_sample_band_doubling_and_scores(engine):
+@pytest.mark.parametrize("nreads", [64, 256])
+def test_c5_sample_band_doubling_and_scores(engine, nreads):
     import bench
     from oracle_engine import OracleEngine
-    t, reads = bench.make_read_shard(5000, 10000, 0.03, 9, 2024, 0, 64)
+    t, reads = bench.make_read_shard(5000, 10000, 0.03, 9, 2024, 0, nreads)
     m = len(t)
     # band doubling on both engines (each mutates its own RifrafSequence copies)
     rh = [copy.copy(r) for r in reads]
@@ -144,7 +196,7 @@ def test_c5_sample_band_doubling_and_scores(engine):
     # bands at the doubled widths, and every STAGE_SCORE total
     n = len(rh)
     engine.realign(np.arange(n), np.arange(n), 0, bw_h, RF_FWD | RF_BWD)
-    for k in (0, 1, n - 1):
+    for k in (0, 1, n // 2, n - 1):
         A_exp, _ = oracle.forward(t, rh[k], bandwidth=bw_h[k])
         B_exp = oracle.backward(t, rh[k], bandwidth=bw_h[k])
         from test_gpu_parity import assert_band_equal
