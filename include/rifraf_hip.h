@@ -99,6 +99,8 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_WIDE     18   /* lean DP task widths: bit 0 H 128..255 as 64-lane
                                     tasks (k_dpr<2,..,64>), bit 1 H 64..127 as 32-lane
                                     tasks (k_dpr<2,..,32>); 0 = 16-lane tasks only   */
+#define RF_OPT_ALN_SUMS_HOST 19 /* 1: rf_aln_error_sums folds the moves on host
+                                    threads instead of the device (k_aln_sums)     */
 /* Keys 3, 5-8 and 14 selected scorer variants measured slower and removed in
    round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg / k_score_segc,
    16-diagonal k_score_segl); rf_set_option rejects them. */

@@ -37,8 +37,10 @@
 #include <vector>
 #include <cstdlib>
 
-// rf_last_error text (rifraf_hip.hip)
+// rf_last_error text; the device form of rf_aln_error_sums (rifraf_hip.hip)
 int rf_internal_fail(rf_ctx *ctx, int code, const char *msg);
+int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                             const int32_t *tlen, double *out);
 
 namespace {
 
@@ -736,6 +738,13 @@ extern "C" int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *sl
 {
     if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !tlen || !bases || !match || !seq_len || !out)))
         return RF_ERR_ARG;
+    // every read row-coded: the moves are folded on the device (k_aln_sums),
+    // with the same additions in the same order
+    {
+        const int e = rf_internal_aln_sums_dev(ctx, ngroups, slot_off, slots, tlen, out);
+        if (e <= 0)
+            return e;
+    }
     const int32_t ns = ngroups > 0 ? slot_off[ngroups] : 0;
     std::vector<int64_t> moff(ns + 1, 0);
     std::vector<int32_t> glen(ns);

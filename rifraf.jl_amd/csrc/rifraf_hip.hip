@@ -575,6 +575,12 @@ __device__ __forceinline__ dvec2 dpl_rd2(const double *R, int u)   // u even
     return *(const dvec2 *)(R + u);
 }
 
+#ifndef DPL_REORDER
+#define DPL_REORDER 0
+#endif
+#ifndef DPL_MASKIN
+#define DPL_MASKIN 0
+#endif
 template <int NP, int PAR, int LPT = 16>
 __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], const double (&lb)[NP],
@@ -589,8 +595,17 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double ms = (R.sb == col[r]) ? R.mt : R.mm;
         const double x_ins = PAR ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : E1);
         const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
-        const double raw = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds);
-        nv[r] = raw + lb[r];
+        // DPL_MASKIN: the inactive-diagonal mask on the insert / delete inputs
+        // (off the step-to-step chain) instead of on the cell; an inactive
+        // diagonal then stays -Inf by induction (its own v2 is -Inf)
+        const double is = DPL_MASKIN ? R.is + lb[r] : R.is;
+        const double ds = DPL_MASKIN ? R.ds + lb[r] : R.ds;
+        double raw;
+        if (DPL_REORDER && PAR == 0 && r == 0)   // the exchanged value (E1) enters the max last
+            raw = fmax(fmax(v2[r] + ms, x_del + ds), x_ins + is);
+        else
+            raw = fmax(fmax(v2[r] + ms, x_ins + is), x_del + ds);
+        nv[r] = DPL_MASKIN ? raw : raw + lb[r];
         if (st[r] && !DPL_NO_LDS_OUT)
             Rb[u0 + r * ostep] = nv[r];
     }
@@ -668,7 +683,13 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 #ifndef DPR_WPE64
 #define DPR_WPE64 2   // minimum waves per SIMD requested for the 64-lane kernels
 #endif
-template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16>
+// PFIX: every task of the launch has row stride exactly PM (the host routes
+// only such tasks to it), so the blocked interior's LDS offsets i * P are
+// compile-time immediates instead of one address register per step.
+#ifndef DPR_PFIX
+#define DPR_PFIX 1
+#endif
+template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16, bool PFIX = false>
 __global__ void __launch_bounds__(64) DPR_ATTR
 __attribute__((amdgpu_waves_per_eu(LPT >= 32 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
@@ -755,7 +776,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         if (LEAN && k == klo && nblk > 0) {
             // ---- blocked lean interior: DPL_B periods (2*DPL_B anti-diagonals)
             // per block, inputs and outputs staged in this task's LDS slice
-            const int P = T.P;
+            const int P = PFIX ? PM : T.P;
             const int t = threadIdx.x / LPT;
             EdgeRec *ein = reinterpret_cast<EdgeRec *>(dpl_smem + t * dpl_task_bytes(NP, PM, LPT));
             // line-aligned flushes: `fl` is the band position (doubles from the
@@ -2751,6 +2772,91 @@ __global__ void k_aln_props(const PropTask *__restrict__ tasks, int ntasks, cons
 }
 
 // ---------------------------------------------------------------------
+// k_aln_sums: alignment_error_probs's per-column sums (model.jl:817-840)
+// on the device, from the backtrace moves already there (k_bt_win /
+// k_backtrace).  One workgroup per group (cluster); its reads are walked in
+// batch order, one read at a time: the 256 threads take 256 consecutive
+// moves, a block prefix sum of the (read, consensus) steps gives each move's
+// (i, j), and a MATCH move adds base_distribution(s[i], match[i]) to column
+// j: out[j][b] += (b == s[i] ? match[i] : errlp(match[i])).  A read matches a
+// column at most once, and a barrier separates the reads, so every column
+// receives the same FP64 additions in the same order as the host loop
+// (rf_aln_error_sums).  errlp = log10(1 - 10^ilp) - log10(3) is evaluated on
+// the host (libm) once per row-code dictionary entry; the read's row-code
+// record gives its entry and base.
+// ---------------------------------------------------------------------
+struct alignas(16) AlnSumRead {
+    int64_t mv;    // moves slot (bytes in the backtrace move buffer; moves end-aligned in n + m)
+    int64_t rec;   // row-code records (doubles offset into the table arena)
+    int32_t n, m, idx, pad;
+};
+struct alignas(16) AlnSumGroup {
+    int64_t out;   // doubles offset of the group's m x 4 sums
+    int32_t r0, r1, m, pad;
+};
+
+__global__ void __launch_bounds__(256) k_aln_sums(const AlnSumGroup *__restrict__ groups,
+                                                  const AlnSumRead *__restrict__ reads,
+                                                  const double *__restrict__ tabs, const int8_t *__restrict__ moves,
+                                                  const int32_t *__restrict__ nmoves, const double *__restrict__ lut,
+                                                  const double *__restrict__ errlut, double *__restrict__ out)
+{
+    __shared__ int wsum[4];
+    const AlnSumGroup G = groups[blockIdx.x];
+    double *o = out + G.out;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int e = tid; e < 4 * G.m; e += 256)
+        o[e] = 0.0;
+    __syncthreads();
+    for (int r = G.r0; r < G.r1; ++r) {
+        const AlnSumRead R = reads[r];
+        const int cnt = nmoves[R.idx];
+        const int8_t *mv = moves + R.mv + (R.n + R.m - cnt);
+        const uint64_t *rec = (const uint64_t *)(tabs + R.rec);
+        int ci = 0, cj = 0;   // read / consensus positions consumed before this tile (block-uniform)
+        for (int b0 = 0; b0 < cnt; b0 += 256) {
+            const int e = b0 + tid;
+            const int v = e < cnt ? mv[e] : 0;
+            // align.jl OFFSETS: MATCH (1,1), INSERT (1,0), DELETE (0,1), CODON_INSERT (3,0), CODON_DELETE (0,3)
+            const int di = (v == 1 || v == 2) ? 1 : (v == 4 ? 3 : 0);
+            const int dj = (v == 1 || v == 3) ? 1 : (v == 5 ? 3 : 0);
+            // a tile moves (i, j) by at most 3 * 256 each: 16-bit fields of one
+            // int hold the tile's prefix sums; the carry across tiles is two ints
+            const int x = di | (dj << 16);
+            int inc = x;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(inc, off);
+                if (lane >= off)
+                    inc += y;
+            }
+            if (lane == 63)
+                wsum[w] = inc;
+            __syncthreads();
+            int before = 0;
+            for (int k = 0; k < w; ++k)
+                before += wsum[k];
+            const int tile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            __syncthreads();   // wsum is rewritten by the next tile
+            if (v == 1) {
+                const int ex = before + inc - x;
+                const int i = ci + (ex & 0xffff), j = cj + (ex >> 16);
+                const uint64_t rc = rec[i];
+                const int code = (int)(rc & 0xffff), sb = (int)(rc >> 48) & 0xff;
+                const double ilp = lut[4 * code], el = errlut[code];
+                double *p = o + (size_t)j * 4;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    p[q] += q == sb ? ilp : el;
+            }
+            ci += tile & 0xffff;
+            cj += tile >> 16;
+        }
+        __syncthreads();   // this read's additions precede the next read's
+    }
+}
+
+// ---------------------------------------------------------------------
 // k_scatter: one staged upload -> per-object device regions (a block per
 // segment), so a batch upload is one H2D copy instead of one per object.
 // ---------------------------------------------------------------------
@@ -2890,6 +2996,11 @@ struct CodeDict {
     int64_t uncoded_reads = 0;      // reads left uncoded because the dictionary was full
     int64_t resets = 0;
     DevBuf lut;
+    // per triple entry: log10(1 - 10^match) - log10(3), the off-base value of
+    // base_distribution (model.jl:804-809), host libm; device copy errlut
+    std::vector<double> errv;
+    size_t uperr = 0;
+    DevBuf errlut;
 
     void reset()
     {
@@ -2897,7 +3008,8 @@ struct CodeDict {
         d1.clear();
         t3v.clear();
         d1v.clear();
-        up3 = up1 = 0;
+        errv.clear();
+        up3 = up1 = uperr = 0;
         ++resets;
     }
 
@@ -2967,6 +3079,7 @@ struct Opts {
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
+    int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -2995,7 +3108,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[17];
+    DevBuf scratch[20];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -3266,6 +3379,7 @@ void load_env_opts(Opts &o)
     o.bt_win_kb = env_int("RIFRAF_BT_WIN_KB", o.bt_win_kb);
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
+    o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3406,6 +3520,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipFree(ctx->grow_segs.p);
     if (ctx->codes.lut.p)
         (void)hipFree(ctx->codes.lut.p);
+    if (ctx->codes.errlut.p)
+        (void)hipFree(ctx->codes.errlut.p);
     if (ctx->pinned)
         (void)hipHostFree(ctx->pinned);
     if (ctx->hout)
@@ -3447,6 +3563,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_STAGE_KB: return &o.stage_kb;
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
     case RF_OPT_DP_WIDE: return &o.dp_wide;
+    case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
     default: return nullptr;
     }
 }
@@ -3975,7 +4092,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
                 if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
-                } else if (lean && ((psplit >> npi) & 1) && np8) {
+                } else if (lean && ((psplit >> npi) & 1) && np8 &&
+                           !(npi == 0 && DPR_PFIX && (t.P < dpr_pm(0, 0) || t.P > dpr_pm(0, 3) || !(t.P & 1)))) {
+                    // NP = 1 stride classes take exactly P = 11, 13, 15, 17 (PFIX
+                    // kernels); other strides stay in the generic lean class
                     int pmi = 0;
                     while (pmi < 3 && t.P > dpr_pm(npi, pmi))
                         ++pmi;
@@ -4126,7 +4246,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         } else if (L.kind >= 16 && L.kind < 32) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
-#define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b)>
+#define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b), 16, (a) == 0 && DPR_PFIX>
             const KFn kp[16] = {KP(0, 0), KP(0, 1), KP(0, 2), KP(0, 3), KP(1, 0), KP(1, 1), KP(1, 2), KP(1, 3),
                                 KP(2, 0), KP(2, 1), KP(2, 2), KP(2, 3), KP(3, 0), KP(3, 1), KP(3, 2), KP(3, 3)};
 #undef KP
@@ -4935,3 +5055,71 @@ int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms, double *g
 }
 
 }  // extern "C"
+
+// alignment_error_probs's per-column sums on the device (k_aln_sums) for
+// rf_aln_error_sums (rifraf_batch.cpp): returns 1 (nothing done) when a read
+// has no row codes -- the caller then folds the moves on the host.
+int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                             const int32_t *tlen, double *out)
+{
+    if (ctx->opt.aln_sums_host)
+        return 1;
+    (void)hipSetDevice(ctx->device);
+    const int32_t ns = ngroups > 0 ? slot_off[ngroups] : 0;
+    for (int32_t k = 0; k < ns; ++k) {
+        if (slots[k] < 0 || slots[k] >= (int32_t)ctx->slots.size() || !ctx->slots[slots[k]].a.valid)
+            return fail(ctx, RF_ERR_STATE, "rf_aln_error_sums: slot has no A band");
+        const SeqObj &S = ctx->seqs[ctx->slots[slots[k]].a.seq];
+        if (!S.coded)
+            return 1;
+    }
+    std::vector<BTTask> tasks;
+    std::vector<int64_t> offs;
+    if (int e = build_bt_tasks(ctx, ns, slots, tasks, offs))
+        return e;
+    // errlut for the dictionary entries added since the last call
+    CodeDict &D = ctx->codes;
+    const size_t n3 = D.t3v.size() / 4;
+    const double log3 = std::log10(3.0);
+    for (size_t e = D.errv.size(); e < n3; ++e)
+        D.errv.push_back(std::log10(1.0 - std::pow(10.0, D.t3v[4 * e])) - log3);
+    if (int e = ensure_buf(ctx, D.errlut, (size_t)RF_CODES * 8))
+        return e;
+    if (n3 > D.uperr)
+        HIPCHK(ctx, hipMemcpyAsync((double *)D.errlut.p + D.uperr, D.errv.data() + D.uperr, (n3 - D.uperr) * 8,
+                                   hipMemcpyHostToDevice, ctx->stream));
+    D.uperr = n3;
+    std::vector<AlnSumRead> rd(ns);
+    std::vector<AlnSumGroup> gr(ngroups);
+    int64_t rows = 0;
+    for (int32_t g = 0; g < ngroups; ++g) {
+        gr[g] = {rows * 4, slot_off[g], slot_off[g + 1], tlen[g], 0};
+        rows += tlen[g];
+        for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
+            const Band &b = ctx->slots[slots[k]].a;
+            const SeqObj &S = ctx->seqs[b.seq];
+            if (b.m != tlen[g])
+                return fail(ctx, RF_ERR_ARG, "rf_aln_error_sums: consensus length differs from the A band's");
+            rd[k] = {offs[k], S.tabs.off / 8 + row_code_off(S.n, S.ncins, S.ncdel), b.n, b.m, k, 0};
+        }
+    }
+    if (ns > 0)
+        if (int e = launch_backtraces(ctx, tasks, nullptr, 0))
+            return e;
+    if (int e = upload(ctx, ctx->scratch[17], rd)) return e;
+    if (int e = upload(ctx, ctx->scratch[18], gr)) return e;
+    if (int e = ensure_buf(ctx, ctx->scratch[19], (size_t)std::max<int64_t>(rows * 4 * 8, 16))) return e;
+    if (ngroups > 0) {
+        hipLaunchKernelGGL(k_aln_sums, dim3((unsigned)ngroups), dim3(256), 0, ctx->stream,
+                           (const AlnSumGroup *)ctx->scratch[18].p, (const AlnSumRead *)ctx->scratch[17].p,
+                           (const double *)ctx->tab_arena.d, (const int8_t *)ctx->scratch[3].p,
+                           (const int32_t *)ctx->scratch[4].p, (const double *)D.lut.p, (const double *)D.errlut.p,
+                           (double *)ctx->scratch[19].p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ns > 0)
+        note_bt_ms(ctx);
+    return check_err(ctx);
+}
