@@ -1512,6 +1512,258 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
     tD += dd;
 }
 
+__device__ __forceinline__ void wg_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Half of lean_chain: the chains of bases 2h and 2h+1 of column a (the
+// other half runs in the neighbouring lane).  The same operands, order and
+// FP64 ops per chain as lean_chain, so the same values; the deletion fold
+// (dd) is carried by both halves and written by h = 0.
+__device__ __forceinline__ void lean_chain2(const ScoreRead &R, const LeanWin &w, int a, int h, int m,
+                                            const double *sA, const double *sB, const double *sT,
+                                            double tI[2], double tS[2], double &tD)
+{
+    const int c = R.c, vb = R.vb, P = R.P;
+    const int jn = min(a + 1, m);
+    const int i0 = max(0, jn - c);
+    const int i1 = min(jn + vb, R.n);
+    const int ilast = min(i1, a + vb);                  // last row of rows(a)
+    int d = i0 - a + c;
+    int idx = w.shift + (d + 2 * a - w.kw0) * P + (d >> 1);
+    double aprev = (d >= 1 && i0 >= 1) ? sA[idx - P - 1 + (d & 1)] : -RF_INF;
+    const bool hasS = a < m;
+    const int sofs = hasS ? P - 1 : 0;
+    const int sodd = hasS ? 1 : 0;
+    const double smask = hasS ? 0.0 : -RF_INF;
+    const double2 *tr = (const double2 *)(sT + 6 * (i0 - w.t0));
+    double prev[2], accI[2], accS[2], dd = -RF_INF;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        prev[k] = -RF_INF;
+        accI[k] = -RF_INF;
+        accS[k] = -RF_INF;
+    }
+    double ac = sA[idx], bI = sB[idx], bSr = sB[idx + sofs + (sodd & d)];
+    double2 us = tr[h], u2 = tr[2];
+    for (int i = i0; i <= ilast; ++i) {
+        idx += P + (d & 1);
+        ++d;
+        tr += 3;
+        const double acn = sA[idx], bIn = sB[idx], bSn = sB[idx + sofs + (sodd & d)];
+        const double2 vs = tr[h], v2 = tr[2];
+        const double bS = bSr + smask;
+        const double dl = ac + u2.y;
+        const double dsum = ac + bS;
+        double x[2], y[2];
+        x[0] = aprev + us.x;
+        x[1] = aprev + us.y;
+        y[0] = prev[0] + u2.x;
+        y[1] = prev[1] + u2.x;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            prev[k] = vmax(vmax(x[k], y[k]), dl);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            accI[k] = vmax(accI[k], prev[k] + bI);
+            accS[k] = vmax(accS[k], prev[k] + bS);
+        }
+        dd = vmax(dd, dsum);
+        aprev = ac;
+        ac = acn;
+        bI = bIn;
+        bSr = bSn;
+        us = vs;
+        u2 = v2;
+    }
+    if (i1 > ilast) {
+        const double sub[2] = {us.x, us.y};
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
+    }
+    const double qnan = __builtin_nan("");
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+        tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+    }
+    tD += dd;
+}
+
+// ---------------------------------------------------------------------
+// k_score_w2: the c4-shape dense scorer without role specialization
+// (round 3).  512 threads cover 256 columns, two lanes per column (lane 2c+h
+// scores the chains of bases 2h, 2h+1 of column a0+c: lean_chain2), and every
+// lane is also a loader: a read's window (bands + table rows) is split over
+// all 512 lanes, and each lane holds the windows of the next TWO reads in
+// registers (two sets, alternating), so each window's loads are issued two
+// reads ahead and two windows are in flight per CU -- k_score_ws has one,
+// whose load latency is exposed once per read.  Per read: commit the
+// window from its register set to LDS, barrier, issue the loads of read
+// r + 2 into the freed set, score read r, barrier.
+// ---------------------------------------------------------------------
+template <int NPF>
+struct W2Set {
+    dvec2 pa[NPF], pb[NPF];
+    double pm, px, pn, pd;
+    int ps;
+    __device__ __forceinline__ void issue(const ScoreRead &R2, const LeanWin &w2, int lt,
+                                          const double *__restrict__ bands, const double *__restrict__ tabs,
+                                          const uint8_t *__restrict__ bases)
+    {
+        const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
+        const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
+#pragma unroll
+        for (int u = 0; u < NPF; ++u) {
+            const int e = u * 512 + lt;
+            if (e < w2.n16) {
+                pa[u] = ga[e];
+                pb[u] = gb[e];
+            }
+        }
+        const double *tm = tabs + R2.tab;
+        const int n2 = R2.n;
+        const int i = min(w2.t0 + lt, w2.t1);
+        const int ks = max(i - 1, 0);
+        pm = tm[ks];
+        px = tm[n2 + ks];
+        pn = tm[2 * (size_t)n2 + ks];
+        pd = tm[3 * (size_t)n2 + i];
+        ps = bases[R2.sb + ks];
+    }
+    __device__ __forceinline__ void commit(const LeanWin &wf, int lt, double *smem) const
+    {
+        dvec2 *sA = (dvec2 *)smem;
+        dvec2 *sB = (dvec2 *)(smem + wf.win);
+        double *sT = smem + 2 * wf.win;
+#pragma unroll
+        for (int u = 0; u < NPF; ++u) {
+            const int e = u * 512 + lt;
+            if (e < wf.n16) {
+                sA[e] = pa[u];
+                sB[e] = pb[u];
+            }
+        }
+        const int i = wf.t0 + lt;
+        if (i <= wf.t1)
+            lean_row(sT + 6 * lt, i >= 1 ? ps : 4, pm, px, pn, pd);
+    }
+};
+
+#ifndef W2_NPF
+#define W2_NPF 10
+#endif
+template <int NPF>
+__global__ void __launch_bounds__(512) k_score_w2(const WorkItem *__restrict__ items,
+                                                  const ScoreGroup *__restrict__ groups,
+                                                  const ScoreRead *__restrict__ reads,
+                                                  const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
+                                                  const double *__restrict__ bands, double *__restrict__ dense,
+                                                  double *__restrict__ split, int split_mode, int lds_elems)
+{
+    constexpr int Q = 256;   // columns per work item
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int xq = nb >> 3, xr = nb & 7, x = b & 7;
+    const int item = x * xq + min(x, xr) + (b >> 3);
+    const WorkItem wi = items[item];
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int la1f = min(a0 + Q - 1, m);
+    int r0 = G.r0, r1 = G.r1;
+    if (split_mode & 1) {
+        r0 = G.r0 + blockIdx.y;
+        if (r0 >= G.r1)
+            return;
+        r1 = r0 + 1;
+    }
+    const int lt = threadIdx.x;
+    const int col = lt >> 1, h = lt & 1;
+    const int a = a0 + col;
+    auto fast = [&](const ScoreRead &R, const LeanWin &w) {   // block-uniform
+        return lean_need(Q, R.H, R.P) <= lds_elems && w.n16 <= NPF * 512 && w.t1 - w.t0 < 512;
+    };
+    auto sub_L = [&](const ScoreRead &R) {
+        int L = Q;
+        while (L > 1 && lean_need(L, R.H, R.P) > lds_elems)
+            L >>= 1;
+        return L;
+    };
+    double tI[2] = {0.0, 0.0}, tS[2] = {0.0, 0.0}, tD = 0.0;
+    W2Set<NPF> s0, s1;   // s0: reads r0, r0+2, ...; s1: r0+1, r0+3, ...
+    auto try_issue = [&](W2Set<NPF> &st, int rr) {
+        if (rr < r1) {
+            const ScoreRead R2 = reads[rr];
+            const LeanWin w2 = lean_win(R2, m, a0, la1f);
+            if (fast(R2, w2))
+                st.issue(R2, w2, lt, bands, tabs, bases);
+        }
+    };
+    auto one_read = [&](W2Set<NPF> &st, int r) {
+        const ScoreRead R = reads[r];
+        const LeanWin wf = lean_win(R, m, a0, la1f);
+        if (fast(R, wf)) {
+            st.commit(wf, lt, smem);
+            wg_barrier();                            // window r ready
+            try_issue(st, r + 2);
+            if (a <= m && !(split_mode & 2))
+                lean_chain2(R, wf, a, h, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
+            wg_barrier();                            // chains of r done
+        } else {
+            // beyond the prefetch or the LDS budget: staged synchronously, in
+            // sub-passes over L columns
+            const int L = sub_L(R);
+            for (int c0 = 0; c0 < Q; c0 += L) {
+                const int la0 = a0 + c0;
+                if (la0 > m)
+                    break;
+                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
+                lean_stage<512>(R, w, lt, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
+                wg_barrier();
+                if (col >= c0 && col < c0 + L && a <= m)
+                    lean_chain2(R, w, a, h, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
+                wg_barrier();
+            }
+            try_issue(st, r + 2);
+        }
+    };
+    try_issue(s0, r0);
+    try_issue(s1, r0 + 1);
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+        one_read(s0, r);
+        one_read(s1, r + 1);
+    }
+    if (r < r1)
+        one_read(s0, r);
+    if (a > m)
+        return;
+    const double qnan = __builtin_nan("");
+    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
+                                    : dense + G.dense_off;
+    double *dst = base + (size_t)a * 9;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        dst[5 + 2 * h + k] = tI[k];
+    if (a < m) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            dst[9 + 2 * h + k] = tS[k];
+        if (h == 0)
+            dst[13] = tD;
+    }
+    if (a == 0 && h == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            dst[k] = qnan;
+    }
+}
+
 // ---------------------------------------------------------------------
 // k_score_ws: the lean scorer with wave specialization (the default)
 //
@@ -1525,12 +1777,6 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
 // prefetch (staged synchronously by the loaders).
 // ---------------------------------------------------------------------
 
-__device__ __forceinline__ void wg_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 #ifndef WS_NPF
 #define WS_NPF 19
@@ -1601,7 +1847,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                 ps[k] = bases[R2.sb + ks];
             }
         };
-        bool held = false;   // registers hold read r
+        bool held = (split_mode & 8) != 0;   // registers hold read r (diagnostics: never load)
         for (int r = r0; r < r1; ++r) {
             const ScoreRead R = reads[r];
             const LeanWin wf = lean_win(R, m, a0, la1f);
@@ -1627,8 +1873,8 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                         lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
                 }
                 wg_barrier();                        // window r ready
-                held = false;
-                if (r + 1 < r1) {
+                held = (split_mode & 8) != 0;
+                if (r + 1 < r1 && !held) {
                     const ScoreRead R2 = reads[r + 1];
                     const LeanWin w2 = lean_win(R2, m, a0, la1f);
                     if (fast(R2, w2)) {
@@ -1731,6 +1977,9 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #define SEGL_UNROLL 32
 #endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifndef SEGL_PF2
+#define SEGL_PF2 0
+#endif
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
 // of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
 // slower at c5: 30.6 ms at one wave per SIMD, 40.6 ms at two with spills,
@@ -1760,7 +2009,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     using Gm = SeglGeo<SEGS>;
     constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
     constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
-    constexpr bool PF = true;   // next segment prefetched into registers
+
     constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
     __shared__ __attribute__((aligned(16))) double sA[SL];
     __shared__ __attribute__((aligned(16))) double sB[SL];
@@ -1837,34 +2086,38 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         g.dlmin = __builtin_amdgcn_readfirstlane(dlmin);
     };
     const bool all_act = __all(active) && wave_s;
-    dvec2 ra[NUA], rb[NUA];
-    double tmt[2], tmm[2], tin[2], tdl[2];
-    int tsb[2];
-    double z0a = 0.0, z0b = 0.0, z1a = 0.0, z1b = 0.0;   // LDS row 0 of a read's first segment
-    // loads of segment D of read g (registers only): issued one segment ahead,
-    // and the next read's first segment during the current read's last one
-    auto load_seg = [&](const RG &g, int D, bool first) {
+    // one segment's registers: its band lines, table rows and (a read's
+    // first segment) LDS row 0.  SEGL_PF2: two sets, so each segment's loads
+    // are issued two segments ahead (two segments in flight per wave)
+    struct SegSet {
+        dvec2 ra[NUA], rb[NUA];
+        double tmt[2], tmm[2], tin[2], tdl[2];
+        int tsb[2];
+        double z0a, z0b, z1a, z1b;
+    };
+    // loads of segment D of read g (registers only)
+    auto load_seg = [&](SegSet &X, const RG &g, int D, bool first) {
         const int kb = D + 2 * a0, eh = D >> 1;
         if ((g.P & 15) == 0) {
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
                 const int kap = min(kb + r8 + RPI * j, g.K - 1);
                 const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
-                ra[j] = *(const dvec2 *)(g.gA + o);
-                rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+                X.ra[j] = *(const dvec2 *)(g.gA + o);
+                X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
             }
         }
         if (first && D > 0) {
             // diagonal D-1 of columns a0 .. a0+64 (the previous segment's last row)
             const int kap = min(D - 1 + 2 * a, g.K - 1);
             const int64_t o = (int64_t)kap * g.P + ((D - 1) >> 1);
-            z0a = g.gA[o];
-            z0b = g.gA[g.dB + o];
+            X.z0a = g.gA[o];
+            X.z0b = g.gA[g.dB + o];
             if (tid == 0) {
                 const int kap1 = min(D - 1 + 2 * (a0 + 64), g.K - 1);
                 const int64_t o1 = (int64_t)kap1 * g.P + ((D - 1) >> 1);
-                z1a = g.gA[o1];
-                z1b = g.gA[g.dB + o1];
+                X.z1a = g.gA[o1];
+                X.z1b = g.gA[g.dB + o1];
             }
         }
         const int ib = a0 - g.c + D;
@@ -1872,14 +2125,14 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         for (int u = 0; u < 2; ++u) {
             const int i = min(max(ib + tid + 64 * u, 0), g.n);
             const int ks = max(i - 1, 0);
-            tsb[u] = g.sq[ks];   // read row 0 (the gap) is selected at the store
-            tmt[u] = g.tm[ks];
-            tmm[u] = g.tm[g.n + ks];
-            tin[u] = g.tm[2 * (size_t)g.n + ks];
-            tdl[u] = g.tm[3 * (size_t)g.n + i];
+            X.tsb[u] = g.sq[ks];   // read row 0 (the gap) is selected at the store
+            X.tmt[u] = g.tm[ks];
+            X.tmm[u] = g.tm[g.n + ks];
+            X.tin[u] = g.tm[2 * (size_t)g.n + ks];
+            X.tdl[u] = g.tm[3 * (size_t)g.n + i];
         }
     };
-    auto store_seg = [&](const RG &g, int D) {
+    auto store_seg = [&](const SegSet &X, const RG &g, int D) {
         if ((g.P & 15) == 0) {
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
@@ -1887,7 +2140,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 for (int h = 0; h < 2; ++h) {
                     const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
                     const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0
-                    const double v = h ? ra[j].y : ra[j].x, w = h ? rb[j].y : rb[j].x;
+                    const double v = h ? X.ra[j].y : X.ra[j].x, w = h ? X.rb[j].y : X.rb[j].x;
                     const int l = (ddl + 1) * LS + col;
                     // rows S..127 always land in [0, 64]; the parallelogram's
                     // first / last S rows hold cells of the neighbouring items
@@ -1941,11 +2194,11 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         for (int u = 0; u < 2; ++u) {
             const int t = tid + 64 * u;
             if (t < NT) {
-                const int sb = ib + t >= 1 ? tsb[u] : 4;
-                const double mt = tmt[u], mm = tmm[u];
+                const int sb = ib + t >= 1 ? X.tsb[u] : 4;
+                const double mt = X.tmt[u], mm = X.tmm[u];
                 sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
                 sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
-                sT2[t] = dvec2{tin[u], tdl[u]};
+                sT2[t] = dvec2{X.tin[u], X.tdl[u]};
             }
         }
     };
@@ -1954,18 +2207,6 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     // rows in every read (each band column holds at least one row)
     if (!__any(active))
         return;
-    // reads and their segments as one stream: the register prefetch always
-    // holds the next segment -- this read's next, or the next read's first --
-    // so no read starts on an exposed load
-    RG g, gn;
-    int r = r0;
-    if (r < r1) {
-        setup(r, g);
-        gn = g;
-    }
-    int D0 = g.dlo & ~(S - 1), D = D0;
-    if (PF && r < r1 && do_load)
-        load_seg(g, D, true);
     double prev[4], accI[4], accS[4], dd = -RF_INF;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1973,43 +2214,11 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         accI[k] = -RF_INF;
         accS[k] = -RF_INF;
     }
-    while (r < r1) {
-        const bool more = r + 1 < r1;
-        const int c = g.c, dfirst = g.dfirst, dlast = g.dlast, dhi = g.dhi;
+    // the chains of segment D of read g (operands from LDS)
+    auto chains = [&](const RG &g, int D) {
+        const int c = g.c, dfirst = g.dfirst, dlast = g.dlast;
         const int dfmax = g.dfmax, dlmin = g.dlmin;
         const bool peel = g.peel;
-        wave_sync();   // previous segment's chains are done with LDS
-        if (!PF && do_load)
-            load_seg(g, D, D == D0);   // no register prefetch: the other waves hide the latency
-        // LDS row 0 = diagonal D-1: the previous segment's row 32, or prefetched
-        if (D == D0) {
-            if (D > 0) {
-                sA[tid] = z0a;
-                sB[tid] = z0b;
-                if (tid == 0) {
-                    sA[64] = z1a;
-                    sB[64] = z1b;
-                }
-            }
-        } else {
-            const double va = sA[S * LS + tid], vbv = sB[S * LS + tid];
-            const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
-            sA[tid] = va;
-            sB[tid] = vbv;
-            if (tid == 0) {
-                sA[64] = va6;
-                sB[64] = vb6;
-            }
-        }
-        store_seg(g, D);
-        wave_sync();
-        const bool last = D + S > dhi;
-        if (last && more)
-            setup(r + 1, gn);
-        if (PF && do_load && (!last || more)) {
-            const RG gl = last ? gn : g;
-            load_seg(gl, last ? (gn.dlo & ~(S - 1)) : D + S, last);
-        }
         if (active && !(split_mode & 2)) {
             const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
             const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];   // unconditional read, then select
@@ -2084,49 +2293,133 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 }
             }
         }
-        if (last) {
-            if (active) {
-                const double qnan = __builtin_nan("");
-                if (split_mode & 1) {
-                    double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
+    };
+    // read r's totals (after its last segment) and fresh chain state
+    auto finish = [&](int r) {
+        if (active) {
+            const double qnan = __builtin_nan("");
+            if (split_mode & 1) {
+                double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+                if (a < m) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
-                    if (a < m) {
+                        dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                    dst[13] = dd;
+                }
+                if (a == 0) {
 #pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
-                        dst[13] = dd;
-                    }
-                    if (a == 0) {
+                    for (int k = 0; k < 5; ++k)
+                        dst[k] = qnan;
+                }
+            } else {
 #pragma unroll
-                        for (int k = 0; k < 5; ++k)
-                            dst[k] = qnan;
-                    }
-                } else {
+                for (int k = 0; k < 4; ++k) {
+                    tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
+                    tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
+                }
+                tD += dd;
+            }
+        }
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
-                        tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
-                    }
-                    tD += dd;
+        for (int k = 0; k < 4; ++k) {
+            prev[k] = -RF_INF;
+            accI[k] = -RF_INF;
+            accS[k] = -RF_INF;
+        }
+        dd = -RF_INF;
+    };
+    // Reads and their segments as one stream: the register prefetch always
+    // holds the next segment(s) -- this read's next, or the next read's
+    // first -- so no read starts on an exposed load.
+    struct Pos {
+        int r, D;
+        RG g;
+    };
+    auto first_of = [&](const RG &g) { return g.dlo & ~(S - 1); };
+    auto adv = [&](Pos &p) {
+        if (p.D + S > p.g.dhi) {
+            ++p.r;
+            if (p.r < r1) {
+                setup(p.r, p.g);
+                p.D = first_of(p.g);
+            }
+        } else {
+            p.D += S;
+        }
+    };
+    // one segment: X holds its loads; afterwards X holds the loads of the
+    // segment DEPTH ahead (nxt: the stream position DEPTH - 1 ahead)
+    auto step = [&](SegSet &X, Pos &cur, Pos &nxt, auto depth) {
+        constexpr int DEPTH = decltype(depth)::value;
+        const int D = cur.D;
+        const bool first = D == first_of(cur.g);
+        wave_sync();   // previous segment's chains are done with LDS
+        // LDS row 0 = diagonal D-1: the previous segment's row 32, or prefetched
+        if (first) {
+            if (D > 0) {
+                sA[tid] = X.z0a;
+                sB[tid] = X.z0b;
+                if (tid == 0) {
+                    sA[64] = X.z1a;
+                    sB[64] = X.z1b;
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                prev[k] = -RF_INF;
-                accI[k] = -RF_INF;
-                accS[k] = -RF_INF;
-            }
-            dd = -RF_INF;
-            g = gn;
-            ++r;
-            D0 = g.dlo & ~(S - 1);
-            D = D0;
         } else {
-            D += S;
+            const double va = sA[S * LS + tid], vbv = sB[S * LS + tid];
+            const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
+            sA[tid] = va;
+            sB[tid] = vbv;
+            if (tid == 0) {
+                sA[64] = va6;
+                sB[64] = vb6;
+            }
         }
+        store_seg(X, cur.g, D);
+        wave_sync();
+        Pos ahead = DEPTH == 2 ? nxt : cur;
+        if (ahead.r < r1)
+            adv(ahead);
+        if (do_load && ahead.r < r1)
+            load_seg(X, ahead.g, ahead.D, ahead.D == first_of(ahead.g));
+        chains(cur.g, D);
+        if (D + S > cur.g.dhi)
+            finish(cur.r);
+        if (DEPTH == 2) {
+            cur = nxt;
+            nxt = ahead;
+        } else {
+            cur = ahead;
+        }
+    };
+    Pos cur;
+    cur.r = r0;
+    if (r0 < r1) {
+        setup(r0, cur.g);
+        cur.D = first_of(cur.g);
     }
+    SegSet X0, X1;
+    if (r0 < r1 && do_load)
+        load_seg(X0, cur.g, cur.D, true);
+#if SEGL_PF2
+    Pos nxt = cur;
+    if (nxt.r < r1)
+        adv(nxt);
+    if (do_load && nxt.r < r1)
+        load_seg(X1, nxt.g, nxt.D, nxt.D == first_of(nxt.g));
+    while (cur.r < r1) {
+        step(X0, cur, nxt, std::integral_constant<int, 2>{});
+        if (cur.r >= r1)
+            break;
+        step(X1, cur, nxt, std::integral_constant<int, 2>{});
+    }
+#else
+    (void)X1;
+    while (cur.r < r1)
+        step(X0, cur, cur, std::integral_constant<int, 1>{});
+#endif
     if (!active || (split_mode & 1))
         return;
     const double qnan = __builtin_nan("");
@@ -3061,6 +3354,9 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
+#ifndef W2_DEFAULT
+#define W2_DEFAULT 0
+#endif
 #ifndef DP_WIDE_DEFAULT
 #define DP_WIDE_DEFAULT 3
 #endif
@@ -3080,6 +3376,7 @@ struct Opts {
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
+    int score_w2 = W2_DEFAULT;   // RF_OPT_SCORE_W2: 1 = k_score_w2 (narrow bands), 0 = k_score_ws
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -3380,6 +3677,7 @@ void load_env_opts(Opts &o)
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
+    o.score_w2 = env_int("RIFRAF_SCORE_W2", o.score_w2);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3439,6 +3737,8 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
         sm |= 2;
     if (ctx->opt.diag_lean_nocomp & 2)   // k_score_segl: skip the segment loads
         sm |= 4;
+    if (ctx->opt.diag_lean_nocomp & 4)   // k_score_ws: loaders skip their global loads (chains alone)
+        sm |= 8;
 #endif
     dim3 grid(nitems, gy);
     if (pk.seg) {
@@ -3451,6 +3751,9 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
                            d_tabs, d_bands, dense, split, sm, rchunk);
     } else if (!pk.lean) {
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
+                           d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+    } else if (ctx->opt.score_w2) {
+        hipLaunchKernelGGL((k_score_w2<W2_NPF>), grid, dim3(512), pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     } else {
         hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
@@ -3499,6 +3802,8 @@ int rf_create(int device, rf_ctx **out)
     }
     // the lean scorer may use up to the whole 160 KiB LDS of a CU
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_score_w2<W2_NPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
@@ -3564,6 +3869,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
     case RF_OPT_DP_WIDE: return &o.dp_wide;
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
+    case RF_OPT_SCORE_W2: return &o.score_w2;
     default: return nullptr;
     }
 }

@@ -20,4 +20,6 @@ pr = cProfile.Profile()
 t0 = time.perf_counter()
 pr.runcall(rifraf_batch, cl, params=RifrafParams(batch_size=0, batch_fixed=False, do_score=True), engine=e)
 print("wall", time.perf_counter() - t0)
+from rifraf_amd import batch as _b
+print("STATS", {k: round(v, 4) for k, v in _b.STATS.items()})
 pstats.Stats(pr).sort_stats("tottime").print_stats(25)
