@@ -135,6 +135,18 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq,
                      const double *ins, const double *del,
                      const double *cins, const int64_t *cins_off,
                      const double *cdel, const int64_t *cdel_off);
+/* The same upload for Phred-coded reads without codon moves, with the
+   tables built on the device from one byte per position: codes[off[k]..]
+   index lp_t[256] (log10 error probability) and match_t[256]
+   (log10(1 - 10^lp), both evaluated by the caller's libm, as the
+   RifrafSequence constructor does, rifrafsequences.jl:19-53); mismatch /
+   ins / del follow with the scores' mismatch / insertion / deletion by FP64
+   addition and maximum -- bit-identical to rf_set_sequences of the host
+   tables.  Moves 2 B per position over PCIe instead of ~41.  Returns
+   RF_ERR_STATE when the row-code dictionary is full (upload host tables). */
+int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
+                           const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
+                           double s_ins, double s_del);
 
 /* Templates (consensus sequences, one per cluster): ids [first, first+n). */
 int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl,

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -3174,6 +3175,75 @@ __global__ void k_scatter(const Segment *__restrict__ segs, const uint8_t *__res
 }
 
 // ---------------------------------------------------------------------
+// k_tables: RifrafSequence tables (rifrafsequences.jl:19-82, no codon
+// moves) and row-code records of phred-coded reads, built on the device
+// from one byte per position (rf_set_sequences_codes).  Per code c the host
+// passes lp[c], match[c] (its own libm values), and the dictionary ids of
+// the (match, mismatch, ins) triple and of the del value lp[c] + s_del:
+//   mismatch = lp + s_mis, ins = lp + s_ins,
+//   del[0] = lp[0] + s_del, del[n] = lp[n-1] + s_del,
+//   del[i] = max(lp[i-1], lp[i]) + s_del,
+// the same FP64 additions and maximum as the host constructor, so the same
+// bits.  One block per sequence.
+// ---------------------------------------------------------------------
+struct alignas(16) CodeSeq {
+    int64_t tab;    // doubles offset of the sequence's tables
+    int64_t src;    // byte offset of its codes / bases in the staged upload
+    int32_t n, pad0;
+    int64_t pad1;
+};
+struct alignas(16) CodeLut {   // per Phred code
+    double lp, match;
+    int32_t id3, id1;
+    int32_t pad0, pad1;
+};
+
+__global__ void __launch_bounds__(256) k_tables(const CodeSeq *__restrict__ seqs, const uint8_t *__restrict__ codes,
+                                                const uint8_t *__restrict__ bases, const CodeLut *__restrict__ lut,
+                                                double s_mis, double s_ins, double s_del, double *__restrict__ tabs)
+{
+    const CodeSeq S = seqs[blockIdx.x];
+    const int n = S.n;
+    const uint8_t *cd = codes + S.src;
+    const uint8_t *bs = bases + S.src;
+    double *t = tabs + S.tab;
+    uint64_t *rec = (uint64_t *)(t + row_code_off(n, 0, 0));
+    for (int i = threadIdx.x; i <= n; i += blockDim.x) {
+        const CodeLut L = lut[cd[min(i, n - 1)]];
+        // del[i] and its dictionary id: the neighbour with the larger lp
+        int idd;
+        double dv;
+        if (i == 0 || i == n) {
+            dv = L.lp + s_del;
+            idd = L.id1;
+        } else {
+            const CodeLut Lp = lut[cd[i - 1]];
+            const double l = Lp.lp, r = L.lp;
+            dv = (r > l ? r : l) + s_del;
+            idd = r > l ? L.id1 : Lp.id1;
+        }
+        t[3 * (size_t)n + i] = dv;
+        if (i < n) {
+            t[i] = L.match;
+            t[n + i] = L.lp + s_mis;
+            t[2 * (size_t)n + i] = L.lp + s_ins;
+        }
+        // records need del[i] and del[i+1]: written by position i with the next id
+        if (i < n) {
+            int idn;
+            if (i + 1 == n) {
+                idn = L.id1;
+            } else {
+                const CodeLut Ln = lut[cd[i + 1]];
+                idn = Ln.lp > L.lp ? Ln.id1 : L.id1;
+            }
+            rec[i] = (uint64_t)(uint32_t)L.id3 | ((uint64_t)(uint32_t)idd << 16) | ((uint64_t)(uint32_t)idn << 32) |
+                     ((uint64_t)bs[i] << 48);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------
 
@@ -3405,7 +3475,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[20];
+    DevBuf scratch[21];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -4175,6 +4245,179 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     }
     for (int32_t k = 0; k < nseq; ++k)
         ctx->seqs[first + k].valid = true;
+    ++ctx->layout_gen;
+    return 0;
+}
+
+int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
+                           const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
+                           double s_ins, double s_del)
+{
+    if (!ctx || first < 0 || nseq < 0 || (nseq > 0 && (!bases || !off || !codes || !lp_t || !match_t)))
+        return fail(ctx, RF_ERR_ARG, "rf_set_sequences_codes: bad arguments");
+    (void)hipSetDevice(ctx->device);
+    ++ctx->state_epoch;
+    for (int32_t k = 0; k < nseq; ++k)
+        if (off[k + 1] - off[k] < 1)
+            return fail(ctx, RF_ERR_ARG, "rf_set_sequences_codes: empty sequence");
+    const int64_t N = nseq > 0 ? off[nseq] - off[0] : 0;
+    // codes present, per-code values and finiteness
+    bool present[256] = {};
+    {
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 22) + 1));
+        std::vector<std::array<uint8_t, 256>> pr(nth);
+        parallel_for(nth, [&](int t) {
+            pr[t].fill(0);
+            for (int64_t i = off[0] + N * t / nth; i < off[0] + N * (t + 1) / nth; ++i)
+                pr[t][codes[i]] = 1;
+        });
+        for (int t = 0; t < nth; ++t)
+            for (int c = 0; c < 256; ++c)
+                present[c] = present[c] || pr[t][c];
+    }
+    double mt[256], mm[256], is[256], dl[256];
+    bool fin[256];
+    for (int c = 0; c < 256; ++c) {
+        mt[c] = match_t[c];
+        mm[c] = lp_t[c] + s_mis;
+        is[c] = lp_t[c] + s_ins;
+        dl[c] = lp_t[c] + s_del;
+        fin[c] = std::isfinite(mt[c]) && std::isfinite(mm[c]) && std::isfinite(is[c]) && std::isfinite(dl[c]);
+    }
+    // a fresh code dictionary when no coded sequence outside this upload is
+    // still valid (as rf_set_sequences)
+    {
+        bool others = false;
+        for (size_t k = 0; k < ctx->seqs.size() && !others; ++k)
+            others = ((int64_t)k < first || (int64_t)k >= (int64_t)first + nseq) && ctx->seqs[k].valid &&
+                     ctx->seqs[k].coded;
+        if (!others && !(ctx->codes.t3.empty() && ctx->codes.d1.empty()))
+            ctx->codes.reset();
+    }
+    CodeDict &D = ctx->codes;
+    std::vector<CodeLut> lut(256);
+    for (int c = 0; c < 256; ++c) {
+        lut[c] = {lp_t[c], mt[c], 0, 0, 0, 0};
+        if (!present[c])
+            continue;
+        const CodeDict::K3 key{CodeDict::bits(mt[c]), CodeDict::bits(mm[c]), CodeDict::bits(is[c])};
+        int32_t i3 = D.find3(key);
+        if (i3 < 0 && D.t3.size() < (size_t)RF_CODES) {
+            i3 = (int32_t)D.t3.size();
+            D.t3.emplace(key, (uint32_t)i3);
+            D.t3v.insert(D.t3v.end(), {mt[c], mm[c], is[c], 0.0});
+        }
+        int32_t i1 = D.find1(CodeDict::bits(dl[c]));
+        if (i1 < 0 && D.d1.size() < (size_t)RF_CODES) {
+            i1 = (int32_t)D.d1.size();
+            D.d1.emplace(CodeDict::bits(dl[c]), (uint32_t)i1);
+            D.d1v.push_back(dl[c]);
+        }
+        if (i3 < 0 || i1 < 0)   // dictionary full: the caller uploads host tables instead
+            return fail(ctx, RF_ERR_STATE, "rf_set_sequences_codes: row-code dictionary full");
+        lut[c].id3 = i3;
+        lut[c].id1 = i1;
+    }
+    if ((int64_t)first + nseq > (int64_t)ctx->seqs.size())
+        ctx->seqs.resize(first + nseq);
+    // regions: bases + tables [match|mismatch|ins|del|row codes] (arena growth
+    // at most once per arena; offsets are read after every allocation)
+    {
+        int64_t need_b = 0, need_t = 0;
+        for (int32_t k = 0; k < nseq; ++k) {
+            const SeqObj &S = ctx->seqs[first + k];
+            const int64_t n = off[k + 1] - off[k];
+            const int64_t bb = align_up(std::max<int64_t>(n, 16), 256);
+            const int64_t tb = align_up(std::max<int64_t>((row_code_off(n, 0, 0) + n) * 8, 16), 256);
+            if (!(S.bases.off >= 0 && S.bases.cap >= bb)) need_b += bb;
+            if (!(S.tabs.off >= 0 && S.tabs.cap >= tb)) need_t += tb;
+        }
+        if (ctx->bytes_arena.top + need_b + ARENA_GUARD > ctx->bytes_arena.cap)
+            if (int e = arena_grow(ctx, ctx->bytes_arena, need_b, nullptr)) return e;
+        if (ctx->tab_arena.top + need_t + ARENA_GUARD > ctx->tab_arena.cap)
+            if (int e = arena_grow(ctx, ctx->tab_arena, need_t, nullptr)) return e;
+    }
+    for (int32_t k = 0; k < nseq; ++k) {
+        SeqObj &S = ctx->seqs[first + k];
+        const int64_t n = off[k + 1] - off[k];
+        S.n = (int32_t)n;
+        S.ncins = S.ncdel = 0;
+        if (int e = region_ensure(ctx, ctx->bytes_arena, S.bases, n)) return e;
+        if (int e = region_ensure(ctx, ctx->tab_arena, S.tabs, (row_code_off(n, 0, 0) + n) * 8)) return e;
+    }
+    // new dictionary entries to the device
+    if (int e = ensure_buf(ctx, D.lut, (size_t)RF_CODES * 5 * 8)) return e;
+    {
+        const size_t n3 = D.t3v.size() / 4, n1 = D.d1v.size();
+        if (n3 > D.up3)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * D.up3, D.t3v.data() + 4 * D.up3, (n3 - D.up3) * 32,
+                                       hipMemcpyHostToDevice, ctx->stream));
+        if (n1 > D.up1)
+            HIPCHK(ctx, hipMemcpyAsync((double *)D.lut.p + 4 * (size_t)RF_CODES + D.up1, D.d1v.data() + D.up1,
+                                       (n1 - D.up1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        D.up3 = n3;
+        D.up1 = n1;
+    }
+    if (int e = upload(ctx, ctx->scratch[20], lut)) return e;
+    // chunks of sequences: codes + bases staged in pinned memory, one H2D,
+    // the bases scattered to their regions, the tables built in place
+    int32_t k0 = 0;
+    const int64_t chunk_bytes = std::max<int64_t>((int64_t)ctx->opt.stage_kb * 1024 / 4, 1 << 20);
+    while (k0 < nseq) {
+        int32_t k1 = k0 + 1;
+        while (k1 < nseq && 2 * (off[k1 + 1] - off[k0]) <= chunk_bytes)
+            ++k1;
+        const int64_t nb = off[k1] - off[k0];
+        const size_t stage = (size_t)(2 * nb);
+        if (ctx->pinned_bytes < stage) {
+            if (ctx->pinned)
+                (void)hipHostFree(ctx->pinned);
+            ctx->pinned = nullptr;
+            ctx->pinned_bytes = 0;
+            const size_t want = std::max(stage + stage / 2, (size_t)1 << 22);
+            if (hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault) != hipSuccess)
+                return fail(ctx, RF_ERR_HIP, "rf_set_sequences_codes: pinned staging allocation failed");
+            ctx->pinned_bytes = want;
+        }
+        uint8_t *hb = (uint8_t *)ctx->pinned, *hc = hb + nb;
+        std::memcpy(hb, bases + off[k0], nb);
+        std::memcpy(hc, codes + off[k0], nb);
+        std::vector<CodeSeq> cs(k1 - k0);
+        std::vector<Segment> sg(k1 - k0);
+        for (int32_t k = k0; k < k1; ++k) {
+            const SeqObj &S = ctx->seqs[first + k];
+            cs[k - k0] = {S.tabs.off / 8, off[k] - off[k0], S.n, 0, 0};
+            sg[k - k0] = {off[k] - off[k0], S.bases.off, S.n, 0};
+        }
+        if (int e = ensure_buf(ctx, ctx->scratch[7], (size_t)std::max<int64_t>(2 * nb, 16))) return e;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[7].p, hb, 2 * nb, hipMemcpyHostToDevice, ctx->stream));
+        if (int e = upload(ctx, ctx->scratch[5], sg)) return e;
+        if (int e = upload(ctx, ctx->scratch[6], cs)) return e;
+        hipLaunchKernelGGL(k_scatter, dim3(k1 - k0), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
+                           (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
+        hipLaunchKernelGGL(k_tables, dim3(k1 - k0), dim3(256), 0, ctx->stream, (const CodeSeq *)ctx->scratch[6].p,
+                           (const uint8_t *)ctx->scratch[7].p + nb, (const uint8_t *)ctx->scratch[7].p,
+                           (const CodeLut *)ctx->scratch[20].p, s_mis, s_ins, s_del, (double *)ctx->tab_arena.d);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // staging and descriptors are reused
+        k0 = k1;
+    }
+    // finiteness per sequence (lean DP / scorer eligibility)
+    {
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 22) + 1));
+        parallel_for(nth, [&](int t) {
+            for (int32_t k = (int32_t)((int64_t)nseq * t / nth); k < (int32_t)((int64_t)nseq * (t + 1) / nth); ++k) {
+                bool f = true;
+                for (int64_t i = off[k]; i < off[k + 1] && f; ++i)
+                    f = fin[codes[i]];
+                ctx->seqs[first + k].finite = f;
+            }
+        });
+    }
+    for (int32_t k = 0; k < nseq; ++k) {
+        ctx->seqs[first + k].coded = true;
+        ctx->seqs[first + k].valid = true;
+    }
     ++ctx->layout_gen;
     return 0;
 }

@@ -27,6 +27,8 @@ _SIGNATURES = {
     "rf_last_error": (c_char_p, [c_void_p]),
     "rf_reserve": (c_int, [c_void_p, c_int64]),
     "rf_device_bytes": (c_int64, [c_void_p]),
+    "rf_set_sequences_codes": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_double, c_double, c_double]),
     "rf_code_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "rf_set_sequences": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

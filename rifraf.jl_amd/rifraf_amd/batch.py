@@ -377,7 +377,12 @@ def _wave_native(part, params, engine):
     engine.reserve(int(est_bytes * 1.5) + (64 << 20))
     STATS["setup_native_s"] += time.perf_counter() - t_setup
     allb = np.concatenate(all_s)
-    engine.set_sequences_concat(0, allb, soff, tabs["match"], tabs["mismatch"], tabs["ins"], tabs["del"])
+    # Phred-coded reads: 2 B per position to the device, tables built there
+    # (rf_set_sequences_codes; the same bits); else the host tables
+    if not (phred_in and hasattr(engine, "set_sequences_codes") and
+            engine.set_sequences_codes(0, allb, soff, tabs["code"], tabs["lp_table"], tabs["match_table"],
+                                       params.scores)):
+        engine.set_sequences_concat(0, allb, soff, tabs["match"], tabs["mismatch"], tabs["ins"], tabs["del"])
     engine.set_templates(0, [st_.consensus for st_ in states])
     STATS["upload_s"] += time.perf_counter() - t_setup
     read_seq = np.arange(len(all_s), dtype=np.int32)

@@ -143,6 +143,25 @@ class Engine:
         self._check(self.lib.rf_set_sequences(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off),
                                               *[ptr(x) for x in a], None, None, None, None))
 
+    def set_sequences_codes(self, first: int, bases, off, codes, lp_table, match_table, scores) -> bool:
+        """rf_set_sequences_codes: Phred-coded reads (no codon moves) with
+        their tables built on the device from one byte per position.  False
+        when the row-code dictionary is full (upload host tables instead)."""
+        off = np.ascontiguousarray(off, np.int64)
+        bases = np.ascontiguousarray(bases, np.uint8)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        lp_t = np.ascontiguousarray(lp_table, np.float64)
+        mt = np.ascontiguousarray(match_table, np.float64)
+        if lp_t.shape != (256,) or mt.shape != (256,) or len(codes) != len(bases):
+            raise ValueError("set_sequences_codes: 256-entry tables and one code per base")
+        rc = self.lib.rf_set_sequences_codes(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off), ptr(codes),
+                                             ptr(lp_t), ptr(mt), float(scores.mismatch), float(scores.insertion),
+                                             float(scores.deletion))
+        if rc == -4:
+            return False
+        self._check(rc)
+        return True
+
     def set_templates(self, first: int, tpls):
         if not tpls:
             return

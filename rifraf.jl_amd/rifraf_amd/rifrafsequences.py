@@ -186,7 +186,7 @@ class RifrafSequence:
             tp10 = np.power(10.0, vals)
             with np.errstate(divide="ignore", invalid="ignore"):
                 tmatch = np.log10(1.0 - tp10)
-            extra = {"code": code, "match_table": tmatch}
+            extra = {"code": code, "match_table": tmatch, "lp_table": vals}
             lib = None
             try:
                 from . import _lib

@@ -792,3 +792,54 @@ def test_removed_option_keys_rejected(engine):
     with pytest.raises(KeyError):
         engine.set_option("seg_ver", 4)
     assert RifrafError is not None
+
+
+@pytest.mark.parametrize("scores", ["seq", "other"])
+def test_set_sequences_codes_matches_host_tables(engine, scores):
+    """rf_set_sequences_codes (tables built on the device from Phred codes)
+    gives the same bands, A[end,end], backtraces and dense totals as
+    rf_set_sequences of the host tables (RifrafSequence.many_concat), and
+    both equal the oracle: lengths from 1 to 400, Phred 0 (an infinite
+    match score: the general kernels) among them."""
+    from rifraf_amd.errormodel import phred_to_log_p
+    from rifraf_amd.sample import sample_sequences
+    sc = SEQ_SCORES if scores == "seq" else Scores.from_errors(ErrorModel(2.0, 1.0, 3.0, 0.0, 0.0))
+    rng = np.random.default_rng(3131)
+    _, t, _, reads, _, phreds, _, _ = sample_sequences(24, 400, error_rate=0.03, rng=rng)
+    reads, phreds = list(reads), [np.asarray(p, np.int8).copy() for p in phreds]
+    reads[3], phreds[3] = reads[3][:1], phreds[3][:1]              # a one-base read
+    phreds[5][7] = 0                                                # Phred 0: match = -Inf
+    lens = np.array([len(r) for r in reads])
+    off = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    cat = np.concatenate(phreds)
+    seqs, tabs = RifrafSequence.many_concat(reads, phred_to_log_p(cat), off, 9, sc, phreds=cat)
+    n = len(seqs)
+    sl = np.arange(n)
+    bws = [9] * n
+    allb = np.concatenate(reads).astype(np.uint8)
+    out = []
+    for path in ("codes", "host"):
+        if path == "codes":
+            assert engine.set_sequences_codes(0, allb, off, tabs["code"], tabs["lp_table"], tabs["match_table"], sc)
+        else:
+            engine.set_sequences_concat(0, allb, off, tabs["match"], tabs["mismatch"], tabs["ins"], tabs["del"])
+        engine.set_templates(0, [t])
+        scs = engine.realign(sl, sl, 0, bws, RF_FWD | RF_BWD)
+        bands = [(engine.download_band(k, RF_BAND_A).data.copy(), engine.download_band(k, RF_BAND_B).data.copy())
+                 for k in range(n)]
+        mv, ne = engine.backtrace(list(range(n)))
+        dense = engine.score_dense([sl])[0]
+        out.append((scs, bands, mv, ne, dense))
+    (s1, b1, m1, e1, d1), (s2, b2, m2, e2, d2) = out
+    np.testing.assert_array_equal(s1, s2)
+    for (a1, bb1), (a2, bb2) in zip(b1, b2):
+        np.testing.assert_array_equal(a1, a2)
+        np.testing.assert_array_equal(bb1, bb2)
+    for x, y in zip(m1, m2):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(e1, e2)
+    np.testing.assert_array_equal(d1, d2)
+    for k in (0, 3, 5, n - 1):
+        A_exp, _ = oracle.forward(t, seqs[k])
+        assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(seqs[k]) + 1, len(t) + 1, 9)
