@@ -311,6 +311,28 @@ def pmc_traffic(config, size, kernel):
     return None
 
 
+def pmc_fp64(config, cells=None, dp_ms=None):
+    """FP64 VALU evidence from rocprof counters (profiles/pmc_fp64.json,
+    scripts/pmc_fp64_summary.py over scripts/pmc_r03.sh's passes):
+    SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 wave instructions.  c4: the DP's
+    measured FP64 lane-ops per in-band cell, scaled by this run's cells and DP
+    time; both: each DP kernel's longest launch against the FP64 peak."""
+    try:
+        pm = json.load(open(os.path.join(REPO, "profiles", "pmc_fp64.json")))
+        ent = pm[config]
+    except (OSError, ValueError, KeyError):
+        return None
+    peak = pm["fp64_lane_ops_peak_per_s"]
+    out = {"source": "profiles/pmc_fp64.json",
+           "per_kernel_frac_of_fp64_peak": {k: v["longest_launch"]["frac_of_fp64_peak"]
+                                            for k, v in ent["kernels"].items() if k.startswith("k_dpr")}}
+    if "dp" in ent and cells and dp_ms:
+        r = ent["dp"]["f64_lane_ops_per_cell"]
+        out.update({"f64_lane_ops_per_cell": r, "achieved_tops": r * cells / (dp_ms * 1e-3) / 1e12,
+                    "frac": r * cells / (dp_ms * 1e-3) / peak})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -577,7 +599,8 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         # ops per cell: 3 adds + 2 max; peak = 78.6 TF FMA / 2 = 39.3 T ops/s)
         "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
                     "peak_tops": FP64_VEC_TFLOPS / 2,
-                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2)},
+                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2),
+                    "counters": pmc_fp64(args.config, cells, dp_ms)},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": byt, "launch_ms": ms},
@@ -750,7 +773,8 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         # ops per cell: 3 adds + 2 max; peak = 78.6 TF FMA / 2 = 39.3 T ops/s)
         "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
                     "peak_tops": FP64_VEC_TFLOPS / 2,
-                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2)},
+                    "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2),
+                    "counters": pmc_fp64("c5")},
         # smart_forward_moves! (first realign of every read): forward fills at
         # bw, the backtrace walks that count errors, the redone fills of the
         # reads whose band doubled -- every executed cell counted (rank 0's

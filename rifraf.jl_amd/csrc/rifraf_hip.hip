@@ -2001,7 +2001,10 @@ struct SeglGeo {
 };
 
 template <int SEGS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+#ifndef SEGL_WPE
+#define SEGL_WPE 1
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SEGL_WPE)))
 k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
              const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
              const double *__restrict__ tabs, const double *__restrict__ bands,
