@@ -69,6 +69,7 @@ extern "C" {
 #define RF_ERR_HIP        (-2)
 #define RF_ERR_NUMERIC    (-3)   /* a reference error() on the numeric path */
 #define RF_ERR_STATE      (-4)   /* stale / mismatched bands */
+#define RF_ERR_NEED_HOST  (-5)   /* rf_aln_error_sums: host bases / match scores needed (passed NULL) */
 
 typedef struct rf_ctx rf_ctx;
 
@@ -111,6 +112,11 @@ int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 
 /* Pre-size the device band arena (bytes); optional. */
 int rf_reserve(rf_ctx *ctx, int64_t band_bytes);
+/* Drop every slot's A and B band (each must be filled again before it is
+ * read) and reuse the band arena from its start; the device memory is kept.
+ * For a caller that starts a new batch of alignments (the batched driver's
+ * waves), so an arena sized once serves every later batch. */
+int rf_release_bands(rf_ctx *ctx);
 /* Bytes currently allocated on the device by this context. */
 int64_t rf_device_bytes(const rf_ctx *ctx);
 /* Row-code dictionary of the context (the lean DP's 8-B per-row records):
@@ -267,7 +273,9 @@ void rf_batch_release(rf_ctx *ctx);
  * base, match score) (model.jl:804-809) at each match move, per consensus
  * column, in batch order: out[(row_g + j) * 4 + b], row_g = sum over h < g
  * of tlen[h].  bases[k] / match[k] point at slot k's read bases and match
- * scores (seq_len[k] each, host memory). */
+ * scores (seq_len[k] each, host memory).  When every read is row-coded the
+ * sums are folded on the device and bases / match may be NULL; if they are
+ * NULL and the host fold is needed, RF_ERR_NEED_HOST. */
 int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
                       const int32_t *tlen, const uint8_t *const *bases, const double *const *match,
                       const int32_t *seq_len, double *out);
@@ -286,6 +294,24 @@ int rf_host_tables_from_codes(int64_t nseg, const uint8_t *codes, const int64_t 
 /* Per segment, the sequential sum of grid[ucode[k] * 256 + codes[i]]. */
 int rf_host_code_seq_sums(int64_t nseg, const uint8_t *codes, const int64_t *off, const int32_t *ucode,
                           const double *grid, double *out);
+/* Native-driver setup from Phred codes without host tables: per sequence
+ * est_n_errors (Julia-order sum of p10_t[code], rifrafsequences.jl:74), a
+ * code of its maximum match score, and logsumexp10 of its match scores
+ * (util.jl:28-38 with grid[u * 256 + x] = 10^(match_t[x] - match_t[u])). */
+int rf_host_code_prep(int64_t nseg, const uint8_t *codes, const int64_t *off, const double *p10_t,
+                      const double *match_t, const double *grid, double *est, int32_t *ucode, double *lse);
+/* estimate_probs (model.jl:742-800) and alignment_error_probs's
+ * normalisation (model.jl:835-839) for K clusters, around the caller's 10^x:
+ * prep checks the stacked dense totals D ((m_k+1) x 9 per cluster) and
+ * writes the exponents xpos (M x 5: subs with the consensus slot = score,
+ * deletion; minus the cluster maximum mx_k) and xins ((M+K) x 4); err[0] =
+ * 1 NaN / 2 sub / 3 del / 4 ins positive, err[1] = cluster.  finish
+ * normalises 10^xpos, 10^xins (with st_pow_k = 10^(score_k - mx_k)) and
+ * 10^sums (M x 4, -> aln[M]) in place. */
+int rf_host_qv_prep(int64_t K, const int64_t *moff, const double *D, const uint8_t *cons, const double *score,
+                    double *xpos, double *xins, double *mx, int32_t *err);
+int rf_host_qv_finish(int64_t K, const int64_t *moff, const double *st_pow, double *epos, double *eins,
+                      const double *ealn, double *aln);
 
 /* Geometry of a slot's band: nrows = n+1, ncols = m+1, bandwidth, H. */
 int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,

@@ -36,9 +36,12 @@
 #include <thread>
 #include <vector>
 #include <cstdlib>
+#include <chrono>
+#include <cstdio>
 
 // rf_last_error text; the device form of rf_aln_error_sums (rifraf_hip.hip)
 int rf_internal_fail(rf_ctx *ctx, int code, const char *msg);
+void rf_internal_arena_stats(const rf_ctx *ctx, int64_t *grows, double *secs);
 int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
                              const int32_t *tlen, double *out);
 
@@ -85,6 +88,21 @@ struct Driver {
     std::vector<Read> reads;
     std::vector<Clu> clu;
     std::vector<int32_t> fixed_off, fixed;   // the caller's fixed batches
+
+    // RIFRAF_BATCH_TIMING: wall time and count of each engine call kind
+    // (stderr at the end of rf_rifraf_batch; diagnostics only)
+    enum { T_FWD, T_BT, T_BWD, T_PROPS, T_SCORE, T_TPL, T_N };
+    double tsum[T_N] = {};
+    int tcnt[T_N] = {};
+    template <class F>
+    int timed(int k, F &&call)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int e = call();
+        tsum[k] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        ++tcnt[k];
+        return e;
+    }
 
     void fail_cluster(int c, const std::string &msg)
     {
@@ -163,8 +181,10 @@ struct Driver {
                 bw.push_back(jobs[j].bw);
             }
             out.resize(pending.size());
-            if (int e = rf_realign(ctx, (int32_t)pending.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_FWD,
-                                   out.data()))
+            if (int e = timed(T_FWD, [&] {
+                    return rf_realign(ctx, (int32_t)pending.size(), sl.data(), sq.data(), tp.data(), bw.data(),
+                                      RF_FWD, out.data());
+                }))
                 return e;
             std::vector<int> check;
             for (size_t i = 0; i < pending.size(); ++i) {
@@ -180,7 +200,9 @@ struct Driver {
             for (int j : check)
                 sl.push_back(clu[jobs[j].c].slot0 + jobs[j].k);
             nerr.resize(check.size());
-            if (int e = rf_backtrace(ctx, (int32_t)check.size(), sl.data(), nullptr, nullptr, nullptr, nerr.data()))
+            if (int e = timed(T_BT, [&] {
+                    return rf_backtrace(ctx, (int32_t)check.size(), sl.data(), nullptr, nullptr, nullptr, nerr.data());
+                }))
                 return e;
             std::vector<int> nxt;
             for (size_t i = 0; i < check.size(); ++i) {
@@ -221,7 +243,9 @@ struct Driver {
                 bw.push_back(R.bw);
             }
         }
-        return rf_realign(ctx, (int32_t)sl.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_BWD, nullptr);
+        return timed(T_BWD, [&] {
+            return rf_realign(ctx, (int32_t)sl.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_BWD, nullptr);
+        });
     }
 
     // ---------------- realign! + rescore! (model.jl:630-719), no reference
@@ -305,7 +329,9 @@ struct Driver {
                     rows += (int64_t)clu[c].cons.size() + 1;
                 }
                 std::vector<uint8_t> mask((size_t)rows * 9);
-                if (int e = rf_alignment_proposals(ctx, (int32_t)s.size(), off.data(), sl.data(), 1, mask.data()))
+                if (int e = timed(T_PROPS, [&] {
+                        return rf_alignment_proposals(ctx, (int32_t)s.size(), off.data(), sl.data(), 1, mask.data());
+                    }))
                     return e;
                 static const int order[9][3] = {{0, SUB, 0}, {1, SUB, 1}, {2, SUB, 2}, {3, SUB, 3}, {5, INS, 0},
                                                 {6, INS, 1}, {7, INS, 2}, {8, INS, 3}, {4, DEL, 0}};
@@ -349,8 +375,10 @@ struct Driver {
                 poff.push_back((int64_t)kind.size());
             }
             std::vector<double> tot(kind.size());
-            if (int e = rf_score(ctx, (int32_t)s.size(), off.data(), sl.data(), ref.data(), poff.data(), kind.data(),
-                                 pos.data(), base.data(), tot.data(), nullptr))
+            if (int e = timed(T_SCORE, [&] {
+                    return rf_score(ctx, (int32_t)s.size(), off.data(), sl.data(), ref.data(), poff.data(),
+                                    kind.data(), pos.data(), base.data(), tot.data(), nullptr);
+                }))
                 return e;
             for (size_t g = 0; g < s.size(); ++g) {
                 const Clu &C = clu[s[g]];
@@ -426,7 +454,9 @@ struct Driver {
             bases.insert(bases.end(), clu[c].cons.begin(), clu[c].cons.end());
             off.push_back((int64_t)bases.size());
         }
-        return rf_set_templates_ids(ctx, (int32_t)ids.size(), ids.data(), bases.data(), off.data());
+        return timed(T_TPL, [&] {
+            return rf_set_templates_ids(ctx, (int32_t)ids.size(), ids.data(), bases.data(), off.data());
+        });
     }
 
     // Set the consensus of clusters `cs` (host copy + device template);
@@ -608,7 +638,26 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
                                     ("rf_rifraf_batch: cluster " + std::to_string(c) +
                                      " is outside the native driver's scope (" + why + ")").c_str());
     }
+    const auto t_run = std::chrono::steady_clock::now();
+    int64_t g0;
+    double gs0;
+    rf_internal_arena_stats(ctx, &g0, &gs0);
     D.run();
+    if (const char *tv = std::getenv("RIFRAF_BATCH_TIMING"); tv && *tv && *tv != '0') {
+        static const char *names[] = {"realign_fwd", "backtrace", "realign_bwd", "aln_props", "score", "templates"};
+        double tot = 0;
+        std::fprintf(stderr, "rf_rifraf_batch: %d clusters, run %.4f s;", nclusters,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count());
+        for (int k = 0; k < Driver::T_N; ++k) {
+            std::fprintf(stderr, " %s %.4f s / %d;", names[k], D.tsum[k], D.tcnt[k]);
+            tot += D.tsum[k];
+        }
+        int64_t g1;
+        double gs1;
+        rf_internal_arena_stats(ctx, &g1, &gs1);
+        std::fprintf(stderr, " engine total %.4f s; arena grows %lld (%.4f s)\n", tot, (long long)(g1 - g0),
+                     gs1 - gs0);
+    }
     BatchResult &R = result_of(ctx);
     R.clu = std::move(D.clu);
     R.reads = std::move(D.reads);
@@ -736,7 +785,7 @@ extern "C" int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *sl
                                  const int32_t *tlen, const uint8_t *const *bases, const double *const *match,
                                  const int32_t *seq_len, double *out)
 {
-    if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !tlen || !bases || !match || !seq_len || !out)))
+    if (!ctx || ngroups < 0 || (ngroups > 0 && (!slot_off || !slots || !tlen || !seq_len || !out)))
         return RF_ERR_ARG;
     // every read row-coded: the moves are folded on the device (k_aln_sums),
     // with the same additions in the same order
@@ -745,6 +794,8 @@ extern "C" int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *sl
         if (e <= 0)
             return e;
     }
+    if (ngroups > 0 && (!bases || !match))   // the host fold needs the reads' bases and match scores
+        return RF_ERR_NEED_HOST;
     const int32_t ns = ngroups > 0 ? slot_off[ngroups] : 0;
     std::vector<int64_t> moff(ns + 1, 0);
     std::vector<int32_t> glen(ns);
@@ -900,5 +951,210 @@ extern "C" int rf_host_code_seq_sums(int64_t nseg, const uint8_t *codes, const i
             s = i == off[k] ? g[codes[i]] : s + g[codes[i]];
         out[k] = s;
     }
+    return 0;
+}
+
+namespace {
+// ranges [lo, hi) of n items over host threads (OMP_NUM_THREADS, at most 16,
+// at least `grain` items per thread)
+template <class F>
+void host_parallel(int64_t n, int64_t grain, F &&fn)
+{
+    const char *ev = std::getenv("OMP_NUM_THREADS");
+    const int64_t want = (ev && *ev) ? std::atoi(ev) : (int64_t)std::thread::hardware_concurrency();
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({want, 16, n / std::max<int64_t>(grain, 1)}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; ++t)
+        th.emplace_back([&, t] { fn(n * t / nth, n * (t + 1) / nth); });
+    fn(0, n / nth);
+    for (auto &x : th)
+        x.join();
+}
+}  // namespace
+
+// Setup of the native driver from Phred codes, without building the host
+// tables: per sequence k (codes[off[k]:off[k+1]], non-empty)
+//   est[k]   = est_n_errors, the Julia-order sum of p10_t[code]
+//              (rifrafsequences.jl:74; the same sum as rf_host_tables_from_codes);
+//   ucode[k] = a code whose match_t value is the sequence's maximum match score;
+//   lse[k]   = logsumexp10 of the match scores (model.jl:1276-1287's initial
+//              consensus choice; the Python mirror model.logsumexp10): the
+//              sequential sum of grid[ucode * 256 + code] (grid = 10^(x - u) per
+//              code pair, evaluated by the caller with numpy), then
+//              log10(sum) + u with the C library's log10 (math.log10).
+// A sequence whose maximum is infinite gets lse = u (the caller checks NaN).
+extern "C" int rf_host_code_prep(int64_t nseg, const uint8_t *codes, const int64_t *off, const double *p10_t,
+                                 const double *match_t, const double *grid, double *est, int32_t *ucode, double *lse)
+{
+    if (nseg < 0 || (nseg > 0 && (!codes || !off || !p10_t || !match_t || !grid || !est || !ucode || !lse)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < nseg; ++k)
+        if (off[k + 1] <= off[k])
+            return RF_ERR_ARG;
+    host_parallel(nseg, 64, [&](int64_t lo, int64_t hi) {
+        std::vector<double> p10;
+        for (int64_t k = lo; k < hi; ++k) {
+            const int64_t a = off[k], n = off[k + 1] - off[k];
+            const uint8_t *c = codes + a;
+            p10.resize((size_t)n);
+            int32_t uc = c[0];
+            for (int64_t i = 0; i < n; ++i) {
+                p10[(size_t)i] = p10_t[c[i]];
+                if (match_t[c[i]] > match_t[uc])
+                    uc = c[i];
+            }
+            double s = p10[0];
+            if (n < 16) {
+                for (int64_t i = 1; i < n; ++i)
+                    s += p10[(size_t)i];
+            } else {
+                s = julia_sum(p10.data(), 0, n - 1);
+            }
+            est[k] = s;
+            ucode[k] = uc;
+            const double u = match_t[uc];
+            if (std::isinf(u)) {
+                lse[k] = u;
+                continue;
+            }
+            const double *g = grid + (size_t)uc * 256;
+            double t = g[c[0]];
+            for (int64_t i = 1; i < n; ++i)
+                t += g[c[i]];
+            lse[k] = std::log10(t) + u;
+        }
+    });
+    return 0;
+}
+
+// estimate_probs (model.jl:742-800 via the dense totals) and the final
+// normalisation of alignment_error_probs (model.jl:835-839) for K clusters at
+// once, in two passes around the caller's 10^x (numpy's power, so the values
+// equal the Python mirror's model.qvs_many, which this restates):
+//
+// rf_host_qv_prep: D = stacked dense totals, (m_k + 1) rows of 9 per cluster
+// (row 0 = position 0: insertions only); cons = stacked consensus bases;
+// score = state scores.  Checks NaN (error 1: "failed to compute a valid
+// score"), forms S = sub totals with the consensus base's slot = score,
+// Dl = deletion totals, I = insertion totals, mx_k = max(max S, max Dl,
+// max I) (Python max order), errors 2/3/4 for a positive sub / del / ins
+// maximum relative to mx, and writes the exponents
+//   xpos[r] = [S - mx, Dl - mx] (M x 5), xins = I - mx ((M + K) x 4).
+// err[0] = error kind, err[1] = its cluster.
+extern "C" int rf_host_qv_prep(int64_t K, const int64_t *moff, const double *D, const uint8_t *cons,
+                               const double *score, double *xpos, double *xins, double *mx, int32_t *err)
+{
+    if (K < 0 || (K > 0 && (!moff || !D || !cons || !score || !xpos || !xins || !mx || !err)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < K; ++k)
+        if (moff[k + 1] <= moff[k])
+            return RF_ERR_ARG;
+    std::vector<uint8_t> bad((size_t)K, 0);
+    host_parallel(K, 8, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; ++k) {
+            const int64_t r0 = moff[k] + k, m = moff[k + 1] - moff[k];   // dense rows r0 .. r0 + m
+            bool nan = false;
+            double mS = -INF, mD = -INF, mI = -INF;
+            bool firstS = true, firstD = true, firstI = true;
+            for (int64_t p = 0; p <= m; ++p) {
+                const double *d = D + (r0 + p) * 9;
+                for (int q = 5; q < 9; ++q) {
+                    nan |= std::isnan(d[q]);
+                    mI = firstI ? d[q] : (d[q] > mI ? d[q] : mI);
+                    firstI = false;
+                }
+                if (p == 0)
+                    continue;
+                const int64_t r = moff[k] + p - 1;
+                const int cb = cons[r];
+                for (int q = 0; q < 5; ++q)
+                    nan |= q != cb && std::isnan(d[q]);
+                for (int q = 0; q < 4; ++q) {
+                    const double v = q == cb ? 0.0 + score[k] : d[q];
+                    mS = firstS ? v : (v > mS ? v : mS);
+                    firstS = false;
+                }
+                mD = firstD ? d[4] : (d[4] > mD ? d[4] : mD);
+                firstD = false;
+            }
+            double x = mS;                       // Python max(mxS, mxD, mxI)
+            if (mD > x)
+                x = mD;
+            if (mI > x)
+                x = mI;
+            mx[k] = x;
+            bad[(size_t)k] = nan ? 1 : mS - x > 0.0 ? 2 : mD - x > 0.0 ? 3 : mI - x > 0.0 ? 4 : 0;
+            if (nan)
+                continue;
+            for (int64_t p = 0; p <= m; ++p) {
+                const double *d = D + (r0 + p) * 9;
+                double *xi = xins + (r0 + p) * 4;
+                for (int q = 0; q < 4; ++q)
+                    xi[q] = d[5 + q] - x;
+                if (p == 0)
+                    continue;
+                const int64_t r = moff[k] + p - 1;
+                const int cb = cons[r];
+                double *xp = xpos + r * 5;
+                for (int q = 0; q < 4; ++q)
+                    xp[q] = (q == cb ? 0.0 + score[k] : d[q]) - x;
+                xp[4] = d[4] - x;
+            }
+        }
+    });
+    err[0] = 0;
+    err[1] = -1;
+    for (int64_t k = 0; k < K; ++k)       // any NaN first (the mirror checks the whole stack), then the first cluster
+        if (bad[(size_t)k] == 1) {
+            err[0] = 1;
+            err[1] = (int32_t)k;
+            return 0;
+        }
+    for (int64_t k = 0; k < K; ++k)
+        if (bad[(size_t)k]) {
+            err[0] = bad[(size_t)k];
+            err[1] = (int32_t)k;
+            return 0;
+        }
+    return 0;
+}
+
+// rf_host_qv_finish: epos / eins / ealn = 10^x of the prep's exponents (and of
+// the alignment_error_probs sums, M x 4); in place:
+//   epos[r] /= epos[r][0] + ... + epos[r][4]                 (pos_probs)
+//   eins[r] /= st_pow[k] + (eins[r][0] + ... + eins[r][3])   (ins_probs)
+//   aln[r]   = 1.0 - max_b ealn[r][b] / (ealn[r][0] + ... + ealn[r][3])
+// with st_pow[k] = 10.0 ** (score_k - mx_k) from the caller; row sums are
+// sequential, as numpy's sum(axis=1) over rows of 4 / 5.
+extern "C" int rf_host_qv_finish(int64_t K, const int64_t *moff, const double *st_pow, double *epos, double *eins,
+                                 const double *ealn, double *aln)
+{
+    if (K < 0 || (K > 0 && (!moff || !st_pow || !epos || !eins || !ealn || !aln)))
+        return RF_ERR_ARG;
+    host_parallel(K, 8, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; ++k) {
+            const int64_t m = moff[k + 1] - moff[k];
+            for (int64_t p = 0; p <= m; ++p) {
+                double *e = eins + (moff[k] + k + p) * 4;
+                const double s = st_pow[k] + (((e[0] + e[1]) + e[2]) + e[3]);
+                for (int q = 0; q < 4; ++q)
+                    e[q] = e[q] / s;
+            }
+            for (int64_t r = moff[k]; r < moff[k + 1]; ++r) {
+                double *e = epos + r * 5;
+                const double s = (((e[0] + e[1]) + e[2]) + e[3]) + e[4];
+                for (int q = 0; q < 5; ++q)
+                    e[q] = e[q] / s;
+                const double *a = ealn + r * 4;
+                const double t = ((a[0] + a[1]) + a[2]) + a[3];
+                double mxq = a[0] / t;
+                for (int q = 1; q < 4; ++q) {   // numpy max: NaN propagates
+                    const double v = a[q] / t;
+                    mxq = (std::isnan(mxq) || !(v <= mxq)) ? (std::isnan(mxq) ? mxq : v) : mxq;
+                }
+                aln[r] = 1.0 - mxq;
+            }
+        }
+    });
     return 0;
 }

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -3474,6 +3475,8 @@ struct rf_ctx {
     std::vector<Slot> slots;
     uint64_t tpl_counter = 0;
     uint64_t layout_gen = 1;   // bumped whenever a device offset / length may change
+    int64_t arena_grows = 0;   // arena_grow calls and their wall seconds (RIFRAF_BATCH_TIMING)
+    double arena_grow_s = 0.0;
     // bumped by every call that changes sequences, templates or band metadata:
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
@@ -3603,7 +3606,17 @@ void live_regions(rf_ctx *ctx, Arena *a, std::vector<Region *> &out)
 
 // Grow (and compact) an arena so that `need` more bytes fit at the top.
 // `skip` is a region about to be rewritten: its content is not preserved.
+int arena_grow_impl(rf_ctx *ctx, Arena &a, int64_t need, Region *skip);
 int arena_grow(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const int e = arena_grow_impl(ctx, a, need, skip);
+    ctx->arena_grow_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ++ctx->arena_grows;
+    return e;
+}
+
+int arena_grow_impl(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
 {
     std::vector<Region *> regs;
     live_regions(ctx, &a, regs);
@@ -3982,6 +3995,24 @@ int rf_reserve(rf_ctx *ctx, int64_t band_bytes)
         return 0;   // room already: nothing moves, cached plans stay valid
     ++ctx->state_epoch;   // regions move (arena_grow also bumps layout_gen)
     return arena_grow(ctx, ctx->band_arena, band_bytes, nullptr);
+}
+
+int rf_release_bands(rf_ctx *ctx)
+{
+    if (!ctx)
+        return RF_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // no launch still reads or writes a band
+    for (auto &s : ctx->slots)
+        for (Band *b : {&s.a, &s.b}) {
+            b->valid = false;
+            b->r.off = -1;
+            b->r.cap = 0;
+        }
+    ctx->band_arena.top = ARENA_GUARD;
+    ++ctx->layout_gen;
+    ++ctx->state_epoch;
+    return 0;
 }
 
 int rf_code_stats(const rf_ctx *ctx, int64_t *entries3, int64_t *entries1, int64_t *uncoded_reads,
@@ -5674,4 +5705,11 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
     if (ns > 0)
         note_bt_ms(ctx);
     return check_err(ctx);
+}
+
+// arena_grow count and seconds of a context (rf_rifraf_batch's RIFRAF_BATCH_TIMING line)
+void rf_internal_arena_stats(const rf_ctx *ctx, int64_t *grows, double *secs)
+{
+    *grows = ctx ? ctx->arena_grows : 0;
+    *secs = ctx ? ctx->arena_grow_s : 0.0;
 }

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("RIFRAF_HIP_LIB", os.path.join(PKG_DIR, "librifraf_hip
 
 RF_FWD, RF_BWD, RF_SKEW, RF_TRIM = 1, 2, 4, 8
 RF_BAND_A, RF_BAND_B = 0, 1
+RF_ERR_NEED_HOST = -5
 RF_ABI_VERSION = 1
 
 # every symbol include/rifraf_hip.h declares, with its ctypes signature
@@ -26,6 +27,7 @@ _SIGNATURES = {
     "rf_destroy": (c_int, [c_void_p]),
     "rf_last_error": (c_char_p, [c_void_p]),
     "rf_reserve": (c_int, [c_void_p, c_int64]),
+    "rf_release_bands": (c_int, [c_void_p]),
     "rf_device_bytes": (c_int64, [c_void_p]),
     "rf_set_sequences_codes": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_double, c_double, c_double]),
@@ -42,6 +44,9 @@ _SIGNATURES = {
     "rf_host_seq_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
     "rf_host_tables_from_codes": (c_int, [c_int64] + [c_void_p] * 5 + [c_double] * 3 + [c_void_p] * 6),
     "rf_host_code_seq_sums": (c_int, [c_int64] + [c_void_p] * 5),
+    "rf_host_code_prep": (c_int, [c_int64] + [c_void_p] * 8),
+    "rf_host_qv_prep": (c_int, [c_int64] + [c_void_p] * 8),
+    "rf_host_qv_finish": (c_int, [c_int64] + [c_void_p] * 6),
     "rf_realign": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "rf_backtrace": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_score": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -120,4 +125,4 @@ def ptr(a: np.ndarray | None):
 
 
 __all__ = ["load", "ptr", "EngineUnavailable", "RF_FWD", "RF_BWD", "RF_SKEW", "RF_TRIM",
-           "RF_BAND_A", "RF_BAND_B", "_SIGNATURES", "c_int8", "c_uint8"]
+           "RF_BAND_A", "RF_BAND_B", "RF_ERR_NEED_HOST", "_SIGNATURES", "c_int8", "c_uint8"]

@@ -306,7 +306,7 @@ def _wave_native(part, params, engine):
     from . import _lib
     from .engine import RF_BWD, RF_FWD
     from .errormodel import phred_to_log_p
-    from .model import RifrafResult, Stage, check_params, initial_state, qvs_many
+    from .model import RifrafResult, Stage, check_params, initial_state, qvs_many_lib
     from .poisson import cquantile_poisson_many
     from .proposals import AmbiguousProposalsError
     from .rifrafsequences import RifrafSequence
@@ -333,11 +333,22 @@ def _wave_native(part, params, engine):
         raise RifrafError("empty read or length mismatch")
     soff = np.zeros(len(all_s) + 1, np.int64)
     np.cumsum(lens, out=soff[1:])
-    # one division / ufunc pass over every read (elementwise: equal to per-read calls)
-    lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
-        [np.asarray(x, np.float64) for x in all_lp])
-    allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
-                                               phreds=cat_lp.astype(np.int8) if phred_in else None)
+    # integer Phred scores: the codes go to the device and the host builds no
+    # tables (est_n_errors and the initial consensus's logsumexp10 in one C++
+    # pass; RifrafSequence.many_coded), else the concatenated host tables
+    coded = None
+    if (phred_in and cat_lp is not None and cat_lp.dtype.kind in "iu" and len(cat_lp)
+            and int(cat_lp.max()) <= 127):
+        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8), soff, params.bandwidth, params.scores)
+    if coded is not None:
+        allseqs, tabs, lse_all = coded
+    else:
+        # one division / ufunc pass over every read (elementwise: equal to per-read calls)
+        lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
+            [np.asarray(x, np.float64) for x in all_lp])
+        allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
+                                                   phreds=cat_lp.astype(np.int8) if phred_in else None)
+        lse_all = None
     nread = np.array(nread, np.int32)
     read_off = np.zeros(K + 1, np.int32)
     np.cumsum(nread, out=read_off[1:])
@@ -346,10 +357,13 @@ def _wave_native(part, params, engine):
     first = {}
     if need:
         ridx = np.concatenate([np.arange(read_off[k], read_off[k + 1]) for k in need])
-        ms = [allseqs[r].match_scores for r in ridx]
-        moff = np.zeros(len(ms) + 1, np.int64)
-        np.cumsum([len(x) for x in ms], out=moff[1:])
-        if len(need) == K and phred_in:
+        if lse_all is None:
+            ms = [allseqs[r].match_scores for r in ridx]
+            moff = np.zeros(len(ms) + 1, np.int64)
+            np.cumsum([len(x) for x in ms], out=moff[1:])
+        if lse_all is not None:
+            lse = lse_all[ridx]
+        elif len(need) == K and phred_in:
             lse = _logsumexp10_many(tabs["match"], moff, codes=tabs["code"], table=tabs["match_table"])
         else:
             lse = _logsumexp10_many(np.concatenate(ms), moff)
@@ -374,6 +388,10 @@ def _wave_native(part, params, engine):
         H = 2 * params.bandwidth + np.abs(ln - m) + 1
         band = (H + 2 * m) * band_stride(H, pad_h=1) * 8   # upper bound: padded rows
         est_bytes += int(np.sort(band)[::-1][:nb[k]].sum()) * 2
+    # a new wave rewrites every slot it uses: the previous wave's bands are
+    # dropped and the arena is reused (sized once for a steady stream of waves)
+    if hasattr(engine, "release_bands"):
+        engine.release_bands()
     engine.reserve(int(est_bytes * 1.5) + (64 << 20))
     STATS["setup_native_s"] += time.perf_counter() - t_setup
     allb = np.concatenate(all_s)
@@ -382,7 +400,8 @@ def _wave_native(part, params, engine):
     if not (phred_in and hasattr(engine, "set_sequences_codes") and
             engine.set_sequences_codes(0, allb, soff, tabs["code"], tabs["lp_table"], tabs["match_table"],
                                        params.scores)):
-        engine.set_sequences_concat(0, allb, soff, tabs["match"], tabs["mismatch"], tabs["ins"], tabs["del"])
+        ft = tabs["source"].full() if coded is not None else tabs
+        engine.set_sequences_concat(0, allb, soff, ft["match"], ft["mismatch"], ft["ins"], ft["del"])
     engine.set_templates(0, [st_.consensus for st_ in states])
     STATS["upload_s"] += time.perf_counter() - t_setup
     read_seq = np.arange(len(all_s), dtype=np.int32)
@@ -444,12 +463,15 @@ def _wave_native(part, params, engine):
                 total += v
             st_.score = total
             at += n
-        dense = engine.score_dense(groups)
+        dense = engine.score_dense(groups, rows=[len(st_.consensus) + 1 for st_ in states])
         ridx = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int64) for k, st_ in enumerate(states)])
-        sums = engine.aln_error_sums_ptr(groups, [len(st_.consensus) for st_ in states],
-                                         allb.ctypes.data + soff[ridx].astype(np.uint64),
-                                         tabs["match"].ctypes.data + 8 * soff[ridx].astype(np.uint64), lens[ridx])
-        for k, (ep, ap) in enumerate(qvs_many(states, dense, sums)):
+        tl = [len(st_.consensus) for st_ in states]
+        sums = engine.aln_error_sums_ptr(groups, tl, None, None, lens[ridx]) if coded is not None else None
+        if sums is None:        # host fold: the reads' bases and match scores
+            ft = tabs["source"].full() if coded is not None else tabs
+            sums = engine.aln_error_sums_ptr(groups, tl, allb.ctypes.data + soff[ridx].astype(np.uint64),
+                                             ft["match"].ctypes.data + 8 * soff[ridx].astype(np.uint64), lens[ridx])
+        for k, (ep, ap) in enumerate(qvs_many_lib(states, dense, sums)):
             results[k].error_probs = ep
             results[k].aln_error_probs = ap
         STATS["score_phase_s"] += time.perf_counter() - t0

@@ -13,7 +13,7 @@ from ctypes import c_int64, byref, c_double, c_int32, c_void_p
 import numpy as np
 
 from . import _lib
-from ._lib import RF_BAND_A, RF_BAND_B, RF_BWD, RF_FWD, RF_SKEW, RF_TRIM, ptr
+from ._lib import RF_BAND_A, RF_BAND_B, RF_BWD, RF_ERR_NEED_HOST, RF_FWD, RF_SKEW, RF_TRIM, ptr
 from .bandedarrays import BandedArray
 from .proposals import to_arrays
 
@@ -93,6 +93,11 @@ class Engine:
 
     def reserve(self, nbytes: int):
         self._check(self.lib.rf_reserve(self.ctx, int(nbytes)))
+
+    def release_bands(self):
+        """rf_release_bands: drop every slot's bands and reuse the band arena
+        from its start (the memory stays allocated)."""
+        self._check(self.lib.rf_release_bands(self.ctx))
 
     def device_bytes(self) -> int:
         return int(self.lib.rf_device_bytes(self.ctx))
@@ -226,19 +231,26 @@ class Engine:
 
     def aln_error_sums_ptr(self, groups, tlens, bptr, mptr, slen):
         """aln_error_sums with the slots' read bases / match scores given as
-        host addresses (uint64 arrays; the caller keeps the memory alive)."""
+        host addresses (uint64 arrays; the caller keeps the memory alive).
+        With bptr / mptr None the sums are folded on the device when every
+        read is row-coded; None is returned when the host fold is needed."""
         off = np.zeros(len(groups) + 1, np.int32)
         np.cumsum([len(g) for g in groups], out=off[1:])
         slots = np.ascontiguousarray(np.concatenate([np.asarray(g, np.int32) for g in groups])
                                      if groups else np.zeros(0, np.int32))
-        bptr, mptr = np.ascontiguousarray(bptr, np.uint64), np.ascontiguousarray(mptr, np.uint64)
+        bptr = None if bptr is None else np.ascontiguousarray(bptr, np.uint64)
+        mptr = None if mptr is None else np.ascontiguousarray(mptr, np.uint64)
         slen = np.ascontiguousarray(slen, np.int32)
         tl = np.ascontiguousarray(tlens, np.int32)
         row = np.zeros(len(groups) + 1, np.int64)
         np.cumsum(tl, out=row[1:])
         out = np.empty((max(int(row[-1]), 1), 4))
-        self._check(self.lib.rf_aln_error_sums(self.ctx, len(groups), ptr(off), ptr(slots), ptr(tl), ptr(bptr),
-                                               ptr(mptr), ptr(slen), ptr(out)))
+        rc = self.lib.rf_aln_error_sums(self.ctx, len(groups), ptr(off), ptr(slots), ptr(tl),
+                                        None if bptr is None else ptr(bptr), None if mptr is None else ptr(mptr),
+                                        ptr(slen), ptr(out))
+        if rc == RF_ERR_NEED_HOST and (bptr is None or mptr is None):
+            return None      # the caller passes the host tables and calls again
+        self._check(rc)
         return [out[row[g]:row[g + 1]] for g in range(len(groups))]
 
     def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:

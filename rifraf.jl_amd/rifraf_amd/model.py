@@ -704,6 +704,70 @@ def qvs_many(states, dense, sums):
     return out
 
 
+def _stacked(parts, rows, cols):
+    """The arrays of `parts` as one (rows, cols) array: their common base
+    when they are consecutive views of it (engine.score_dense /
+    aln_error_sums_ptr results), else a concatenation."""
+    if parts:
+        b = parts[0].base
+        if (isinstance(b, np.ndarray) and b.dtype == np.float64 and b.flags.c_contiguous and b.ndim == 2
+                and b.shape[1] == cols and b.shape[0] >= rows and parts[0].ctypes.data == b.ctypes.data):
+            at, ok = b.ctypes.data, True
+            for x in parts:
+                if x.base is not b or x.ctypes.data != at:
+                    ok = False
+                    break
+                at += x.shape[0] * cols * 8
+            if ok and at == b.ctypes.data + rows * cols * 8:
+                return b[:rows]
+    return np.ascontiguousarray(np.concatenate([np.asarray(x, np.float64) for x in parts]) if parts
+                                else np.zeros((0, cols)))
+
+
+def qvs_many_lib(states, dense, sums):
+    """qvs_many with its passes in C++ (rf_host_qv_prep / rf_host_qv_finish,
+    host threads) and numpy's power in between: the same exponents, the same
+    10^x, the same sequential row sums and divisions, so the same values
+    (tests/test_host_batch.py compares every bit).  Falls back to qvs_many
+    without the library or for an empty consensus."""
+    K = len(states)
+    ms = np.array([len(st.consensus) for st in states], np.int64)
+    try:
+        from . import _lib
+        lib = _lib.load()
+    except Exception:  # noqa: BLE001 -- host-only use without the library
+        lib = None
+    if lib is None or K == 0 or (ms == 0).any():
+        return qvs_many(states, dense, sums)
+    moff = np.zeros(K + 1, np.int64)
+    np.cumsum(ms, out=moff[1:])
+    M = int(moff[-1])
+    D = _stacked(dense, M + K, 9)
+    A = _stacked(sums, M, 4)
+    cons = np.ascontiguousarray(np.concatenate([np.asarray(st.consensus, np.uint8) for st in states]))
+    score = np.array([st.score for st in states], np.float64)
+    xpos, xins, mx = np.empty((M, 5)), np.empty((M + K, 4)), np.empty(K)
+    err = np.zeros(2, np.int32)
+    P = _lib.ptr
+    if lib.rf_host_qv_prep(K, P(moff), P(D), P(cons), P(score), P(xpos), P(xins), P(mx), P(err)) != 0:
+        raise RifrafError("rf_host_qv_prep: invalid arguments")
+    if err[0]:
+        raise RifrafError({1: "failed to compute a valid score", 2: "sub scores cannot be positive",
+                           3: "deletion scores cannot be positive",
+                           4: "insertion scores cannot be positive"}[int(err[0])])
+    epos, eins, ealn = _power10(xpos), _power10(xins), _power10(A)
+    # 10.0 ** (score - mx) with mx a numpy float64, as qvs_many evaluates it
+    st_pow = np.array([10.0 ** (st.score - mx[k]) for k, st in enumerate(states)])
+    aln = np.empty(M)
+    if lib.rf_host_qv_finish(K, P(moff), P(st_pow), P(epos), P(eins), P(ealn), P(aln)) != 0:
+        raise RifrafError("rf_host_qv_finish: invalid arguments")
+    out = []
+    for k in range(K):
+        a, b, c, d = moff[k], moff[k + 1], moff[k] + k, moff[k + 1] + k + 1
+        out.append((EstimatedProbs(epos[a:b, :4], epos[a:b, 4], eins[c:d]), aln[a:b]))
+    return out
+
+
 def aln_error_probs_from_sums(sums):
     """alignment_error_probs's final normalisation (model.jl:835-839) of the
     per-column base-distribution sums (rf_aln_error_sums)."""

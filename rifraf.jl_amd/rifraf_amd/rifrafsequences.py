@@ -236,6 +236,58 @@ class RifrafSequence:
             {"match": match, "mismatch": mism, "ins": ins, "del": dele, **extra}
 
     @classmethod
+    def many_coded(cls, seqs, phreds, off, bandwidth: int, scores: Scores):
+        """The native driver's setup (batch._wave_native) from concatenated
+        int8 Phred scores, without building host tables: one C++ pass
+        (rf_host_code_prep) gives est_n_errors (the same Julia-order sum as
+        many_concat) and logsumexp10 of every sequence's match scores (the
+        values batch._logsumexp10_many returns).  The objects build their
+        tables from the codes on first access (CodedRifrafSequence: the same
+        gathers, adds and maxima as many_concat, so the same bits).  Returns
+        (objects, tables-dict with the codes and per-code tables, lse), or
+        None when the library is absent."""
+        try:
+            from . import _lib
+            lib = _lib.load()
+        except Exception:  # noqa: BLE001 -- host-only use: the caller takes many_concat
+            return None
+        code = np.ascontiguousarray(np.asarray(phreds, np.int8).view(np.uint8))
+        vals = phred_to_log_p(np.arange(256, dtype=np.uint8).view(np.int8))
+        tp10 = np.power(10.0, vals)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            tmatch = np.log10(1.0 - tp10)
+            grid = np.ascontiguousarray(np.power(10.0, tmatch[None, :] - tmatch[:, None]))   # [u code, x code]
+        if (code >= 128).any():
+            raise ValueError("phred score cannot be negative")
+        if not (vals[:128] <= 0.0).all() or np.isinf(vals[:128]).any():
+            raise ValueError("a log error probability is out of range")
+        K = len(off) - 1
+        off64 = np.ascontiguousarray(off, np.int64)
+        est, lse = np.empty(K), np.empty(K)
+        ucode = np.empty(K, np.int32)
+        P = _lib.ptr
+        if lib.rf_host_code_prep(K, P(code), P(off64), P(tp10), P(tmatch), P(grid), P(est), P(ucode), P(lse)) != 0:
+            raise ValueError("rf_host_code_prep: invalid segments (empty sequence?)")
+        src = _CodeSource(code, off64, vals, tmatch, scores)
+        out = []
+        new = object.__new__
+        bw = int(bandwidth)
+        estl = est.tolist()
+        for k, sq in enumerate(seqs):
+            r = new(CodedRifrafSequence)
+            r.seq = sq
+            r._src = src
+            r._k = k
+            r.codon_ins_scores = _EMPTY
+            r.codon_del_scores = _EMPTY
+            r.est_n_errors = estl[k]
+            r.bandwidth = bw
+            r.bandwidth_fixed = False
+            out.append(r)
+        tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src}
+        return out, tabs, lse
+
+    @classmethod
     def rescored(cls, other: "RifrafSequence", scores: Scores) -> "RifrafSequence":
         """RifrafSequence(seq, scores), rifrafsequences.jl:90-95."""
         r = cls(other.seq, other.error_log_p, other.bandwidth, scores)
@@ -253,3 +305,71 @@ class RifrafSequence:
 
     def do_codon_moves(self):          # :104
         return self.do_codon_ins() or self.do_codon_del()
+
+
+_EMPTY = np.empty(0)
+_TABLES = ("error_log_p", "match_scores", "mismatch_scores", "ins_scores", "del_scores")
+
+
+class _CodeSource:
+    """Codes and per-code tables shared by the CodedRifrafSequence objects of
+    one many_coded call; full() gives the concatenated tables of
+    many_concat (rf_host_tables_from_codes) when a caller needs them all."""
+
+    def __init__(self, code, off, vals, tmatch, scores):
+        self.code, self.off, self.vals, self.tmatch, self.scores = code, off, vals, tmatch, scores
+        self._full = None
+
+    def tables(self, k):
+        a, b = int(self.off[k]), int(self.off[k + 1])
+        lp = self.vals[self.code[a:b]]
+        sc = self.scores
+        d = np.empty(b - a + 1)
+        d[0] = lp[0] + sc.deletion                                         # rifrafsequences.jl:49-53
+        d[-1] = lp[-1] + sc.deletion
+        if b - a > 1:
+            d[1:-1] = np.maximum(lp[:-1], lp[1:]) + sc.deletion
+        return lp, self.tmatch[self.code[a:b]], lp + sc.mismatch, lp + sc.insertion, d
+
+    def full(self):
+        if self._full is None:
+            from . import _lib
+            N, K = len(self.code), len(self.off) - 1
+            lp, match, mism, ins = (np.empty(N) for _ in range(4))
+            dele, est = np.empty(N + K), np.empty(K)
+            P = _lib.ptr
+            _lib.load().rf_host_tables_from_codes(K, P(self.code), P(self.off), P(self.vals),
+                                                  P(np.power(10.0, self.vals)), P(self.tmatch),
+                                                  float(self.scores.mismatch), float(self.scores.insertion),
+                                                  float(self.scores.deletion), P(lp), P(match), P(mism), P(ins),
+                                                  P(dele), P(est))
+            self._full = {"match": match, "mismatch": mism, "ins": ins, "del": dele}
+        return self._full
+
+
+def _coded_table(name, idx):
+    slot = RifrafSequence.__dict__[name]
+
+    def get(self):
+        try:
+            return slot.__get__(self)
+        except AttributeError:
+            for nm, v in zip(_TABLES, self._src.tables(self._k)):
+                RifrafSequence.__dict__[nm].__set__(self, v)
+            return slot.__get__(self)
+
+    def put(self, v):
+        slot.__set__(self, v)
+    return property(get, put)
+
+
+class CodedRifrafSequence(RifrafSequence):
+    """A RifrafSequence of RifrafSequence.many_coded: its tables are built
+    from the Phred codes on first access (the same values as the eager
+    constructor's)."""
+
+    __slots__ = ("_src", "_k")
+
+
+for _i, _n in enumerate(_TABLES):
+    setattr(CodedRifrafSequence, _n, _coded_table(_n, _i))

@@ -709,6 +709,32 @@ def test_validation_skip_follows_state(engine):
     assert not np.array_equal(d1[1:, 5:], d2[1:, 5:])
 
 
+def test_release_bands_then_refill(engine):
+    """rf_release_bands drops every band (scoring a dropped slot is refused,
+    not read from reused memory), keeps the device memory, and slots filled
+    again give the same totals; a second set of alignments then reuses the
+    arena from its start."""
+    rng = np.random.default_rng(404)
+    t = random_seq(150, rng)
+    seqs = [make_read(t, rng, 0.03, 9) for _ in range(6)]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    sl = np.arange(6)
+    engine.realign(sl, sl, 0, [9] * 6, RF_FWD | RF_BWD)
+    d1 = engine.score_dense([sl])[0]
+    nbytes = engine.device_bytes()
+    engine.release_bands()
+    assert engine.device_bytes() == nbytes
+    with pytest.raises(RifrafError):
+        engine.score_dense([sl])
+    engine.realign(sl[::-1], sl[::-1], 0, [9] * 6, RF_FWD | RF_BWD)   # other order: other offsets
+    d2 = engine.score_dense([sl])[0]
+    np.testing.assert_array_equal(d1, d2)
+    ref, _ = oracle.cpu_pass(t, seqs, nthreads=2)
+    np.testing.assert_array_equal(d2[1:, 5:], ref[1:, 5:])
+    assert engine.device_bytes() == nbytes
+
+
 def test_plan_cache_follows_slot_contents(engine):
     """rf_score_dense reuses its descriptors only while every scored band
     still describes the same alignment: re-filling the same slots with other

@@ -129,3 +129,86 @@ def test_threaded_power10_is_elementwise():
     from rifraf_amd.model import _power10
     x = -np.random.default_rng(12).uniform(0, 40, (700_001, 3))
     np.testing.assert_array_equal(_power10(x), np.power(10.0, x))
+
+
+def _qv_inputs(rng, n=30, stacked=False):
+    from types import SimpleNamespace
+    states, dense, sums = [], [], []
+    ms = rng.integers(1, 400, n)
+    ms[:3] = [1, 2, 1500]
+    for m in ms:
+        cons = rng.integers(0, 4, m).astype(np.uint8)
+        score = -float(rng.uniform(50, 500))
+        d = score + rng.uniform(-30, 2, (m + 1, 9))
+        d[0, :5] = np.nan
+        d[1 + np.arange(m), cons] = np.nan          # not a proposal: ignored
+        d[rng.random((m + 1, 9)) < 0.01] = -np.inf  # empty summax columns
+        d[0, :5] = np.nan
+        states.append(SimpleNamespace(consensus=cons, score=score))
+        dense.append(d)
+        s = -rng.uniform(0, 60, (m, 4))
+        s[rng.random((m, 4)) < 0.01] = 0.0
+        sums.append(s)
+    if stacked:   # consecutive views of one array, as engine.score_dense returns
+        D, S = np.concatenate(dense), np.concatenate(sums)
+        at, bt, dense, sums = 0, 0, [], []
+        for m in ms:
+            dense.append(D[at:at + m + 1])
+            sums.append(S[bt:bt + m])
+            at += m + 1
+            bt += m
+    return states, dense, sums
+
+
+def test_qvs_many_lib_equals_qvs_many():
+    """The C++ passes of the QV post-processing (rf_host_qv_prep /
+    rf_host_qv_finish around numpy's power) equal qvs_many bit for bit,
+    for stacked views and separate arrays, with -Inf totals and zero sums."""
+    from rifraf_amd.model import qvs_many, qvs_many_lib
+    for stacked in (False, True):
+        states, dense, sums = _qv_inputs(np.random.default_rng(18), stacked=stacked)
+        got = qvs_many_lib(states, dense, sums)
+        exp = qvs_many(states, dense, sums)
+        for (ep, ap), (e, a) in zip(got, exp):
+            for f in ("sub", "dele", "ins"):
+                assert getattr(ep, f).tobytes() == getattr(e, f).tobytes(), f
+            assert ap.tobytes() == a.tobytes()
+
+
+def test_qvs_many_lib_errors():
+    import pytest
+
+    from rifraf_amd.engine import RifrafError
+    from rifraf_amd.model import qvs_many, qvs_many_lib
+    states, dense, sums = _qv_inputs(np.random.default_rng(19), n=5)
+    dense[3][4, 6] = np.nan
+    for f in (qvs_many, qvs_many_lib):
+        with pytest.raises(RifrafError, match="failed to compute a valid score"):
+            f(states, dense, sums)
+
+
+def test_many_coded_equals_constructor():
+    """many_coded's lazily built tables, est_n_errors and logsumexp10 equal the
+    per-sequence constructor's and model.logsumexp10's, bit for bit."""
+    from rifraf_amd.model import logsumexp10
+    from rifraf_amd.rifrafsequences import CodedRifrafSequence
+    rng = np.random.default_rng(21)
+    ph = [rng.integers(0, 94, int(n)).astype(np.int8) for n in rng.integers(1, 3000, 60)]
+    ph[0][:] = 0                                      # all match scores -Inf
+    ph += [np.array([7], np.int8), rng.integers(0, 94, 1025).astype(np.int8)]
+    seqs = [rng.integers(0, 4, len(p)).astype(np.uint8) for p in ph]
+    off = np.zeros(len(ph) + 1, np.int64)
+    np.cumsum([len(p) for p in ph], out=off[1:])
+    sc = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0))
+    objs, tabs, lse = RifrafSequence.many_coded(seqs, np.concatenate(ph), off, 9, sc)
+    full = tabs["source"].full()
+    for k, (o, s, p) in enumerate(zip(objs, seqs, ph)):
+        assert isinstance(o, CodedRifrafSequence)
+        e = RifrafSequence(s, p, 9, sc)
+        assert o.est_n_errors == e.est_n_errors
+        assert lse[k] == logsumexp10(e.match_scores)
+        for f in ("error_log_p", "match_scores", "mismatch_scores", "ins_scores", "del_scores"):
+            assert getattr(o, f).tobytes() == getattr(e, f).tobytes(), f
+        assert full["match"][off[k]:off[k + 1]].tobytes() == e.match_scores.tobytes()
+        assert full["del"][off[k] + k:off[k + 1] + k + 1].tobytes() == e.del_scores.tobytes()
+        assert len(o) == len(e) and o.bandwidth == 9 and not o.bandwidth_fixed
