@@ -259,10 +259,56 @@ int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *param
                     const int32_t *slot_base, const int32_t *tpl_id, const uint8_t *cons,
                     const int64_t *cons_off, double *out_score, int32_t *out_iters,
                     int32_t *out_status, int64_t *out_len, int32_t *out_bw);
+/* Reference-guided clusters (FRAME and REFINE, model.jl:937-995, 499-562):
+ * rf_rifraf_batch with, per cluster, a reference record (ref_seq < 0: none).
+ * The stage machine then runs INIT -> FRAME -> REFINE like rifraf():
+ * edit_distance at FRAME entry (align.jl:253-260, on edit_seq: the
+ * reference's copy with log p = -1 and ErrorModel(1, 1, 1) scores, uploaded
+ * by the caller), has_single_indels / single_indel_proposals (the reference
+ * aligned to the consensus in scratch_slot), seeded all_proposals, scoring
+ * with the reference's codon moves (ref_slot) and the reference term of
+ * rescore!.  The two host steps that need the caller's transcendental
+ * functions go through `cb`:
+ *   event 0 (FRAME entry), value = ref_error_rate: build the reference with
+ *     log p = log10(value) and the current reference scores, upload it at
+ *     ref_seq, write *thr = cquantile(Poisson(est_n_errors), bandwidth_pvalue);
+ *   event 1 (penalty increase), value = n_ref_indel_mults: rescale the
+ *     reference's indel scores by ref_indel_mult^n (model.jl:978-985) and
+ *     upload it again.
+ * cb returns 0, or nonzero to fail the cluster.  Scope as rf_rifraf_batch,
+ * plus: a cluster with a reference and do_refine needs batch_size >= #reads
+ * (REFINE resamples at random otherwise). */
+typedef struct rf_batch_ref_params {
+    int32_t do_frame, do_refine, seed_indels, indel_correction_only;
+    int32_t max_ref_indel_mults, pad;
+    double ref_error_mult;
+} rf_batch_ref_params;
+typedef struct rf_batch_ref {
+    int32_t ref_seq, edit_seq, ref_slot, scratch_slot;
+    int64_t ref_off, ref_len;   /* the reference's bases in ref_bases */
+} rf_batch_ref;
+typedef int (*rf_ref_callback)(void *user, int32_t cluster, int32_t event, double value, double *thr);
+int rf_rifraf_batch_ref(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
+                        const rf_batch_ref_params *ref_params, const int32_t *read_off,
+                        const int32_t *read_seq, const int32_t *read_len, const double *threshold,
+                        const int32_t *fixed_off, const int32_t *fixed, const int32_t *slot_base,
+                        const int32_t *tpl_id, const uint8_t *cons, const int64_t *cons_off,
+                        const rf_batch_ref *refs, const uint8_t *ref_bases, rf_ref_callback cb,
+                        void *cb_user, double *out_score, int32_t *out_iters, int32_t *out_status,
+                        int64_t *out_len, int32_t *out_bw);
+/* Stage record of cluster c of the last batch: iterations per stage (INIT,
+ * FRAME, REFINE), the stage of each recorded consensus (1/2/3, as many as
+ * rf_batch_fetch's stages), the reference's final bandwidth (negated once
+ * fixed; 0 without one), A_ref[end,end], n_ref_indel_mults and the length
+ * of the final batch (what rf_batch_fetch's `batch` receives: REFINE's
+ * batch holds every read even when INIT / FRAME used the fixed batch). */
+int rf_batch_fetch_ref(rf_ctx *ctx, int32_t cluster, int32_t *stage_iters, int8_t *stage_of,
+                       int32_t *ref_bw, double *ref_score, int32_t *n_ref_indel_mults, int32_t *batch_len);
 /* Cluster c of the last rf_rifraf_batch: consensus (out_len[c] bytes), the
  * consensus at each INIT iteration (stage_len[i] bytes each, concatenated
- * in `stages`), the final batch (local read indices) and the error message
- * of a failed cluster.  Any output may be NULL. */
+ * in `stages`), the final batch (local read indices; room for every read of
+ * the cluster, or rf_batch_fetch_ref's batch_len) and the error message of a
+ * failed cluster.  Any output may be NULL. */
 int rf_batch_fetch(rf_ctx *ctx, int32_t cluster, uint8_t *cons, int64_t *stage_len, uint8_t *stages,
                    int32_t *batch, char *err, int64_t err_cap);
 /* Free the context's stored batch results. */

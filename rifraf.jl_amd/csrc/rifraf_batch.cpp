@@ -64,27 +64,44 @@ struct Read {
     double thr = 0.0;   // cquantile(Poisson(est_n_errors), bandwidth_pvalue)
 };
 
+// stages (model.jl:1-5)
+constexpr int ST_INIT = 1, ST_FRAME = 2, ST_REFINE = 3, ST_SCORE = 4;
+
 struct Clu {
     int32_t r0 = 0, nreads = 0;   // reads [r0, r0 + nreads) of the read table
     int32_t slot0 = 0, tpl = 0;
     std::vector<uint8_t> cons, old_cons;
-    std::vector<std::vector<uint8_t>> stages;   // consensus at each INIT iteration
+    std::vector<std::vector<uint8_t>> stages;   // consensus at each iteration
+    std::vector<int8_t> stage_of;               // ... and the stage it ran in
     std::vector<int32_t> batch;                 // batch_seqs (local read indices)
     int32_t batch_size = 0, base_batch_size = 0;
     int32_t n_slots = 0;
     std::vector<double> slot_scores;
     double score = -INF, old_score = -INF;
     bool realign_As = true, realign_Bs = true, penalties_increased = false;
-    int32_t iters = 0;
-    bool converged = false, failed = false;
+    int32_t iters = 0;                          // all stages
+    int32_t stage = ST_INIT, stage_iters[3] = {0, 0, 0};
+    bool converged = false, failed = false, done = false;
     std::string err;
     std::vector<Prop> props;
     std::vector<Cand> chosen;
+    // reference (model.jl:167-193): its read-table entry (sequence id, length,
+    // bandwidth, threshold), A/B slot, scratch slot for one-off alignments,
+    // the edit-distance copy of its sequence (align.jl:253-260) and its bases
+    bool has_ref = false;
+    int32_t ref_read = -1, ref_slot = -1, scratch_slot = -1, edit_seq = -1;
+    std::vector<uint8_t> ref_bases;
+    double ref_score = -INF;
+    int32_t n_ref_indel_mults = 0;
+    std::vector<Prop> seeds;                    // FRAME indel seeds
 };
 
 struct Driver {
     rf_ctx *ctx;
     rf_batch_params P;
+    rf_batch_ref_params RP{};
+    rf_ref_callback cb = nullptr;
+    void *cb_user = nullptr;
     std::vector<Read> reads;
     std::vector<Clu> clu;
     std::vector<int32_t> fixed_off, fixed;   // the caller's fixed batches
@@ -135,7 +152,7 @@ struct Driver {
     // ---------------- resample! (model.jl:1038-1066), deterministic cases
     void resample(Clu &C, int c)
     {
-        if (P.batch_fixed) {
+        if (P.batch_fixed && (C.stage == ST_INIT || C.stage == ST_FRAME)) {
             C.batch.assign(fixed.begin() + fixed_off[c], fixed.begin() + fixed_off[c + 1]);
         } else {
             // batch_size >= #reads (the caller guarantees it): every read
@@ -147,23 +164,31 @@ struct Driver {
 
     // ---------------- smart_forward_moves! (model.jl:643-672) over the
     // batch slots of every cluster in `cs`, then A[end,end] -> slot_scores.
+    // use_ref (model.jl:617-628) inside the stage machine: FRAME only
+    bool ref_on(const Clu &C) const { return C.has_ref && C.stage == ST_FRAME; }
+
     int smart_forward(const std::vector<int> &cs)
     {
         struct Job {
-            int c, k;
+            int c, k;          // k = batch index, -1 = the reference
+            int32_t slot, ridx;
             int32_t bw, max_bw;
             int64_t old_err, n_err;
         };
         std::vector<Job> jobs;
         for (int c : cs) {
             const Clu &C = clu[c];
-            for (int k = 0; k < (int)C.batch.size(); ++k) {
-                const Read &R = reads[C.r0 + C.batch[k]];
+            auto add = [&](int k, int32_t slot, int32_t ridx) {
+                const Read &R = reads[ridx];
                 const int32_t mx = R.fixed ? R.bw
                                            : std::min<int64_t>(std::min<int64_t>((int64_t)R.bw * 32, (int64_t)C.cons.size()),
                                                                (int64_t)R.len);
-                jobs.push_back({c, k, R.bw, mx, INT64_MAX, INT64_MAX});
-            }
+                jobs.push_back({c, k, slot, ridx, R.bw, mx, INT64_MAX, INT64_MAX});
+            };
+            for (int k = 0; k < (int)C.batch.size(); ++k)
+                add(k, C.slot0 + k, C.r0 + C.batch[k]);
+            if (ref_on(C))   // model.jl:695-698: the reference after the batch (independent slots)
+                add(-1, C.ref_slot, C.ref_read);
         }
         std::vector<double> score(jobs.size());
         std::vector<int> pending(jobs.size());
@@ -174,10 +199,9 @@ struct Driver {
         while (!pending.empty()) {
             sl.clear(), sq.clear(), tp.clear(), bw.clear();
             for (int j : pending) {
-                const Clu &C = clu[jobs[j].c];
-                sl.push_back(C.slot0 + jobs[j].k);
-                sq.push_back(reads[C.r0 + C.batch[jobs[j].k]].seq);
-                tp.push_back(C.tpl);
+                sl.push_back(jobs[j].slot);
+                sq.push_back(reads[jobs[j].ridx].seq);
+                tp.push_back(clu[jobs[j].c].tpl);
                 bw.push_back(jobs[j].bw);
             }
             out.resize(pending.size());
@@ -190,15 +214,14 @@ struct Driver {
             for (size_t i = 0; i < pending.size(); ++i) {
                 const int j = pending[i];
                 score[j] = out[i];
-                const Read &R = reads[clu[jobs[j].c].r0 + clu[jobs[j].c].batch[jobs[j].k]];
-                if (!(R.fixed || jobs[j].bw >= jobs[j].max_bw))
+                if (!(reads[jobs[j].ridx].fixed || jobs[j].bw >= jobs[j].max_bw))
                     check.push_back(j);
             }
             if (check.empty())
                 break;
             sl.clear();
             for (int j : check)
-                sl.push_back(clu[jobs[j].c].slot0 + jobs[j].k);
+                sl.push_back(jobs[j].slot);
             nerr.resize(check.size());
             if (int e = timed(T_BT, [&] {
                     return rf_backtrace(ctx, (int32_t)check.size(), sl.data(), nullptr, nullptr, nullptr, nerr.data());
@@ -207,7 +230,7 @@ struct Driver {
             std::vector<int> nxt;
             for (size_t i = 0; i < check.size(); ++i) {
                 Job &J = jobs[check[i]];
-                const Read &R = reads[clu[J.c].r0 + clu[J.c].batch[J.k]];
+                const Read &R = reads[J.ridx];
                 J.old_err = J.n_err;
                 J.n_err = nerr[i];
                 if ((double)J.n_err > R.thr && J.n_err < J.old_err) {
@@ -217,16 +240,17 @@ struct Driver {
             }
             pending.swap(nxt);
         }
-        // success: commit bandwidths (bandwidth_fixed for every batch read) and scores
+        // success: commit bandwidths (bandwidth_fixed) and scores
         for (size_t j = 0; j < jobs.size(); ++j) {
             Clu &C = clu[jobs[j].c];
-            Read &R = reads[C.r0 + C.batch[jobs[j].k]];
+            Read &R = reads[jobs[j].ridx];
             R.bw = jobs[j].bw;
-            C.slot_scores[jobs[j].k] = score[j];
+            R.fixed = true;
+            if (jobs[j].k >= 0)
+                C.slot_scores[jobs[j].k] = score[j];
+            else
+                C.ref_score = score[j];
         }
-        for (int c : cs)
-            for (int k : clu[c].batch)
-                reads[clu[c].r0 + k].fixed = true;
         return 0;
     }
 
@@ -238,6 +262,13 @@ struct Driver {
             for (int k = 0; k < (int)C.batch.size(); ++k) {
                 const Read &R = reads[C.r0 + C.batch[k]];
                 sl.push_back(C.slot0 + k);
+                sq.push_back(R.seq);
+                tp.push_back(C.tpl);
+                bw.push_back(R.bw);
+            }
+            if (ref_on(C)) {   // model.jl:710-712
+                const Read &R = reads[C.ref_read];
+                sl.push_back(C.ref_slot);
                 sq.push_back(R.seq);
                 tp.push_back(C.tpl);
                 bw.push_back(R.bw);
@@ -272,6 +303,8 @@ struct Driver {
             double total = C.slot_scores[0];   // left fold over every slot, stale ones included
             for (int k = 1; k < C.n_slots; ++k)
                 total += C.slot_scores[k];
+            if (ref_on(C))                     // rescore!: + A_ref[end, end] (model.jl:630-635)
+                total += C.ref_score;
             C.score = total;
         }
     }
@@ -281,12 +314,13 @@ struct Driver {
     bool check_score(Clu &C, int c, std::vector<int> &redo)
     {
         const bool all = C.batch_size == C.nreads;
-        if (!C.penalties_increased && all && C.iters > 1) {
+        const int32_t sit = C.stage_iters[C.stage - 1];
+        if (!C.penalties_increased && all && sit > 1) {
             if (C.score == C.old_score)
                 return false;
         }
         const double rel = (C.score - C.old_score) / C.old_score;   // IEEE: +-Inf / NaN, never a trap
-        if (rel > P.batch_threshold && !C.penalties_increased && C.batch_size < C.nreads && C.iters > 1) {
+        if (rel > P.batch_threshold && !C.penalties_increased && C.batch_size < C.nreads && sit > 1) {
             C.batch_size = std::min(C.batch_size + C.base_batch_size, C.nreads);
             resample(C, c);
             C.realign_As = true;
@@ -296,30 +330,132 @@ struct Driver {
         return true;
     }
 
-    // ---------------- all_proposals(STAGE_INIT, consensus) without seeds (model.jl:401-456)
-    static void all_proposals_init(const std::vector<uint8_t> &t, std::vector<Prop> &out)
+    // ---------------- all_proposals (model.jl:401-456): indel seeds widen to
+    // +-CODON_LENGTH positions; subs unless FRAME with indel_correction_only;
+    // indels in INIT / FRAME (SCORE does not reach the driver)
+    void all_proposals(int stage, const std::vector<uint8_t> &t, const std::vector<Prop> &seeds,
+                       std::vector<Prop> &out) const
     {
-        out.clear();
-        for (int b = 0; b < 4; ++b)
-            out.push_back({INS, 0, b});
-        for (int j = 1; j <= (int)t.size(); ++j) {
-            for (int b = 0; b < 4; ++b)
-                if (t[j - 1] != b)
-                    out.push_back({SUB, j, b});
-            out.push_back({DEL, j, 0});
-            for (int b = 0; b < 4; ++b)
-                out.push_back({INS, j, b});
+        const int len = (int)t.size(), nb = 3;
+        std::vector<uint8_t> ins_pos(len + 1, 0), del_pos(len + 1, 0);
+        for (const Prop &p : seeds) {
+            if (p.kind == INS) {
+                for (int j = std::max(p.pos - nb, 0); j <= std::min(p.pos + nb, len); ++j)
+                    ins_pos[j] = 1;
+            } else {
+                for (int j = std::max(p.pos - nb, 1); j <= std::min(p.pos + nb, len); ++j)
+                    del_pos[j] = 1;
+            }
         }
+        const bool do_subs = stage != ST_FRAME || !RP.indel_correction_only;
+        const bool do_indels = stage == ST_INIT || stage == ST_FRAME;
+        const bool no_seeds = seeds.empty();
+        out.clear();
+        if (do_indels)
+            for (int b = 0; b < 4; ++b)
+                out.push_back({INS, 0, b});
+        for (int j = 1; j <= len; ++j) {
+            if (do_subs)
+                for (int b = 0; b < 4; ++b)
+                    if (t[j - 1] != b)
+                        out.push_back({SUB, j, b});
+            if (do_indels) {
+                if (no_seeds || del_pos[j])
+                    out.push_back({DEL, j, 0});
+                if (no_seeds || ins_pos[j])
+                    for (int b = 0; b < 4; ++b)
+                        out.push_back({INS, j, b});
+            }
+        }
+    }
+
+    // ---------------- the reference aligned to the consensus (align_moves,
+    // align.jl:337-344; model.jl:532-562): forward fill of the reference
+    // (rows) against the consensus in the cluster's scratch slot with the
+    // reference's bandwidth, then the backtrace moves
+    int ref_moves(const std::vector<int> &cs, bool skew, std::vector<std::vector<int8_t>> &mv)
+    {
+        std::vector<int32_t> sl, sq, tp, bw, nm(cs.size());
+        std::vector<int64_t> moff{0};
+        for (int c : cs) {
+            const Clu &C = clu[c];
+            const Read &R = reads[C.ref_read];
+            sl.push_back(C.scratch_slot);
+            sq.push_back(R.seq);
+            tp.push_back(C.tpl);
+            bw.push_back(R.bw);
+            moff.push_back(moff.back() + R.len + (int64_t)C.cons.size());
+        }
+        if (int e = timed(T_FWD, [&] {
+                return rf_realign(ctx, (int32_t)cs.size(), sl.data(), sq.data(), tp.data(), bw.data(),
+                                  RF_FWD | (skew ? RF_SKEW : 0), nullptr);
+            }))
+            return e;
+        std::vector<int8_t> moves((size_t)std::max<int64_t>(moff.back(), 1));
+        if (int e = timed(T_BT, [&] {
+                return rf_backtrace(ctx, (int32_t)cs.size(), sl.data(), moves.data(), moff.data(), nm.data(), nullptr);
+            }))
+            return e;
+        mv.resize(cs.size());
+        for (size_t i = 0; i < cs.size(); ++i)
+            mv[i].assign(moves.begin() + moff[i], moves.begin() + moff[i] + nm[i]);
+        return 0;
+    }
+
+    // has_single_indels (model.jl:532-536) of clusters `cs` -> flags
+    void has_single_indels(std::vector<int> &cs, std::vector<uint8_t> &flag)
+    {
+        flag.assign(clu.size(), 0);
+        batched(cs, [&](const std::vector<int> &s) {
+            std::vector<std::vector<int8_t>> mv;
+            if (int e = ref_moves(s, false, mv))
+                return e;
+            for (size_t i = 0; i < s.size(); ++i)
+                for (int8_t m : mv[i])
+                    flag[s[i]] |= (m == 2 || m == 3);   // TRACE_INSERT / TRACE_DELETE
+            return 0;
+        });
+    }
+
+    // single_indel_proposals (model.jl:538-562) -> clu[c].seeds
+    void single_indel_proposals(std::vector<int> &cs)
+    {
+        batched(cs, [&](const std::vector<int> &s) {
+            std::vector<std::vector<int8_t>> mv;
+            if (int e = ref_moves(s, true, mv))
+                return e;
+            for (size_t i = 0; i < s.size(); ++i) {
+                Clu &C = clu[s[i]];
+                C.seeds.clear();
+                int cons_idx = 0, ref_idx = 0;
+                for (int8_t m : mv[i]) {
+                    switch (m) {
+                    case 1: ++cons_idx, ++ref_idx; break;                                   // MATCH
+                    case 2: ++ref_idx; C.seeds.push_back({INS, cons_idx, C.ref_bases[ref_idx - 1]}); break;
+                    case 3: ++cons_idx; C.seeds.push_back({DEL, cons_idx, 0}); break;       // DELETE
+                    case 4: ref_idx += 3; break;                                             // CODON_INSERT
+                    case 5: cons_idx += 3; break;                                            // CODON_DELETE
+                    default: break;
+                    }
+                }
+            }
+            return 0;
+        });
     }
 
     // ---------------- get_candidates (model.jl:499-526) for `cs`; returns the
     // candidates (score > state.score, in proposal order) per cluster
     void get_candidates(std::vector<int> cs, std::vector<std::vector<Cand>> &cands)
     {
-        if (P.do_alignment_proposals) {
-            // alignment_proposals (model.jl:483-497): the device union mask of the batch
-            // backtraces, read out in (pos, kind, base) order
-            batched(cs, [&](const std::vector<int> &s) {
+        // alignment_proposals (model.jl:483-497) in INIT (with indels) and
+        // REFINE (substitutions only): the device union mask of the batch
+        // backtraces, read out in (pos, kind, base) order
+        for (int indels = 1; indels >= 0; --indels) {
+            std::vector<int> ap;
+            for (int c : cs)
+                if (P.do_alignment_proposals && clu[c].stage == (indels ? ST_INIT : ST_REFINE))
+                    ap.push_back(c);
+            batched(ap, [&](const std::vector<int> &s) {
                 std::vector<int32_t> off{0}, sl;
                 int64_t rows = 0;
                 for (int c : s) {
@@ -330,7 +466,8 @@ struct Driver {
                 }
                 std::vector<uint8_t> mask((size_t)rows * 9);
                 if (int e = timed(T_PROPS, [&] {
-                        return rf_alignment_proposals(ctx, (int32_t)s.size(), off.data(), sl.data(), 1, mask.data());
+                        return rf_alignment_proposals(ctx, (int32_t)s.size(), off.data(), sl.data(), indels,
+                                                      mask.data());
                     }))
                     return e;
                 static const int order[9][3] = {{0, SUB, 0}, {1, SUB, 1}, {2, SUB, 2}, {3, SUB, 3}, {5, INS, 0},
@@ -348,11 +485,15 @@ struct Driver {
                 }
                 return 0;
             });
-        } else {
-            for (int c : cs)
-                all_proposals_init(clu[c].cons, clu[c].props);
         }
-        // score_proposals (model.jl:385-399): batch fold, no reference
+        for (int c : cs) {
+            Clu &C = clu[c];
+            if (C.failed || ((C.stage == ST_INIT || C.stage == ST_REFINE) && P.do_alignment_proposals))
+                continue;
+            static const std::vector<Prop> none;
+            all_proposals(C.stage, C.cons, C.stage == ST_FRAME ? C.seeds : none, C.props);
+        }
+        // score_proposals (model.jl:385-399): batch fold, + the reference in FRAME
         std::vector<int> sc;
         for (int c : cs)
             if (!clu[c].failed && !clu[c].props.empty())
@@ -366,7 +507,7 @@ struct Driver {
                 for (int k = 0; k < (int)C.batch.size(); ++k)
                     sl.push_back(C.slot0 + k);
                 off.push_back((int32_t)sl.size());
-                ref.push_back(-1);
+                ref.push_back(C.stage == ST_FRAME ? C.ref_slot : -1);
                 for (const Prop &p : C.props) {
                     kind.push_back((uint8_t)p.kind);
                     pos.push_back(p.pos);
@@ -513,6 +654,113 @@ struct Driver {
     }
     static constexpr double DBL_EPSILON_ = std::numeric_limits<double>::epsilon();
 
+    // ---------------- finish_stage! (model.jl:937-995)
+    void finish_stage(std::vector<int> cs)
+    {
+        std::vector<int> to_frame, in_frame;
+        for (int c : cs) {
+            Clu &C = clu[c];
+            if (C.failed)
+                continue;
+            if (C.stage == ST_INIT) {
+                if (!C.has_ref || !RP.do_frame)
+                    C.converged = true;
+                else
+                    to_frame.push_back(c);
+            } else if (C.stage == ST_FRAME) {
+                in_frame.push_back(c);
+            } else if (C.stage == ST_REFINE) {
+                C.converged = true;
+            } else {
+                fail_cluster(c, "  invalid stage: " + std::to_string(C.stage));
+            }
+        }
+        std::vector<uint8_t> flag;
+        if (!to_frame.empty()) {
+            // edit_distance(consensus, reference) (align.jl:253-260): the errors of
+            // the skewed alignment of the reference's edit-distance copy (log p
+            // -1, ErrorModel(1, 1, 1) scores) at bandwidth ceil(min(len) * 0.5)
+            std::vector<int64_t> ed(clu.size(), 0);
+            batched(to_frame, [&](const std::vector<int> &s) {
+                std::vector<int32_t> sl, sq, tp, bw, nerr(s.size());
+                for (int c : s) {
+                    const Clu &C = clu[c];
+                    sl.push_back(C.scratch_slot);
+                    sq.push_back(C.edit_seq);
+                    tp.push_back(C.tpl);
+                    const int64_t mn = std::min<int64_t>((int64_t)C.cons.size(), (int64_t)C.ref_bases.size());
+                    bw.push_back((int32_t)((mn + 1) / 2));
+                }
+                if (int e = timed(T_FWD, [&] {
+                        return rf_realign(ctx, (int32_t)s.size(), sl.data(), sq.data(), tp.data(), bw.data(),
+                                          RF_FWD | RF_SKEW, nullptr);
+                    }))
+                    return e;
+                if (int e = timed(T_BT, [&] {
+                        return rf_backtrace(ctx, (int32_t)s.size(), sl.data(), nullptr, nullptr, nullptr, nerr.data());
+                    }))
+                    return e;
+                for (size_t i = 0; i < s.size(); ++i)
+                    ed[s[i]] = nerr[i];
+                return 0;
+            });
+            std::vector<int> entered;
+            for (int c : to_frame) {
+                Clu &C = clu[c];
+                C.stage = ST_FRAME;
+                double rate = (double)ed[c] / (double)std::max(C.ref_bases.size(), C.cons.size());
+                rate *= RP.ref_error_mult;
+                rate = std::min(std::max(rate, 1e-10), 0.5);
+                double thr = 0.0;
+                // the caller builds the reference with log p = log10(rate) and
+                // uploads it (rifrafsequences.jl constructor), returns its threshold
+                if (cb(cb_user, c, 0, rate, &thr) != 0) {
+                    fail_cluster(c, "reference callback failed (FRAME entry)");
+                    continue;
+                }
+                Read &R = reads[C.ref_read];
+                R.bw = P.bandwidth;
+                R.fixed = false;
+                R.thr = thr;
+                entered.push_back(c);
+            }
+            has_single_indels(entered, flag);
+            for (int c : entered)
+                if (!clu[c].failed && !flag[c])
+                    clu[c].converged = true;
+        }
+        if (!in_frame.empty()) {
+            has_single_indels(in_frame, flag);
+            for (int c : in_frame) {
+                Clu &C = clu[c];
+                if (C.failed)
+                    continue;
+                if (!flag[c]) {
+                    C.stage = ST_REFINE;
+                } else if (C.n_ref_indel_mults == RP.max_ref_indel_mults) {
+                    C.stage = ST_REFINE;   // single indels remain, penalty limit reached
+                } else {
+                    C.penalties_increased = true;
+                    if (C.n_ref_indel_mults < RP.max_ref_indel_mults) {
+                        C.n_ref_indel_mults += 1;
+                    } else {
+                        fail_cluster(c, "Tried to illegally increase n_ref_indel_mults");
+                        continue;
+                    }
+                    double thr = 0.0;
+                    // the caller rescales the reference's indel scores and re-uploads it
+                    if (cb(cb_user, c, 1, (double)C.n_ref_indel_mults, &thr) != 0)
+                        fail_cluster(c, "reference callback failed (penalty increase)");
+                }
+            }
+        }
+    }
+
+    bool enabled(int stage) const
+    {
+        return stage == ST_INIT || (stage == ST_FRAME && RP.do_frame) || (stage == ST_REFINE && RP.do_refine);
+    }
+
     void run()
     {
         std::vector<int> live;
@@ -520,15 +768,25 @@ struct Driver {
             live.push_back(c);
         std::vector<std::vector<Cand>> cands(clu.size());
         for (int it = 1; it <= P.max_iters && !live.empty(); ++it) {
+            std::vector<int> act;
             for (int c : live) {
                 Clu &C = clu[c];
+                while (C.stage < ST_SCORE && !enabled(C.stage))
+                    ++C.stage;
+                if (C.stage == ST_SCORE) {
+                    C.done = true;
+                    continue;
+                }
                 C.iters += 1;
+                C.stage_iters[C.stage - 1] += 1;
                 C.stages.push_back(C.cons);
+                C.stage_of.push_back((int8_t)C.stage);
                 resample(C, c);
+                act.push_back(c);
             }
-            realign_rescore(live);
+            realign_rescore(act);
             std::vector<int> ok, redo, fin;
-            for (int c : live) {
+            for (int c : act) {
                 if (clu[c].failed)
                     continue;
                 if (check_score(clu[c], c, redo))
@@ -538,7 +796,7 @@ struct Driver {
             }
             if (!redo.empty())
                 realign_rescore(redo);
-            std::vector<int> gc;
+            std::vector<int> gc, sd;
             for (int c : ok) {
                 Clu &C = clu[c];
                 if (C.failed)
@@ -546,7 +804,12 @@ struct Driver {
                 C.old_score = C.score;
                 C.penalties_increased = false;
                 gc.push_back(c);
+                if (C.stage == ST_FRAME && RP.seed_indels)
+                    sd.push_back(c);
+                else
+                    C.seeds.clear();
             }
+            single_indel_proposals(sd);
             for (int c : gc)
                 cands[c].clear();
             get_candidates(gc, cands);
@@ -559,12 +822,10 @@ struct Driver {
                 (cands[c].empty() ? fin : hc).push_back(c);
             }
             handle_candidates(hc, cands);
-            // finish_stage! (model.jl:937-948): no reference -> converged
-            for (int c : fin)
-                clu[c].converged = true;
+            finish_stage(fin);
             std::vector<int> nl;
-            for (int c : live)
-                if (!clu[c].failed && !clu[c].converged)
+            for (int c : act)
+                if (!clu[c].failed && !clu[c].converged && !clu[c].done)
                     nl.push_back(c);
             live.swap(nl);
         }
@@ -600,6 +861,20 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
                                const int64_t *cons_off, double *out_score, int32_t *out_iters,
                                int32_t *out_status, int64_t *out_len, int32_t *out_bw)
 {
+    return rf_rifraf_batch_ref(ctx, nclusters, params, nullptr, read_off, read_seq, read_len, threshold, fixed_off,
+                               fixed, slot_base, tpl_id, cons, cons_off, nullptr, nullptr, nullptr, nullptr,
+                               out_score, out_iters, out_status, out_len, out_bw);
+}
+
+extern "C" int rf_rifraf_batch_ref(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
+                                   const rf_batch_ref_params *ref_params, const int32_t *read_off,
+                                   const int32_t *read_seq, const int32_t *read_len, const double *threshold,
+                                   const int32_t *fixed_off, const int32_t *fixed, const int32_t *slot_base,
+                                   const int32_t *tpl_id, const uint8_t *cons, const int64_t *cons_off,
+                                   const rf_batch_ref *refs, const uint8_t *ref_bases, rf_ref_callback cb,
+                                   void *cb_user, double *out_score, int32_t *out_iters, int32_t *out_status,
+                                   int64_t *out_len, int32_t *out_bw)
+{
     if (!ctx)
         return RF_ERR_ARG;
     if (nclusters < 0 || !params || (nclusters > 0 && (!read_off || !read_seq || !read_len || !threshold ||
@@ -607,7 +882,15 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
         return rf_internal_fail(ctx, RF_ERR_ARG, "rf_rifraf_batch: bad arguments");
     if (params->batch_fixed && (!fixed_off || !fixed))
         return rf_internal_fail(ctx, RF_ERR_ARG, "rf_rifraf_batch: batch_fixed needs fixed_off and fixed");
-    Driver D{ctx, *params, {}, {}, {}, {}};
+    if (refs && (!ref_params || !ref_bases || !cb))
+        return rf_internal_fail(ctx, RF_ERR_ARG, "rf_rifraf_batch_ref: references need ref_params, ref_bases and cb");
+    Driver D{};
+    D.ctx = ctx;
+    D.P = *params;
+    if (ref_params)
+        D.RP = *ref_params;
+    D.cb = cb;
+    D.cb_user = cb_user;
     const int32_t nreads = nclusters > 0 ? read_off[nclusters] : 0;
     D.reads.resize(nreads);
     for (int32_t r = 0; r < nreads; ++r)
@@ -627,11 +910,26 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
         // initial_state (model.jl:564-615)
         const int32_t bs = params->batch_size > 1 ? std::min(params->batch_size, C.nreads) : C.nreads;
         C.batch_size = C.base_batch_size = bs;
+        C.has_ref = refs && refs[c].ref_seq >= 0;
+        if (C.has_ref) {
+            const rf_batch_ref &F = refs[c];
+            C.ref_bases.assign(ref_bases + F.ref_off, ref_bases + F.ref_off + F.ref_len);
+            C.ref_slot = F.ref_slot;
+            C.scratch_slot = F.scratch_slot;
+            C.edit_seq = F.edit_seq;
+            C.ref_read = (int32_t)D.reads.size();   // the reference's read-table entry (bandwidth, threshold)
+            D.reads.push_back({F.ref_seq, (int32_t)F.ref_len, params->bandwidth, false, 0.0});
+        }
         // outside the native driver's scope (the caller checks first)
+        const bool ref_ok = !C.has_ref || (refs[c].ref_len > 0 && refs[c].edit_seq >= 0 && refs[c].ref_slot >= 0 &&
+                                           refs[c].scratch_slot >= 0);
+        const bool refine_random = C.has_ref && D.RP.do_refine && bs < C.nreads;   // REFINE resamples
         const char *why = C.nreads < 1 ? "no reads"
                           : C.cons.empty() ? "empty consensus"
                           : (!params->batch_fixed && bs < C.nreads) ? "a random batch smaller than the read count"
                           : (params->batch_fixed && fixed_off[c + 1] - fixed_off[c] < 1) ? "an empty fixed batch"
+                          : !ref_ok ? "an incomplete reference record"
+                          : refine_random ? "a REFINE stage with a random batch"
                           : nullptr;
         if (why)
             return rf_internal_fail(ctx, RF_ERR_ARG,
@@ -675,6 +973,31 @@ extern "C" int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_pa
     if (out_bw)
         for (int32_t r = 0; r < nreads; ++r)
             out_bw[r] = R.reads[r].bw * (R.reads[r].fixed ? -1 : 1);
+    return 0;
+}
+
+extern "C" int rf_batch_fetch_ref(rf_ctx *ctx, int32_t cluster, int32_t *stage_iters, int8_t *stage_of,
+                                  int32_t *ref_bw, double *ref_score, int32_t *n_ref_indel_mults,
+                                  int32_t *batch_len)
+{
+    if (!ctx)
+        return RF_ERR_ARG;
+    BatchResult &R = result_of(ctx);
+    if (cluster < 0 || cluster >= (int32_t)R.clu.size())
+        return RF_ERR_ARG;
+    const Clu &C = R.clu[cluster];
+    if (stage_iters)
+        std::copy(C.stage_iters, C.stage_iters + 3, stage_iters);
+    if (stage_of)
+        std::copy(C.stage_of.begin(), C.stage_of.end(), stage_of);
+    if (ref_bw)
+        *ref_bw = C.has_ref ? R.reads[C.ref_read].bw * (R.reads[C.ref_read].fixed ? -1 : 1) : 0;
+    if (ref_score)
+        *ref_score = C.ref_score;
+    if (n_ref_indel_mults)
+        *n_ref_indel_mults = C.n_ref_indel_mults;
+    if (batch_len)
+        *batch_len = (int32_t)C.batch.size();
     return 0;
 }
 

@@ -38,6 +38,8 @@ _SIGNATURES = {
     "rf_set_templates_ids": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "rf_rifraf_batch": (c_int, [c_void_p, c_int32, c_void_p] + [c_void_p] * 14),
     "rf_batch_fetch": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
+    "rf_rifraf_batch_ref": (c_int, [c_void_p, c_int32] + [c_void_p] * 21),
+    "rf_batch_fetch_ref": (c_int, [c_void_p, c_int32] + [c_void_p] * 6),
     "rf_batch_release": (None, [c_void_p]),
     "rf_aln_error_sums": (c_int, [c_void_p, c_int32] + [c_void_p] * 7),
     "rf_host_julia_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
@@ -81,6 +83,23 @@ class BatchParams(ctypes.Structure):
     _fields_ = [("max_iters", c_int32), ("min_dist", c_int32), ("bandwidth", c_int32),
                 ("do_alignment_proposals", c_int32), ("batch_fixed", c_int32), ("batch_size", c_int32),
                 ("batch_threshold", c_double)]
+
+
+class BatchRefParams(ctypes.Structure):
+    """rf_batch_ref_params (include/rifraf_hip.h)."""
+    _fields_ = [("do_frame", c_int32), ("do_refine", c_int32), ("seed_indels", c_int32),
+                ("indel_correction_only", c_int32), ("max_ref_indel_mults", c_int32), ("pad", c_int32),
+                ("ref_error_mult", c_double)]
+
+
+class BatchRef(ctypes.Structure):
+    """rf_batch_ref (include/rifraf_hip.h): one cluster's reference record."""
+    _fields_ = [("ref_seq", c_int32), ("edit_seq", c_int32), ("ref_slot", c_int32), ("scratch_slot", c_int32),
+                ("ref_off", c_int64), ("ref_len", c_int64)]
+
+
+# rf_ref_callback: (user, cluster, event, value, thr*) -> 0 / nonzero
+RefCallback = ctypes.CFUNCTYPE(c_int, c_void_p, c_int32, c_int32, c_double, POINTER(c_double))
 
 
 _lib = None

@@ -227,21 +227,31 @@ STATS = {"launches": 0, "engine_s": 0.0, "native_s": 0.0, "score_phase_s": 0.0, 
 
 
 def native_eligible(clusters, params) -> bool:
-    """Whether rf_rifraf_batch (rifraf_batch.cpp) can run these clusters: no
-    reference (the INIT stage then ends the run, model.jl:937-948), INIT
-    enabled, and a deterministic batch -- the fixed lowest-error batch or
-    every read (random resampling stays in the Python stage machine)."""
+    """Whether rf_rifraf_batch(_ref) (rifraf_batch.cpp) can run these
+    clusters: INIT enabled and deterministic batches -- the fixed
+    lowest-error batch or every read (random resampling stays in the Python
+    stage machine).  Clusters with a reference run INIT -> FRAME -> REFINE
+    natively when REFINE (which resamples at random below the read count)
+    sees every read, and the quality pass does not use the reference."""
     if not params.do_init:
         return False
     for kw in clusters:
-        ref = kw.get("reference")
-        if ref is not None and len(ref) > 0:
-            return False
         n = len(kw["dnaseqs"])
         if n < 1:
             return False
         if not params.batch_fixed and 1 < params.batch_size < n:
             return False
+        ref = kw.get("reference")
+        if ref is not None and len(ref) > 0:
+            if params.do_score and params.use_ref_for_qvs:
+                return False
+            if params.do_refine and 1 < params.batch_size < n:
+                return False
+            try:
+                from .model import check_params
+                check_params(params.scores, ref, params)
+            except Exception:  # noqa: BLE001 -- the Python stage machine raises it per cluster
+                return False
         # an empty read or a per-base vector of the wrong length keeps the
         # cluster on the Python stage machine, whose RifrafSequence
         # constructor (rifrafsequences.jl:19-35) gives the reference's
@@ -297,6 +307,75 @@ def _logsumexp10_many(values, off, codes=None, table=None):
         else:
             out.append(math.log10(float(s[k])) + uk)
     return out
+
+
+def _native_refs(part, states, refs, params, engine, nseq, nslot):
+    """The reference records of a native wave (rf_rifraf_batch_ref), or None
+    when no cluster has a reference.  Ids past the reads: cluster j-th
+    reference at sequence nseq + j (uploaded by the callback at FRAME entry),
+    its edit-distance copy at nseq + nref + j (uploaded here: log p -1,
+    ErrorModel(1, 1, 1) scores, as align.edit_distance builds it), slots
+    nslot + 2j (A/B) and nslot + 2j + 1 (scratch).  The callback performs the
+    two host steps of finish_stage! that need the mirror's numerics."""
+    import math
+
+    from . import _lib
+    from .errormodel import ErrorModel, Scores
+    from .poisson import cquantile_poisson
+    from .rifrafsequences import RifrafSequence
+    has = [k for k, r in enumerate(refs) if len(r) > 0]
+    if not has:
+        return None
+    nref = len(has)
+    recs = (_lib.BatchRef * len(part))()
+    ref_id = {}
+    bases, at = [], 0
+    for k in range(len(part)):
+        recs[k].ref_seq = -1
+    edit = []
+    ed_scores = Scores.from_errors(ErrorModel(1.0, 1.0, 1.0))
+    for j, k in enumerate(has):
+        r = refs[k]
+        ref_id[k] = nseq + j
+        recs[k].ref_seq = nseq + j
+        recs[k].edit_seq = nseq + nref + j
+        recs[k].ref_slot = nslot + 2 * j
+        recs[k].scratch_slot = nslot + 2 * j + 1
+        recs[k].ref_off = at
+        recs[k].ref_len = len(r)
+        bases.append(np.asarray(r, np.uint8))
+        at += len(r)
+        edit.append(RifrafSequence(r, np.full(len(r), -1.0), max(1, (len(r) + 1) // 2), ed_scores))
+    engine.set_sequences(nseq + nref, edit)
+    errors = {}
+
+    def cb(user, c, event, value, thr):
+        try:
+            st = states[c]
+            if event == 0:                                   # finish_stage!, INIT -> FRAME (model.jl:944-957)
+                st.ref_error_rate = value
+                lp = np.full(len(st.reference), math.log10(st.ref_error_rate))
+                st.reference = RifrafSequence(st.reference.seq, lp, params.bandwidth, st.ref_scores)
+                engine.set_sequences(ref_id[c], [st.reference])
+                thr[0] = cquantile_poisson(st.reference.est_n_errors, params.bandwidth_pvalue)
+            else:                                            # penalty increase (model.jl:973-985)
+                st.n_ref_indel_mults = int(value)
+                mult = params.ref_indel_mult ** st.n_ref_indel_mults
+                rs = st.ref_scores
+                st.ref_scores = Scores(rs.mismatch, rs.insertion * mult, rs.deletion * mult, rs.codon_insertion,
+                                       rs.codon_deletion)
+                st.reference = RifrafSequence.rescored(st.reference, st.ref_scores)
+                engine.set_sequences(ref_id[c], [st.reference])
+            return 0
+        except Exception as e:  # noqa: BLE001 -- the driver fails the cluster
+            errors[c] = e
+            return 1
+
+    rp = _lib.BatchRefParams(int(params.do_frame), int(params.do_refine), int(params.seed_indels),
+                             int(params.indel_correction_only), int(params.max_ref_indel_mults), 0,
+                             float(params.ref_error_mult))
+    return {"params": rp, "refs": recs, "bases": np.concatenate(bases), "cb": _lib.RefCallback(cb),
+            "cb_errors": errors}
 
 
 def _wave_native(part, params, engine):
@@ -373,9 +452,11 @@ def _wave_native(part, params, engine):
             first[k] = allseqs[read_off[k] + int(np.argmax(sc))].seq.copy()
             at += nread[k]
     states = []
+    refs_in = [DNASeq(kw["reference"]) if kw.get("reference") is not None and len(kw["reference"]) > 0
+               else np.zeros(0, np.uint8) for kw in part]
     for k, kw in enumerate(part):
         cons = first[k] if k in first else DNASeq(kw["consensus"])
-        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], np.zeros(0, np.uint8), params))
+        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], refs_in[k], params))
     # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
     # The bands of every batch read in one arena reservation (growing it in
     # steps would re-allocate and compact tens of GB several times): A and B
@@ -420,9 +501,12 @@ def _wave_native(part, params, engine):
     np.cumsum([len(c) for c in cons], out=cons_off[1:])
     bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
                           int(params.batch_fixed), params.batch_size, params.batch_threshold)
+    ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
     t0 = time.perf_counter()
     res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
-                                         read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons), cons_off)
+                                         read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons),
+                                         cons_off, ref=ref)
+    cb_errors = ref["cb_errors"] if ref is not None else {}
     STATS["native_s"] += time.perf_counter() - t0
     for s, b in zip(allseqs, bw.tolist()):
         s.bandwidth = abs(b)
@@ -430,17 +514,25 @@ def _wave_native(part, params, engine):
     results, errors = [], [None] * K
     for k, (st_, r) in enumerate(zip(states, res)):
         if r["status"] == 2:
-            errors[k] = AmbiguousProposalsError() if r["error"] == "AmbiguousProposalsError" else RifrafError(r["error"])
+            errors[k] = (cb_errors[k] if k in cb_errors else AmbiguousProposalsError()
+                         if r["error"] == "AmbiguousProposalsError" else RifrafError(r["error"]))
         st_.consensus = DNASeq(r["consensus"])
         st_.score = r["score"]
-        st_.stage_iterations = [r["iters"], 0, 0, 0]
+        st_.stage_iterations = list(r["stage_iters"]) + [0]
         st_.converged = r["status"] == 1
         st_.batch_seqs = r["batch"]
         st_.n_slots = len(r["batch"])
         st_.slot_scores = [0.0] * st_.n_slots
         st_.stage = Stage.SCORE
+        if len(st_.reference) > 0:
+            st_.ref_score = r["ref_score"]
+            st_.reference.bandwidth = abs(r["ref_bw"])
+            st_.reference.bandwidth_fixed = r["ref_bw"] < 0
+        stages = [[], [], []]
+        for c, sg in zip(r["stages"], r["stage_of"]):
+            stages[sg - 1].append(DNASeq(c))
         results.append(RifrafResult(consensus=st_.consensus, params=params, state=st_,
-                                    consensus_stages=[[DNASeq(c) for c in r["stages"]], [], []]))
+                                    consensus_stages=stages))
     for e in errors:
         if e is not None:
             raise e

@@ -177,11 +177,15 @@ class Engine:
         self._check(self.lib.rf_set_templates(self.ctx, int(first), len(tpls), ptr(bases), ptr(off)))
 
     def rifraf_batch_native(self, bparams, read_off, read_seq, read_len, threshold, fixed_off, fixed,
-                            slot_base, tpl_id, cons, cons_off):
-        """rf_rifraf_batch + rf_batch_fetch: the native lockstep INIT stage of
-        many reference-free clusters (rifraf_batch.cpp).  Returns one dict per
-        cluster: consensus, score, iters, status, stages, batch, error; and
-        the final bandwidth per read (negative once bandwidth_fixed)."""
+                            slot_base, tpl_id, cons, cons_off, ref=None):
+        """rf_rifraf_batch(_ref) + rf_batch_fetch(_ref): the native lockstep
+        stage machine over many clusters (rifraf_batch.cpp).  Returns one dict
+        per cluster: consensus, score, iters, status, stages, stage_of,
+        stage_iters, batch, error (and ref_bw, ref_score, n_ref_indel_mults);
+        and the final bandwidth per read (negative once bandwidth_fixed).
+        ref: None (no references) or a dict with "params"
+        (_lib.BatchRefParams), "refs" (a _lib.BatchRef array, one per
+        cluster), "bases" (uint8) and "cb" (a _lib.RefCallback)."""
         nclu = len(slot_base)
         c = lambda a, t: np.ascontiguousarray(a, t)   # noqa: E731
         read_off, read_seq, read_len = c(read_off, np.int32), c(read_seq, np.int32), c(read_len, np.int32)
@@ -195,24 +199,41 @@ class Engine:
         status = np.empty(max(nclu, 1), np.int32)
         length = np.empty(max(nclu, 1), np.int64)
         bw = np.empty(max(len(read_seq), 1), np.int32)
-        self._check(self.lib.rf_rifraf_batch(self.ctx, nclu, byref(bparams), ptr(read_off), ptr(read_seq),
-                                             ptr(read_len), ptr(threshold), ptr(fixed_off), ptr(fixed),
-                                             ptr(slot_base), ptr(tpl_id), ptr(cons), ptr(cons_off), ptr(score),
-                                             ptr(iters), ptr(status), ptr(length), ptr(bw)))
+        if ref is None:
+            self._check(self.lib.rf_rifraf_batch(self.ctx, nclu, byref(bparams), ptr(read_off), ptr(read_seq),
+                                                 ptr(read_len), ptr(threshold), ptr(fixed_off), ptr(fixed),
+                                                 ptr(slot_base), ptr(tpl_id), ptr(cons), ptr(cons_off),
+                                                 ptr(score), ptr(iters), ptr(status), ptr(length), ptr(bw)))
+        else:
+            rb = np.ascontiguousarray(ref["bases"], np.uint8)
+            self._check(self.lib.rf_rifraf_batch_ref(
+                self.ctx, nclu, byref(bparams), byref(ref["params"]), ptr(read_off), ptr(read_seq),
+                ptr(read_len), ptr(threshold), ptr(fixed_off), ptr(fixed), ptr(slot_base), ptr(tpl_id), ptr(cons),
+                ptr(cons_off), ctypes.cast(ref["refs"], c_void_p), ptr(rb) if len(rb) else ptr(np.zeros(1, np.uint8)),
+                ctypes.cast(ref["cb"], c_void_p), None, ptr(score), ptr(iters), ptr(status), ptr(length),
+                ptr(bw)))
         out = []
         err = ctypes.create_string_buffer(512)
         try:
             for k in range(nclu):
                 cs = np.empty(int(length[k]), np.uint8)
                 slen = np.empty(max(int(iters[k]), 1), np.int64)
-                nb = int(fixed_off[k + 1] - fixed_off[k]) if fixed_off is not None else int(read_off[k + 1] - read_off[k])
-                batch = np.empty(nb, np.int32)
+                sit = np.zeros(3, np.int32)
+                sof = np.zeros(max(int(iters[k]), 1), np.int8)
+                rbw, rsc, nmul, nb = ctypes.c_int32(0), ctypes.c_double(0.0), ctypes.c_int32(0), ctypes.c_int32(0)
+                self._check(self.lib.rf_batch_fetch_ref(self.ctx, k, ptr(sit), ptr(sof), byref(rbw), byref(rsc),
+                                                        byref(nmul), byref(nb)))
+                batch = np.empty(max(int(read_off[k + 1] - read_off[k]), int(nb.value), 1), np.int32)
                 self._check(self.lib.rf_batch_fetch(self.ctx, k, ptr(cs), ptr(slen), None, ptr(batch), err, 512))
+                batch = batch[:int(nb.value)]
                 st = np.empty(int(slen[:iters[k]].sum()), np.uint8)
                 self._check(self.lib.rf_batch_fetch(self.ctx, k, None, None, ptr(st), None, None, 0))
                 cut = np.cumsum(slen[:iters[k]])[:-1]
                 out.append({"consensus": cs, "score": float(score[k]), "iters": int(iters[k]),
                             "status": int(status[k]), "stages": np.split(st, cut) if iters[k] else [],
+                            "stage_of": sof[:int(iters[k])].tolist(), "stage_iters": sit.tolist(),
+                            "ref_bw": int(rbw.value), "ref_score": float(rsc.value),
+                            "n_ref_indel_mults": int(nmul.value),
                             "batch": batch.tolist(), "error": err.value.decode() if status[k] == 2 else None})
         finally:
             self.lib.rf_batch_release(self.ctx)

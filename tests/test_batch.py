@@ -167,7 +167,17 @@ def test_native_scope():
     assert native_eligible(clusters, RifrafParams())
     assert native_eligible(clusters, RifrafParams(batch_size=0, batch_fixed=False))
     assert not native_eligible(clusters, RifrafParams(batch_size=4, batch_fixed=False))
-    assert not native_eligible(_clusters(), RifrafParams())          # references
+    # references: native when REFINE (random resampling below the read
+    # count) sees every read and the QV pass does not score the reference
+    ref_clusters = _ref_clusters()
+    assert native_eligible(ref_clusters, RifrafParams(batch_size=0, batch_fixed=False))
+    assert native_eligible(ref_clusters, RifrafParams(batch_size=0))
+    assert not native_eligible(ref_clusters, RifrafParams(batch_size=5))
+    assert native_eligible(ref_clusters, RifrafParams(batch_size=5, do_refine=False))
+    assert not native_eligible(ref_clusters, RifrafParams(batch_size=0, do_score=True, use_ref_for_qvs=True))
+    from rifraf_amd import ErrorModel, Scores
+    bad_ref = RifrafParams(batch_size=0, ref_scores=Scores(-1.0, -1.0, -1.0, 0.0, -1.0))
+    assert not native_eligible(ref_clusters, bad_ref)                # check_params: the hub raises it
     assert not native_eligible(clusters, RifrafParams(do_init=False))
     # an empty read or a quality vector of another length: the Python stage
     # machine (RifrafSequence's own handling), never a whole-wave native error
@@ -180,6 +190,82 @@ def test_native_scope():
     assert not native_eligible(short, RifrafParams())
     with pytest.raises(RifrafError):
         rifraf_batch(clusters[:1], params=RifrafParams(max_iters=2), engine=OracleEngine(), native=True)
+
+
+def _ref_clusters(seed=41):
+    """Clusters with a reference carrying a frameshift (INIT -> FRAME with
+    codon scoring, seeded indel proposals, penalty increases -> REFINE),
+    mixed with reference-free ones."""
+    from rifraf_amd import ErrorModel
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    out = []
+    for n, L, shift in [(12, 300, 150), (20, 450, 200), (8, 240, 0), (15, 360, 90), (10, 200, -1),
+                        (25, 420, 300)]:
+        ref, _, _, reads, _, phreds, _, _ = sample_sequences(
+            n, L, error_rate=0.02, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+        ref = np.asarray(ref, np.uint8)
+        if shift > 0:   # a one-base deletion and, later, a one-base insertion in the reference
+            ref = np.concatenate([ref[:shift], ref[shift + 1:shift + 60], [2], ref[shift + 60:]]).astype(np.uint8)
+        kw = dict(dnaseqs=reads, phreds=phreds)
+        if shift >= 0:
+            kw["reference"] = ref
+        out.append(kw)
+    return out
+
+
+REF_PARAMS = {
+    "throughput_qv": dict(batch_size=0, batch_fixed=False, do_score=True),
+    "fixed_batch": dict(batch_size=0, batch_fixed=True, batch_fixed_size=4, max_iters=40),
+    "unseeded_subs": dict(batch_size=0, batch_fixed=False, seed_indels=False, indel_correction_only=False,
+                          max_ref_indel_mults=1, do_alignment_proposals=False, max_iters=30),
+    "no_refine": dict(batch_size=6, do_refine=False, ref_error_mult=2.0, do_score=True),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pset", sorted(REF_PARAMS))
+def test_native_reference_batch_matches_hub(engine, pset):
+    """rf_rifraf_batch_ref: reference-guided clusters (FRAME, REFINE) in the
+    library's stage machine against the Python stage machine on the same
+    engine -- consensus per iteration and stage, score, stage iterations,
+    convergence, QVs, penalty increases and the reference's error rate."""
+    from rifraf_amd import ErrorModel, Scores
+    from rifraf_amd.batch import native_eligible, rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), **REF_PARAMS[pset])
+    clusters = _ref_clusters()
+    assert native_eligible(clusters, params)
+    hub = rifraf_batch(clusters, params=params, engine=engine, native=False)
+    nat = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    frames = 0
+    for a, b in zip(nat, hub):
+        assert_same_run(summary(a), summary(b))
+        assert a.state.n_ref_indel_mults == b.state.n_ref_indel_mults
+        assert a.state.ref_error_rate == b.state.ref_error_rate or (
+            np.isinf(a.state.ref_error_rate) and np.isinf(b.state.ref_error_rate))
+        assert a.state.reference.bandwidth == b.state.reference.bandwidth
+        frames += a.state.stage_iterations[1] > 0
+    assert frames >= 3
+    if pset == "throughput_qv":   # the whole FRAME path: penalty increases, then REFINE
+        assert any(r.state.n_ref_indel_mults >= 1 for r in nat)
+        assert any(r.state.stage_iterations[2] > 0 for r in nat)
+
+
+@pytest.mark.gpu
+def test_native_reference_batch_matches_oracle_runs(engine):
+    """Native reference-guided clusters against separate rifraf() runs on the
+    CPU oracle engine (throughput settings, QVs on)."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd import ErrorModel, Scores
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams, rifraf
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), **REF_PARAMS["throughput_qv"])
+    clusters = _ref_clusters(seed=43)[:4]
+    ref = [summary(rifraf(params=params, engine=OracleEngine(), **kw)) for kw in clusters]
+    got = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    for r, g in zip(ref, got):
+        assert_same_run(summary(g), r)
 
 
 @pytest.mark.gpu

@@ -112,6 +112,13 @@ def test_c3_throughput_frame_run_matches_oracle(engine):
     assert a.state.batch_size == 1000
     assert a.state.stage_iterations[1] >= 2 and a.state.n_ref_indel_mults >= 1
     assert np.array_equal(a.consensus, template)
+    # the same cluster through the library's stage machine (rf_rifraf_batch_ref)
+    from rifraf_amd.batch import native_eligible, rifraf_batch
+    kw = dict(dnaseqs=reads, phreds=phreds, reference=ref)
+    assert native_eligible([kw], params)
+    n = rifraf_batch([kw], params=params, engine=engine, native=True)[0]
+    assert_same_run(n, b)
+    assert n.state.n_ref_indel_mults == b.state.n_ref_indel_mults
 
 
 def test_c3_qv_with_reference_matches_oracle(engine):
