@@ -102,11 +102,10 @@ const char *rf_last_error(const rf_ctx *ctx);
                                     tasks (k_dpr<2,..,32>); 0 = 16-lane tasks only   */
 #define RF_OPT_ALN_SUMS_HOST 19 /* 1: rf_aln_error_sums folds the moves on host
                                     threads instead of the device (k_aln_sums)     */
-#define RF_OPT_SCORE_W2    20   /* narrow-band dense scorer: 1 k_score_w2 (two reads'
-                                    windows in flight), 0 k_score_ws               */
-/* Keys 3, 5-8 and 14 selected scorer variants measured slower and removed in
-   round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg / k_score_segc,
-   16-diagonal k_score_segl); rf_set_option rejects them. */
+/* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
+   in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
+   k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);
+   rf_set_option rejects them. */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

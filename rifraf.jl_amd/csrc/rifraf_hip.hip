@@ -1514,256 +1514,101 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
     tD += dd;
 }
 
-__device__ __forceinline__ void wg_barrier()
+// lean_chain for an interior lane of a read with row stride exactly PT (the
+// c4 strides 11..17): a < m, a >= c and a + 1 + vb <= n, so the chain runs
+// diagonals d = 1 .. H-1 of column a and then the peeled row d = H.  Over two
+// rows (d odd, then even) the window index advances by 2 PT + 1, so with the
+// stride a template constant every LDS operand of a row pair is at an
+// immediate offset from one pointer per array: the per-row index arithmetic
+// of lean_chain (about 15 of its 51 VALU ops per row) drops out.  Same
+// operands, same FP64 ops in the same order: the same values.
+template <int PT>
+__device__ __forceinline__ void lean_chain_fix(const ScoreRead &R, const LeanWin &w, int a, const double *sA,
+                                               const double *sB, const double *sT, double tI[4], double tS[4],
+                                               double &tD)
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// Half of lean_chain: the chains of bases 2h and 2h+1 of column a (the
-// other half runs in the neighbouring lane).  The same operands, order and
-// FP64 ops per chain as lean_chain, so the same values; the deletion fold
-// (dd) is carried by both halves and written by h = 0.
-__device__ __forceinline__ void lean_chain2(const ScoreRead &R, const LeanWin &w, int a, int h, int m,
-                                            const double *sA, const double *sB, const double *sT,
-                                            double tI[2], double tS[2], double &tD)
-{
-    const int c = R.c, vb = R.vb, P = R.P;
-    const int jn = min(a + 1, m);
-    const int i0 = max(0, jn - c);
-    const int i1 = min(jn + vb, R.n);
-    const int ilast = min(i1, a + vb);                  // last row of rows(a)
-    int d = i0 - a + c;
-    int idx = w.shift + (d + 2 * a - w.kw0) * P + (d >> 1);
-    double aprev = (d >= 1 && i0 >= 1) ? sA[idx - P - 1 + (d & 1)] : -RF_INF;
-    const bool hasS = a < m;
-    const int sofs = hasS ? P - 1 : 0;
-    const int sodd = hasS ? 1 : 0;
-    const double smask = hasS ? 0.0 : -RF_INF;
-    const double2 *tr = (const double2 *)(sT + 6 * (i0 - w.t0));
-    double prev[2], accI[2], accS[2], dd = -RF_INF;
+    const int idx0 = w.shift + (1 + 2 * a - w.kw0) * PT;   // d = 1
+    const double *pa = sA + idx0, *pb = sB + idx0;
+    const double *pt = sT + 6 * (a + 1 - R.c - w.t0);
+    double aprev = pa[-PT];
+    double prev[4], accI[4], accS[4], dd = -RF_INF;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 4; ++k) {
         prev[k] = -RF_INF;
         accI[k] = -RF_INF;
         accS[k] = -RF_INF;
     }
-    double ac = sA[idx], bI = sB[idx], bSr = sB[idx + sofs + (sodd & d)];
-    double2 us = tr[h], u2 = tr[2];
-    for (int i = i0; i <= ilast; ++i) {
-        idx += P + (d & 1);
-        ++d;
-        tr += 3;
-        const double acn = sA[idx], bIn = sB[idx], bSn = sB[idx + sofs + (sodd & d)];
-        const double2 vs = tr[h], v2 = tr[2];
-        const double bS = bSr + smask;
+    // one row: A / B at offset o, B(i, a+1) at offset os, table record at t
+    auto row = [&](int o, int os, int t) {
+        const double ac = pa[o], bI = pb[o], bS = pb[os];
+        const double2 u0 = *(const double2 *)(pt + t), u1 = *(const double2 *)(pt + t + 2),
+                      u2 = *(const double2 *)(pt + t + 4);
+        const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
         const double dl = ac + u2.y;
         const double dsum = ac + bS;
-        double x[2], y[2];
-        x[0] = aprev + us.x;
-        x[1] = aprev + us.y;
-        y[0] = prev[0] + u2.x;
-        y[1] = prev[1] + u2.x;
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            prev[k] = vmax(vmax(x[k], y[k]), dl);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            accI[k] = vmax(accI[k], prev[k] + bI);
-            accS[k] = vmax(accS[k], prev[k] + bS);
-        }
+        chain_row(aprev, sub, u2.x, dl, bI, bS, prev, accI, accS);
         dd = vmax(dd, dsum);
         aprev = ac;
-        ac = acn;
-        bI = bIn;
-        bSr = bSn;
-        us = vs;
-        u2 = v2;
+    };
+    const int nrows = R.c + R.vb;   // i0 = a + 1 - c .. ilast = a + vb
+    for (int u = 0; u < (nrows >> 1); ++u) {
+        row(0, PT, 0);                        // d odd
+        row(PT + 1, 2 * PT, 6);               // d even
+        pa += 2 * PT + 1;
+        pb += 2 * PT + 1;
+        pt += 12;
     }
-    if (i1 > ilast) {
-        const double sub[2] = {us.x, us.y};
+    // the last odd row (H even), then the peeled row d = H below column a's band
+    const bool odd_tail = nrows & 1;
+    if (odd_tail)
+        row(0, PT, 0);
+    const double bSr = odd_tail ? pb[2 * PT] : pb[PT];
+    const double *tp = pt + (odd_tail ? 6 : 0);
+    const double2 u0 = *(const double2 *)tp, u1 = *(const double2 *)(tp + 2), u2 = *(const double2 *)(tp + 4);
+    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
-            accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
-    }
+    for (int k = 0; k < 4; ++k)
+        accS[k] = vmax(accS[k], vmax(aprev + sub[k], prev[k] + u2.x) + bSr);
     const double qnan = __builtin_nan("");
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 4; ++k) {
         tI[k] += accI[k] == -RF_INF ? qnan : accI[k];
         tS[k] += accS[k] == -RF_INF ? qnan : accS[k];
     }
     tD += dd;
 }
 
-// ---------------------------------------------------------------------
-// k_score_w2: the c4-shape dense scorer without role specialization
-// (round 3).  512 threads cover 256 columns, two lanes per column (lane 2c+h
-// scores the chains of bases 2h, 2h+1 of column a0+c: lean_chain2), and every
-// lane is also a loader: a read's window (bands + table rows) is split over
-// all 512 lanes, and each lane holds the windows of the next TWO reads in
-// registers (two sets, alternating), so each window's loads are issued two
-// reads ahead and two windows are in flight per CU -- k_score_ws has one,
-// whose load latency is exposed once per read.  Per read: commit the
-// window from its register set to LDS, barrier, issue the loads of read
-// r + 2 into the freed set, score read r, barrier.
-// ---------------------------------------------------------------------
-template <int NPF>
-struct W2Set {
-    dvec2 pa[NPF], pb[NPF];
-    double pm, px, pn, pd;
-    int ps;
-    __device__ __forceinline__ void issue(const ScoreRead &R2, const LeanWin &w2, int lt,
-                                          const double *__restrict__ bands, const double *__restrict__ tabs,
-                                          const uint8_t *__restrict__ bases)
-    {
-        const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
-        const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
-#pragma unroll
-        for (int u = 0; u < NPF; ++u) {
-            const int e = u * 512 + lt;
-            if (e < w2.n16) {
-                pa[u] = ga[e];
-                pb[u] = gb[e];
-            }
-        }
-        const double *tm = tabs + R2.tab;
-        const int n2 = R2.n;
-        const int i = min(w2.t0 + lt, w2.t1);
-        const int ks = max(i - 1, 0);
-        pm = tm[ks];
-        px = tm[n2 + ks];
-        pn = tm[2 * (size_t)n2 + ks];
-        pd = tm[3 * (size_t)n2 + i];
-        ps = bases[R2.sb + ks];
-    }
-    __device__ __forceinline__ void commit(const LeanWin &wf, int lt, double *smem) const
-    {
-        dvec2 *sA = (dvec2 *)smem;
-        dvec2 *sB = (dvec2 *)(smem + wf.win);
-        double *sT = smem + 2 * wf.win;
-#pragma unroll
-        for (int u = 0; u < NPF; ++u) {
-            const int e = u * 512 + lt;
-            if (e < wf.n16) {
-                sA[e] = pa[u];
-                sB[e] = pb[u];
-            }
-        }
-        const int i = wf.t0 + lt;
-        if (i <= wf.t1)
-            lean_row(sT + 6 * lt, i >= 1 ? ps : 4, pm, px, pn, pd);
-    }
-};
-
-#ifndef W2_NPF
-#define W2_NPF 10
-#endif
-template <int NPF>
-__global__ void __launch_bounds__(512) k_score_w2(const WorkItem *__restrict__ items,
-                                                  const ScoreGroup *__restrict__ groups,
-                                                  const ScoreRead *__restrict__ reads,
-                                                  const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
-                                                  const double *__restrict__ bands, double *__restrict__ dense,
-                                                  double *__restrict__ split, int split_mode, int lds_elems)
+// Whether every chain lane of this wave is interior for read R (lean_chain_fix).
+__device__ __forceinline__ bool ws_wave_interior(const ScoreRead &R, int a, int m)
 {
-    constexpr int Q = 256;   // columns per work item
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int xq = nb >> 3, xr = nb & 7, x = b & 7;
-    const int item = x * xq + min(x, xr) + (b >> 3);
-    const WorkItem wi = items[item];
-    const ScoreGroup G = groups[wi.group];
-    const int m = G.m;
-    const int a0 = wi.p0;
-    const int la1f = min(a0 + Q - 1, m);
-    int r0 = G.r0, r1 = G.r1;
-    if (split_mode & 1) {
-        r0 = G.r0 + blockIdx.y;
-        if (r0 >= G.r1)
-            return;
-        r1 = r0 + 1;
-    }
-    const int lt = threadIdx.x;
-    const int col = lt >> 1, h = lt & 1;
-    const int a = a0 + col;
-    auto fast = [&](const ScoreRead &R, const LeanWin &w) {   // block-uniform
-        return lean_need(Q, R.H, R.P) <= lds_elems && w.n16 <= NPF * 512 && w.t1 - w.t0 < 512;
-    };
-    auto sub_L = [&](const ScoreRead &R) {
-        int L = Q;
-        while (L > 1 && lean_need(L, R.H, R.P) > lds_elems)
-            L >>= 1;
-        return L;
-    };
-    double tI[2] = {0.0, 0.0}, tS[2] = {0.0, 0.0}, tD = 0.0;
-    W2Set<NPF> s0, s1;   // s0: reads r0, r0+2, ...; s1: r0+1, r0+3, ...
-    auto try_issue = [&](W2Set<NPF> &st, int rr) {
-        if (rr < r1) {
-            const ScoreRead R2 = reads[rr];
-            const LeanWin w2 = lean_win(R2, m, a0, la1f);
-            if (fast(R2, w2))
-                st.issue(R2, w2, lt, bands, tabs, bases);
+    return __all(a < m && a >= R.c && a + 1 + R.vb <= R.n);
+}
+
+#ifndef WS_PFIX
+#define WS_PFIX 1   // interior waves of reads with stride 11..17 run lean_chain_fix
+#endif
+// lean_chain, or lean_chain_fix<P> when the wave is interior and P is a c4 stride
+__device__ __forceinline__ void lean_chain_any(const ScoreRead &R, const LeanWin &w, int a, int m, const double *sA,
+                                               const double *sB, const double *sT, double tI[4], double tS[4],
+                                               double &tD)
+{
+    if (WS_PFIX && ws_wave_interior(R, a, m)) {
+        switch (R.P) {
+        case 11: lean_chain_fix<11>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 13: lean_chain_fix<13>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 15: lean_chain_fix<15>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 17: lean_chain_fix<17>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        default: break;
         }
-    };
-    auto one_read = [&](W2Set<NPF> &st, int r) {
-        const ScoreRead R = reads[r];
-        const LeanWin wf = lean_win(R, m, a0, la1f);
-        if (fast(R, wf)) {
-            st.commit(wf, lt, smem);
-            wg_barrier();                            // window r ready
-            try_issue(st, r + 2);
-            if (a <= m && !(split_mode & 2))
-                lean_chain2(R, wf, a, h, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
-            wg_barrier();                            // chains of r done
-        } else {
-            // beyond the prefetch or the LDS budget: staged synchronously, in
-            // sub-passes over L columns
-            const int L = sub_L(R);
-            for (int c0 = 0; c0 < Q; c0 += L) {
-                const int la0 = a0 + c0;
-                if (la0 > m)
-                    break;
-                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
-                lean_stage<512>(R, w, lt, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
-                wg_barrier();
-                if (col >= c0 && col < c0 + L && a <= m)
-                    lean_chain2(R, w, a, h, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
-                wg_barrier();
-            }
-            try_issue(st, r + 2);
-        }
-    };
-    try_issue(s0, r0);
-    try_issue(s1, r0 + 1);
-    int r = r0;
-    for (; r + 1 < r1; r += 2) {
-        one_read(s0, r);
-        one_read(s1, r + 1);
     }
-    if (r < r1)
-        one_read(s0, r);
-    if (a > m)
-        return;
-    const double qnan = __builtin_nan("");
-    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
-                                    : dense + G.dense_off;
-    double *dst = base + (size_t)a * 9;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        dst[5 + 2 * h + k] = tI[k];
-    if (a < m) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            dst[9 + 2 * h + k] = tS[k];
-        if (h == 0)
-            dst[13] = tD;
-    }
-    if (a == 0 && h == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            dst[k] = qnan;
-    }
+    lean_chain(R, w, a, m, sA, sB, sT, tI, tS, tD);
+}
+
+__device__ __forceinline__ void wg_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // ---------------------------------------------------------------------
@@ -1916,7 +1761,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
         if (fast(R, wf)) {
             wg_barrier();                            // window r ready
             if (a <= m && !(split_mode & 2))
-                lean_chain(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
+                lean_chain_any(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
             wg_barrier();                            // chains of r done
         } else {
             const int L = sub_L(R);
@@ -1927,7 +1772,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                 const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
                 wg_barrier();
                 if (tid >= s0 && tid < s0 + L && a <= m)
-                    lean_chain(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
+                    lean_chain_any(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
                 wg_barrier();
             }
         }
@@ -3428,9 +3273,6 @@ struct CodeDict {
 // Tuning options (rf_set_option keys, include/rifraf_hip.h).  Every option
 // selects between bit-identical code paths; defaults come from the RIFRAF_*
 // environment once, at rf_create, and never from a hot path.
-#ifndef W2_DEFAULT
-#define W2_DEFAULT 0
-#endif
 #ifndef DP_WIDE_DEFAULT
 #define DP_WIDE_DEFAULT 3
 #endif
@@ -3450,7 +3292,6 @@ struct Opts {
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
-    int score_w2 = W2_DEFAULT;   // RF_OPT_SCORE_W2: 1 = k_score_w2 (narrow bands), 0 = k_score_ws
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -3763,7 +3604,6 @@ void load_env_opts(Opts &o)
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
-    o.score_w2 = env_int("RIFRAF_SCORE_W2", o.score_w2);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3838,9 +3678,6 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     } else if (!pk.lean) {
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
-    } else if (ctx->opt.score_w2) {
-        hipLaunchKernelGGL((k_score_w2<W2_NPF>), grid, dim3(512), pk.lds * 8, ctx->stream, items, groups, reads,
-                           d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     } else {
         hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
                            groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
@@ -3888,8 +3725,6 @@ int rf_create(int device, rf_ctx **out)
     }
     // the lean scorer may use up to the whole 160 KiB LDS of a CU
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_score_w2<W2_NPF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
@@ -3955,7 +3790,6 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
     case RF_OPT_DP_WIDE: return &o.dp_wide;
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
-    case RF_OPT_SCORE_W2: return &o.score_w2;
     default: return nullptr;
     }
 }

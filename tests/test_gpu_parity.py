@@ -812,7 +812,7 @@ def test_removed_option_keys_rejected(engine):
     """Scorer-variant keys removed in round 3 (include/rifraf_hip.h) are
     refused with an error, not silently accepted."""
     from rifraf_amd.engine import RifrafError
-    for key in (3, 5, 6, 7, 8, 14):
+    for key in (3, 5, 6, 7, 8, 14, 20):
         assert engine.lib.rf_set_option(engine.ctx, key, 1) != 0
         assert "unknown option" in engine.lib.rf_last_error(engine.ctx).decode()
     with pytest.raises(KeyError):
