@@ -1824,9 +1824,6 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #define SEGL_UNROLL 32
 #endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
-#ifndef SEGL_PF2
-#define SEGL_PF2 0
-#endif
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
 // of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
 // slower at c5: 30.6 ms at one wave per SIMD, 40.6 ms at two with spills,
@@ -1937,8 +1934,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     };
     const bool all_act = __all(active) && wave_s;
     // one segment's registers: its band lines, table rows and (a read's
-    // first segment) LDS row 0.  SEGL_PF2: two sets, so each segment's loads
-    // are issued two segments ahead (two segments in flight per wave)
+    // first segment) LDS row 0
     struct SegSet {
         dvec2 ra[NUA], rb[NUA];
         double tmt[2], tmm[2], tin[2], tdl[2];
@@ -2200,10 +2196,8 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             p.D += S;
         }
     };
-    // one segment: X holds its loads; afterwards X holds the loads of the
-    // segment DEPTH ahead (nxt: the stream position DEPTH - 1 ahead)
-    auto step = [&](SegSet &X, Pos &cur, Pos &nxt, auto depth) {
-        constexpr int DEPTH = decltype(depth)::value;
+    // one segment: X holds its loads; afterwards X holds the next segment's
+    auto step = [&](SegSet &X, Pos &cur) {
         const int D = cur.D;
         const bool first = D == first_of(cur.g);
         wave_sync();   // previous segment's chains are done with LDS
@@ -2229,7 +2223,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         }
         store_seg(X, cur.g, D);
         wave_sync();
-        Pos ahead = DEPTH == 2 ? nxt : cur;
+        Pos ahead = cur;
         if (ahead.r < r1)
             adv(ahead);
         if (do_load && ahead.r < r1)
@@ -2237,12 +2231,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         chains(cur.g, D);
         if (D + S > cur.g.dhi)
             finish(cur.r);
-        if (DEPTH == 2) {
-            cur = nxt;
-            nxt = ahead;
-        } else {
-            cur = ahead;
-        }
+        cur = ahead;
     };
     Pos cur;
     cur.r = r0;
@@ -2250,26 +2239,11 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         setup(r0, cur.g);
         cur.D = first_of(cur.g);
     }
-    SegSet X0, X1;
+    SegSet X0;
     if (r0 < r1 && do_load)
         load_seg(X0, cur.g, cur.D, true);
-#if SEGL_PF2
-    Pos nxt = cur;
-    if (nxt.r < r1)
-        adv(nxt);
-    if (do_load && nxt.r < r1)
-        load_seg(X1, nxt.g, nxt.D, nxt.D == first_of(nxt.g));
-    while (cur.r < r1) {
-        step(X0, cur, nxt, std::integral_constant<int, 2>{});
-        if (cur.r >= r1)
-            break;
-        step(X1, cur, nxt, std::integral_constant<int, 2>{});
-    }
-#else
-    (void)X1;
     while (cur.r < r1)
-        step(X0, cur, cur, std::integral_constant<int, 1>{});
-#endif
+        step(X0, cur);
     if (!active || (split_mode & 1))
         return;
     const double qnan = __builtin_nan("");
