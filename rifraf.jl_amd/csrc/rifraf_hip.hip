@@ -814,9 +814,26 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 const int ii = max(1, min(top_c + (kk >> 1), T.n));
                 return rev ? T.n - ii : ii - 1;
             };
+#if defined(RIFRAF_DIAG) && defined(DPL_NOEDGE_DIAG)
+            (void)codes;
+            auto code_load = [&](int kb) -> uint64_t { return (uint64_t)kb; };
+#else
             auto code_load = [&](int kb) -> uint64_t { return coded ? codes[edge_ks(kb)] : 0; };
+#endif
             auto edge_load = [&](int kb, uint64_t rec) {
                 EdgeRec e;
+#if defined(RIFRAF_DIAG) && defined(DPL_NOEDGE_DIAG)
+                // diagnostic builds only (wrong bands, timing): edge records made
+                // up in registers, no edge loads behind the band stores
+                (void)rec;
+                e.mt = -0.01 - 1e-6 * (kb & 1023);
+                e.mm = -2.0 - 1e-6 * q;
+                e.is = -1.5;
+                e.ds = -1.5;
+                e.sb = (kb + q) & 3;
+                e.col = (kb >> 1) & 3;
+                return e;
+#endif
                 const int kk = kb + 2 * min(q, DPL_B - 1);
 #if defined(RIFRAF_DIAG) && defined(DPL_TAB_DIAG)   // diagnostic builds only: one L2-resident table slice
                 const int ks = edge_ks(kb) & 255;
