@@ -488,6 +488,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         cold, _ = aggregate(cold, [0.0], coll)
         elapsed, tot = aggregate(elapsed, tot, coll)
     return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": tot[0] / elapsed,
+            "clusters_per_s_per_gpu": tot[0] / elapsed / max(world, 1), "ranks": world,
             "clusters": int(tot[0]), "seconds": elapsed,
             "cold_clusters_per_s": tot[0] / cold,
             "timing": "steady state: the second full run over the clusters (the first, 'cold', also allocates "
