@@ -373,6 +373,58 @@ def test_score_dense_clusters(engine, opts, mode):
         np.testing.assert_array_equal(got[c][mask], ref_tot[mask])
 
 
+def _indel_read(t, rng, k, bw=9):
+    """t with k bases inserted (k > 0) or -k bases deleted (k < 0) at random
+    positions, plus ~1 % substitutions: |n - m| = |k|, so H = |k| + 2 bw + 1."""
+    s = list(t)
+    for _ in range(abs(k)):
+        j = int(rng.integers(0, len(s) + (1 if k > 0 else 0)))
+        if k > 0:
+            s.insert(j, int(rng.integers(0, 4)))
+        else:
+            del s[j]
+    s = np.array(s, np.uint8)
+    sub = rng.random(len(s)) < 0.01
+    s[sub] = (s[sub] + rng.integers(1, 4, int(sub.sum()))) % 4
+    ph = rng.integers(8, 40, len(s)).astype(np.float64)
+    return RifrafSequence(s, ph / -10.0, bw, SEQ_SCORES)
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_score_dense_fixed_stride_chains(engine, opts, mode):
+    """k_score_ws's fixed-stride chains (lean_chain_fix<P>, P = 11, 13, 15,
+    17) against the oracle: one cluster per |n - m| = 0..13 (H = 19..32, both
+    parities, every c4 stride), reads longer and shorter than the template,
+    m = 700 so that most waves are interior and the first / last are not."""
+    opts("score_mode", mode)
+    rng = np.random.default_rng(2417)
+    templates, seqs = [], []
+    for k in range(14):
+        t = random_seq(700, rng)
+        templates.append(t)
+        seqs.append([_indel_read(t, rng, k if r % 2 == 0 else -k) for r in range(3)])
+    flat = [r for rs in seqs for r in rs]
+    assert {r.bandwidth for r in flat} == {9}
+    engine.set_sequences(0, flat)
+    engine.set_templates(0, templates)
+    tpl = np.concatenate([[c] * len(rs) for c, rs in enumerate(seqs)])
+    n = len(flat)
+    engine.realign(np.arange(n), np.arange(n), tpl, [9] * n, RF_FWD | RF_BWD)
+    groups, at = [], 0
+    for rs in seqs:
+        groups.append(np.arange(at, at + len(rs)))
+        at += len(rs)
+    got = engine.score_dense(groups)
+    for c in range(len(templates)):
+        ref_tot, _ = oracle.cpu_pass(templates[c], seqs[c], nthreads=4)
+        t = templates[c]
+        mask = np.ones_like(ref_tot, bool)
+        mask[0, :5] = False
+        for j in range(1, len(t) + 1):
+            mask[j, t[j - 1]] = False
+        np.testing.assert_array_equal(got[c][mask], ref_tot[mask], err_msg=f"|n - m| = {c}")
+
+
 def test_plan_cache_follows_template_content(engine):
     """A repeated realign/score with identical arguments reuses the uploaded
     plan; a same-length consensus change must still be picked up."""
