@@ -122,8 +122,9 @@ struct alignas(16) ScoreRead {
     int32_t n, bw, H, c;
     int32_t vb;       // v_off + bw
     int32_t P, K;
-    int32_t pad;
+    int32_t flags;    // SR_CODED: row-code records follow the tables (no codon tables)
 };
+constexpr int SR_CODED = 1;
 
 struct alignas(16) ScoreGroup {
     int64_t tb;         // template bases
@@ -1645,13 +1646,17 @@ __device__ __forceinline__ void wg_barrier()
 #ifndef WS_NPF
 #define WS_NPF 19
 #endif
+#ifndef WS_CODES
+#define WS_CODES 1   // loaders read row-coded reads' tables through the code dictionary
+#endif
 
 template <int NPF, int Q>
 __global__ void __launch_bounds__(2 * Q)
 k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
            const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
            const double *__restrict__ tabs, const double *__restrict__ bands,
-           double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems)
+           double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems,
+           const double *__restrict__ lut)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int nb = gridDim.x, b = blockIdx.x;
@@ -1686,6 +1691,24 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
         double pm[2], px[2], pn[2], pd[2];
         int ps[2];
         auto issue = [&](const ScoreRead &R2, const LeanWin &w2) {
+            const double *tm = tabs + R2.tab;
+            const int n2 = R2.n;
+            // Row-coded reads (SR_CODED): one 8-B code record per row from HBM
+            // (issued first, so that the wait for them leaves the band loads in
+            // flight) and the values from the context's L2-resident dictionary
+            // -- the same doubles as the tables (rf_set_sequences), 8 instead of
+            // 33 B per row.  Record of position ks: triple code | del[ks] code
+            // << 16 | del[ks+1] code << 32 | base << 48.
+            const bool coded = (R2.flags & SR_CODED) && lut != nullptr;
+            uint64_t rc[2];
+            if (coded) {
+                const uint64_t *rec = (const uint64_t *)(tm + row_code_off(n2, 0, 0));
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = min(w2.t0 + lt + k * Q, w2.t1);
+                    rc[k] = rec[max(i - 1, 0)];
+                }
+            }
             const dvec2 *ga = (const dvec2 *)(bands + R2.A + (size_t)w2.kw0 * R2.P - w2.shift);
             const dvec2 *gb = (const dvec2 *)(bands + R2.B + (size_t)w2.kw0 * R2.P - w2.shift);
 #pragma unroll
@@ -1698,17 +1721,28 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                     pb[u] = gb[e];
                 }
             }
-            const double *tm = tabs + R2.tab;
-            const int n2 = R2.n;
+            if (coded) {
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int i = min(w2.t0 + lt + k * Q, w2.t1);
-                const int ks = max(i - 1, 0);
-                pm[k] = tm[ks];
-                px[k] = tm[n2 + ks];
-                pn[k] = tm[2 * (size_t)n2 + ks];
-                pd[k] = tm[3 * (size_t)n2 + i];
-                ps[k] = bases[R2.sb + ks];
+                for (int k = 0; k < 2; ++k) {
+                    const int i = min(w2.t0 + lt + k * Q, w2.t1);
+                    const double *l3 = lut + 4 * (size_t)(rc[k] & 0xffff);
+                    pm[k] = l3[0];
+                    px[k] = l3[1];
+                    pn[k] = l3[2];
+                    pd[k] = lut[4 * (size_t)RF_CODES + ((rc[k] >> (i == 0 ? 16 : 32)) & 0xffff)];
+                    ps[k] = (int)((rc[k] >> 48) & 0xff);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = min(w2.t0 + lt + k * Q, w2.t1);
+                    const int ks = max(i - 1, 0);
+                    pm[k] = tm[ks];
+                    px[k] = tm[n2 + ks];
+                    pn[k] = tm[2 * (size_t)n2 + ks];
+                    pd[k] = tm[3 * (size_t)n2 + i];
+                    ps[k] = bases[R2.sb + ks];
+                }
             }
         };
         bool held = (split_mode & 8) != 0;   // registers hold read r (diagnostics: never load)
@@ -3671,7 +3705,8 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     } else {
         hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
-                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
+                           groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds,
+                           WS_CODES ? (const double *)ctx->codes.lut.p : nullptr);
     }
 }
 
@@ -4974,6 +5009,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             R.vb = std::max(A.n - A.m, 0) + A.bw;
             R.P = A.P;
             R.K = (int32_t)band_K(A.H, A.m);
+            R.flags = (S.coded && S.ncins == 0 && S.ncdel == 0) ? SR_CODED : 0;
             reads.push_back(R);
         }
         const int32_t r1 = (int32_t)reads.size();
@@ -5240,6 +5276,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
                 R.vb = std::max(A.n - A.m, 0) + A.bw;
                 R.P = A.P;
                 R.K = (int32_t)band_K(A.H, A.m);
+                R.flags = (S.coded && S.ncins == 0 && S.ncdel == 0) ? SR_CODED : 0;
                 reads.push_back(R);
             }
             G.r1 = (int32_t)reads.size();
