@@ -1603,7 +1603,7 @@ __device__ __forceinline__ bool ws_wave_interior(const ScoreRead &R, int a, int 
 }
 
 #ifndef WS_PFIX
-#define WS_PFIX 1   // interior waves of reads with stride 11..17 run lean_chain_fix
+#define WS_PFIX 2   // interior waves of reads with stride 11..17 (1) / 11..25 (2) run lean_chain_fix
 #endif
 // lean_chain, or lean_chain_fix<P> when the wave is interior and P is a c4 stride
 __device__ __forceinline__ void lean_chain_any(const ScoreRead &R, const LeanWin &w, int a, int m, const double *sA,
@@ -1616,6 +1616,13 @@ __device__ __forceinline__ void lean_chain_any(const ScoreRead &R, const LeanWin
         case 13: lean_chain_fix<13>(R, w, a, sA, sB, sT, tI, tS, tD); return;
         case 15: lean_chain_fix<15>(R, w, a, sA, sB, sT, tI, tS, tD); return;
         case 17: lean_chain_fix<17>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+#if WS_PFIX > 1
+        // doubled bands (bw 18 after smart_forward_moves!, H 37..51)
+        case 19: lean_chain_fix<19>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 21: lean_chain_fix<21>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 23: lean_chain_fix<23>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+        case 25: lean_chain_fix<25>(R, w, a, sA, sB, sT, tI, tS, tD); return;
+#endif
         default: break;
         }
     }
@@ -1684,6 +1691,36 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
             L >>= 1;
         return L;
     };
+    // Work units: a read whose whole window fits LDS and the loaders'
+    // registers is one unit of Q columns; a wider one is split into sub-
+    // windows of L columns that fit LDS (sub_L).  Units stream through the
+    // same register prefetch as whole reads whenever a unit's window fits the
+    // loaders' registers (doubled bands, P 19..25, at L = Q / 2), otherwise
+    // they are staged synchronously.  Both roles walk the same sequence.
+    struct Unit {
+        int r, s0, L;
+    };
+    auto unit_first = [&](int r) {
+        Unit u{r, 0, Q};
+        if (r < r1) {
+            const ScoreRead R = reads[r];
+            if (!fast(R, lean_win(R, m, a0, la1f)))
+                u.L = sub_L(R);
+        }
+        return u;
+    };
+    auto unit_next = [&](const Unit &u) {
+        const int s0 = u.s0 + u.L;
+        if (s0 < Q && a0 + s0 <= m)
+            return Unit{u.r, s0, u.L};
+        return unit_first(u.r + 1);
+    };
+    auto unit_win = [&](const ScoreRead &R, const Unit &u) {
+        return lean_win(R, m, a0 + u.s0, min(a0 + u.s0 + u.L - 1, m));
+    };
+    auto unit_pf = [&](const ScoreRead &R, const Unit &u, const LeanWin &w) {   // register-prefetched
+        return lean_need(u.L, R.H, R.P) <= lds_elems && w.n16 <= NPF * Q && w.t1 - w.t0 < 2 * Q;
+    };
     if (threadIdx.x >= Q) {
         // =========================== loader waves ===========================
         const int lt = threadIdx.x - Q;
@@ -1745,55 +1782,50 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                 }
             }
         };
-        bool held = (split_mode & 8) != 0;   // registers hold read r (diagnostics: never load)
-        for (int r = r0; r < r1; ++r) {
-            const ScoreRead R = reads[r];
-            const LeanWin wf = lean_win(R, m, a0, la1f);
-            if (fast(R, wf)) {
+        bool held = (split_mode & 8) != 0;   // registers hold the unit (diagnostics: never load)
+        for (Unit u = unit_first(r0); u.r < r1;) {
+            const ScoreRead R = reads[u.r];
+            const LeanWin w = unit_win(R, u);
+            const Unit nx = unit_next(u);
+            if (unit_pf(R, u, w)) {
                 if (!held)
-                    issue(R, wf);
+                    issue(R, w);
                 dvec2 *sA = (dvec2 *)smem;
-                dvec2 *sB = (dvec2 *)(smem + wf.win);
-                double *sT = smem + 2 * wf.win;
+                dvec2 *sB = (dvec2 *)(smem + w.win);
+                double *sT = smem + 2 * w.win;
 #pragma unroll
-                for (int u = 0; u < NPF; ++u) {
-                    const int e = u * Q + lt;
-                    if (e < wf.n16) {
-                        sA[e] = pa[u];
-                        sB[e] = pb[u];
+                for (int k = 0; k < NPF; ++k) {
+                    const int e = k * Q + lt;
+                    if (e < w.n16) {
+                        sA[e] = pa[k];
+                        sB[e] = pb[k];
                     }
                 }
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int e = lt + k * Q;
-                    const int i = wf.t0 + e;
-                    if (i <= wf.t1)
+                    const int i = w.t0 + e;
+                    if (i <= w.t1)
                         lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
                 }
-                wg_barrier();                        // window r ready
+                wg_barrier();                        // unit ready
                 held = (split_mode & 8) != 0;
-                if (r + 1 < r1 && !held) {
-                    const ScoreRead R2 = reads[r + 1];
-                    const LeanWin w2 = lean_win(R2, m, a0, la1f);
-                    if (fast(R2, w2)) {
+                if (nx.r < r1 && !held) {
+                    const ScoreRead R2 = reads[nx.r];
+                    const LeanWin w2 = unit_win(R2, nx);
+                    if (unit_pf(R2, nx, w2)) {
                         issue(R2, w2);
                         held = true;
                     }
                 }
-                wg_barrier();                        // chains of r done
+                wg_barrier();                        // chains of the unit done
             } else {
-                const int L = sub_L(R);
-                for (int s0 = 0; s0 < Q; s0 += L) {
-                    const int la0 = a0 + s0;
-                    if (la0 > m)
-                        break;
-                    const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
-                    lean_stage<Q>(R, w, lt, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
-                    wg_barrier();
-                    wg_barrier();
-                }
+                lean_stage<Q>(R, w, lt, bands, tabs, bases, smem, smem + w.win, smem + 2 * w.win);
+                wg_barrier();
+                wg_barrier();
                 held = false;
             }
+            u = nx;
         }
         return;
     }
@@ -1806,27 +1838,13 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
         tI[k] = 0.0;
         tS[k] = 0.0;
     }
-    for (int r = r0; r < r1; ++r) {
-        const ScoreRead R = reads[r];
-        const LeanWin wf = lean_win(R, m, a0, la1f);
-        if (fast(R, wf)) {
-            wg_barrier();                            // window r ready
-            if (a <= m && !(split_mode & 2))
-                lean_chain_any(R, wf, a, m, smem, smem + wf.win, smem + 2 * wf.win, tI, tS, tD);
-            wg_barrier();                            // chains of r done
-        } else {
-            const int L = sub_L(R);
-            for (int s0 = 0; s0 < Q; s0 += L) {
-                const int la0 = a0 + s0;
-                if (la0 > m)
-                    break;
-                const LeanWin w = lean_win(R, m, la0, min(la0 + L - 1, m));
-                wg_barrier();
-                if (tid >= s0 && tid < s0 + L && a <= m)
-                    lean_chain_any(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
-                wg_barrier();
-            }
-        }
+    for (Unit u = unit_first(r0); u.r < r1; u = unit_next(u)) {
+        const ScoreRead R = reads[u.r];
+        const LeanWin w = unit_win(R, u);
+        wg_barrier();                                // unit ready
+        if (tid >= u.s0 && tid < u.s0 + u.L && a <= m && !(split_mode & 2))
+            lean_chain_any(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
+        wg_barrier();                                // chains of the unit done
     }
     if (a > m)
         return;
