@@ -109,12 +109,13 @@ def device_identity(torch, gpu):
     return f"cpu-rank-device-{gpu}"   # --dry-run on a host without GPUs: the assignment itself
 
 
-def distinct_devices(dist, ident: str) -> int:
+def distinct_devices(dist, ident: str):
+    """(distinct physical devices, most ranks on one device) over all ranks."""
     if dist is None:
-        return 1
+        return 1, 1
     ids = [None] * dist.get_world_size()
     dist.all_gather_object(ids, ident)
-    return len(set(ids))
+    return len(set(ids)), max(ids.count(i) for i in set(ids))
 
 
 def band_cells(n: int, m: int, bw: int) -> int:
@@ -300,30 +301,36 @@ def aggregate(elapsed: float, units, device="cpu"):
 def pmc_traffic(config, size, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_<config>.json, scripts/pmc_summary.py), when it was taken at
-    the same size (clusters for c4, reads per rank for c5); else None."""
+    the same size (clusters per rank for c4, reads per rank for c5); else None."""
     pmc_file = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    key = "reads" if config == "c5" else "clusters"
     try:
         pm = json.load(open(pmc_file))
-        if pm.get("clusters") == size and kernel in pm.get("kernels", {}):
+        if pm.get(key) == size and kernel in pm.get("kernels", {}):
             return pm["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         pass
     return None
 
 
-def pmc_fp64(config, cells=None, dp_ms=None):
-    """FP64 VALU evidence from rocprof counters (profiles/pmc_fp64.json,
-    scripts/pmc_fp64_summary.py over scripts/pmc_r03.sh's passes):
-    SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 wave instructions.  c4: the DP's
-    measured FP64 lane-ops per in-band cell, scaled by this run's cells and DP
-    time; both: each DP kernel's longest launch against the FP64 peak."""
+def pmc_fp64(config, cells=None, dp_ms=None, world=1):
+    """FP64 VALU evidence from a PAST rocprof counter run, not this run
+    (profiles/pmc_fp64.json, scripts/pmc_fp64_summary.py over
+    scripts/pmc_r03.sh's passes): SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 wave
+    instructions.  c4: the DP's measured FP64 lane-ops per in-band cell,
+    scaled by this run's cells and DP time; both: each DP kernel's longest
+    launch in the profiled run against the FP64 peak.  Only quoted for the
+    profiled shape: one rank (the profile was taken at world size 1)."""
+    if world != 1:
+        return None
     try:
         pm = json.load(open(os.path.join(REPO, "profiles", "pmc_fp64.json")))
         ent = pm[config]
     except (OSError, ValueError, KeyError):
         return None
     peak = pm["fp64_lane_ops_peak_per_s"]
-    out = {"source": "profiles/pmc_fp64.json",
+    out = {"source": "profiles/pmc_fp64.json (a past rocprofv3 --pmc run at one rank, not this run)",
+           "profiled": pm.get("source"),
            "per_kernel_frac_of_fp64_peak": {k: v["longest_launch"]["frac_of_fp64_peak"]
                                             for k, v in ent["kernels"].items() if k.startswith("k_dpr")}}
     if "dp" in ent and cells and dp_ms:
@@ -335,7 +342,8 @@ def pmc_fp64(config, cells=None, dp_ms=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks = GPUs (default: WORLD_SIZE under an external launcher, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
@@ -357,8 +365,12 @@ def main():
                     help="launch, rendezvous, workload and device assignment only (no engine): checks the "
                          "multi-rank plumbing on a host without GPUs")
     args = ap.parse_args()
+    launched = "RANK" in os.environ or "WORLD_SIZE" in os.environ
+    if args.gpus is None:
+        # under torch.distributed.run without --gpus: the launcher's world size
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1")) if launched else 1
 
-    if args.gpus > 1 and "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+    if args.gpus > 1 and not launched:
         # no external launcher: one child process per GPU, started before this
         # process touches the GPU
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -385,7 +397,8 @@ def main():
             torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
         coll = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
-    n_dev = distinct_devices(dist, device_identity(torch, gpu)) if world > 1 else 1
+    n_dev, per_dev = distinct_devices(dist, device_identity(torch, gpu)) if world > 1 else (1, 1)
+    args.processes_per_gpu = per_dev
 
     if args.dry_run:
         result = run_dry(args, rank, world, gpu, dist, coll, n_dev)
@@ -493,7 +506,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "cold_clusters_per_s": tot[0] / cold,
             "timing": "steady state: the second full run over the clusters (the first, 'cold', also allocates "
                       "the band arena); host setup from reads included, read simulation excluded",
-            "processes_per_gpu": 1,
+            "processes_per_gpu": getattr(args, "processes_per_gpu", 1),
             "engines_per_gpu": ne,
             "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; clusters sharded "
                       "over engines_per_gpu contexts (own HIP stream, own host thread) in one process",
@@ -614,7 +627,7 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
                     "peak_tops": FP64_VEC_TFLOPS / 2,
                     "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2),
-                    "counters": pmc_fp64(args.config, cells, dp_ms)},
+                    "counters_from_profile": pmc_fp64(args.config, cells, dp_ms, world)},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": byt, "launch_ms": ms},
@@ -788,7 +801,7 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
         "dp_valu": {"ops_per_cell": 5, "achieved_tops": 5 * cells / (dp_ms * 1e-3) / 1e12,
                     "peak_tops": FP64_VEC_TFLOPS / 2,
                     "frac": 5 * cells / (dp_ms * 1e-3) / 1e12 / (FP64_VEC_TFLOPS / 2),
-                    "counters": pmc_fp64("c5")},
+                    "counters_from_profile": pmc_fp64("c5", world=world)},
         # smart_forward_moves! (first realign of every read): forward fills at
         # bw, the backtrace walks that count errors, the redone fills of the
         # reads whose band doubled -- every executed cell counted (rank 0's

@@ -59,6 +59,8 @@ def lib():
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int]
         L.or_pass.restype = c_int64
         L.or_pass.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int]
+        L.or_pass_continue.restype = c_int64
+        L.or_pass_continue.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int]
         L.or_seq_tables.restype = None
         L.or_seq_tables.argtypes = [c_void_p, c_int, c_double, c_double, c_double, c_double, c_double,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -209,14 +211,21 @@ def score_list(props, As, Bs, rss, t, Aref=None, Bref=None, ref=None, per_seq=Fa
     return total[:P]
 
 
-def cpu_pass(t, rss, nthreads=1):
+def cpu_pass(t, rss, nthreads=1, totals=None):
     """CPU baseline: realign every read + score every STAGE_SCORE proposal.
-    Returns (totals[(m+1), 9], cells)."""
+    Returns (totals[(m+1), 9], cells).  With `totals` (the running totals of
+    the batch's earlier reads, updated in place) the fold continues from
+    them, so a large batch can be folded chunk by chunk in batch order."""
     seqs = [Seq(r) for r in rss]
     arr = (OrSeq * len(seqs))(*[s.st for s in seqs])
     t = np.ascontiguousarray(t, np.uint8)
-    totals = np.zeros((len(t) + 1, 9))
-    cells = lib().or_pass(_p(t), len(t), len(seqs), ctypes.cast(arr, c_void_p), _p(totals), int(nthreads))
+    fn = lib().or_pass
+    if totals is None:
+        totals = np.zeros((len(t) + 1, 9))
+    else:
+        assert totals.shape == (len(t) + 1, 9) and totals.dtype == np.float64 and totals.flags.c_contiguous
+        fn = lib().or_pass_continue
+    cells = fn(_p(t), len(t), len(seqs), ctypes.cast(arr, c_void_p), _p(totals), int(nthreads))
     if cells < 0:
         raise OracleError("oracle pass failed")
     return totals, int(cells)

@@ -528,13 +528,14 @@ int or_score_proposal(int kind, int pos, int base,
 }
 
 /* model.jl:385-399 */
-int or_score_total(int kind, int pos, int base, int nseqs,
-                   const double *const *As, const double *const *Bs,
-                   const or_seq *seqs, const double *Aref, const double *Bref,
-                   const or_seq *ref, const uint8_t *t, int m,
-                   double *newcols, double *total)
+/* the left fold of model.jl:389-397 continued from `score` (0.0 for a whole
+   batch; a running total when a batch is scored chunk by chunk) */
+static int score_fold(double score, int kind, int pos, int base, int nseqs,
+                      const double *const *As, const double *const *Bs,
+                      const or_seq *seqs, const double *Aref, const double *Bref,
+                      const or_seq *ref, const uint8_t *t, int m,
+                      double *newcols, double *total)
 {
-    double score = 0.0;
     for (int si = 0; si < nseqs; si++) {
         double sc;
         int err = or_score_proposal(kind, pos, base, As[si], Bs[si], t, m, &seqs[si], newcols, &sc);
@@ -551,6 +552,15 @@ int or_score_total(int kind, int pos, int base, int nseqs,
     }
     *total = score;
     return OR_OK;
+}
+
+int or_score_total(int kind, int pos, int base, int nseqs,
+                   const double *const *As, const double *const *Bs,
+                   const or_seq *seqs, const double *Aref, const double *Bref,
+                   const or_seq *ref, const uint8_t *t, int m,
+                   double *newcols, double *total)
+{
+    return score_fold(0.0, kind, pos, base, nseqs, As, Bs, seqs, Aref, Bref, ref, t, m, newcols, total);
 }
 
 /* model.jl:385-399 for a proposal list, proposals in parallel */
@@ -605,8 +615,27 @@ int or_score_list(int nprops, const int32_t *kind, const int32_t *pos, const int
 /* CPU baseline pass: realign (forward_moves! + backward!) every read, then
  * score the dense STAGE_SCORE all_proposals set (model.jl:401-456) with the
  * left-fold total of model.jl:385-399. */
+static int64_t pass_fold(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
+                         double *totals, int cont, int nthreads);
+
 int64_t or_pass(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
                 double *totals, int nthreads)
+{
+    return pass_fold(t, m, nseqs, seqs, totals, 0, nthreads);
+}
+
+/* or_pass over the next chunk of a batch: every proposal's fold continues
+   from totals[] (the previous chunks' running totals, in batch order), so a
+   batch too large to hold all its bands at once is folded chunk by chunk
+   with the reference's order and rounding */
+int64_t or_pass_continue(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
+                         double *totals, int nthreads)
+{
+    return pass_fold(t, m, nseqs, seqs, totals, 1, nthreads);
+}
+
+static int64_t pass_fold(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
+                         double *totals, int cont, int nthreads)
 {
     double **As = (double **)calloc((size_t)nseqs, sizeof(double *));
     double **Bs = (double **)calloc((size_t)nseqs, sizeof(double *));
@@ -646,24 +675,27 @@ int64_t or_pass(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
 #endif
             for (int p = 0; p <= m; p++) {
                 double *row = totals + (size_t)p * 9;
-                for (int k = 0; k < 9; k++)
+                double st[9];
+                for (int k = 0; k < 9; k++) {
+                    st[k] = cont ? row[k] : 0.0;
                     row[k] = -INFINITY;
+                }
                 for (int b = 0; b < 4 && p >= 1; b++) {
                     if (t[p - 1] == b)
                         continue;
-                    if (or_score_total(OR_SUB, p, b, nseqs, (const double *const *)As,
-                                       (const double *const *)Bs, seqs, NULL, NULL, NULL,
-                                       t, m, newcols, &row[b]))
+                    if (score_fold(st[b], OR_SUB, p, b, nseqs, (const double *const *)As,
+                                   (const double *const *)Bs, seqs, NULL, NULL, NULL,
+                                   t, m, newcols, &row[b]))
                         failed = 1;
                 }
-                if (p >= 1 && or_score_total(OR_DEL, p, 0, nseqs, (const double *const *)As,
-                                             (const double *const *)Bs, seqs, NULL, NULL, NULL,
-                                             t, m, newcols, &row[4]))
+                if (p >= 1 && score_fold(st[4], OR_DEL, p, 0, nseqs, (const double *const *)As,
+                                         (const double *const *)Bs, seqs, NULL, NULL, NULL,
+                                         t, m, newcols, &row[4]))
                     failed = 1;
                 for (int b = 0; b < 4; b++)
-                    if (or_score_total(OR_INS, p, b, nseqs, (const double *const *)As,
-                                       (const double *const *)Bs, seqs, NULL, NULL, NULL,
-                                       t, m, newcols, &row[5 + b]))
+                    if (score_fold(st[5 + b], OR_INS, p, b, nseqs, (const double *const *)As,
+                                   (const double *const *)Bs, seqs, NULL, NULL, NULL,
+                                   t, m, newcols, &row[5 + b]))
                         failed = 1;
             }
             free(newcols);

@@ -144,6 +144,9 @@ int or_score_list(int nprops, const int32_t *kind, const int32_t *pos, const int
 
 int64_t or_pass(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
                 double *totals, int nthreads);
+/* or_pass continuing every proposal's fold from totals[] (chunked batches) */
+int64_t or_pass_continue(const uint8_t *t, int m, int nseqs, const or_seq *seqs,
+                         double *totals, int nthreads);
 
 #ifdef __cplusplus
 }

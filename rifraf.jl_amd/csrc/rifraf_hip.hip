@@ -4208,6 +4208,11 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
     }
     CodeDict &D = ctx->codes;
     std::vector<CodeLut> lut(256);
+    // entries added by this call, dropped again if the dictionary fills up
+    // (the caller then uploads host tables; codes no sequence uses must not
+    // crowd out later uploads)
+    std::vector<CodeDict::K3> added3;
+    std::vector<uint64_t> added1;
     for (int c = 0; c < 256; ++c) {
         lut[c] = {lp_t[c], mt[c], 0, 0, 0, 0};
         if (!present[c])
@@ -4218,15 +4223,24 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
             i3 = (int32_t)D.t3.size();
             D.t3.emplace(key, (uint32_t)i3);
             D.t3v.insert(D.t3v.end(), {mt[c], mm[c], is[c], 0.0});
+            added3.push_back(key);
         }
         int32_t i1 = D.find1(CodeDict::bits(dl[c]));
         if (i1 < 0 && D.d1.size() < (size_t)RF_CODES) {
             i1 = (int32_t)D.d1.size();
             D.d1.emplace(CodeDict::bits(dl[c]), (uint32_t)i1);
             D.d1v.push_back(dl[c]);
+            added1.push_back(CodeDict::bits(dl[c]));
         }
-        if (i3 < 0 || i1 < 0)   // dictionary full: the caller uploads host tables instead
+        if (i3 < 0 || i1 < 0) {   // dictionary full: the caller uploads host tables instead
+            for (const auto &k : added3)
+                D.t3.erase(k);
+            for (const auto &k : added1)
+                D.d1.erase(k);
+            D.t3v.resize(D.t3v.size() - 4 * added3.size());
+            D.d1v.resize(D.d1v.size() - added1.size());
             return fail(ctx, RF_ERR_STATE, "rf_set_sequences_codes: row-code dictionary full");
+        }
         lut[c].id3 = i3;
         lut[c].id1 = i1;
     }

@@ -469,6 +469,17 @@ def _wave_native(part, params, engine):
         H = 2 * params.bandwidth + np.abs(ln - m) + 1
         band = (H + 2 * m) * band_stride(H, pad_h=1) * 8   # upper bound: padded rows
         est_bytes += int(np.sort(band)[::-1][:nb[k]].sum()) * 2
+        L = len(refs_in[k])
+        if L > 0:
+            # reference-guided cluster (_native_refs): the reference's A and B
+            # at the read bandwidth, and the scratch slot's forward band, which
+            # at FRAME entry holds edit_distance's band at bw = ceil(min / 2)
+            # (align.jl:253-260) -- it grows with the square of the length
+            Hr = 2 * params.bandwidth + abs(L - m) + 1
+            est_bytes += 2 * (Hr + 2 * m) * band_stride(Hr, pad_h=1) * 8
+            bwe = -(-min(L, m) // 2)
+            He = 2 * bwe + abs(L - m) + 1
+            est_bytes += (He + 2 * m) * band_stride(He, pad_h=1) * 8
     # a new wave rewrites every slot it uses: the previous wave's bands are
     # dropped and the arena is reused (sized once for a steady stream of waves)
     if hasattr(engine, "release_bands"):

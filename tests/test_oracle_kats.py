@@ -341,3 +341,23 @@ def test_oracle_pass_matches_scalar():
         if pos >= 1:
             assert totals[pos, 4] == oracle.score_total((2, pos, 0), As, Bs, reads, t)
     assert cells > 0
+
+
+def test_cpu_pass_continues_the_fold_chunk_by_chunk():
+    """oracle.cpu_pass(totals=...) continues every proposal's left fold from
+    the running totals, so chunked folds equal the whole-batch fold bit for bit
+    (model.jl:389-397) -- the full-size c5 parity test relies on it."""
+    import numpy as np
+    import oracle
+    from rifraf_amd import ErrorModel, RifrafSequence, Scores
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(3)
+    _, t, _, reads, _, ph, _, _ = sample_sequences(12, 200, error_rate=0.03, rng=rng)
+    sc = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0))
+    seqs = [RifrafSequence(r, p, 9, sc) for r, p in zip(reads, ph)]
+    whole, _ = oracle.cpu_pass(t, seqs, nthreads=2)
+    tot, _ = oracle.cpu_pass(t, seqs[:5], nthreads=2)
+    oracle.cpu_pass(t, seqs[5:9], nthreads=2, totals=tot)
+    oracle.cpu_pass(t, seqs[9:], nthreads=2, totals=tot)
+    assert np.array_equal(whole, tot)
+    assert np.isfinite(whole).sum() == 8 * len(t) + 4

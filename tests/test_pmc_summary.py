@@ -92,3 +92,19 @@ def test_main_doubles_fetch(tmp_path):
     assert res["k_score"]["fetch_bytes"] == 2 * 1024 * 40.0     # KiB -> bytes, x2 (gfx950)
     assert res["k_score"]["write_bytes"] == 1024 * 40.0
     assert res["k_dp"]["hbm_bytes_per_launch"] == 2 * 1024 * 10.0 + 1024 * 10.0
+
+
+def test_bench_quotes_traffic_at_the_profiled_size():
+    """bench.py's roofline.traffic comes from profiles/pmc_<config>.json only
+    when that profile was taken at the run's size: clusters per rank (c4),
+    reads per rank (c5; round 3 compared 5000 reads with 'clusters': 1)."""
+    import json
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    for cfg, key in (("c4", "clusters"), ("c5", "reads")):
+        pm = json.load(open(os.path.join(REPO, "profiles", f"pmc_{cfg}.json")))
+        size = pm[key]
+        got = bench.pmc_traffic(cfg, size, "k_score")
+        assert got == pm["kernels"]["k_score"]["hbm_bytes_per_launch"]
+        assert bench.pmc_traffic(cfg, size + 1, "k_score") is None

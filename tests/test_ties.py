@@ -9,6 +9,11 @@ engine (Python stage machine and the native driver alike) uses the sorted
 These tests pin that behaviour on a cluster with seven tied
 homopolymer-equivalent insertions, and check that every tied choice yields
 the same consensus, so for such ties the order cannot change the result.
+
+The fixture is a self-consistency pin (made by this repo's oracle engine),
+not reference parity: the tie-break the reference's Set order would make is
+unpinned.  The parity-relevant assertion is that every tied choice yields
+the same consensus (test_every_tied_choice_gives_the_same_consensus).
 """
 import json
 import os

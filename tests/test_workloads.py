@@ -213,3 +213,70 @@ def test_c5_sample_band_doubling_and_scores(engine, nreads):
     ref, _ = oracle.cpu_pass(t, rh, nthreads=NTHREADS)
     g, e = _masked(got, ref, t)
     np.testing.assert_array_equal(g, e)
+
+
+def _progress(msg):
+    """A line per stage under gpurun_out/ (a long test keeps the GPU call's
+    output moving; captured stdout would not)."""
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "c5_full_parity.log"), "a") as f:
+            f.write(msg + "\n")
+    except OSError:
+        pass
+
+
+@pytest.mark.timeout(600)
+def test_c5_full_cluster_dense_bitexact():
+    """The bench's whole c5 cluster (5,000 reads x 10 kb, 3 % error) at its
+    final bandwidths: band doubling on the GPU (smart_forward_moves!,
+    model.jl:643-672), fwd + bwd DP, and the dense fold of all 80,004
+    STAGE_SCORE proposals over all 5,000 reads -- the split-mode scorer plus
+    its cross-read fold, exactly the path bench --config c5 times -- against
+    oracle.cpu_pass folding the same reads in batch order (model.jl:385-399),
+    chunk by chunk (oracle.cpu_pass(totals=...) continues the fold), on every
+    core.  Bit-exact."""
+    import time
+    import bench
+    from rifraf_amd.bandedarrays import BAND_PAD_H
+    from rifraf_amd.engine import Engine
+    t0 = time.time()
+    t, reads = bench.make_read_shard(5000, 10000, 0.03, 9, 2024, 0, 5000)
+    m = len(t)
+    n = len(reads)
+    _progress(f"generated {n} reads in {time.time() - t0:.0f} s")
+    e = Engine(0)
+    try:
+        e.reserve(sum(bench.band_bytes(len(r), m, 9) + bench.band_bytes(len(r), m, 18, pad=True) for r in reads)
+                  + (256 << 20))
+        for a in range(0, n, 1024):
+            e.set_sequences(a, reads[a:a + 1024])
+        e.set_templates(0, [t])
+        smart_forward_moves(SimpleNamespace(e=e), [(k, k) for k in range(n)], reads, m, 0.1)
+    finally:
+        e.close()
+    bws = [r.bandwidth for r in reads]
+    assert sum(b > 9 for b in bws) >= n // 2
+    _progress(f"band doubling done, {sum(b > 9 for b in bws)} reads doubled")
+    e = Engine(0)
+    try:
+        pad = max(2 * r.bandwidth + abs(len(r) - m) + 1 for r in reads) >= BAND_PAD_H
+        e.reserve(sum(2 * bench.band_bytes(len(r), m, r.bandwidth, pad) for r in reads) + (256 << 20))
+        for a in range(0, n, 1024):
+            e.set_sequences(a, reads[a:a + 1024])
+        e.set_templates(0, [t])
+        e.realign(np.arange(n), np.arange(n), 0, bws, RF_FWD | RF_BWD)
+        got = e.score_dense([np.arange(n)])[0]
+    finally:
+        e.close()
+    _progress(f"GPU pass done at {time.time() - t0:.0f} s")
+    ref = None
+    for a in range(0, n, 400):
+        if ref is None:
+            ref, _ = oracle.cpu_pass(t, reads[a:a + 400], nthreads=NTHREADS)
+        else:
+            oracle.cpu_pass(t, reads[a:a + 400], nthreads=NTHREADS, totals=ref)
+        _progress(f"oracle reads {a}..{min(a + 400, n)} folded at {time.time() - t0:.0f} s")
+    g, x = _masked(got, ref, t)
+    np.testing.assert_array_equal(g, x)
