@@ -2333,6 +2333,498 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------
+// k_score_segw: k_score_segl over 128-column work items (round 4, default)
+//
+// A segment of k_score_segl's 64-column item reads 160 kappa rows for 128
+// rows' worth of cells: its first and last 32 rows are shared with the
+// neighbouring items (1.25x the algorithmic bytes, PMC 1.23-1.27x fetched).
+// Here one wave owns 128 columns [a0, a0 + 128) and scores each segment in
+// two halves of 64 columns, one after the other, through the same 39 KB LDS
+// slice: half 0 loads kappa rows [kb, kb + 160), half 1 needs
+// [kb + 128, kb + 288), whose first 32 rows are half 0's last 32 -- they
+// stay in the prefetch registers (rows j in [NUA - 4, NUA) move to j in
+// [0, 4)) and only 128 rows are loaded.  288 rows per 256 rows of cells:
+// 1.125x.  Each lane carries the chain state of two columns (a0 + tid and
+// a0 + 64 + tid); LDS row 0 (diagonal D - 1) of each half is the half's own
+// previous segment, kept in registers while the other half uses the slice.
+// Same chains, operands, FP64 order and fold as k_score_segl: identical
+// results.  SPLIT selects the per-read partial output (k_reduce folds) at
+// compile time, so the fused kernel carries no partial-write code and the
+// split kernel no running totals.
+// ---------------------------------------------------------------------
+template <int SEGS, bool SPLIT>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
+             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
+             const double *__restrict__ tabs, const double *__restrict__ bands,
+             double *__restrict__ dense, double *__restrict__ split, int diag_mode, int rchunk)
+{
+    using Gm = SeglGeo<SEGS>;
+    constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
+    constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
+    constexpr int NCAR = S / RPI;   // prefetch rows carried from half 0 to half 1
+    static_assert(NUA * RPI == 128 + S && NCAR * RPI == S, "segment geometry");
+
+    constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
+    __shared__ __attribute__((aligned(16))) double sA[SL];
+    __shared__ __attribute__((aligned(16))) double sB[SL];
+    __shared__ __attribute__((aligned(16))) dvec2 sT0[NT], sT1[NT], sT2[NT];
+    const int nx = gridDim.x;
+    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
+    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
+    const int cell = x * xq + min(x, xr) + (lin >> 3);
+    const int bx = cell % nx, by = cell / nx;
+    const WorkItem wi = items[bx];
+    const ScoreGroup G = groups[wi.group];
+    const int m = G.m;
+    const int a0 = wi.p0;
+    const int tid = threadIdx.x;
+    int r0 = G.r0, r1 = G.r1;
+    if (SPLIT) {
+        r0 = G.r0 + by * rchunk;
+        if (r0 >= G.r1)
+            return;
+        r1 = min(r0 + rchunk, G.r1);
+    }
+    // the lane's two columns
+    struct Lane {
+        int a;
+        bool active, hasS, all_act;
+        double smask;
+    };
+    Lane hl[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        hl[h].a = a0 + 64 * h + tid;
+        hl[h].active = hl[h].a <= m;
+        hl[h].hasS = hl[h].a < m;
+        hl[h].smask = hl[h].hasS ? 0.0 : -RF_INF;
+        hl[h].all_act = __all(hl[h].active) && __all(hl[h].hasS);
+    }
+    // a wave with no column writes nothing; half 1 is skipped when it has none
+    if (!__any(hl[0].active))
+        return;
+    const int NH = __any(hl[1].active) ? 2 : 1;
+    // aligned-row loader lane roles: row r8 + RPI j, 16-B chunk cc8 of the row piece
+    const int r8 = tid / CPR, cc8 = tid % CPR, p8 = r8 & 1;
+    struct RG {
+        const double *gA;
+        const double *tm;
+        const uint8_t *sq;
+        int64_t dB;
+        int c, P, K, n;
+        int dfirst[2], dlast[2];   // this lane's chain rows (band diagonals) per half
+        bool peel[2];
+        int dlo, dhi;              // wave-wide over both halves
+        int dfmax[2], dlmin[2];    // wave-wide per half
+    };
+    auto setup = [&](int r, RG &g) {
+        const ScoreRead R = reads[r];
+        g.c = R.c;
+        g.P = R.P;
+        g.K = R.K;
+        g.n = R.n;
+        g.gA = bands + R.A;
+        g.dB = R.B - R.A;
+        g.tm = tabs + R.tab;
+        g.sq = bases + R.sb;
+        int dlo = INT_MAX, dhi = -1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int a = hl[h].a;
+            const int jn = min(a + 1, m);
+            const int i0 = max(0, jn - g.c);
+            const int i1 = min(jn + R.vb, g.n);
+            const int ilast = min(i1, a + R.vb);
+            g.dfirst[h] = i0 - a + g.c;
+            g.dlast[h] = ilast - a + g.c;
+            g.peel[h] = i1 > ilast;
+            const bool act = hl[h].active && h < NH;
+            dlo = min(dlo, act ? g.dfirst[h] : INT_MAX);
+            dhi = max(dhi, act ? g.dlast[h] + (g.peel[h] ? 1 : 0) : -1);
+            int dfmax = act ? g.dfirst[h] : INT_MAX, dlmin = act ? g.dlast[h] : -1;
+            for (int off = 32; off >= 1; off >>= 1) {
+                dfmax = max(dfmax, __shfl_xor(dfmax, off));
+                dlmin = min(dlmin, __shfl_xor(dlmin, off));
+            }
+            g.dfmax[h] = __builtin_amdgcn_readfirstlane(dfmax);
+            g.dlmin[h] = __builtin_amdgcn_readfirstlane(dlmin);
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            dlo = min(dlo, __shfl_xor(dlo, off));
+            dhi = max(dhi, __shfl_xor(dhi, off));
+        }
+        g.dlo = __builtin_amdgcn_readfirstlane(dlo);
+        g.dhi = __builtin_amdgcn_readfirstlane(dhi);
+    };
+    struct SegSet {
+        dvec2 ra[NUA], rb[NUA];
+        double tmt[2], tmm[2], tin[2], tdl[2];
+        int tsb[2];
+        double z0a, z0b, z1a, z1b;
+    };
+    // loads of half h of segment D of read g (registers only); half 1 takes
+    // its first NCAR row groups from half 0's last, already in X
+    auto load_seg = [&](SegSet &X, const RG &g, int D, int h, bool first) {
+        const int a0h = a0 + 64 * h;
+        const int kb = D + 2 * a0h, eh = D >> 1;
+        if ((g.P & 15) == 0) {
+            if (h == 0) {
+#pragma unroll
+                for (int j = 0; j < NUA; ++j) {
+                    const int kap = min(kb + r8 + RPI * j, g.K - 1);
+                    const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
+                    X.ra[j] = *(const dvec2 *)(g.gA + o);
+                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NCAR; ++j) {
+                    X.ra[j] = X.ra[j + NUA - NCAR];
+                    X.rb[j] = X.rb[j + NUA - NCAR];
+                }
+#pragma unroll
+                for (int j = NCAR; j < NUA; ++j) {
+                    const int kap = min(kb + r8 + RPI * j, g.K - 1);
+                    const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
+                    X.ra[j] = *(const dvec2 *)(g.gA + o);
+                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+                }
+            }
+        }
+        if (first && D > 0) {
+            // diagonal D-1 of columns a0h .. a0h+64 (the previous segment's last row)
+            const int kap = min(D - 1 + 2 * (a0h + tid), g.K - 1);
+            const int64_t o = (int64_t)kap * g.P + ((D - 1) >> 1);
+            X.z0a = g.gA[o];
+            X.z0b = g.gA[g.dB + o];
+            if (tid == 0) {
+                const int kap1 = min(D - 1 + 2 * (a0h + 64), g.K - 1);
+                const int64_t o1 = (int64_t)kap1 * g.P + ((D - 1) >> 1);
+                X.z1a = g.gA[o1];
+                X.z1b = g.gA[g.dB + o1];
+            }
+        }
+        const int ib = a0h - g.c + D;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = min(max(ib + tid + 64 * u, 0), g.n);
+            const int ks = max(i - 1, 0);
+            X.tsb[u] = g.sq[ks];   // read row 0 (the gap) is selected at the store
+            X.tmt[u] = g.tm[ks];
+            X.tmm[u] = g.tm[g.n + ks];
+            X.tin[u] = g.tm[2 * (size_t)g.n + ks];
+            X.tdl[u] = g.tm[3 * (size_t)g.n + i];
+        }
+    };
+    auto store_seg = [&](const SegSet &X, const RG &g, int D, int h) {
+        const int a0h = a0 + 64 * h;
+        if ((g.P & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < NUA; ++j) {
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int ddl = 4 * cc8 + 2 * hh + p8;      // d - D
+                    const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0h
+                    const double v = hh ? X.ra[j].y : X.ra[j].x, w = hh ? X.rb[j].y : X.rb[j].x;
+                    const int l = (ddl + 1) * LS + col;
+                    if ((j * RPI >= S && (j + 1) * RPI <= 128) || (col >= 0 && col <= 64)) {
+                        sA[l] = v;
+                        sB[l] = w;
+                    }
+                }
+            }
+        } else {
+            // odd-stride rows: NC pair-aligned chunks per row, loaded here
+            const int kb = D + 2 * a0h, eh = D >> 1;
+#pragma unroll 1
+            for (int j0 = 0; j0 < NUG; j0 += 4) {
+                dvec2 ga[4], gb[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int t = min(tid + 64 * (j0 + jj), Gm::NROW * NC - 1);
+                    const int rr = t / NC, cc = t - NC * rr;
+                    const int kap = min(kb + rr, g.K - 1);
+                    const int o = ((kap * g.P + eh) & ~1) + 2 * cc;
+                    ga[jj] = *(const dvec2 *)(g.gA + o);
+                    gb[jj] = *(const dvec2 *)(g.gA + g.dB + o);
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int t = tid + 64 * (j0 + jj);
+                    const int rr = t / NC, cc = t - NC * rr;
+                    const int sh = (kb + rr + eh) & 1;   // P odd
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const int xl = 2 * cc + hh - sh;
+                        const int ddl = 2 * xl + (rr & 1);
+                        const int col = (rr - ddl) >> 1;
+                        if (t < Gm::NROW * NC && xl >= 0 && xl < S / 2 && col >= 0 && col <= 64) {
+                            const int l = (ddl + 1) * LS + col;
+                            sA[l] = hh ? ga[jj].y : ga[jj].x;
+                            sB[l] = hh ? gb[jj].y : gb[jj].x;
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+        }
+        const int ib = a0h - g.c + D;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int t = tid + 64 * u;
+            if (t < NT) {
+                const int sb = ib + t >= 1 ? X.tsb[u] : 4;
+                const double mt = X.tmt[u], mm = X.tmm[u];
+                sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
+                sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
+                sT2[t] = dvec2{X.tin[u], X.tdl[u]};
+            }
+        }
+    };
+    const bool do_load = !(diag_mode & 4);
+    double prev[2][4], accI[2][4], accS[2][4], dd[2];
+    double tI[2][4], tS[2][4], tD[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        dd[h] = -RF_INF;
+        tD[h] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            prev[h][k] = accI[h][k] = accS[h][k] = -RF_INF;
+            tI[h][k] = tS[h][k] = 0.0;
+        }
+    }
+    // the chains of half H of segment D of read g (operands from LDS)
+    auto chains = [&](auto hc, const RG &g, int D) {
+        constexpr int H = decltype(hc)::value;
+        const Lane &L = hl[H];
+        const int a = L.a;
+        const int c = g.c, dfirst = g.dfirst[H], dlast = g.dlast[H];
+        const int dfmax = g.dfmax[H], dlmin = g.dlmin[H];
+        const bool peel = g.peel[H];
+        double(&pv)[4] = prev[H];
+        double(&aI)[4] = accI[H];
+        double(&aS)[4] = accS[H];
+        double &ddh = dd[H];
+        if (L.active && !(diag_mode & 2)) {
+            const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
+            const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];
+            double aprev = (lo <= hi && lo >= 1 && a - c + lo >= 1) ? a0v : -RF_INF;
+            const double *pA = sA + LS + tid;
+            const double *pB = sB + LS + tid;
+            const double *pS = sB + tid + 1;
+            const dvec2 *q0 = sT0 + tid, *q1 = sT1 + tid, *q2 = sT2 + tid;
+            struct Ops {
+                double ac, bI, bs;
+                dvec2 u0, u1, u2;
+            };
+            auto ld = [&](int s) {
+                Ops o;
+                o.ac = pA[s * LS];
+                o.bI = pB[s * LS];
+                o.bs = pS[s * LS];
+                o.u0 = q0[s];
+                o.u1 = q1[s];
+                o.u2 = q2[s];
+                return o;
+            };
+            auto stp = [&](const Ops &o, auto alls) {
+                const double bS = ((decltype(alls)::value || L.hasS) ? o.bs : o.bI) + L.smask;
+                const double sub[4] = {o.u0.x, o.u0.y, o.u1.x, o.u1.y};
+                const double dl = o.ac + o.u2.y;
+                const double dsum = o.ac + bS;
+                chain_row(aprev, sub, o.u2.x, dl, o.bI, bS, pv, aI, aS);
+                ddh = vmax(ddh, dsum);
+                aprev = o.ac;
+            };
+            if (L.all_act && dfmax <= D && dlmin >= D + S - 1) {
+                Ops cur = ld(0);
+#pragma unroll SEGL_UNROLL
+                for (int s = 0; s < S; ++s) {
+                    const Ops nxt = ld(s + 1 < S ? s + 1 : s);
+                    SEGL_FENCE();
+                    stp(cur, std::true_type{});
+                    cur = nxt;
+                }
+            } else {
+                const int slo = max(lo - D, 0), shi = hi - D;
+                if (slo <= shi) {
+                    Ops cur = ld(slo);
+                    for (int s = slo; s <= shi; ++s) {
+                        const Ops nxt = ld(s < shi ? s + 1 : s);
+                        SEGL_FENCE();
+                        stp(cur, std::false_type{});
+                        cur = nxt;
+                    }
+                }
+                const int dp = dlast + 1;
+                if (peel && dp >= D && dp < D + S) {
+                    const int sp = dp - D;
+                    const double ap = sA[sp * LS + tid];
+                    const double bSr = sB[sp * LS + tid + 1];
+                    const dvec2 u0 = sT0[tid + sp], u1 = sT1[tid + sp], u2 = sT2[tid + sp];
+                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        aS[k] = vmax(aS[k], vmax(ap + sub[k], pv[k] + u2.x) + bSr);
+                }
+            }
+        }
+    };
+    // read r's totals (after its last segment) and fresh chain state
+    auto finish = [&](int r) {
+        const double qnan = __builtin_nan("");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h < NH && hl[h].active) {
+                const int a = hl[h].a;
+                if (SPLIT) {
+                    double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        dst[5 + k] = accI[h][k] == -RF_INF ? qnan : accI[h][k];
+                    if (a < m) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            dst[9 + k] = accS[h][k] == -RF_INF ? qnan : accS[h][k];
+                        dst[13] = dd[h];
+                    }
+                    if (a == 0) {
+#pragma unroll
+                        for (int k = 0; k < 5; ++k)
+                            dst[k] = qnan;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        tI[h][k] += accI[h][k] == -RF_INF ? qnan : accI[h][k];
+                        tS[h][k] += accS[h][k] == -RF_INF ? qnan : accS[h][k];
+                    }
+                    tD[h] += dd[h];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                prev[h][k] = accI[h][k] = accS[h][k] = -RF_INF;
+            dd[h] = -RF_INF;
+        }
+    };
+    // units (read, segment, half) as one stream: the register prefetch
+    // always holds the next unit
+    struct Pos {
+        int r, D, h;
+        RG g;
+    };
+    auto first_of = [&](const RG &g) { return g.dlo & ~(S - 1); };
+    auto adv = [&](Pos &p) {
+        if (p.h + 1 < NH) {
+            ++p.h;
+        } else {
+            p.h = 0;
+            if (p.D + S > p.g.dhi) {
+                ++p.r;
+                if (p.r < r1) {
+                    setup(p.r, p.g);
+                    p.D = first_of(p.g);
+                }
+            } else {
+                p.D += S;
+            }
+        }
+    };
+    // LDS row S of each half's last scored segment (its next segment's row 0)
+    double svA[2] = {0.0, 0.0}, svB[2] = {0.0, 0.0}, svA6[2] = {0.0, 0.0}, svB6[2] = {0.0, 0.0};
+    int held = -1;   // half whose segment the LDS slice holds
+    auto unit = [&](SegSet &X, Pos &cur) {
+        const int D = cur.D, h = cur.h;
+        const bool first = D == first_of(cur.g);
+        wave_sync();   // previous unit's chains are done with LDS
+        if (held >= 0) {
+            const double va = sA[S * LS + tid], vb = sB[S * LS + tid];
+            const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
+            if (held == 0) {
+                svA[0] = va; svB[0] = vb; svA6[0] = va6; svB6[0] = vb6;
+            } else {
+                svA[1] = va; svB[1] = vb; svA6[1] = va6; svB6[1] = vb6;
+            }
+        }
+        // LDS row 0 = diagonal D-1: prefetched for a read's first segment, else
+        // the half's previous segment's row S
+        if (first) {
+            if (D > 0) {
+                sA[tid] = X.z0a;
+                sB[tid] = X.z0b;
+                if (tid == 0) {
+                    sA[64] = X.z1a;
+                    sB[64] = X.z1b;
+                }
+            }
+        } else {
+            const double va = h ? svA[1] : svA[0], vb = h ? svB[1] : svB[0];
+            const double va6 = h ? svA6[1] : svA6[0], vb6 = h ? svB6[1] : svB6[0];
+            sA[tid] = va;
+            sB[tid] = vb;
+            if (tid == 0) {
+                sA[64] = va6;
+                sB[64] = vb6;
+            }
+        }
+        store_seg(X, cur.g, D, h);
+        wave_sync();
+        held = h;
+        Pos ahead = cur;
+        if (ahead.r < r1)
+            adv(ahead);
+        if (do_load && ahead.r < r1)
+            load_seg(X, ahead.g, ahead.D, ahead.h, ahead.D == first_of(ahead.g));
+        if (h == 0)
+            chains(std::integral_constant<int, 0>{}, cur.g, D);
+        else
+            chains(std::integral_constant<int, 1>{}, cur.g, D);
+        if (h + 1 == NH && D + S > cur.g.dhi)
+            finish(cur.r);
+        cur = ahead;
+    };
+    Pos cur;
+    cur.r = r0;
+    cur.h = 0;
+    if (r0 < r1) {
+        setup(r0, cur.g);
+        cur.D = first_of(cur.g);
+    }
+    SegSet X0;
+    if (r0 < r1 && do_load)
+        load_seg(X0, cur.g, cur.D, 0, true);
+    while (cur.r < r1)
+        unit(X0, cur);
+    if (SPLIT)
+        return;
+    const double qnan = __builtin_nan("");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h < NH && hl[h].active) {
+            const int a = hl[h].a;
+            double *dst = dense + G.dense_off + (size_t)a * 9;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                dst[5 + k] = tI[h][k];
+            if (a < m) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    dst[9 + k] = tS[h][k];
+                dst[13] = tD[h];
+            }
+            if (a == 0) {
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    dst[k] = qnan;
+            }
+        }
+    }
+}
+
 // Read-bandwidth probe over the band arena (calibrates the HBM roofline of
 // the scorer on the same allocation): grid-stride 16-B loads, 8 in flight.
 __global__ void __launch_bounds__(256) k_probe_stream(const dvec2 *__restrict__ src, int64_t n16,
@@ -3187,9 +3679,12 @@ struct Slot {
 // Choice of dense scorer for one launch.
 struct ScorePick {
     bool lean = false;
-    bool seg = false;   // k_score_segl: wide bands (window too large for LDS), finite tables
+    bool seg = false;   // k_score_segw / k_score_segl: wide bands (window too large for LDS), finite tables
+    int segq = 128;     // seg: columns per work item (128: k_score_segw, 64: k_score_segl)
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
     int q() const { return 256; }   // k_score_ws chain columns per work item
+    // columns per work item of the chosen scorer (k_score: 64)
+    int cols() const { return lean ? q() : seg ? segq : 64; }
 };
 
 struct DevBuf {
@@ -3335,6 +3830,7 @@ struct Opts {
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
+    int seg_cols = 128;     // RF_OPT_SEG_COLS: wide-band scorer columns per work item (128 segw, 64 segl)
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -3647,6 +4143,7 @@ void load_env_opts(Opts &o)
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
+    o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -3675,6 +4172,7 @@ ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool a
     // wide bands: the row-segment scorer (same chains, H-independent LDS)
     if (all_finite && !force_general && !reads.empty()) {
         p.seg = true;
+        p.segq = o.seg_cols == 64 ? 64 : 128;
         return p;
     }
     p.lds = score_lds_elems(reads);
@@ -3716,8 +4214,15 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
             rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
-        hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                           d_tabs, d_bands, dense, split, sm, rchunk);
+        if (pk.segq == 64)
+            hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
+                               d_tabs, d_bands, dense, split, sm, rchunk);
+        else if (split)
+            hipLaunchKernelGGL((k_score_segw<32, true>), grid, dim3(64), 0, ctx->stream, items, groups, reads,
+                               d_bases, d_tabs, d_bands, dense, split, sm, rchunk);
+        else
+            hipLaunchKernelGGL((k_score_segw<32, false>), grid, dim3(64), 0, ctx->stream, items, groups, reads,
+                               d_bases, d_tabs, d_bands, dense, split, sm, rchunk);
     } else if (!pk.lean) {
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
@@ -3834,6 +4339,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
     case RF_OPT_DP_WIDE: return &o.dp_wide;
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
+    case RF_OPT_SEG_COLS: return &o.seg_cols;
     default: return nullptr;
     }
 }
@@ -5120,8 +5626,8 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
         split = true;
 
     const ScorePick pick = pick_scorer(ctx->opt, reads, all_finite);
-    if (pick.lean && pick.q() != 64)
-        items = make_items(groups, pick.q());
+    if (pick.cols() != 64)
+        items = make_items(groups, pick.cols());
 
     std::vector<int32_t> pgroup(nprops);
     for (int32_t g = 0; g < ngroups; ++g)
@@ -5329,8 +5835,8 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             gstart[g] = groups[g].dense_off;
         gstart[ngroups] = dense_total;
         P.pick = pick_scorer(ctx->opt, reads, all_finite);
-        if (P.pick.lean && P.pick.q() != 64)
-            items = make_items(groups, P.pick.q());
+        if (P.pick.cols() != 64)
+            items = make_items(groups, P.pick.cols());
         if (int e = upload(ctx, ctx->scratch[11], items)) return e;
         if (int e = upload(ctx, ctx->scratch[12], groups)) return e;
         if (int e = upload(ctx, ctx->scratch[13], reads)) return e;

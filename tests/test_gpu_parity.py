@@ -456,9 +456,12 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (score_kernel, lean_lds_kb) engine options
     ("general", None),
-    ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segl
-    ("seglodd", None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
-    ("seglpad", None),   # k_score_segl with every band line-padded (band_pad 1)
+    ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segw (128 columns)
+    ("seglodd", None),   # k_score_segw over odd-stride rows only (band_pad 0: 9-chunk loader)
+    ("seglpad", None),   # k_score_segw with every band line-padded (band_pad 1)
+    ("seg64", None),     # the same three on 64-column items: k_score_segl (RF_OPT_SEG_COLS 64)
+    ("seglodd64", None),
+    ("seglpad64", None),
     (None, None),        # k_score_ws (the default for these shapes)
     (None, "8"),         # windows exceed the budget: sub-passes over fewer lanes
     (None, "12"),
@@ -471,9 +474,13 @@ SCORER_CONFIGS = [
 @pytest.mark.parametrize("kern,lds", SCORER_CONFIGS)
 @pytest.mark.parametrize("mode", ["fused", "split"])
 def test_score_dense_kernels(engine, opts, kern, lds, mode):
-    """The dense scorers (general, k_score_ws, k_score_segl) over ragged
-    clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the oracle."""
+    """The dense scorers (general, k_score_ws, k_score_segw, k_score_segl) over
+    ragged clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs
+    the oracle."""
     pad = 64
+    if kern and kern.endswith("64"):
+        opts("seg_cols", 64)
+        kern = kern[:-2]
     if kern in ("seglodd", "seglpad"):
         pad = 0 if kern == "seglodd" else 1
         kern = "seg"
@@ -548,14 +555,19 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "general"])
+@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "general",
+                                  "segl64", "seglodd64", "seglmix64"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    line-aligned row-segment scorer k_score_segl (default; line-padded rows,
-    odd-stride rows, both in one launch) and the in-place k_score ("general")
-    are bit-exact against the oracle."""
+    line-aligned row-segment scorers k_score_segw (default, 128-column items)
+    and k_score_segl (64-column items, "...64") on line-padded rows,
+    odd-stride rows and both in one launch, and the in-place k_score
+    ("general"), are bit-exact against the oracle."""
     opts("band_pad", 64)
+    if kern and kern.endswith("64"):
+        opts("seg_cols", 64)
+        kern = None if kern == "segl64" else kern[:-2]
     if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
     elif kern in ("seglodd", "seglpad"):
