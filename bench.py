@@ -352,6 +352,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="c4 only: skip the secondary c5 (10 kb, band doubling) workload")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="c4 only: skip the c3 field (configs[2] run with the reference's codon moves)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--e2e-clusters", type=int, default=512,
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
@@ -408,6 +410,10 @@ def main():
         result = run_clusters(args, rank, world, gpu, dist, torch, coll)
         if args.config == "c4" and args.e2e_clusters > 0:
             result["e2e"] = run_e2e(args, rank, world, gpu, dist, coll)
+        if args.config == "c4" and not args.no_c3 and rank == 0:
+            # configs[2] beside the headline line: the reference-informed path
+            # (FRAME, codon moves) end to end, rank 0 only (one cluster)
+            result["c3"] = run_c3(args, gpu)
         if args.config == "c4" and not args.no_secondary:
             # configs[4] beside the headline line: driver-measured 10 kb reads
             # with band doubling, read-sharded over the same ranks
@@ -651,6 +657,157 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         result["parity"] = parity_check(dense[:len(ref)], ref, [t for t, _ in clusters[:len(ref)]])
     eng.close()
     return result
+
+
+C3_SEED = 3   # the c3 parity tests' cluster (tests/test_workloads.py::test_c3_*)
+
+
+def c3_cluster(seed=C3_SEED):
+    """configs[2]: sample_sequences(1000, 2601; error_rate=0.01,
+    ref_error_rate=0.1, ref_errors=ErrorModel(10,0,0,1,1)) with a one-base
+    frameshift in the reference, so that FRAME runs (codon scoring of the
+    reference, seeded indel proposals, penalty increases)."""
+    from rifraf_amd import ErrorModel
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    ref, template, _, reads, _, phreds, _, _ = sample_sequences(
+        1000, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+    ref = np.concatenate([ref[:1300], ref[1301:2000], [2], ref[2000:]]).astype(np.uint8)
+    return template, reads, phreds, ref
+
+
+class _StageTimer:
+    """Engine proxy for one rifraf() run: kernel milliseconds of every engine
+    call (HIP events on the engine stream), DP cells and proposals scored,
+    attributed to the stage / iteration the stage machine is in
+    (rifraf_amd.model.ITERATION_HOOK)."""
+
+    def __init__(self, eng):
+        self.e = eng
+        self.lens, self.tlen = {}, {}
+        self.key = ("INIT", 0)
+        self.rec = {}
+
+    def __getattr__(self, name):
+        return getattr(self.e, name)
+
+    def hook(self, it, stage):
+        self.key = (stage.name, it)
+
+    def _add(self, **kw):
+        r = self.rec.setdefault(self.key, {})
+        for k, v in kw.items():
+            r[k] = r.get(k, 0) + v
+
+    def set_sequences(self, first, seqs):
+        for k, s in enumerate(seqs):
+            self.lens[first + k] = len(s)
+        return self.e.set_sequences(first, seqs)
+
+    def set_templates(self, first, tpls):
+        for k, t in enumerate(tpls):
+            self.tlen[first + k] = len(t)
+        return self.e.set_templates(first, tpls)
+
+    def realign(self, slots, seqs, tpls, bws, flags):
+        out = self.e.realign(slots, seqs, tpls, bws, flags)
+        n = len(np.atleast_1d(slots))
+        sq = np.broadcast_to(seqs, (n,))
+        tp = np.broadcast_to(tpls, (n,))
+        bw = np.broadcast_to(bws, (n,))
+        from rifraf_amd.engine import RF_BWD, RF_FWD
+        dirs = int(bool(flags & RF_FWD)) + int(bool(flags & RF_BWD))
+        cells = dirs * sum(band_cells(self.lens[int(a)], self.tlen[int(b)], int(c)) for a, b, c in zip(sq, tp, bw))
+        self._add(dp_ms=self.e.last_timing()[0], dp_cells=cells, realign_calls=1)
+        return out
+
+    def backtrace(self, slots, want_moves=True):
+        out = self.e.backtrace(slots, want_moves)
+        self._add(walk_ms=self.e.last_backtrace_ms())
+        return out
+
+    def alignment_proposals(self, groups, do_indels):
+        out = self.e.alignment_proposals(groups, do_indels)
+        self._add(walk_ms=self.e.last_backtrace_ms())
+        return out
+
+    def score(self, groups, per_seq=False):
+        out = self.e.score(groups, per_seq)
+        _, sc, ga = self.e.last_timing()
+        props = sum(len(p[0]) if isinstance(p, tuple) else len(p) for _, _, p in groups)
+        ref = sum(1 for _, r, _ in groups if r >= 0)
+        self._add(score_ms=sc + ga, codon_ms=self.e.last_codon_ms(), proposals=props,
+                  codon_proposals=props if ref else 0, score_calls=1)
+        return out
+
+    def score_dense(self, groups, to_host=True, rows=None):
+        out = self.e.score_dense(groups, to_host, rows)
+        self._add(score_ms=self.e.last_timing()[1], proposals=len(groups) * (8 * self.tlen.get(0, 0) + 4),
+                  score_calls=1)
+        return out
+
+
+def run_c3(args, gpu):
+    """configs[2] end to end (rank 0): one rifraf() run of the 1000-read
+    2.6 kb cluster with its frameshifted reference at the throughput settings
+    (every read in every batch, QV pass on) -- INIT, FRAME with the
+    reference's codon moves (k_codon), REFINE, SCORE.  Reports the native
+    driver's wall time per run (rf_rifraf_batch_ref) and, from a run of the
+    Python stage machine on the same engine, every stage's and every FRAME
+    iteration's kernel time (DP fill, proposal scoring, the codon scorer,
+    walks) and work; both runs must give the same result."""
+    import rifraf_amd.model as model
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.engine import Engine
+    template, reads, phreds, ref = c3_cluster()
+    params = model.RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True)
+    kw = dict(dnaseqs=reads, phreds=phreds, reference=ref)
+    eng = Engine(gpu)
+    try:
+        rifraf_batch([kw], params=params, engine=eng, native=True)        # warm-up (kernels, arena)
+        t0 = time.perf_counter()
+        nat = rifraf_batch([kw], params=params, engine=eng, native=True)[0]
+        native_s = time.perf_counter() - t0
+        timer = _StageTimer(eng)
+        model.ITERATION_HOOK = timer.hook
+        try:
+            t0 = time.perf_counter()
+            py = model.rifraf(reads, phreds, reference=ref, params=params, engine=timer)
+            py_s = time.perf_counter() - t0
+        finally:
+            model.ITERATION_HOOK = None
+    finally:
+        eng.close()
+    same = (np.array_equal(nat.consensus, py.consensus) and nat.state.score == py.state.score and
+            nat.state.stage_iterations == py.state.stage_iterations and
+            np.array_equal(nat.aln_error_probs, py.aln_error_probs))
+    stages = {}
+    for (st, it), r in timer.rec.items():
+        a = stages.setdefault(st, {"iterations": 0})
+        a["iterations"] += 1 if it > 0 else 0
+        for k, v in r.items():
+            a[k] = a.get(k, 0) + v
+    for a in stages.values():
+        if a.get("dp_ms"):
+            a["dp_gcups"] = a["dp_cells"] / (a["dp_ms"] * 1e-3) / 1e9
+    frame = [dict(iteration=it, **r) for (st, it), r in sorted(timer.rec.items(), key=lambda x: x[0][1])
+             if st == "FRAME"]
+    tot = {k: sum(r.get(k, 0) for r in timer.rec.values())
+           for k in ("dp_ms", "score_ms", "codon_ms", "walk_ms", "dp_cells", "proposals", "codon_proposals")}
+    return {"metric": "one rifraf() run of configs[2] (reference-informed, codon frame correction)",
+            "workload": "c3", "reads": len(reads), "template_len": len(template), "reference_len": len(ref),
+            "params": "batch = all 1000 reads, do_score (QVs), seed 1; reference with a one-base frameshift",
+            "native_seconds_per_run": native_s, "runs_per_s": 1.0 / native_s,
+            "python_stage_machine_seconds": py_s, "same_as_python_stage_machine": bool(same),
+            "consensus_equals_template": bool(np.array_equal(nat.consensus, template)),
+            "stage_iterations": list(nat.state.stage_iterations),
+            "penalty_increases": int(nat.state.n_ref_indel_mults),
+            "kernel_ms_total": tot, "codon_share_of_kernel_ms": tot["codon_ms"] / max(
+                tot["dp_ms"] + tot["score_ms"] + tot["walk_ms"], 1e-9),
+            "per_stage": stages, "frame_iterations": frame,
+            "timing": "kernel ms: HIP events on the engine stream, summed per stage from the Python stage "
+                      "machine's run (score_ms includes codon_ms); native_seconds_per_run: wall time of the "
+                      "library's stage machine, host work included"}
 
 
 class _TimedEngine:

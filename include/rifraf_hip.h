@@ -387,6 +387,10 @@ int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms,
 /* Kernel time of the walks of the last rf_backtrace / rf_alignment_proposals
  * call (k_bt_win / k_backtrace / k_aln_props), milliseconds. */
 int rf_last_backtrace_ms(const rf_ctx *ctx, double *ms);
+/* Kernel time of the reference's codon score_proposal (k_codon,
+ * model.jl:287-383) in the last rf_score call, milliseconds (0 when the call
+ * scored no reference); it is part of that call's score_ms. */
+int rf_last_codon_ms(const rf_ctx *ctx, double *ms);
 
 #ifdef __cplusplus
 }

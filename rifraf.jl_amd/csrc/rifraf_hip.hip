@@ -3873,6 +3873,8 @@ struct rf_ctx {
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
+    double codon_ms = 0;        // k_codon of the last rf_score (inside score_ms)
+    hipEvent_t ev_codon = nullptr;
     Opts opt;
     uint64_t opt_gen = 0;      // bumped by rf_set_option (scorer plan key)
     std::vector<BTTask> bt_win, bt_old;   // backtrace descriptors of the last launch
@@ -4267,6 +4269,7 @@ int rf_create(int device, rf_ctx **out)
     load_env_opts(ctx->opt);
     for (auto &e : ctx->ev)
         (void)hipEventCreate(&e);
+    (void)hipEventCreate(&ctx->ev_codon);
     (void)hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
     for (int i = 0; i < 3; ++i) {
         (void)hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
@@ -4305,6 +4308,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
         (void)hipEventDestroy(e);
+    if (ctx->ev_codon)
+        (void)hipEventDestroy(ctx->ev_codon);
     for (int i = 0; i < 3; ++i) {
         if (ctx->side[i]) {
             (void)hipStreamSynchronize(ctx->side[i]);
@@ -5690,6 +5695,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                                ctx->stream, (const ScoreGroup *)ctx->scratch[1].p, ngroups, d_gstart,
                                dense_total, d_split, d_dense);
     }
+    HIPCHK(ctx, hipEventRecord(ctx->ev_codon, ctx->stream));
     if (!ctasks.empty())
         hipLaunchKernelGGL(k_codon, dim3((unsigned)((ctasks.size() + 63) / 64)), dim3(64), 0,
                            ctx->stream, (const CodonTask *)ctx->scratch[3].p, (int)ctasks.size(),
@@ -5715,11 +5721,13 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
         HIPCHK(ctx, hipMemcpyAsync(ref_host.data(), d_ref, nprops * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    float a = 0, b = 0;
+    float a = 0, b = 0, cms = 0;
     (void)hipEventElapsedTime(&a, ctx->ev[2], ctx->ev[3]);
     (void)hipEventElapsedTime(&b, ctx->ev[3], ctx->ev[4]);
+    (void)hipEventElapsedTime(&cms, ctx->ev_codon, ctx->ev[3]);
     ctx->score_ms = a;
     ctx->gather_ms = b;
+    ctx->codon_ms = ctasks.empty() ? 0.0 : cms;
     if (out_per_seq) {
         // [k][r] rows, r = batch position (+1 column for the reference, if any)
         int64_t row = 0;
@@ -6024,6 +6032,14 @@ int rf_last_backtrace_ms(const rf_ctx *ctx, double *ms)
     if (!ctx || !ms)
         return RF_ERR_ARG;
     *ms = ctx->bt_ms;
+    return 0;
+}
+
+int rf_last_codon_ms(const rf_ctx *ctx, double *ms)
+{
+    if (!ctx || !ms)
+        return RF_ERR_ARG;
+    *ms = ctx->codon_ms;
     return 0;
 }
 

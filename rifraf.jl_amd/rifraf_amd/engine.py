@@ -433,6 +433,12 @@ class Engine:
         self._check(self.lib.rf_last_backtrace_ms(self.ctx, byref(v)))
         return v.value
 
+    def last_codon_ms(self) -> float:
+        """k_codon ms of the last score call (the reference's codon moves)."""
+        v = c_double()
+        self._check(self.lib.rf_last_codon_ms(self.ctx, byref(v)))
+        return v.value
+
     def last_timing(self):
         a, b, c = c_double(), c_double(), c_double()
         self._check(self.lib.rf_last_timing(self.ctx, byref(a), byref(b), byref(c)))

@@ -839,6 +839,12 @@ def _add_base_distributions(probs, moves, seqs):
 # rifraf (model.jl:1116-1287)
 # ---------------------------------------------------------------------
 
+# Instrumentation (bench.py's per-stage kernel times): called with
+# (iteration, stage) when an iteration starts and with (0, Stage.SCORE) before
+# the quality pass.  None in normal use.
+ITERATION_HOOK = None
+
+
 def rifraf(dnaseqs, phreds=None, *, error_log_ps=None, consensus=None, reference=None,
            params: RifrafParams | None = None, engine: Engine | None = None) -> RifrafResult:
     """rifraf(dnaseqs, phreds; consensus, reference, params) -> RifrafResult.
@@ -887,6 +893,8 @@ def rifraf(dnaseqs, phreds=None, *, error_log_ps=None, consensus=None, reference
         state.stage_iterations[int(state.stage) - 1] += 1
         consensus_stages[int(state.stage) - 1].append(state.consensus.copy())
         log(params, 1, f"iteration {it} : {state.stage.name} : {state.score}")
+        if ITERATION_HOOK is not None:
+            ITERATION_HOOK(it, state.stage)
         if params.verbose >= 3:
             log(params, 3, f"  consensus: {dna_str(state.consensus)}")
         else:
@@ -918,6 +926,8 @@ def rifraf(dnaseqs, phreds=None, *, error_log_ps=None, consensus=None, reference
             state.batch_randomness *= params.batch_mult
             log(params, 2, f"  batch randomness decreased to {state.batch_randomness}")
     state.stage = Stage.SCORE
+    if ITERATION_HOOK is not None:
+        ITERATION_HOOK(0, Stage.SCORE)
     result = RifrafResult(consensus=state.consensus, params=params, state=state,
                           consensus_stages=consensus_stages)
     if params.do_score:
