@@ -357,6 +357,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--e2e-clusters", type=int, default=512,
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
+    ap.add_argument("--e2e-pin-cores", type=int, default=2,
+                    help="c4 only: also time the e2e run with the rank pinned to this many host cores (0: skip)")
     ap.add_argument("--e2e-engines", type=int, default=1,
                     help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
@@ -495,6 +497,26 @@ def run_e2e(args, rank, world, gpu, dist, coll):
     t0 = time.perf_counter()
     res = rifraf_batch(clusters, params=params, engines=engs)
     elapsed = time.perf_counter() - t0
+    # the same steady-state run with this rank held to 2 host cores -- its
+    # share at 8 ranks on the GPU box's 16 (every thread of the process pinned
+    # in place, no relaunch); the library's worker pools follow the mask
+    pin = pin_rate = None
+    if args.e2e_pin_cores > 0:
+        allowed = sorted(os.sched_getaffinity(0))
+        if len(allowed) > args.e2e_pin_cores:
+            k = args.e2e_pin_cores
+            pin = allowed[(rank * k) % len(allowed):][:k] or allowed[:k]
+            saved = pin_threads(pin)
+            try:
+                if dist is not None:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                res_pin = rifraf_batch(clusters, params=params, engines=engs)
+                pin_s = time.perf_counter() - t0
+            finally:
+                unpin_threads(saved)
+            same_pin = all(np.array_equal(a.consensus, b.consensus) for a, b in zip(res, res_pin))
+            pin_rate = (pin_s, same_pin)
     ref = rifraf_batch(clusters[:2], params=params, engine=engs[0], native=False)
     same = all(np.array_equal(a.consensus, b.consensus) and a.state.score == b.state.score and
                np.array_equal(a.aln_error_probs, b.aln_error_probs) for a, b in zip(res[:2], ref))
@@ -503,8 +525,10 @@ def run_e2e(args, rank, world, gpu, dist, coll):
     ok = sum(int(np.array_equal(r.consensus, t)) for r, t in zip(res, templates))
     iters = sum(sum(r.state.stage_iterations) for r in res)
     tot = [float(n), float(ok), float(iters), 1.0 if same else 0.0]
+    pin_s = pin_rate[0] if pin_rate else 0.0
     if dist is not None:
         cold, _ = aggregate(cold, [0.0], coll)
+        pin_s, _ = aggregate(pin_s, [0.0], coll)
         elapsed, tot = aggregate(elapsed, tot, coll)
     return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": tot[0] / elapsed,
             "clusters_per_s_per_gpu": tot[0] / elapsed / max(world, 1), "ranks": world,
@@ -518,7 +542,35 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                       "over engines_per_gpu contexts (own HIP stream, own host thread) in one process",
             "params": "batch = all 50 reads, do_score (QVs), no reference",
             "consensus_equals_template": int(tot[1]), "stage_iterations": int(tot[2]),
-            "same_as_python_stage_machine": tot[3] == world}
+            "consensus_misses_explained": "profiles/r04_e2e_misses.json: every miss converges at a consensus "
+                                          "no single edit improves and that scores above the template",
+            "same_as_python_stage_machine": tot[3] == world,
+            "pinned": None if pin_rate is None else {
+                "cores": len(pin), "clusters_per_s": tot[0] / pin_s, "ratio_to_unpinned": elapsed / pin_s,
+                "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(pin_rate[1]),
+                "note": "the same steady-state run with every thread of the rank pinned to this many cores "
+                        "(a rank's share of the box's 16 at 8 ranks)"}}
+
+
+def pin_threads(cpus):
+    """Pin every thread of this process to `cpus` (in place, no exec);
+    returns the previous masks for unpin_threads."""
+    saved = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            saved[int(tid)] = os.sched_getaffinity(int(tid))
+            os.sched_setaffinity(int(tid), set(cpus))
+        except OSError:
+            pass
+    return saved
+
+
+def unpin_threads(saved):
+    for tid, mask in saved.items():
+        try:
+            os.sched_setaffinity(tid, mask)
+        except OSError:
+            pass
 
 
 def _sync_fn(torch):

@@ -41,6 +41,9 @@
 
 // rf_last_error text; the device form of rf_aln_error_sums (rifraf_hip.hip)
 int rf_internal_fail(rf_ctx *ctx, int code, const char *msg);
+// host worker threads (OMP_NUM_THREADS / machine, <= 16, <= the CPUs of this
+// thread's affinity mask); defined in rifraf_hip.hip
+int rf_internal_host_threads();
 void rf_internal_arena_stats(const rf_ctx *ctx, int64_t *grows, double *secs);
 int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
                              const int32_t *tlen, double *out);
@@ -1138,9 +1141,7 @@ extern "C" int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *sl
         rows[g + 1] = rows[g] + tlen[g];
     // groups are independent: ranges of groups on host threads (each with its
     // own base_distribution cache; the values do not depend on the thread)
-    const char *ev = std::getenv("OMP_NUM_THREADS");
-    const int nth = std::max(1, std::min({(ev && *ev) ? std::atoi(ev) : (int)std::thread::hardware_concurrency(), 16,
-                                          std::max(1, (int)(moff[ns] >> 20))}));
+    const int nth = std::max(1, std::min(rf_internal_host_threads(), std::max(1, (int)(moff[ns] >> 20))));
     auto work = [&](int t) {
     auto cache = std::vector<std::pair<double, double>>(4096, {std::nan(""), 0.0});
     auto err_lp = [&](double ilp) {
@@ -1213,10 +1214,8 @@ extern "C" int rf_host_tables_from_codes(int64_t nseg, const uint8_t *codes, con
     if (nseg < 0 || (nseg > 0 && (!codes || !off || !lp_t || !p10_t || !match_t || !lp || !match || !mism || !ins ||
                                   !del || !est)))
         return RF_ERR_ARG;
-    const char *ev = std::getenv("OMP_NUM_THREADS");
     const int64_t N = nseg > 0 ? off[nseg] : 0;
-    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)((ev && *ev) ? std::atoi(ev) : (int)std::thread::hardware_concurrency()),
-                                                                16, (N >> 20) + 1}));
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)rf_internal_host_threads(), (N >> 20) + 1));
     auto work = [&](int t) {
         std::vector<double> p10;
         for (int64_t k = nseg * t / nth; k < nseg * (t + 1) / nth; ++k) {
@@ -1283,9 +1282,8 @@ namespace {
 template <class F>
 void host_parallel(int64_t n, int64_t grain, F &&fn)
 {
-    const char *ev = std::getenv("OMP_NUM_THREADS");
-    const int64_t want = (ev && *ev) ? std::atoi(ev) : (int64_t)std::thread::hardware_concurrency();
-    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>({want, 16, n / std::max<int64_t>(grain, 1)}));
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)rf_internal_host_threads(),
+                                                                n / std::max<int64_t>(grain, 1)));
     std::vector<std::thread> th;
     for (int t = 1; t < nth; ++t)
         th.emplace_back([&, t] { fn(n * t / nth, n * (t + 1) / nth); });

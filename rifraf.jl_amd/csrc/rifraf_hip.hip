@@ -20,6 +20,7 @@
 // upload, the C-ABI of include/rifraf_hip.h.
 
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <array>
@@ -3692,17 +3693,29 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+}  // namespace
+
 // Host worker threads: OMP_NUM_THREADS when set (the GPU box's CPU share),
-// else the machine's, at most 16.
-inline int host_threads()
+// else the machine's, at most 16, and never more than the CPUs this thread
+// may run on (sched_getaffinity, read per call: a rank pinned to its share of
+// the host's cores -- e.g. 2 of 16 at 8 ranks -- gets that many workers).
+// Shared with rifraf_batch.cpp (C++ linkage, not part of the C-ABI).
+int rf_internal_host_threads()
 {
-    static const int n = [] {
+    static const int cap = [] {
         const char *v = std::getenv("OMP_NUM_THREADS");
         int t = (v && *v) ? std::atoi(v) : (int)std::thread::hardware_concurrency();
         return std::max(1, std::min(t, 16));
     }();
-    return n;
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0)
+        return std::max(1, std::min(cap, (int)CPU_COUNT(&cs)));
+    return cap;
 }
+
+namespace {
+inline int host_threads() { return rf_internal_host_threads(); }
 template <class F>
 void parallel_for(int nth, F fn)
 {

@@ -40,6 +40,8 @@ Exchange and exactness:
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from .engine import RF_BAND_A, RifrafError
@@ -61,6 +63,8 @@ class ShardedEngine:
         self.dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
                     else torch.device("cpu"))
         self.last_dense = None
+        self.tlen, self.slot_tpl = {}, {}    # template lengths, slot -> template (replicated)
+        self.exchange_s, self.exchanges = 0.0, 0   # time in (and number of) collectives
 
     @classmethod
     def for_params(cls, local, nreads: int, params=None, group=None):
@@ -91,21 +95,74 @@ class ShardedEngine:
         return self.owned_by(self.rank, slots)
 
     # ------------------------------------------------------------------
-    # collectives
+    # collectives: fixed-shape tensors (RCCL on GPUs, gloo on CPU).  Every
+    # rank knows which rank owns which job (the deal is deterministic) and
+    # the shape of every result (template lengths are replicated), so one
+    # all-gather or all-reduce per call carries the results, with an error
+    # flag as the last element; error messages (Python objects) travel only
+    # when a rank actually failed.
+    def _timed(self, fn):
+        t0 = time.perf_counter()
+        out = fn()
+        self.exchange_s += time.perf_counter() - t0
+        self.exchanges += 1
+        return out
+
+    def _allgather(self, arr: np.ndarray, dtype) -> np.ndarray:
+        """(W, len) array of every rank's 1-D `arr` (equal lengths)."""
+        torch = self.torch
+
+        def go():
+            t = torch.from_numpy(np.ascontiguousarray(arr, dtype=dtype)).to(self.dev)
+            if self.dev.type == "cuda":
+                out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=self.dev)
+                self.dist.all_gather_into_tensor(out, t, group=self.group)
+                return out.view(self.world, -1).cpu().numpy()
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            self.dist.all_gather(parts, t, group=self.group)
+            return torch.stack(parts).numpy()
+        return self._timed(go)
+
+    def _allreduce_max_u8(self, arr: np.ndarray) -> np.ndarray:
+        torch = self.torch
+
+        def go():
+            t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)).to(self.dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+            return t.cpu().numpy()
+        return self._timed(go)
+
     def _gather(self, obj):
         out = [None] * self.world
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
-    def _raise_any(self, err):
-        """Collective error check: a reference error() on any rank is raised on all."""
-        errs = self._gather(err)
-        for e in errs:
+    def _raise_first(self, err):
+        """Slow path after a flagged collective: the error text of the first
+        failing rank (in rank order) is raised on every rank."""
+        for e in self._gather(err):
             if e is not None:
                 raise RifrafError(e)
+        raise RifrafError("sharded engine: a rank reported an error")
+
+    def _raise_any(self, err):
+        """Collective error check: a reference error() on any rank is raised on all."""
+        flag = self._allreduce_max_u8(np.array([0 if err is None else 1], np.uint8))
+        if flag[0]:
+            self._raise_first(err)
 
     def _global(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
+
+    def owners(self, slots) -> np.ndarray:
+        """Owner rank of every slot (vectorised owner())."""
+        slots = np.asarray(slots, np.int64)
+        return np.where(slots < self.nreads, slots % self.world, self.world - 1)
+
+    def _rows(self, slot: int) -> int:
+        """m + 1 for the template the slot's bands were last filled against
+        (replicated bookkeeping: every rank sees every realign call)."""
+        return self.tlen[self.slot_tpl[int(slot)]] + 1
 
     # ------------------------------------------------------------------
     # replicated state
@@ -113,6 +170,8 @@ class ShardedEngine:
         self.e.set_sequences(first, seqs)
 
     def set_templates(self, first, tpls):
+        for k, t in enumerate(tpls):
+            self.tlen[first + k] = len(t)
         self.e.set_templates(first, tpls)
 
     def reserve(self, nbytes):
@@ -123,72 +182,92 @@ class ShardedEngine:
 
     # ------------------------------------------------------------------
     def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
-        """Each rank fills the bands of its own slots; per-job scores are
-        gathered verbatim (exact)."""
+        """Each rank fills the bands of its own slots; per-job scores travel
+        in one all-gather of n + 1 doubles (verbatim, so rescore!'s fold is
+        exact)."""
         slots = np.atleast_1d(np.asarray(slots, np.int32))
         n = slots.shape[0]
         seqs = np.broadcast_to(np.asarray(seqs, np.int32), (n,))
         tpls = np.broadcast_to(np.asarray(tpls, np.int32), (n,))
         bws = np.broadcast_to(np.asarray(bws, np.int32), (n,))
+        for sl, tp in zip(slots.tolist(), tpls.tolist()):
+            self.slot_tpl[sl] = tp
         mine = np.flatnonzero(self.owned(slots))
-        err, vals = None, None
+        err = None
+        buf = np.zeros(n + 1)
         if len(mine):
             try:
-                vals = self.e.realign(slots[mine], seqs[mine], tpls[mine], bws[mine], flags)
+                buf[mine] = self.e.realign(slots[mine], seqs[mine], tpls[mine], bws[mine], flags)
             except RifrafError as e:
                 err = str(e)
-        parts = self._gather((err, mine, vals))
-        out = np.empty(n)
-        for e, idx, v in parts:
-            if e is not None:
-                raise RifrafError(e)
-            if v is not None:
-                out[idx] = v
-        return out
+        buf[n] = 0.0 if err is None else 1.0
+        allv = self._allgather(buf, np.float64)
+        if allv[:, n].any():
+            self._raise_first(err)
+        return allv[self.owners(slots), np.arange(n)]
 
     def backtrace(self, slots, want_moves: bool = True):
+        """Error counts (and move lengths) in one all-gather; the moves, when
+        wanted, in a second one of padded byte strings."""
         slots = np.atleast_1d(np.asarray(slots, np.int32))
+        n = len(slots)
         mine = np.flatnonzero(self.owned(slots))
-        err, mv, ne = None, None, None
+        err, mv = None, None
+        head = np.zeros(2 * n + 1)
         if len(mine):
             try:
                 mv, ne = self.e.backtrace(slots[mine], want_moves)
+                head[mine] = ne
+                if want_moves:
+                    head[n + mine] = [len(x) for x in mv]
             except RifrafError as e:
                 err = str(e)
-        parts = self._gather((err, mine, mv, ne))
-        nerr = np.empty(len(slots), np.int32)
-        moves = [None] * len(slots) if want_moves else None
-        for e, idx, m, c in parts:
-            if e is not None:
-                raise RifrafError(e)
-            if c is None:
-                continue
-            nerr[idx] = c
-            if want_moves:
-                for k, i in enumerate(idx):
-                    moves[i] = m[k]
+        head[2 * n] = 0.0 if err is None else 1.0
+        allh = self._allgather(head, np.float64)
+        if allh[:, 2 * n].any():
+            self._raise_first(err)
+        own = self.owners(slots)
+        nerr = allh[own, np.arange(n)].astype(np.int32)
+        if not want_moves:
+            return None, nerr
+        lens = allh[own, n + np.arange(n)].astype(np.int64)
+        per_rank = [int(lens[own == r].sum()) for r in range(self.world)]
+        pay = np.zeros(max(max(per_rank), 1), np.int8)
+        if mv is not None and len(mine):
+            flat = np.concatenate([np.asarray(x, np.int8) for x in mv])
+            pay[:len(flat)] = flat
+        allm = self._allgather(pay, np.int8)
+        moves = [None] * n
+        at = [0] * self.world
+        for i in range(n):
+            r = int(own[i])
+            moves[i] = allm[r, at[r]:at[r] + lens[i]].copy()
+            at[r] += int(lens[i])
         return moves, nerr
 
     def alignment_proposals(self, groups, do_indels: bool):
-        """Per-rank masks of the owned batch slots, OR-ed over the ranks (the
-        union is order-free, so the result equals one GPU's)."""
-        err, masks = None, {}
+        """Per-rank masks of the owned batch slots, OR-ed over the ranks by
+        one byte-wise MAX all-reduce (the union is order-free, so the result
+        equals one GPU's)."""
+        rows = [self._rows(np.asarray(sl)[0]) for sl in groups]
+        off = np.zeros(len(groups) + 1, np.int64)
+        np.cumsum(np.asarray(rows, np.int64) * 9, out=off[1:])
+        buf = np.zeros(int(off[-1]) + 1, np.uint8)
+        err = None
         local = [(g, np.asarray(sl, np.int32)[self.owned(sl)]) for g, sl in enumerate(groups)]
         local = [(g, s) for g, s in local if len(s)]
         if local:
             try:
                 res = self.e.alignment_proposals([s for _, s in local], do_indels)
-                masks = {g: m for (g, _), m in zip(local, res)}
+                for (g, _), mk in zip(local, res):
+                    buf[off[g]:off[g + 1]] = np.asarray(mk, np.uint8).reshape(-1)
             except RifrafError as e:
                 err = str(e)
-        parts = self._gather((err, masks))
-        out = [None] * len(groups)
-        for e, ms in parts:
-            if e is not None:
-                raise RifrafError(e)
-            for g, m in ms.items():
-                out[g] = m.copy() if out[g] is None else (out[g] | m)
-        return out
+        buf[-1] = 0 if err is None else 1
+        out = self._allreduce_max_u8(buf)
+        if out[-1]:
+            self._raise_first(err)
+        return [out[off[g]:off[g + 1]].reshape(rows[g], 9).copy() for g in range(len(groups))]
 
     def geometry(self, slot: int, which: int = RF_BAND_A):
         src = self.owner(slot)
@@ -218,19 +297,26 @@ class ShardedEngine:
         """Proposal-list scoring (get_candidates, estimate_probs): every rank
         scores its own reads (and the reference when it owns the reference
         slot) against every proposal; ONE tensor all-gather (RCCL / gloo) of
-        the padded per-read score matrices of all groups; every rank then
-        folds the columns in batch order, 0.0 + s_1 + ... + s_R, and adds the
-        reference last -- the reference's own order (model.jl:389-397), so the
-        totals are bit-identical to one GPU.  Three collectives per call
-        (errors, lengths, scores), whatever the world size and group count."""
-        torch = self.torch
+        the padded per-read score matrices of all groups, with the error flag
+        as the last element (every rank knows every rank's payload size from
+        the deal); every rank then folds the columns in batch order,
+        0.0 + s_1 + ... + s_R, and adds the reference last -- the reference's
+        own order (model.jl:389-397), so the totals are bit-identical to one
+        GPU."""
         arrs, local, err = [], [], None
+        sizes = np.zeros(self.world, np.int64)
         for bslots, ref, props in groups:
             k, p, b = props if isinstance(props, tuple) else to_arrays(props)
             P = len(k)
             bslots = np.asarray(bslots, np.int32)
             own = self.owned(bslots)
-            mine_ref = ref >= 0 and self.owner(ref) == self.rank
+            ref_owner = self.owner(ref) if ref >= 0 else -1
+            mine_ref = ref_owner == self.rank
+            cols = np.bincount(self.owners(bslots), minlength=self.world) if len(bslots) else \
+                np.zeros(self.world, np.int64)
+            if ref_owner >= 0:
+                cols[ref_owner] += 1
+            sizes += P * cols
             per = np.zeros((P, int(own.sum()) + (1 if mine_ref else 0)))
             if (own.any() or mine_ref) and P > 0 and err is None:
                 try:
@@ -238,27 +324,23 @@ class ShardedEngine:
                     per = np.asarray(m[0], np.float64).reshape(P, -1)
                 except RifrafError as e:
                     err = str(e)
-            arrs.append((P, bslots, ref))
+            arrs.append((P, bslots, ref, ref_owner))
             local.append(per)
-        self._raise_any(err)
+        buf = np.zeros(int(sizes.max()) + 1)
         flat = np.concatenate([x.reshape(-1) for x in local]) if local else np.zeros(0)
-        n = torch.tensor([flat.size], dtype=torch.int64, device=self.dev)
-        ns = [torch.zeros_like(n) for _ in range(self.world)]
-        self.dist.all_gather(ns, n, group=self.group)
-        ns = [int(x.item()) for x in ns]
-        buf = torch.zeros(max(max(ns), 1), dtype=torch.float64, device=self.dev)
-        buf[:flat.size] = torch.from_numpy(flat).to(self.dev)
-        parts = [torch.empty_like(buf) for _ in range(self.world)]
-        self.dist.all_gather(parts, buf, group=self.group)
-        parts = [x.cpu().numpy() for x in parts]
+        buf[:flat.size] = flat
+        buf[-1] = 0.0 if err is None else 1.0
+        parts = self._allgather(buf, np.float64)
+        if parts[:, -1].any():
+            self._raise_first(err)
         at = [0] * self.world
         totals, mats = [], []
-        for P, bslots, ref in arrs:
+        for P, bslots, ref, ref_owner in arrs:
             R = len(bslots)
             full = np.empty((P, R + (1 if ref >= 0 else 0)))
-            ref_owner = self.owner(ref) if ref >= 0 else -1
+            own = self.owners(bslots)
             for r in range(self.world):
-                idx = np.flatnonzero(self.owned_by(r, bslots))
+                idx = np.flatnonzero(own == r)
                 cols = len(idx) + (1 if r == ref_owner else 0)
                 m = parts[r][at[r]:at[r] + P * cols].reshape(P, cols)
                 at[r] += P * cols
@@ -275,16 +357,15 @@ class ShardedEngine:
     # ------------------------------------------------------------------
     def score_dense(self, groups, to_host: bool = True, rows=None):
         """All proposals of every group: per-rank device fold of the owned
-        reads, RCCL all-gather of the partial vectors, rank-order sum."""
+        reads, RCCL all-gather of the partial vectors (an error count rides
+        as the last element), rank-order sum."""
         torch = self.torch
         G = len(groups)
         if rows is None:
-            rows = self._gather([self.e.geometry(int(s), RF_BAND_A)[1] if self.owned([s])[0] else None
-                                 for s in (np.asarray(sl)[0] for sl in groups)])
-            rows = [next(r[g] for r in rows if r[g] is not None) for g in range(G)]
+            rows = [self._rows(np.asarray(sl)[0]) for sl in groups]
         off = np.zeros(G + 1, np.int64)
         np.cumsum(np.asarray(rows, np.int64) * 9, out=off[1:])
-        partial = torch.zeros(int(off[-1]), dtype=torch.float64, device=self.dev)
+        partial = torch.zeros(int(off[-1]) + 1, dtype=torch.float64, device=self.dev)
         local = [(g, np.asarray(sl, np.int32)[self.owned(sl)]) for g, sl in enumerate(groups)]
         local = [(g, s) for g, s in local if len(s)]
         err = None
@@ -307,8 +388,12 @@ class ShardedEngine:
                         at += w
             except RifrafError as e:
                 err = str(e)
-        self._raise_any(err)
-        total = allgather_fold(partial, self.dist, self.group)
+        if err is not None:
+            partial[-1] = 1.0
+        total = self._timed(lambda: allgather_fold(partial, self.dist, self.group))
+        if float(total[-1].item()) != 0.0:
+            self._raise_first(err)
+        total = total[:-1]
         self.last_dense = total
         if not to_host:
             return None
