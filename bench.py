@@ -157,23 +157,32 @@ def make_workload(nclusters, nreads, length, error_rate, bw, seed):
     return clusters
 
 
-def make_read_shard(nreads, length, error_rate, bw, seed, lo, hi):
-    """One cluster (template + reads lo..hi-1) from the restated sample module;
-    read k has its own seeded stream, so every rank simulates only its reads."""
-    from rifraf_amd import ErrorModel, RifrafSequence, Scores
+def read_shard_raw(length, error_rate, seed, lo, hi):
+    """One cluster's template and raw reads lo..hi-1 (bases, Phred scores)
+    from the restated sample module; read k has its own seeded stream, so
+    every rank simulates only its reads."""
+    from rifraf_amd import ErrorModel
     from rifraf_amd.sample import MAX_PROB, MIN_PROB, random_seq, sample_from_template
     rng = np.random.default_rng(seed)
-    scores = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0, 0.0, 0.0))
     alpha = 0.1
     beta = alpha * (error_rate - MAX_PROB) / (MIN_PROB - error_rate)
     t = random_seq(length, rng)
     t_p = rng.beta(alpha, beta, size=length) * (MAX_PROB - MIN_PROB) + MIN_PROB
-    reads = []
+    seqs, phreds = [], []
     for k in range(lo, hi):
         s, _, ph, _, _ = sample_from_template(t, t_p, ErrorModel(1, 5, 5), 1.5, 3.0, 1.0,
                                               np.random.default_rng([seed, k]))
-        reads.append(RifrafSequence(s, ph, bw, scores))
-    return t, reads
+        seqs.append(s)
+        phreds.append(ph)
+    return t, seqs, phreds
+
+
+def make_read_shard(nreads, length, error_rate, bw, seed, lo, hi):
+    """One cluster (template + reads lo..hi-1) as RifrafSequences."""
+    from rifraf_amd import ErrorModel, RifrafSequence, Scores
+    scores = Scores.from_errors(ErrorModel(1.0, 2.0, 2.0, 0.0, 0.0))
+    t, seqs, phreds = read_shard_raw(length, error_rate, seed, lo, hi)
+    return t, [RifrafSequence(s, ph, bw, scores) for s, ph in zip(seqs, phreds)]
 
 
 def cpu_threads():
@@ -354,6 +363,8 @@ def main():
                     help="c4 only: skip the secondary c5 (10 kb, band doubling) workload")
     ap.add_argument("--no-c3", action="store_true",
                     help="c4 only: skip the c3 field (configs[2] run with the reference's codon moves)")
+    ap.add_argument("--no-sharded-rifraf", action="store_true",
+                    help="c5 at N > 1: skip the read-sharded whole-rifraf() rehearsal field")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--e2e-clusters", type=int, default=512,
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
@@ -884,6 +895,48 @@ class _TimedEngine:
         return out
 
 
+def run_sharded_rifraf(args, rank, world, local, dist, nreads=256):
+    """Whole rifraf() runs through ShardedEngine (rifraf_amd.sharded) on the
+    first `nreads` reads of the c5 cluster (10 kb, 3 % error; every read in
+    every batch): every rank runs the same stage machine, owns every W-th
+    read's bands, and exchanges per-read results through fixed-shape tensor
+    collectives.  Reports the collectives' time per stage-machine iteration
+    and checks the result against one unsharded engine on rank 0."""
+    from rifraf_amd.engine import Engine
+    from rifraf_amd.model import RifrafParams, rifraf
+    from rifraf_amd.sharded import ShardedEngine
+    _, _, length, err, bw, _ = CONFIGS["c5"]
+    t, seqs, phreds = read_shard_raw(length, err, args.seed, 0, nreads)
+    params = RifrafParams(batch_size=0, batch_fixed=False)
+    se = ShardedEngine(Engine(local), len(seqs))
+    try:
+        dist.barrier()
+        t0 = time.perf_counter()
+        res = rifraf(seqs, phreds, params=params, engine=se)
+        wall = time.perf_counter() - t0
+        xs, nx = se.exchange_s, se.exchanges
+    finally:
+        se.close()
+    iters = int(sum(res.state.stage_iterations))
+    same = None
+    if rank == 0:
+        e = Engine(local)
+        try:
+            one = rifraf(seqs, phreds, params=params, engine=e)
+        finally:
+            e.close()
+        same = bool(np.array_equal(one.consensus, res.consensus) and one.state.score == res.state.score
+                    and one.state.stage_iterations == res.state.stage_iterations)
+    return {"reads": len(seqs), "template_len": len(t), "ranks": world, "iterations": iters,
+            "seconds_rank0": wall, "exchange_ms_rank0": 1e3 * xs, "collectives_rank0": nx,
+            "exchange_ms_per_iteration": 1e3 * xs / max(iters, 1),
+            "collectives_per_iteration": nx / max(iters, 1),
+            "same_as_one_gpu": same,
+            "note": "ShardedEngine: realign / backtrace / alignment_proposals / score exchange fixed-shape "
+                    "tensors (one all-gather or all-reduce per call, error flag in the payload); "
+                    "every read in every batch, no QV pass"}
+
+
 def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
     """configs[4]: ONE cluster whose reads are split over the ranks.  Setup
     (untimed, reported): each rank simulates and uploads its block of reads
@@ -1032,6 +1085,8 @@ def run_read_sharded(args, rank, world, local, dist, torch, coll=None):
                                        "bytes": score_bytes, "ms": sc_ms}},
         "setup_s": gen_s,
     }
+    if world > 1 and not args.no_sharded_rifraf:
+        result["sharded_rifraf"] = run_sharded_rifraf(args, rank, world, local, dist)
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         if world == 1 and not args.no_cpu:
