@@ -1959,6 +1959,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         tI[k] = 0.0;
         tS[k] = 0.0;
     }
+    const bool all_act = __all(active) && wave_s;
     // aligned-row loader lane roles: row r8 + RPI j, 16-B chunk cc8 of the row piece
     const int r8 = tid / CPR, cc8 = tid % CPR, p8 = r8 & 1;
     // per-read geometry: wave-uniform fields plus the lane's diagonal range
@@ -1971,6 +1972,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         int dfirst, dlast;           // this lane's chain rows as band diagonals
         bool peel;
         int dlo, dhi, dfmax, dlmin;  // wave-wide
+        bool uni;                    // every lane active with the same [dfirst, dlast] and peel
     };
     auto setup = [&](int r, RG &g) {
         const ScoreRead R = reads[r];
@@ -2001,8 +2003,11 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         g.dhi = __builtin_amdgcn_readfirstlane(dhi);
         g.dfmax = __builtin_amdgcn_readfirstlane(dfmax);
         g.dlmin = __builtin_amdgcn_readfirstlane(dlmin);
+        // interior waves: every lane has the same chain rows [dfirst, dlast]
+        // and a peel row dlast + 1 (uniform), so the first and last segments
+        // of the read can run the unrolled steps too (see chains)
+        g.uni = all_act && __all(g.dfirst == g.dlo && g.dlast == g.dlmin && g.peel);
     };
-    const bool all_act = __all(active) && wave_s;
     // one segment's registers: its band lines, table rows and (a read's
     // first segment) LDS row 0
     struct SegSet {
@@ -2050,13 +2055,21 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     };
     auto store_seg = [&](const SegSet &X, const RG &g, int D) {
         if ((g.P & 15) == 0) {
+            // an interior wave's last segment: rows past the peel row (d >
+            // dlast + 1 in A, d > dlast in B beyond column a) read -Inf, so the
+            // unrolled steps past the chain's end leave it unchanged (chains)
+            const int dm = (g.uni && D + S > g.dlmin + 1) ? g.dlmin + 1 - D : INT_MAX;
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
                     const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0
-                    const double v = h ? X.ra[j].y : X.ra[j].x, w = h ? X.rb[j].y : X.rb[j].x;
+                    double v = h ? X.ra[j].y : X.ra[j].x, w = h ? X.rb[j].y : X.rb[j].x;
+                    if (dm != INT_MAX && ddl >= dm) {
+                        v = -RF_INF;
+                        w = -RF_INF;
+                    }
                     const int l = (ddl + 1) * LS + col;
                     // rows S..127 always land in [0, 64]; the parallelogram's
                     // first / last S rows hold cells of the neighbouring items
@@ -2170,12 +2183,14 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 dd = vmax(dd, dsum);
                 aprev = o.ac;
             };
-            if (all_act && dfmax <= D && dlmin >= D + S - 1) {
-                // every lane scores all 32 diagonals (no peel inside: dlast >= D+31);
-                // all_act includes wave_s, so the bS select is the identity
-                Ops cur = ld(0);
+            // unrolled steps s0 .. shi (wave-uniform) of the segment; s0 = 0 or 1
+            auto run = [&](auto s0c, int shi) {
+                constexpr int S0 = decltype(s0c)::value;
+                Ops cur = ld(S0);
 #pragma unroll SEGL_UNROLL
-                for (int s = 0; s < S; ++s) {
+                for (int s = S0; s < S; ++s) {
+                    if (s > shi)   // scalar exit (the last segment of a read)
+                        break;
                     const Ops nxt = ld(s + 1 < S ? s + 1 : s);
                     // keep the reads ahead of this step's chain (hipcc's scheduler
                     // otherwise sinks them next to their use); the arithmetic may
@@ -2184,6 +2199,25 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                     step(cur, std::true_type{});
                     cur = nxt;
                 }
+            };
+            if (all_act && dfmax <= D && dlmin >= D + S - 1) {
+                // every lane scores all 32 diagonals (no peel inside: dlast >= D+31);
+                // all_act includes wave_s, so the bS select is the identity
+                run(std::integral_constant<int, 0>{}, S - 1);
+            } else if (g.uni && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0) {
+                // interior wave, first segment of the read (round 4): every lane's
+                // chain starts at diagonal 1 -- the unrolled steps 1 .. S-1
+                run(std::integral_constant<int, 1>{}, S - 1);
+            } else if (g.uni && D > 0 && D <= dlast + 1 && dlast + 1 < D + S && (g.P & 15) == 0) {
+                // interior wave, last segment (round 4): the rows past the peel row
+                // were stored as -Inf (store_seg), so all S unrolled steps give the
+                // chain's rows up to dlast, then the peel row dlast + 1 exactly as
+                // below (max(x, -Inf) = x; B(dlast, a + 1) is the peel's operand),
+                // and leave the state unchanged afterwards.  The first step's MATCH
+                // predecessor is diagonal D - 1 (LDS row 0) also when only the
+                // peel row falls in this segment
+                aprev = sA[tid];
+                run(std::integral_constant<int, 0>{}, S - 1);
             } else {
                 const int slo = max(lo - D, 0), shi = hi - D;
                 if (slo <= shi) {
