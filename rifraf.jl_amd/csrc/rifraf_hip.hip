@@ -1893,6 +1893,12 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #ifndef SEGL_UNROLL
 #define SEGL_UNROLL 32
 #endif
+// an interior wave's last segment runs the unrolled steps over rows staged as
+// -Inf past the peel row when it holds at least this many rows (fewer: the
+// generic loop, which costs more per step but runs only the real rows)
+#ifndef SEGL_MASKED_MIN
+#define SEGL_MASKED_MIN 20
+#endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
 // of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
@@ -2058,18 +2064,15 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             // an interior wave's last segment: rows past the peel row (d >
             // dlast + 1 in A, d > dlast in B beyond column a) read -Inf, so the
             // unrolled steps past the chain's end leave it unchanged (chains)
-            const int dm = (g.uni && D + S > g.dlmin + 1) ? g.dlmin + 1 - D : INT_MAX;
+            const int dm = (g.uni && D > 0 && g.dlmin + 1 < D + S && g.dlmin + 1 - D >= SEGL_MASKED_MIN)
+                               ? g.dlmin + 1 - D : INT_MAX;
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int ddl = 4 * cc8 + 2 * h + p8;       // d - D
                     const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0
-                    double v = h ? X.ra[j].y : X.ra[j].x, w = h ? X.rb[j].y : X.rb[j].x;
-                    if (dm != INT_MAX && ddl >= dm) {
-                        v = -RF_INF;
-                        w = -RF_INF;
-                    }
+                    const double v = h ? X.ra[j].y : X.ra[j].x, w = h ? X.rb[j].y : X.rb[j].x;
                     const int l = (ddl + 1) * LS + col;
                     // rows S..127 always land in [0, 64]; the parallelogram's
                     // first / last S rows hold cells of the neighbouring items
@@ -2077,6 +2080,14 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                         sA[l] = v;
                         sB[l] = w;
                     }
+                }
+            }
+            if (dm != INT_MAX) {
+                // LDS rows dm + 1 .. S (diagonals D + dm ..) of both bands: -Inf
+                for (int e = tid; e < (S - dm) * LS; e += 64) {
+                    const int l = (dm + 1) * LS + e;
+                    sA[l] = -RF_INF;
+                    sB[l] = -RF_INF;
                 }
             }
         } else {
@@ -2184,40 +2195,42 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 aprev = o.ac;
             };
             // unrolled steps s0 .. shi (wave-uniform) of the segment; s0 = 0 or 1
-            auto run = [&](auto s0c, int shi) {
-                constexpr int S0 = decltype(s0c)::value;
-                Ops cur = ld(S0);
+            // the unrolled steps 0 .. S-1 (one copy of the body: instruction
+            // cache); skip0 -- a read's first segment in an interior wave,
+            // whose chains start at diagonal 1 -- only takes row 0 as the next
+            // step's MATCH predecessor (a scalar branch on the first step)
+            auto run = [&](bool skip0) {
+                Ops cur = ld(0);
 #pragma unroll SEGL_UNROLL
-                for (int s = S0; s < S; ++s) {
-                    if (s > shi)   // scalar exit (the last segment of a read)
-                        break;
+                for (int s = 0; s < S; ++s) {
                     const Ops nxt = ld(s + 1 < S ? s + 1 : s);
                     // keep the reads ahead of this step's chain (hipcc's scheduler
                     // otherwise sinks them next to their use); the arithmetic may
                     // still move across (a full sched_barrier costs hazard nops)
                     SEGL_FENCE();
-                    step(cur, std::true_type{});
+                    if (s == 0 && skip0)
+                        aprev = a - c >= 0 ? cur.ac : -RF_INF;   // diagonal 0: read row a - c
+                    else
+                        step(cur, std::true_type{});
                     cur = nxt;
                 }
             };
-            if (all_act && dfmax <= D && dlmin >= D + S - 1) {
-                // every lane scores all 32 diagonals (no peel inside: dlast >= D+31);
-                // all_act includes wave_s, so the bS select is the identity
-                run(std::integral_constant<int, 0>{}, S - 1);
-            } else if (g.uni && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0) {
-                // interior wave, first segment of the read (round 4): every lane's
-                // chain starts at diagonal 1 -- the unrolled steps 1 .. S-1
-                run(std::integral_constant<int, 1>{}, S - 1);
-            } else if (g.uni && D > 0 && D <= dlast + 1 && dlast + 1 < D + S && (g.P & 15) == 0) {
-                // interior wave, last segment (round 4): the rows past the peel row
-                // were stored as -Inf (store_seg), so all S unrolled steps give the
-                // chain's rows up to dlast, then the peel row dlast + 1 exactly as
-                // below (max(x, -Inf) = x; B(dlast, a + 1) is the peel's operand),
-                // and leave the state unchanged afterwards.  The first step's MATCH
-                // predecessor is diagonal D - 1 (LDS row 0) also when only the
-                // peel row falls in this segment
-                aprev = sA[tid];
-                run(std::integral_constant<int, 0>{}, S - 1);
+            // every lane scores all 32 diagonals (no peel inside: dlast >= D+31);
+            // all_act includes wave_s, so the bS select is the identity
+            const bool full = all_act && dfmax <= D && dlmin >= D + S - 1;
+            // interior wave, first segment of the read (round 4): every lane's
+            // chain covers diagonals 1 .. S-1 of it
+            const bool first_u = g.uni && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0;
+            // interior wave, last segment with at least SEGL_MASKED_MIN rows
+            // (round 4): the rows past the peel row were stored as -Inf
+            // (store_seg), so all S unrolled steps give the chain's rows up to
+            // dlast, then the peel row dlast + 1 exactly as below (max(x, -Inf)
+            // = x; B(dlast, a + 1) is the peel's operand), and leave the state
+            // unchanged afterwards
+            const bool last_u = g.uni && D > 0 && dlast + 1 < D + S && dlast + 1 - D >= SEGL_MASKED_MIN &&
+                                (g.P & 15) == 0;
+            if (full || first_u || last_u) {
+                run(__builtin_amdgcn_readfirstlane((int)first_u) != 0);   // one call site: one body
             } else {
                 const int slo = max(lo - D, 0), shi = hi - D;
                 if (slo <= shi) {
@@ -2453,6 +2466,7 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         bool peel[2];
         int dlo, dhi;              // wave-wide over both halves
         int dfmax[2], dlmin[2];    // wave-wide per half
+        bool uni[2];               // interior half: same [dfirst, dlast] and a peel in every lane
     };
     auto setup = [&](int r, RG &g) {
         const ScoreRead R = reads[r];
@@ -2485,6 +2499,8 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             }
             g.dfmax[h] = __builtin_amdgcn_readfirstlane(dfmax);
             g.dlmin[h] = __builtin_amdgcn_readfirstlane(dlmin);
+            g.uni[h] = hl[h].all_act && h < NH &&
+                       __all(g.dfirst[h] == g.dfmax[h] && g.dlast[h] == g.dlmin[h] && g.peel[h]);
         }
         for (int off = 32; off >= 1; off >>= 1) {
             dlo = min(dlo, __shfl_xor(dlo, off));
@@ -2556,6 +2572,11 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     auto store_seg = [&](const SegSet &X, const RG &g, int D, int h) {
         const int a0h = a0 + 64 * h;
         if ((g.P & 15) == 0) {
+            // an interior half's last segment: rows past the peel row read -Inf
+            // (k_score_segl's store_seg)
+            const bool un = h ? g.uni[1] : g.uni[0];
+            const int dl = h ? g.dlmin[1] : g.dlmin[0];
+            const int dm = (un && D > 0 && dl + 1 < D + S && dl + 1 - D >= SEGL_MASKED_MIN) ? dl + 1 - D : INT_MAX;
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
 #pragma unroll
@@ -2568,6 +2589,13 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                         sA[l] = v;
                         sB[l] = w;
                     }
+                }
+            }
+            if (dm != INT_MAX) {
+                for (int e = tid; e < (S - dm) * LS; e += 64) {
+                    const int l = (dm + 1) * LS + e;
+                    sA[l] = -RF_INF;
+                    sB[l] = -RF_INF;
                 }
             }
         } else {
@@ -2674,15 +2702,26 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 ddh = vmax(ddh, dsum);
                 aprev = o.ac;
             };
-            if (L.all_act && dfmax <= D && dlmin >= D + S - 1) {
+            // one copy of the unrolled body per half (k_score_segl's run)
+            auto run = [&](bool skip0) {
                 Ops cur = ld(0);
 #pragma unroll SEGL_UNROLL
                 for (int s = 0; s < S; ++s) {
                     const Ops nxt = ld(s + 1 < S ? s + 1 : s);
                     SEGL_FENCE();
-                    stp(cur, std::true_type{});
+                    if (s == 0 && skip0)
+                        aprev = a - c >= 0 ? cur.ac : -RF_INF;
+                    else
+                        stp(cur, std::true_type{});
                     cur = nxt;
                 }
+            };
+            const bool full = L.all_act && dfmax <= D && dlmin >= D + S - 1;
+            const bool first_u = g.uni[H] && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0;
+            const bool last_u = g.uni[H] && D > 0 && dlast + 1 < D + S && dlast + 1 - D >= SEGL_MASKED_MIN &&
+                                (g.P & 15) == 0;
+            if (full || first_u || last_u) {
+                run(__builtin_amdgcn_readfirstlane((int)first_u) != 0);
             } else {
                 const int slo = max(lo - D, 0), shi = hi - D;
                 if (slo <= shi) {
