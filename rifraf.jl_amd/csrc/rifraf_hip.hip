@@ -190,14 +190,19 @@ __device__ __forceinline__ void wave_sync()
 // (bandedarrays.jl:176-198): kappa' = K-1-kappa, d' = H-1-d.
 // ---------------------------------------------------------------------
 
-template <int W, bool GRING>
-__global__ void __launch_bounds__(64)
+// NT threads per block (64: one wave, 64 / W tasks; 256: one task per block
+// of four waves, W = 256 -- the very wide bands of edit_distance, H ~ m, whose
+// single task is latency-bound: four times the lanes per anti-diagonal and
+// the ring in LDS (up to DPW_LDS_H) instead of global memory, round 4).
+template <int W, bool GRING, int NT = 64>
+__global__ void __launch_bounds__(NT)
 k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
      const double *__restrict__ tabs, double *__restrict__ bands,
      double *__restrict__ out_score, int *__restrict__ err, int ring_ld,
      double *__restrict__ gring)
 {
-    constexpr int SEGS = 64 / W;
+    constexpr int SEGS = NT / W;
+    constexpr bool BLOCK_SYNC = GRING || NT > 64;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int seg = threadIdx.x / W;
     const int q = threadIdx.x % W;
@@ -213,7 +218,7 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
     int kmax = T.klen;
     for (int off = 32; off >= 1; off >>= 1)
         kmax = max(kmax, __shfl_xor(kmax, off));
-    if (GRING)
+    if (BLOCK_SYNC)
         __syncthreads();
     else
         wave_sync();
@@ -293,12 +298,14 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
                 r0[d] = v;
             }
         }
-        if (GRING)
+        if (BLOCK_SYNC)
             __syncthreads();
         else
             wave_sync();
     }
 }
+// widest band whose four-diagonal ring fits the LDS of k_dp<256, false, 256>
+constexpr int DPW_LDS_H = 160 * 1024 / 32 - 6;
 
 // ---------------------------------------------------------------------
 // k_dpr: register-resident variant of k_dp for bands up to H <= 32*NP.
@@ -4361,8 +4368,11 @@ int rf_create(int device, rf_ctx **out)
         (void)hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
         (void)hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
     }
-    // the lean scorer may use up to the whole 160 KiB LDS of a CU
+    // the lean scorer may use up to the whole 160 KiB LDS of a CU, and so may
+    // the very-wide-band DP's ring
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_dp<256, false, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
@@ -5341,9 +5351,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
         } else {
+            // H > 2040: one task per 256-thread block, the ring in LDS when it fits
             const int ld = P.hmaxg + 6;
-            hipLaunchKernelGGL((k_dp<64, true>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
-                               d_bands, d_out, ctx->d_err, ld, (double *)ctx->scratch[10].p);
+            if (P.hmaxg <= DPW_LDS_H)
+                hipLaunchKernelGGL((k_dp<256, false, 256>), dim3(n), dim3(256), 4 * ld * 8, st, d_tasks + L.at, n,
+                                   d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
+            else
+                hipLaunchKernelGGL((k_dp<256, true, 256>), dim3(n), dim3(256), 0, st, d_tasks + L.at, n, d_bases,
+                                   d_tabs, d_bands, d_out, ctx->d_err, ld, (double *)ctx->scratch[10].p);
         }
     }
     for (int si : used_side) {

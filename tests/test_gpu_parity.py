@@ -203,7 +203,8 @@ def test_dp_skew_trim(engine, flags):
 
 
 def test_dp_huge_band_global_ring(engine):
-    """H > 2040 takes the global-memory ring path (edit_distance-sized bands)."""
+    """H > 2040 (edit_distance-sized bands) takes the one-task-per-block path
+    (k_dp<256, false, 256>: 256 lanes per anti-diagonal, the ring in LDS)."""
     rng = np.random.default_rng(5)
     t = random_seq(2300, rng)
     s = make_read(t, rng, 0.02, 1100)
@@ -214,6 +215,23 @@ def test_dp_huge_band_global_ring(engine):
     assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, 2301, 1100)
     B_exp = oracle.backward(t, s)
     assert_band_equal(engine.download_band(0, RF_BAND_B), B_exp, len(s) + 1, 2301, 1100)
+
+
+def test_dp_band_beyond_lds_ring(engine):
+    """H > DPW_LDS_H (5114): the same block-wide DP with its ring in global
+    memory (k_dp<256, true, 256>); forward and backward bands bit-exact."""
+    rng = np.random.default_rng(6)
+    t = random_seq(5300, rng)
+    s = make_read(t, rng, 0.02, 2600)
+    engine.set_sequences(0, [s])
+    engine.set_templates(0, [t])
+    engine.realign([0], [0], 0, [2600], RF_FWD | RF_BWD)
+    H = 2 * 2600 + abs(len(s) - len(t)) + 1
+    assert H > 5114
+    A_exp, _ = oracle.forward(t, s, moves=True)
+    assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, len(t) + 1, 2600)
+    B_exp = oracle.backward(t, s)
+    assert_band_equal(engine.download_band(0, RF_BAND_B), B_exp, len(s) + 1, len(t) + 1, 2600)
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
