@@ -2667,17 +2667,20 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         }
     }
     // the chains of half H of segment D of read g (operands from LDS)
-    auto chains = [&](auto hc, const RG &g, int D) {
-        constexpr int H = decltype(hc)::value;
-        const Lane &L = hl[H];
+    // The chains of the unit's half always run on state slot 0: the halves'
+    // states are swapped after every unit of a two-half item (unit), so the
+    // unrolled body exists once (instruction cache).
+    auto chains = [&](int h, const RG &g, int D) {
+        const Lane L = h ? hl[1] : hl[0];
         const int a = L.a;
-        const int c = g.c, dfirst = g.dfirst[H], dlast = g.dlast[H];
-        const int dfmax = g.dfmax[H], dlmin = g.dlmin[H];
-        const bool peel = g.peel[H];
-        double(&pv)[4] = prev[H];
-        double(&aI)[4] = accI[H];
-        double(&aS)[4] = accS[H];
-        double &ddh = dd[H];
+        const int c = g.c, dfirst = h ? g.dfirst[1] : g.dfirst[0], dlast = h ? g.dlast[1] : g.dlast[0];
+        const int dfmax = h ? g.dfmax[1] : g.dfmax[0], dlmin = h ? g.dlmin[1] : g.dlmin[0];
+        const bool peel = h ? g.peel[1] : g.peel[0];
+        const bool uni = h ? g.uni[1] : g.uni[0];
+        double(&pv)[4] = prev[0];
+        double(&aI)[4] = accI[0];
+        double(&aS)[4] = accS[0];
+        double &ddh = dd[0];
         if (L.active && !(diag_mode & 2)) {
             const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
             const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];
@@ -2724,8 +2727,8 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
                 }
             };
             const bool full = L.all_act && dfmax <= D && dlmin >= D + S - 1;
-            const bool first_u = g.uni[H] && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0;
-            const bool last_u = g.uni[H] && D > 0 && dlast + 1 < D + S && dlast + 1 - D >= SEGL_MASKED_MIN &&
+            const bool first_u = uni && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0;
+            const bool last_u = uni && D > 0 && dlast + 1 < D + S && dlast + 1 - D >= SEGL_MASKED_MIN &&
                                 (g.P & 15) == 0;
             if (full || first_u || last_u) {
                 run(__builtin_amdgcn_readfirstlane((int)first_u) != 0);
@@ -2754,9 +2757,29 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             }
         }
     };
-    // read r's totals (after its last segment) and fresh chain state
+    // read r's totals (after its last segment) and fresh chain state.  Called
+    // after the read's last unit, before the swap: half NH-1 is in slot 0, and
+    // with two halves half 0 is in slot 1 -- swap first so that slot h holds
+    // half h
+    auto swap_slots = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double p0 = prev[0][k], i0 = accI[0][k], s0 = accS[0][k];
+            prev[0][k] = prev[1][k];
+            accI[0][k] = accI[1][k];
+            accS[0][k] = accS[1][k];
+            prev[1][k] = p0;
+            accI[1][k] = i0;
+            accS[1][k] = s0;
+        }
+        const double d0 = dd[0];
+        dd[0] = dd[1];
+        dd[1] = d0;
+    };
     auto finish = [&](int r) {
         const double qnan = __builtin_nan("");
+        if (NH == 2)
+            swap_slots();
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (h < NH && hl[h].active) {
@@ -2860,12 +2883,11 @@ k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             adv(ahead);
         if (do_load && ahead.r < r1)
             load_seg(X, ahead.g, ahead.D, ahead.h, ahead.D == first_of(ahead.g));
-        if (h == 0)
-            chains(std::integral_constant<int, 0>{}, cur.g, D);
-        else
-            chains(std::integral_constant<int, 1>{}, cur.g, D);
+        chains(h, cur.g, D);
         if (h + 1 == NH && D + S > cur.g.dhi)
-            finish(cur.r);
+            finish(cur.r);            // leaves slot h = half h, fresh: the next unit is half 0
+        else if (NH == 2)
+            swap_slots();             // slot 0 = the next unit's half
         cur = ahead;
     };
     Pos cur;
