@@ -104,6 +104,9 @@ const char *rf_last_error(const rf_ctx *ctx);
                                     threads instead of the device (k_aln_sums)     */
 #define RF_OPT_SEG_COLS    21   /* wide-band scorer columns per work item: 128
                                    (k_score_segw, default) or 64 (k_score_segl)   */
+#define RF_OPT_ALN_MARKS_MIN 22 /* rf_aln_error_sums on the device: groups of more
+                                   than this many reads (default 128) use the
+                                   per-read marks + per-column fold launches      */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -3637,6 +3637,88 @@ __global__ void __launch_bounds__(256) k_aln_sums(const AlnSumGroup *__restrict_
     }
 }
 
+// Groups with many reads (c3: one cluster of 1,000 reads) leave k_aln_sums
+// one workgroup walking every read in turn (16.6 ms per call at c3, round 4
+// profile).  There the sums run in two launches instead: k_aln_marks, one
+// wave per read, writes each MATCH move's row-code entry and base into a
+// (read, column) record; k_aln_fold, one lane per (group, column), adds the
+// records of the column's reads in batch order -- the same FP64 additions in
+// the same order per column as k_aln_sums and the host loop.
+__global__ void __launch_bounds__(64) k_aln_marks(const AlnSumGroup *__restrict__ groups, int ngroups,
+                                                  const AlnSumRead *__restrict__ reads,
+                                                  const int64_t *__restrict__ rbase,
+                                                  const double *__restrict__ tabs, const int8_t *__restrict__ moves,
+                                                  const int32_t *__restrict__ nmoves, uint32_t *__restrict__ marks)
+{
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const AlnSumRead R = reads[r];
+    const int cnt = nmoves[R.idx];
+    const int8_t *mv = moves + R.mv + (R.n + R.m - cnt);
+    const uint64_t *rec = (const uint64_t *)(tabs + R.rec);
+    uint32_t *row = marks + rbase[r];   // this read's m records
+    int ci = 0, cj = 0;
+    for (int b0 = 0; b0 < cnt; b0 += 64) {
+        const int e = b0 + lane;
+        const int v = e < cnt ? mv[e] : 0;
+        const int di = (v == 1 || v == 2) ? 1 : (v == 4 ? 3 : 0);
+        const int dj = (v == 1 || v == 3) ? 1 : (v == 5 ? 3 : 0);
+        const int x = di | (dj << 16);   // a tile moves (i, j) by at most 3 * 64 each
+        int inc = x;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(inc, off);
+            if (lane >= off)
+                inc += y;
+        }
+        if (v == 1) {
+            const int ex = inc - x;
+            const int i = ci + (ex & 0xffff), j = cj + (ex >> 16);
+            const uint64_t rc = rec[i];
+            row[j] = (uint32_t)(rc & 0xffff) | ((uint32_t)((rc >> 48) & 0xff) << 16) | 0x80000000u;
+        }
+        const int tile = __shfl(inc, 63);
+        ci += tile & 0xffff;
+        cj += tile >> 16;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_aln_fold(const AlnSumGroup *__restrict__ groups, int ngroups,
+                                                  const int64_t *__restrict__ gcol, const int64_t *__restrict__ gbase,
+                                                  const uint32_t *__restrict__ marks, const double *__restrict__ lut,
+                                                  const double *__restrict__ errlut, double *__restrict__ out,
+                                                  int64_t ncols)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ncols)
+        return;
+    int lo = 0, hi = ngroups - 1;   // the group whose columns hold e
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (gcol[mid] <= e)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const AlnSumGroup G = groups[lo];
+    const int j = (int)(e - gcol[lo]);
+    const uint32_t *col = marks + gbase[lo] + j;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < G.r1 - G.r0; ++r) {
+        const uint32_t rc = col[(int64_t)r * G.m];
+        if (rc & 0x80000000u) {
+            const int code = (int)(rc & 0xffff), sb = (int)((rc >> 16) & 0xff);
+            const double ilp = lut[4 * code], el = errlut[code];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                acc[q] += q == sb ? ilp : el;
+        }
+    }
+    double *o = out + G.out + (int64_t)j * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        o[q] = acc[q];
+}
+
 // ---------------------------------------------------------------------
 // k_scatter: one staged upload -> per-object device regions (a block per
 // segment), so a batch upload is one H2D copy instead of one per object.
@@ -3946,6 +4028,7 @@ struct Opts {
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
     int seg_cols = 128;     // RF_OPT_SEG_COLS: wide-band scorer columns per work item (128 segw, 64 segl)
+    int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -3976,7 +4059,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[21];
+    DevBuf scratch[25];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -4463,6 +4546,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_WIDE: return &o.dp_wide;
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
     case RF_OPT_SEG_COLS: return &o.seg_cols;
+    case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
     default: return nullptr;
     }
 }
@@ -6180,7 +6264,9 @@ int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms, double *g
 
 // alignment_error_probs's per-column sums on the device (k_aln_sums) for
 // rf_aln_error_sums (rifraf_batch.cpp): returns 1 (nothing done) when a read
-// has no row codes -- the caller then folds the moves on the host.
+// has no row codes -- the caller then folds the moves on the host.  A launch
+// whose largest group has more than ALN_MARKS_MIN_READS reads uses
+// k_aln_marks + k_aln_fold (RF_OPT_ALN_MARKS_MIN; tests set 0: always).
 int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
                              const int32_t *tlen, double *out)
 {
@@ -6231,7 +6317,41 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
     if (int e = upload(ctx, ctx->scratch[17], rd)) return e;
     if (int e = upload(ctx, ctx->scratch[18], gr)) return e;
     if (int e = ensure_buf(ctx, ctx->scratch[19], (size_t)std::max<int64_t>(rows * 4 * 8, 16))) return e;
-    if (ngroups > 0) {
+    int maxr = 0;
+    for (int32_t g = 0; g < ngroups; ++g)
+        maxr = std::max(maxr, slot_off[g + 1] - slot_off[g]);
+    if (ngroups > 0 && maxr > ctx->opt.aln_marks_min && ns > 0) {
+        // two launches: per-read marks, then a per-column ordered fold
+        std::vector<int64_t> rbase(ns), gcol(ngroups + 1), gbase(ngroups);
+        int64_t nm = 0, nc = 0;
+        for (int32_t g = 0; g < ngroups; ++g) {
+            gcol[g] = nc;
+            gbase[g] = nm;
+            nc += tlen[g];
+            for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
+                rbase[k] = nm;
+                nm += tlen[g];
+            }
+        }
+        gcol[ngroups] = nc;
+        if (int e = upload(ctx, ctx->scratch[21], rbase)) return e;
+        if (int e = upload(ctx, ctx->scratch[22], gcol)) return e;
+        if (int e = upload(ctx, ctx->scratch[23], gbase)) return e;
+        if (int e = ensure_buf(ctx, ctx->scratch[24], (size_t)std::max<int64_t>(nm * 4, 16))) return e;
+        HIPCHK(ctx, hipMemsetAsync(ctx->scratch[24].p, 0, (size_t)nm * 4, ctx->stream));
+        hipLaunchKernelGGL(k_aln_marks, dim3((unsigned)ns), dim3(64), 0, ctx->stream,
+                           (const AlnSumGroup *)ctx->scratch[18].p, ngroups, (const AlnSumRead *)ctx->scratch[17].p,
+                           (const int64_t *)ctx->scratch[21].p, (const double *)ctx->tab_arena.d,
+                           (const int8_t *)ctx->scratch[3].p, (const int32_t *)ctx->scratch[4].p,
+                           (uint32_t *)ctx->scratch[24].p);
+        if (nc > 0)
+            hipLaunchKernelGGL(k_aln_fold, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, ctx->stream,
+                               (const AlnSumGroup *)ctx->scratch[18].p, ngroups, (const int64_t *)ctx->scratch[22].p,
+                               (const int64_t *)ctx->scratch[23].p, (const uint32_t *)ctx->scratch[24].p,
+                               (const double *)D.lut.p, (const double *)D.errlut.p, (double *)ctx->scratch[19].p, nc);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    } else if (ngroups > 0) {
         hipLaunchKernelGGL(k_aln_sums, dim3((unsigned)ngroups), dim3(256), 0, ctx->stream,
                            (const AlnSumGroup *)ctx->scratch[18].p, (const AlnSumRead *)ctx->scratch[17].p,
                            (const double *)ctx->tab_arena.d, (const int8_t *)ctx->scratch[3].p,

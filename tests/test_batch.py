@@ -364,15 +364,18 @@ def test_native_batch_engines_one_gpu(engine):
 
 
 @pytest.mark.gpu
-def test_aln_error_sums_device_equals_host(engine, opts):
+@pytest.mark.parametrize("marks_min", [128, 0])
+def test_aln_error_sums_device_equals_host(engine, opts, marks_min):
     """alignment_error_probs's sums (model.jl:817-840) folded on the device
-    (k_aln_sums, default) and on host threads (RF_OPT_ALN_SUMS_HOST) are the
-    same bits, through the native driver's quality pass; both equal the
-    Python stage machine's."""
+    (k_aln_sums, default; with marks_min 0 the per-read marks + per-column
+    fold launches that large clusters use) and on host threads
+    (RF_OPT_ALN_SUMS_HOST) are the same bits, through the native driver's
+    quality pass; both equal the Python stage machine's."""
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams
     params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True, max_iters=20)
     clusters = _ref_free_clusters(seed=21) + _doubling_clusters()
+    opts("aln_marks_min", marks_min)
     dev = rifraf_batch(clusters, params=params, engine=engine, native=True)
     opts("aln_sums_host", 1)
     host = rifraf_batch(clusters, params=params, engine=engine, native=True)
