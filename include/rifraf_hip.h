@@ -102,8 +102,8 @@ const char *rf_last_error(const rf_ctx *ctx);
                                     tasks (k_dpr<2,..,32>); 0 = 16-lane tasks only   */
 #define RF_OPT_ALN_SUMS_HOST 19 /* 1: rf_aln_error_sums folds the moves on host
                                     threads instead of the device (k_aln_sums)     */
-#define RF_OPT_SEG_COLS    21   /* wide-band scorer columns per work item: 128
-                                   (k_score_segw, default) or 64 (k_score_segl)   */
+#define RF_OPT_SEG_COLS    21   /* wide-band scorer columns per work item: 64
+                                   (k_score_segl, default) or 128 (k_score_segw)  */
 #define RF_OPT_ALN_MARKS_MIN 22 /* rf_aln_error_sums on the device: groups of more
                                    than this many reads (default 128) use the
                                    per-read marks + per-column fold launches      */

@@ -409,9 +409,98 @@ __device__ __forceinline__ RowRec load_row(const DPTask &T, bool rev, const uint
     return r;
 }
 
+// A row record as loaded (no select applied yet: selecting right after the
+// loads would make the wave wait for them at once) -- RowRec via row_val.
+struct RawRow {
+    int sb, fl;   // fl: bit 0 row in range, bit 1 base row (ii >= 1), bit 2 codon insert, bit 3 codon delete
+    double mt, mm, is, ds, ci, cd;
+};
+__device__ __forceinline__ RawRow load_row_raw(const DPTask &T, bool rev, const uint8_t *sbase,
+                                               const double *tb, int ii, bool codon)
+{
+    const bool in = ii >= 0 && ii <= T.n;
+    const int ic = min(max(ii, 1), T.n);
+    const int iz = min(max(ii, 0), T.n);
+    const int ks = rev ? min(T.n - 1, T.n - iz) : max(iz - 1, 0);
+    const int kd = rev ? T.n - iz : iz;
+    const int ci_i = rev ? T.ncins - iz + 2 : iz - 3;
+    const int64_t ci_off = T.ncins > 0 ? 4 * (int64_t)T.n + 1 + min(max(ci_i, 0), T.ncins - 1) : ks;
+    const int64_t cd_off = T.ncdel > 0 ? 4 * (int64_t)T.n + 1 + T.ncins + kd : ks;
+    RawRow r;
+    r.sb = sbase[rev ? T.n - ic : ic - 1];
+    r.mt = tb[ks];
+    r.mm = tb[T.n + ks];
+    r.is = tb[2 * (size_t)T.n + ks];
+    r.ds = tb[3 * (size_t)T.n + kd];
+    r.ci = tb[ci_off];
+    r.cd = tb[cd_off];
+    r.fl = (in ? 1 : 0) | ((in && ii >= 1) ? 2 : 0) | ((codon && T.ncins > 0 && ii >= 3 && in) ? 4 : 0) |
+           ((codon && T.ncdel > 0 && in) ? 8 : 0);
+    return r;
+}
+__device__ __forceinline__ RowRec row_val(const RawRow &x)
+{
+    RowRec r;
+    const bool in = x.fl & 1;
+    r.sb = (x.fl & 2) ? x.sb : 4;
+    r.mt = in ? x.mt : -RF_INF;
+    r.mm = in ? x.mm : -RF_INF;
+    r.is = in ? x.is : -RF_INF;
+    r.ds = in ? x.ds : -RF_INF;
+    r.ci = (x.fl & 4) ? x.ci : -RF_INF;
+    r.cd = (x.fl & 8) ? x.cd : -RF_INF;
+    return r;
+}
+
+// load_row without branches around its loads (the non-lean kernels): every
+// load is issued at a clamped, valid index and the out-of-range values are
+// selected afterwards, so each step issues the same loads on every path and
+// hipcc's wait for them counts only the memory operations issued after them
+// (a load in a branch makes the count path-dependent: vmcnt(0), i.e. a wait
+// for every band store as well).  Same values as load_row.
+__device__ __forceinline__ RowRec load_row_flat(const DPTask &T, bool rev, const uint8_t *sbase,
+                                                const double *tb, int ii, bool codon)
+{
+    const bool in = ii >= 0 && ii <= T.n;
+    const int ic = min(max(ii, 1), T.n);   // a valid read row for the base
+    const int iz = min(max(ii, 0), T.n);
+    const int ks = rev ? min(T.n - 1, T.n - iz) : max(iz - 1, 0);
+    const int kd = rev ? T.n - iz : iz;
+    const int sb = sbase[rev ? T.n - ic : ic - 1];
+    const double mt = tb[ks], mm = tb[T.n + ks], is = tb[2 * (size_t)T.n + ks], ds = tb[3 * (size_t)T.n + kd];
+    // codon tables (align.jl:87-98): t_cins has n - 2 entries, t_cdel n + 1;
+    // a task without them reads the match table instead and discards it
+    const double *t_cins = tb + 4 * (size_t)T.n + 1;
+    const int ci_i = rev ? T.ncins - iz + 2 : iz - 3;
+    const bool has_ci = codon && T.ncins > 0 && ii >= 3 && in;
+    const bool has_cd = codon && T.ncdel > 0 && in;
+    // one load each at a selected offset (no branch): a task without the
+    // table reads its own match entry instead, never past its region
+    const int64_t ci_off = T.ncins > 0 ? 4 * (int64_t)T.n + 1 + min(max(ci_i, 0), T.ncins - 1) : ks;
+    const int64_t cd_off = T.ncdel > 0 ? 4 * (int64_t)T.n + 1 + T.ncins + kd : ks;
+    const double ci = tb[ci_off], cd = tb[cd_off];
+    (void)t_cins;
+    RowRec r;
+    r.sb = (in && ii >= 1) ? sb : 4;
+    r.mt = in ? mt : -RF_INF;
+    r.mm = in ? mm : -RF_INF;
+    r.is = in ? is : -RF_INF;
+    r.ds = in ? ds : -RF_INF;
+    r.ci = has_ci ? ci : -RF_INF;
+    r.cd = has_cd ? cd : -RF_INF;
+    return r;
+}
+
 __device__ __forceinline__ int load_col(const DPTask &T, bool rev, const uint8_t *tbase, int jj)
 {
     return (jj >= 1 && jj <= T.m) ? tbase[rev ? T.m - jj : jj - 1] : 4;
+}
+// load_col with its load issued unconditionally (load_row_flat)
+__device__ __forceinline__ int load_col_flat(const DPTask &T, bool rev, const uint8_t *tbase, int jj)
+{
+    const int jc = min(max(jj, 1), max(T.m, 1));
+    const int b = tbase[rev ? max(T.m - jc, 0) : jc - 1];
+    return (jj >= 1 && jj <= T.m) ? b : 4;
 }
 
 // Row record of the lane above (row_shl:1 / wave_shl:1); lane LPT-1 receives `edge`.
@@ -470,12 +559,18 @@ __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &
 // with the strict order.
 // ---------------------------------------------------------------------
 
-template <int NP, int PAR, int LPT = 16>
+// FLAT (the non-lean kernels): no branch around a store -- a cell outside
+// the band goes to the sink, the final score's store to the sink when this
+// is not the final cell -- and the error flag is collected in `eflag` and
+// raised once after the loop, so every step issues the same memory
+// operations on every path (load_row_flat).
+template <int NP, int PAR, int LPT = 16, bool FLAT = false>
 __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool codon, bool rev,
                                          bool skew, bool trim, double (&v1)[NP], double (&v2)[NP],
                                          double (&v3)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], double *__restrict__ band,
-                                         double *__restrict__ out_score, int *__restrict__ err)
+                                         double *__restrict__ out_score, int *__restrict__ err,
+                                         double *__restrict__ sink = nullptr, int *eflag = nullptr)
 {
     // block-edge neighbours at kappa-1 (every lane shifts: uniform control flow)
     double E1;
@@ -533,12 +628,19 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
         }
         const bool origin = ii == 0 && jj == 0;
         const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
-        if (valid && !origin && best == -RF_INF)
-            set_err(err, 1);  // "new score is invalid"
-        if (valid && ii == T.n && jj == T.m && out_score)
-            out_score[T.out_idx] = v;
-        if (stored)
-            orow[(rev ? T.H - 1 - d : d) >> 1] = v;
+        if (FLAT) {
+            *eflag |= (valid && !origin && best == -RF_INF) ? 1 : 0;   // "new score is invalid"
+            const bool fin = valid && ii == T.n && jj == T.m && out_score;
+            *(fin ? out_score + T.out_idx : sink + 2 * q + 1) = v;
+            *(stored ? orow + ((rev ? T.H - 1 - d : d) >> 1) : sink + 2 * q) = v;
+        } else {
+            if (valid && !origin && best == -RF_INF)
+                set_err(err, 1);  // "new score is invalid"
+            if (valid && ii == T.n && jj == T.m && out_score)
+                out_score[T.out_idx] = v;
+            if (stored)
+                orow[(rev ? T.H - 1 - d : d) >> 1] = v;
+        }
         nv[r] = v;
     }
 #pragma unroll
@@ -740,7 +842,84 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         col[r] = load_col(T, rev, tbase, -pp);
     }
     const int top = LPT * NP - 1;
-    RowRec nxt = load_row(T, rev, sbase, tb, top + 1 - T.c, codon);   // enters at kappa = 1
+    // general steps of the non-lean kernels: branch-free loads and stores
+    // (load_row_flat, dpr_step<FLAT>), so hipcc waits for a prefetched
+    // load without draining the band stores issued after it
+    constexpr bool FLAT = !LEAN;
+    auto lrow = [&](int ii, bool cod) {
+        return FLAT ? load_row_flat(T, rev, sbase, tb, ii, cod) : load_row(T, rev, sbase, tb, ii, cod);
+    };
+    auto lcol = [&](int jj) { return FLAT ? load_col_flat(T, rev, tbase, jj) : load_col(T, rev, tbase, jj); };
+    int eflag = 0;
+    double *gsink = sink + 64 * (threadIdx.x >> 4);   // 32 doubles per 16-lane row of the wave
+    if (FLAT) {
+        // Non-lean kernels (codon moves, skew / trim, non-finite tables; e.g. the
+        // reference's codon DP, often a single long task per launch, whose
+        // period is shorter than a load's latency): the edge row entering lane
+        // 15 at odd steps and the column base entering lane 0 at even steps are
+        // loaded QD periods ahead into QD static slots (the loop is unrolled
+        // over QD periods, so no slot is moved between registers), and their
+        // selects run at use; stores and loads are branch-free (dpr_step<FLAT>),
+        // so every wait counts only the operations issued after its load.
+        constexpr int QD = 4;
+        RawRow nq[QD];
+        int cq[QD];
+        bool cv[QD];
+#pragma unroll
+        for (int j = 0; j < QD; ++j) {
+            nq[j] = load_row_raw(T, rev, sbase, tb, top + 1 + j - T.c, codon);   // period j's edge row
+            const int jj = 1 + j;                                                // column of period 1 + j
+            cq[j] = tbase[rev ? max(T.m - min(max(jj, 1), max(T.m, 1)), 0) : min(max(jj, 1), max(T.m, 1)) - 1];
+            cv[j] = jj >= 1 && jj <= T.m;
+        }
+        for (int k0 = 0; k0 < kmax; k0 += 2 * QD) {
+#pragma unroll
+            for (int j = 0; j < QD; ++j) {
+                const int k = k0 + 2 * j;
+                if (k >= kmax)
+                    break;
+                if (k > 0) {
+                    // even step: lane 0 receives column k/2, from slot (k/2 - 1) mod QD
+                    const int cs = (j + QD - 1) % QD;   // static after unrolling
+                    const int edge = cv[cs] ? cq[cs] : 4;
+                    const int jn = k / 2 + QD;
+                    const int jc = min(max(jn, 1), max(T.m, 1));
+                    cq[cs] = tbase[rev ? max(T.m - jc, 0) : jc - 1];
+                    cv[cs] = jn >= 1 && jn <= T.m;
+                    int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF,
+                                                           false);
+                    if (TaskLanes<LPT>::EDGE_FIX && q == 0)
+                        from = edge;
+#pragma unroll
+                    for (int r = NP - 1; r > 0; --r)
+                        col[r] = col[r - 1];
+                    col[0] = from;
+                }
+                dpr_step<NP, 0, LPT, true>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score,
+                                           err, gsink, &eflag);
+                if (k + 1 < kmax) {
+                    // odd step: rows advance; lane 15 receives period k/2's row (slot j)
+                    const RowRec up = row_from_above<LPT>(row[0], row_val(nq[j]), codon);
+#pragma unroll
+                    for (int r = 0; r < NP - 1; ++r)
+                        row[r] = row[r + 1];
+                    row[NP - 1] = up;
+                    nq[j] = load_row_raw(T, rev, sbase, tb, top + k / 2 + 1 + QD - T.c, codon);
+                    dpr_step<NP, 1, LPT, true>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
+                                               out_score, err, gsink, &eflag);
+                }
+            }
+        }
+        if (eflag)
+            set_err(err, 1);  // "new score is invalid"
+        return;
+    }
+    // lean kernels: the edge row / column of the next period (one ahead)
+    constexpr int QD = 1;
+    RowRec nq[QD];
+    int cq[QD];
+    nq[0] = lrow(top + 1 - T.c, codon);   // enters at kappa = 1
+    cq[0] = lcol(1);                      // enters at kappa = 2
 
     // Lean interior [klo, khi]: the kappa range in which every cell of every
     // active diagonal of the wave's four tasks is inside the matrix, minus the
@@ -1031,14 +1210,20 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 wave_sync();
                 k += 2 * DPL_B;
             }
-            // back to the general steps: the edge row they expect
-            nxt = load_row(T, rev, sbase, tb, top + k / 2 + 1 - T.c, false);
+            // back to the general steps: the edge row and column they expect
+            // (lean kernels only, QD = 1)
+            nq[0] = lrow(top + k / 2 + 1 - T.c, false);
+            cq[0] = lcol(k / 2);
             if (k >= kmax)
                 break;
         }
         if (k > 0) {
             // even step: columns advance; lane 0 receives column k/2
-            const int edge = load_col(T, rev, tbase, k / 2);
+            const int edge = cq[0];
+#pragma unroll
+            for (int j = 0; j + 1 < QD; ++j)
+                cq[j] = cq[j + 1];
+            cq[QD - 1] = lcol(k / 2 + QD);
             int from = __builtin_amdgcn_update_dpp(edge, col[NP - 1], TaskLanes<LPT>::FROM_L1, 0xF, 0xF, false);
             if (TaskLanes<LPT>::EDGE_FIX && q == 0)
                 from = edge;
@@ -1047,19 +1232,25 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 col[r] = col[r - 1];
             col[0] = from;
         }
-        dpr_step<NP, 0, LPT>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err);
+        dpr_step<NP, 0, LPT, FLAT>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err,
+                                   gsink, &eflag);
         if (k + 1 < kmax) {
             // odd step: rows advance; lane 15 receives the prefetched row
-            const RowRec up = row_from_above<LPT>(row[0], nxt, codon);
+            const RowRec up = row_from_above<LPT>(row[0], nq[0], codon);
 #pragma unroll
             for (int r = 0; r < NP - 1; ++r)
                 row[r] = row[r + 1];
             row[NP - 1] = up;
-            nxt = load_row(T, rev, sbase, tb, top + (k + 2) / 2 + 1 - T.c, codon);
-            dpr_step<NP, 1, LPT>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
-                            out_score, err);
+#pragma unroll
+            for (int j = 0; j + 1 < QD; ++j)
+                nq[j] = nq[j + 1];
+            nq[QD - 1] = lrow(top + (k + 2) / 2 + QD - T.c, codon);
+            dpr_step<NP, 1, LPT, FLAT>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
+                                       out_score, err, gsink, &eflag);
         }
     }
+    if (FLAT && eflag)
+        set_err(err, 1);  // "new score is invalid"
 }
 
 // ---------------------------------------------------------------------
@@ -3864,8 +4055,8 @@ struct Slot {
 // Choice of dense scorer for one launch.
 struct ScorePick {
     bool lean = false;
-    bool seg = false;   // k_score_segw / k_score_segl: wide bands (window too large for LDS), finite tables
-    int segq = 128;     // seg: columns per work item (128: k_score_segw, 64: k_score_segl)
+    bool seg = false;   // k_score_segl / k_score_segw: wide bands (window too large for LDS), finite tables
+    int segq = 64;      // seg: columns per work item (64: k_score_segl, 128: k_score_segw)
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
     int q() const { return 256; }   // k_score_ws chain columns per work item
     // columns per work item of the chosen scorer (k_score: 64)
@@ -4027,7 +4218,8 @@ struct Opts {
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
-    int seg_cols = 128;     // RF_OPT_SEG_COLS: wide-band scorer columns per work item (128 segw, 64 segl)
+    int seg_cols = 64;      // RF_OPT_SEG_COLS: wide-band scorer columns per work item (64 segl, 128 segw:
+                            // measured slower at c5, round 4)
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
@@ -4372,7 +4564,7 @@ ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool a
     // wide bands: the row-segment scorer (same chains, H-independent LDS)
     if (all_finite && !force_general && !reads.empty()) {
         p.seg = true;
-        p.segq = o.seg_cols == 64 ? 64 : 128;
+        p.segq = o.seg_cols == 128 ? 128 : 64;
         return p;
     }
     p.lds = score_lds_elems(reads);

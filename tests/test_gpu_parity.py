@@ -474,10 +474,10 @@ def test_plan_cache_follows_template_content(engine):
 SCORER_CONFIGS = [
     # (score_kernel, lean_lds_kb) engine options
     ("general", None),
-    ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segw (128 columns)
-    ("seglodd", None),   # k_score_segw over odd-stride rows only (band_pad 0: 9-chunk loader)
-    ("seglpad", None),   # k_score_segw with every band line-padded (band_pad 1)
-    ("seg64", None),     # the same three on 64-column items: k_score_segl (RF_OPT_SEG_COLS 64)
+    ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segl (64 columns)
+    ("seglodd", None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
+    ("seglpad", None),   # k_score_segl with every band line-padded (band_pad 1)
+    ("seg64", None),     # the same three on 128-column items: k_score_segw (RF_OPT_SEG_COLS 128)
     ("seglodd64", None),
     ("seglpad64", None),
     (None, None),        # k_score_ws (the default for these shapes)
@@ -497,7 +497,7 @@ def test_score_dense_kernels(engine, opts, kern, lds, mode):
     the oracle."""
     pad = 64
     if kern and kern.endswith("64"):
-        opts("seg_cols", 64)
+        opts("seg_cols", 128)   # the "...64" variants: the non-default item width
         kern = kern[:-2]
     if kern in ("seglodd", "seglpad"):
         pad = 0 if kern == "seglodd" else 1
@@ -578,13 +578,13 @@ def test_score_lean_ineligible_tables(engine):
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    line-aligned row-segment scorers k_score_segw (default, 128-column items)
-    and k_score_segl (64-column items, "...64") on line-padded rows,
+    line-aligned row-segment scorers k_score_segl (default, 64-column items)
+    and k_score_segw (128-column items, the "...64" variants) on line-padded rows,
     odd-stride rows and both in one launch, and the in-place k_score
     ("general"), are bit-exact against the oracle."""
     opts("band_pad", 64)
     if kern and kern.endswith("64"):
-        opts("seg_cols", 64)
+        opts("seg_cols", 128)   # the "...64" variants: the non-default item width
         kern = None if kern == "segl64" else kern[:-2]
     if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
