@@ -2097,6 +2097,11 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #ifndef SEGL_MASKED_MIN
 #define SEGL_MASKED_MIN 20
 #endif
+// a read's last segment with all its rows in the first 16 diagonals loads
+// half lines (64 B per kappa row)
+#ifndef SEGL_HALF16
+#define SEGL_HALF16 1
+#endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
 // of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
@@ -2224,12 +2229,20 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     auto load_seg = [&](SegSet &X, const RG &g, int D, bool first) {
         const int kb = D + 2 * a0, eh = D >> 1;
         if ((g.P & 15) == 0) {
+            // a read's last segment whose rows (chain rows and the peel row,
+            // up to dhi) all lie in its first 16 diagonals reads half lines
+            // (round 4): the lanes of the upper 16 leave their registers as
+            // they are -- those LDS rows are never read (generic steps stop
+            // at dhi, the masked steps overwrite them with -Inf)
+            const bool lo16 = SEGL_HALF16 && D + 16 > g.dhi;
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
                 const int kap = min(kb + r8 + RPI * j, g.K - 1);
                 const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
-                X.ra[j] = *(const dvec2 *)(g.gA + o);
-                X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+                if (!lo16 || cc8 < 4) {
+                    X.ra[j] = *(const dvec2 *)(g.gA + o);
+                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
+                }
             }
         }
         if (first && D > 0) {
