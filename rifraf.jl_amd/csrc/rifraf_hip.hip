@@ -750,6 +750,9 @@ __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
 #endif
 #define DPL_SPREAD_ON(np, lpt) (DPL_SPREAD && (np) == 1 && (lpt) == 16)
+#ifndef DPL_SKIP_PAD
+#define DPL_SKIP_PAD 1   // lean flushes leave the padding pairs of line-padded rows unwritten
+#endif
 #ifndef DPR_WPE1
 #define DPR_WPE1 1   // minimum waves per SIMD requested for the NP = 1 kernels
 #endif
@@ -1062,6 +1065,21 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // pipeline.  Before the first block the pending set is the sink.
             constexpr int FL = dpl_flush_stores(NP, PM, LPT);
             constexpr int FLS = DPL_SPREAD_ON(NP, LPT) ? FL : 1;
+            // line-padded rows (P % 16 == 0, the wide-band stride) of a 64-lane
+            // task (round 4): every block is 2*DPL_B whole rows [g0, g0 + blk)
+            // with g0 a row start, so flush pair e is pair e % (P/2) of its
+            // row.  Pairs at or past vp = ceil(ceil(H/2) / 2) hold no in-band
+            // cell (d >= 4 vp >= H); a store that would write one writes its
+            // row's pair vp - 1 again instead (same line, same bytes), so the
+            // row's trailing padding sectors are never written.  The task is
+            // the whole wave: ph, vp and the reciprocal are scalars; e / ph is
+            // (e * (2^20 / ph + 1)) >> 20, exact for e < 2^11 and ph <= 64
+            // (error below 2^-9 against a fractional part of at most 1 - 1/ph).
+            const bool padrows = DPL_SKIP_PAD && LPT == 64 && (P & 15) == 0;
+            const int pk_ph = __builtin_amdgcn_readfirstlane(max(P >> 1, 1));
+            const int pk_vq = __builtin_amdgcn_readfirstlane((((T.H + 1) >> 1) + 1) >> 1) - 1;
+            const unsigned pk_m = (1u << 20) / (unsigned)pk_ph + 1u;
+            static_assert(LPT != 64 || dpl_b(NP, LPT) * PM < 2048, "pad-skip reciprocal range");
             dvec2 pv[FLS];
             dvec2 *pg = (dvec2 *)sink;
             int pnu = 0;
@@ -1185,9 +1203,15 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                             }
                         }
                     } else {
+                        // padded rows: whole-row blocks only (lo2 == g0, nu == DPL_B * P)
+                        const bool skp = padrows && real && lo2 == g0 && nu == DPL_B * P;
 #pragma unroll
                         for (int j = 0; j < FL; ++j) {
-                            const int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
+                            int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
+                            if (skp) {
+                                const int r = e - pk_ph * (int)(((unsigned)e * pk_m) >> 20);
+                                e -= max(r - pk_vq, 0);
+                            }
                             DP_STORE(g + e, dpl_rd2<NP>(R, u2 + 2 * (real ? e : 0)));
                         }
                     }

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 bash scripts/r04_check.sh r04g || exit 1
 bash scripts/r04_ab_c5.sh r04g_ab "RIFRAF_SEG_COLS=64" "RIFRAF_HIP_LIB=rifraf.jl_amd/librifraf_nohalf.so" \
-  "RIFRAF_HIP_LIB=rifraf.jl_amd/librifraf_mm1.so" "RIFRAF_HIP_LIB=rifraf.jl_amd/librifraf_mm10.so" || exit 1
+  "RIFRAF_HIP_LIB=rifraf.jl_amd/librifraf_mm1.so" "RIFRAF_HIP_LIB=rifraf.jl_amd/librifraf_noskip.so" || exit 1
 mkdir -p gpurun_out/r04g_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04g_prof/c3 -o p --output-format csv -- python3 scripts/c3_run.py \
   > gpurun_out/r04g_prof/c3.log 2>&1 || { echo "c3 prof failed"; tail -5 gpurun_out/r04g_prof/c3.log; exit 1; }
