@@ -1065,8 +1065,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // pipeline.  Before the first block the pending set is the sink.
             constexpr int FL = dpl_flush_stores(NP, PM, LPT);
             constexpr int FLS = DPL_SPREAD_ON(NP, LPT) ? FL : 1;
-            // line-padded rows (P % 16 == 0, the wide-band stride) of a 64-lane
-            // task (round 4): every block is 2*DPL_B whole rows [g0, g0 + blk)
+            // line-padded rows (P % 16 == 0, the wide-band stride) of 32- and
+            // 64-lane tasks (round 4): every block is 2*DPL_B whole rows [g0, g0 + blk)
             // with g0 a row start, so flush pair e is pair e % (P/2) of its
             // row.  Pairs at or past vp = ceil(ceil(H/2) / 2) hold no in-band
             // cell (d >= 4 vp >= H); a store that would write one writes its
@@ -1075,11 +1075,15 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // the whole wave: ph, vp and the reciprocal are scalars; e / ph is
             // (e * (2^20 / ph + 1)) >> 20, exact for e < 2^11 and ph <= 64
             // (error below 2^-9 against a fractional part of at most 1 - 1/ph).
-            const bool padrows = DPL_SKIP_PAD && LPT == 64 && (P & 15) == 0;
-            const int pk_ph = __builtin_amdgcn_readfirstlane(max(P >> 1, 1));
-            const int pk_vq = __builtin_amdgcn_readfirstlane((((T.H + 1) >> 1) + 1) >> 1) - 1;
+            // (32-lane tasks: two per wave, per-lane values)
+            const bool padrows = DPL_SKIP_PAD && LPT >= 32 && (P & 15) == 0;
+            int pk_ph = max(P >> 1, 1), pk_vq = ((((T.H + 1) >> 1) + 1) >> 1) - 1;
+            if (LPT == 64) {
+                pk_ph = __builtin_amdgcn_readfirstlane(pk_ph);
+                pk_vq = __builtin_amdgcn_readfirstlane(pk_vq);
+            }
             const unsigned pk_m = (1u << 20) / (unsigned)pk_ph + 1u;
-            static_assert(LPT != 64 || dpl_b(NP, LPT) * PM < 2048, "pad-skip reciprocal range");
+            static_assert(LPT < 32 || dpl_b(NP, LPT) * PM < 2048, "pad-skip reciprocal range");
             dvec2 pv[FLS];
             dvec2 *pg = (dvec2 *)sink;
             int pnu = 0;
