@@ -3511,8 +3511,9 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 }
 
 // ---------------------------------------------------------------------
-// k_bt_win: backtrace + count_errors (align.jl:229-245) for reads (no codon
-// moves, H <= 255), one wave per read, from LDS windows.
+// k_bt_win: backtrace + count_errors (align.jl:229-245), one wave per
+// alignment, from LDS windows (round 4: codon moves and any band height too --
+// the reference's codon alignment and edit_distance's wide bands).
 //
 // The walk is sequential, so the wave parallelises it across a "box" of the
 // cells it can reach next: from the current cell (ii0, jj0) lane l computes
@@ -3534,6 +3535,11 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 // With a mask, the walk also marks the proposals its alignment implies
 // (moves_to_proposals, model.jl:458-480; k_aln_props fused into the walk --
 // the set union does not depend on the walk direction).
+// Codon moves (align.jl:77-104, TRACE_CODON_INSERT / _DELETE) reach cells
+// 3 diagonals off the walk's: the windows then extend 2 more kappa rows,
+// diagonals and table rows, the box evaluates the two codon candidates after
+// the three others (the same strict-> order), and a codon move leaves the box
+// (|u| = 3), so the next box starts at the cell it reaches.
 // ---------------------------------------------------------------------
 constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
@@ -3547,6 +3553,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
 {
     __shared__ double sA[BTW_A];
     __shared__ double sTm[BTW_T], sTx[BTW_T], sTi[BTW_T], sTd[BTW_T];
+    __shared__ double sTci[BTW_T], sTcd[BTW_T];   // codon tables (codon alignments only)
     __shared__ uint8_t sS[BTW_T], sTt[BTW_T];
     const BTTask T = tasks[blockIdx.x];
     const int lane = threadIdx.x;
@@ -3560,6 +3567,10 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     const int wd = min(P, BTW_WD);
     const int W = BTW_A / wd;                          // kappa rows per window (>= 256)
     const bool skew = T.flags & 2, trim = T.flags & 4;
+    const bool cod = T.ncins > 0 || T.ncdel > 0;
+    const int ext = cod ? 2 : 0;                       // codon predecessors: 2 more rows / diagonals
+    const double *t_cins = tb + 4 * (size_t)n + 1;     // cins[ii - 3], ncins = n - 2 entries
+    const double *t_cdel = t_cins + T.ncins;           // cdel[ii], ncdel = n + 1 entries
     int8_t *out = moves + T.out;
     uint8_t *mk = mask ? mask + T.mask : nullptr;
     // this lane's box cell offsets
@@ -3573,8 +3584,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
         const int d0 = ii - jj + c;
-        const int klo_need = max(kap0 - 2 * BT_DMAX - 3, 0);
-        const int elo = max(d0 - 2, 0) >> 1, ehi = min(d0 + 2, H - 1) >> 1;
+        const int klo_need = max(kap0 - 2 * BT_DMAX - 3 - ext, 0);
+        const int elo = max(d0 - 2 - ext, 0) >> 1, ehi = min(d0 + 2 + ext, H - 1) >> 1;
         if (klo < 0 || klo_need < klo || elo < e0 || ehi >= e0 + wd) {
             const int khi = min(kap0 - 1, K - 1);
             klo = max(0, khi - W + 1);
@@ -3611,7 +3622,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             wave_sync();
         }
-        const int qlo_need = max(ii - BT_DMAX - 1, 0), rlo_need = max(jj - BT_DMAX - 2, 0);
+        const int qlo_need = max(ii - BT_DMAX - 1 - ext, 0), rlo_need = max(jj - BT_DMAX - 2, 0);
         if (q0 < 0 || qlo_need < q0 || rlo_need < r0 || ii > q0 + BTW_T - 1 || max(jj - 1, 0) > r0 + BTW_T - 1) {
             q0 = max(0, ii - BTW_T + 1);               // del index ii .. ; ks = ii - 1 ..
             r0 = max(0, max(jj - 1, 0) - BTW_T + 1);
@@ -3641,6 +3652,19 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                 sTd[e] = vd[u];
                 sS[e] = (uint8_t)vs[u];
                 sTt[e] = (uint8_t)vt[u];
+            }
+            if (cod) {
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int q = q0 + lane + 64 * u;
+                    vm[u] = T.ncins > 0 ? t_cins[min(q, T.ncins - 1)] : 0.0;
+                    vx[u] = T.ncdel > 0 ? t_cdel[min(q, T.ncdel - 1)] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    sTci[lane + 64 * u] = vm[u];
+                    sTcd[lane + 64 * u] = vx[u];
+                }
             }
             wave_sync();
         }
@@ -3683,6 +3707,16 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             if (in2 && x > best) { best = x; mv = 2; }
             x = a3 + ds;
             if (in3 && x > best) { best = x; mv = 3; }
+            if (cod) {
+                // TRACE_CODON_INSERT from (ci - 3, cj), TRACE_CODON_DELETE from (ci, cj - 3)
+                const bool in4 = valid && T.ncins > 0 && ci >= 3 && inb(ci - 3, cj);
+                const bool in5 = valid && T.ncdel > 0 && cj >= 3 && inb(ci, cj - 3);
+                const double a4 = sA[aix(in4, ci - 3, cj)], a5 = sA[aix(in5, ci, cj - 3)];
+                x = a4 + sTci[in4 ? ci - 3 - q0 : 0];
+                if (in4 && x > best) { best = x; mv = 4; }
+                x = a5 + sTcd[valid ? ci - q0 : 0];
+                if (in5 && x > best) { best = x; mv = 5; }
+            }
             pack = valid ? (mv | ((sb != tbb) ? 8 : 0) | (sb << 4)) : 0;
         }
         // ---- walk the box (uniform control flow, one readlane per move)
@@ -3721,9 +3755,15 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             } else if (mv == 2) {
                 errs += 1;
                 --ii;
-            } else {
+            } else if (mv == 3) {
                 errs += 1;
                 --jj;
+            } else if (mv == 4) {   // codon moves propose nothing (k_aln_props)
+                errs += 3;
+                ii -= 3;
+            } else {
+                errs += 3;
+                jj -= 3;
             }
         }
     }
@@ -5722,9 +5762,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     return check_err_landed(ctx);
 }
 
-// k_bt_win takes reads (no codon tables) with H <= 255; the rest (the
-// reference's codon alignments, edit_distance-sized bands) walk in k_backtrace
-static bool bt_windowed(const BTTask &t) { return t.ncins == 0 && t.ncdel == 0 && t.H <= 255; }
+// Every walk runs in k_bt_win (round 4: codon alignments and bands of any
+// height too); RF_OPT_BT_GLOBAL = 1 sends them all to k_backtrace instead
+static bool bt_windowed(const BTTask &) { return true; }
 
 // Launch the backtraces of `tasks` (moves into scratch[3] at t.out, counts in
 // scratch[4]); with d_mask, the windowed walks also mark alignment proposals.

@@ -11,7 +11,7 @@ CTRS=${3:-"FETCH_SIZE WRITE_SIZE"}
 D=gpurun_out/$TAG
 export TMPDIR=/tmp
 mkdir -p $D
-C4="python3 bench.py --no-cpu --no-secondary --e2e-clusters 0 --steps 5 --warmup 2"
+C4="python3 bench.py --no-cpu --no-secondary --no-c3 --e2e-clusters 0 --steps 5 --warmup 2"
 C5="python3 bench.py --config c5 --no-cpu --steps 5 --warmup 2"
 run() {   # name, rocprof args..., -- command
   local name=$1; shift

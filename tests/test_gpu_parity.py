@@ -763,6 +763,54 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
 
 
+@pytest.mark.parametrize("L,bw,codon", [(90, 9, True), (400, 70, True), (700, 150, False), (520, 140, True)])
+def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
+    """Round 4: k_bt_win also walks codon alignments (reference-style tables:
+    TRACE_CODON_INSERT / _DELETE leave the box, the windows cover the +-3
+    predecessors) and bands of any height (H = 301 .. 281 here, above the old
+    255 limit): moves and error counts against the oracle's trace band, and
+    the same moves as k_backtrace (bt_global = 1); alignment_proposals' fused
+    marking against the host union (codon moves propose nothing)."""
+    from rifraf_amd.align import moves_to_proposals_np
+    rng = np.random.default_rng(L * 3 + bw)
+    t = random_seq(L, rng)
+    seqs = []
+    for k in range(4):
+        if codon:
+            # a frameshifted copy of the template: codon moves on the path
+            r = make_read(t, rng, 0.03, bw).seq
+            cut = int(rng.integers(5, len(r) - 5))
+            r = np.concatenate([r[:cut], r[cut + 3:]]) if k % 2 else \
+                np.concatenate([r[:cut], random_seq(3, rng), r[cut:]])
+            lp = np.log10(rng.uniform(0.01, 0.2, len(r)))
+            seqs.append(RifrafSequence(r, lp, bw, REF_SCORES))
+        else:
+            seqs.append(make_read(t, rng, 0.05, bw))
+    n = len(seqs)
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, [t])
+    engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
+    opts("bt_global", 0)
+    got, nerr = engine.backtrace(np.arange(n))
+    opts("bt_global", 1)
+    legacy, nerr_l = engine.backtrace(np.arange(n))
+    opts("bt_global", 0)
+    exp_mask = np.zeros((L + 1, 9), np.uint8)
+    ncod = 0
+    for k, s in enumerate(seqs):
+        _, mv = oracle.forward(t, s, moves=True, bandwidth=bw)
+        ref = oracle.backtrace(mv, len(s) + 1, L + 1, bw)
+        ncod += int(np.sum(ref >= 4))
+        np.testing.assert_array_equal(got[k], ref)
+        np.testing.assert_array_equal(legacy[k], ref)
+        assert nerr[k] == nerr_l[k] == oracle.count_errors(ref, t, s.seq)
+        kk, p, b = moves_to_proposals_np(ref, t, s.seq)
+        exp_mask[p, np.where(kk == 0, b, np.where(kk == 2, 4, 5 + b))] = 1
+    if codon:
+        assert ncod > 0
+    np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
+
+
 def test_validation_skip_follows_state(engine):
     """rf_realign / rf_score_dense skip their per-job checks only for the same
     job / slot list with nothing changed since it was validated: a template
