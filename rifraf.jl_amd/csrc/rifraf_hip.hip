@@ -4302,6 +4302,7 @@ struct Opts {
     int seg_cols = 64;      // RF_OPT_SEG_COLS: wide-band scorer columns per work item (64 segl, 128 segw:
                             // measured slower at c5, round 4)
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
+    int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -4346,6 +4347,7 @@ struct rf_ctx {
     double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
     double codon_ms = 0;        // k_codon of the last rf_score (inside score_ms)
     hipEvent_t ev_codon = nullptr;
+    hipEvent_t ev_block = nullptr;   // blocking-sync event (RF_OPT_SYNC_BLOCK)
     Opts opt;
     uint64_t opt_gen = 0;      // bumped by rf_set_option (scorer plan key)
     std::vector<BTTask> bt_win, bt_old;   // backtrace descriptors of the last launch
@@ -4412,12 +4414,25 @@ int fail(rf_ctx *ctx, int code, const std::string &msg)
 
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+// The host's wait for the context's stream.  HIP's stream synchronize spins
+// on the completion signal; with RF_OPT_SYNC_BLOCK the thread sleeps on a
+// blocking-sync event instead, so a rank held to a 2-core share leaves the
+// core to its other host work (quality pass, table setup, another engine's
+// thread) while its kernels run.
+hipError_t stream_wait(rf_ctx *ctx)
+{
+    if (!ctx->opt.sync_block || !ctx->ev_block)
+        return hipStreamSynchronize(ctx->stream);
+    const hipError_t e = hipEventRecord(ctx->ev_block, ctx->stream);
+    return e != hipSuccess ? e : hipEventSynchronize(ctx->ev_block);
+}
+
 int ensure_buf(rf_ctx *ctx, DevBuf &b, size_t bytes)
 {
     if (b.cap >= bytes)
         return 0;
     if (b.p) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, stream_wait(ctx));
         HIPCHK(ctx, hipFree(b.p));
     }
     size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 16);
@@ -4506,7 +4521,7 @@ int arena_grow_impl(rf_ctx *ctx, Arena &a, int64_t need, Region *skip)
                            (const Segment *)ctx->grow_segs.p, (const uint8_t *)a.d, (uint8_t *)d);
         HIPCHK(ctx, hipGetLastError());
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     if (a.d)
         HIPCHK(ctx, hipFree(a.d));
     a.d = d;
@@ -4565,7 +4580,7 @@ int check_err(rf_ctx *ctx)
 {
     int h = 0;
     HIPCHK(ctx, hipMemcpyAsync(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     if (h) {
         int z = 0;
         HIPCHK(ctx, hipMemcpy(ctx->d_err, &z, sizeof(int), hipMemcpyHostToDevice));
@@ -4617,6 +4632,7 @@ void load_env_opts(Opts &o)
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
     o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
+    o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4741,6 +4757,7 @@ int rf_create(int device, rf_ctx **out)
     for (auto &e : ctx->ev)
         (void)hipEventCreate(&e);
     (void)hipEventCreate(&ctx->ev_codon);
+    (void)hipEventCreateWithFlags(&ctx->ev_block, hipEventBlockingSync | hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
     for (int i = 0; i < 3; ++i) {
         (void)hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
@@ -4784,6 +4801,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipEventDestroy(e);
     if (ctx->ev_codon)
         (void)hipEventDestroy(ctx->ev_codon);
+    if (ctx->ev_block)
+        (void)hipEventDestroy(ctx->ev_block);
     for (int i = 0; i < 3; ++i) {
         if (ctx->side[i]) {
             (void)hipStreamSynchronize(ctx->side[i]);
@@ -4820,6 +4839,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
     case RF_OPT_SEG_COLS: return &o.seg_cols;
     case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
+    case RF_OPT_SYNC_BLOCK: return &o.sync_block;
     default: return nullptr;
     }
 }
@@ -4866,7 +4886,7 @@ int rf_release_bands(rf_ctx *ctx)
     if (!ctx)
         return RF_ERR_ARG;
     (void)hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // no launch still reads or writes a band
+    HIPCHK(ctx, stream_wait(ctx));   // no launch still reads or writes a band
     for (auto &s : ctx->slots)
         for (Band *b : {&s.a, &s.b}) {
             b->valid = false;
@@ -5049,12 +5069,12 @@ int upload_sequence_chunk(rf_ctx *ctx, int32_t first, int32_t k0, int32_t k1, co
         if (int e = upload(ctx, ctx->scratch[5], st)) return e;
         hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
                            (const uint8_t *)ctx->scratch[6].p, (uint8_t *)ctx->tab_arena.d);
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // scratch[5] is reused below
+        HIPCHK(ctx, stream_wait(ctx));   // scratch[5] is reused below
         if (int e = upload(ctx, ctx->scratch[5], sb)) return e;
         hipLaunchKernelGGL(k_scatter, dim3(nseq), dim3(256), 0, ctx->stream, (const Segment *)ctx->scratch[5].p,
                            (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, stream_wait(ctx));
     }
     return 0;
 }
@@ -5311,7 +5331,7 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
                            (const uint8_t *)ctx->scratch[7].p + nb, (const uint8_t *)ctx->scratch[7].p,
                            (const CodeLut *)ctx->scratch[20].p, s_mis, s_ins, s_del, (double *)ctx->tab_arena.d);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // staging and descriptors are reused
+        HIPCHK(ctx, stream_wait(ctx));   // staging and descriptors are reused
         k0 = k1;
     }
     // finiteness per sequence (lean DP / scorer eligibility)
@@ -5386,7 +5406,7 @@ int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids, const ui
                            (const uint8_t *)ctx->scratch[7].p, (uint8_t *)ctx->bytes_arena.d);
         HIPCHK(ctx, hipGetLastError());
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     return 0;
 }
 
@@ -5753,7 +5773,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     HIPCHK(ctx, hipMemcpyAsync(ctx->hout, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     if (ob)
         HIPCHK(ctx, hipMemcpyAsync((char *)ctx->hout + 16, d_out, ob, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     if (ob)
         std::memcpy(out_score, (const char *)ctx->hout + 16, ob);
     float ms = 0;
@@ -5881,7 +5901,7 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
             HIPCHK(ctx, hipMemcpyAsync(all.data(), ctx->scratch[3].p, total, hipMemcpyDeviceToHost,
                                        ctx->stream));
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     if (nslots > 0)
         note_bt_ms(ctx);
     if (int e = check_err(ctx))
@@ -5953,7 +5973,7 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     note_bt_ms(ctx);
     return check_err(ctx);
 }
@@ -6200,7 +6220,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
         ref_host.resize(nprops);
         HIPCHK(ctx, hipMemcpyAsync(ref_host.data(), d_ref, nprops * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     float a = 0, b = 0, cms = 0;
     (void)hipEventElapsedTime(&a, ctx->ev[2], ctx->ev[3]);
     (void)hipEventElapsedTime(&b, ctx->ev[3], ctx->ev[4]);
@@ -6367,7 +6387,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     if (out && P.dense_total > 0)
         HIPCHK(ctx, hipMemcpyAsync(out, d_dense, sizeof(double) * P.dense_total, out_kind, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
     ctx->score_ms = ms;
@@ -6418,7 +6438,7 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     std::vector<double> buf((size_t)K * P);
     HIPCHK(ctx, hipMemcpyAsync(buf.data(), ctx->band_arena.d + b.r.off, buf.size() * 8,
                                hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     for (int jj = 0; jj <= b.m; ++jj)
         for (int d = 0; d < b.H; ++d)
             out[(size_t)jj * b.H + d] = buf[(size_t)(d + 2 * jj) * P + (d >> 1)];
@@ -6475,7 +6495,7 @@ int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes
                        mode, chunk_bytes / 16, nstreams);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     float t = 0;
     (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
     *ms = t;
@@ -6500,7 +6520,7 @@ int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms)
                            (const dvec2 *)ctx->band_arena.d, bytes / 16, (double *)ctx->scratch[9].p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     float t = 0;
     (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
     *ms = t / reps;
@@ -6633,7 +6653,7 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
     if (ns > 0)
         note_bt_ms(ctx);
     return check_err(ctx);

@@ -645,7 +645,8 @@ def _power10(x):
     import os
     from concurrent.futures import ThreadPoolExecutor
     out = np.empty_like(x)
-    nth = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    nth = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                     len(os.sched_getaffinity(0))))   # the cores this thread may use
     cut = np.linspace(0, len(x), nth + 1).astype(int)
     with ThreadPoolExecutor(nth) as ex:
         list(ex.map(lambda t: np.power(10.0, x[cut[t]:cut[t + 1]], out=out[cut[t]:cut[t + 1]]), range(nth)))

@@ -10,6 +10,6 @@ mkdir -p gpurun_out/r04g_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04g_prof/c3 -o p --output-format csv -- python3 scripts/c3_run.py \
   > gpurun_out/r04g_prof/c3.log 2>&1 || { echo "c3 prof failed"; tail -5 gpurun_out/r04g_prof/c3.log; exit 1; }
 tail -1 gpurun_out/r04g_prof/c3.log
-timeout -k 10 400 python3 scripts/e2e_pinned.py 512 16,1 2,1 2,2 16,2 > gpurun_out/r04g/e2e_pinned.jsonl 2> gpurun_out/r04g/e2e_pinned.err \
+timeout -k 10 400 python3 scripts/e2e_pinned.py 512 16,1 2,1 2,1,1 2,2 2,2,1 16,2 > gpurun_out/r04g/e2e_pinned.jsonl 2> gpurun_out/r04g/e2e_pinned.err \
   || { echo "e2e pinned failed"; tail -5 gpurun_out/r04g/e2e_pinned.err; exit 1; }
 cat gpurun_out/r04g/e2e_pinned.jsonl
