@@ -421,13 +421,15 @@ __device__ __forceinline__ RawRow load_row_raw(const DPTask &T, bool rev, const 
     const bool in = ii >= 0 && ii <= T.n;
     const int ic = min(max(ii, 1), T.n);
     const int iz = min(max(ii, 0), T.n);
-    const int ks = rev ? min(T.n - 1, T.n - iz) : max(iz - 1, 0);
+    // every index >= 0 also for a padding task (T = {}: n = 0), whose loads
+    // read the first entries of the arenas and are discarded
+    const int ks = max(rev ? min(T.n - 1, T.n - iz) : iz - 1, 0);
     const int kd = rev ? T.n - iz : iz;
     const int ci_i = rev ? T.ncins - iz + 2 : iz - 3;
     const int64_t ci_off = T.ncins > 0 ? 4 * (int64_t)T.n + 1 + min(max(ci_i, 0), T.ncins - 1) : ks;
     const int64_t cd_off = T.ncdel > 0 ? 4 * (int64_t)T.n + 1 + T.ncins + kd : ks;
     RawRow r;
-    r.sb = sbase[rev ? T.n - ic : ic - 1];
+    r.sb = sbase[max(rev ? T.n - ic : ic - 1, 0)];
     r.mt = tb[ks];
     r.mm = tb[T.n + ks];
     r.is = tb[2 * (size_t)T.n + ks];
@@ -464,9 +466,10 @@ __device__ __forceinline__ RowRec load_row_flat(const DPTask &T, bool rev, const
     const bool in = ii >= 0 && ii <= T.n;
     const int ic = min(max(ii, 1), T.n);   // a valid read row for the base
     const int iz = min(max(ii, 0), T.n);
-    const int ks = rev ? min(T.n - 1, T.n - iz) : max(iz - 1, 0);
+    // indices >= 0 for a padding task too (T = {}: n = 0; load_row_raw)
+    const int ks = max(rev ? min(T.n - 1, T.n - iz) : iz - 1, 0);
     const int kd = rev ? T.n - iz : iz;
-    const int sb = sbase[rev ? T.n - ic : ic - 1];
+    const int sb = sbase[max(rev ? T.n - ic : ic - 1, 0)];
     const double mt = tb[ks], mm = tb[T.n + ks], is = tb[2 * (size_t)T.n + ks], ds = tb[3 * (size_t)T.n + kd];
     // codon tables (align.jl:87-98): t_cins has n - 2 entries, t_cdel n + 1;
     // a task without them reads the match table instead and discards it
