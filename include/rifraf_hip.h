@@ -110,6 +110,9 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_SYNC_BLOCK  23   /* 1: host waits for the engine's stream sleep on
                                    a blocking-sync event instead of spinning
                                    (ranks held to a few host cores)             */
+#define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H 32..127
+                                   per call (codon / skew / trim) run as one
+                                   64-lane task per wave (default 1024; 0 never) */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

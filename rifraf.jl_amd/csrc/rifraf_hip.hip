@@ -190,9 +190,9 @@ __device__ __forceinline__ void wave_sync()
 // (bandedarrays.jl:176-198): kappa' = K-1-kappa, d' = H-1-d.
 // ---------------------------------------------------------------------
 
-// NT threads per block (64: one wave, 64 / W tasks; 256: one task per block
-// of four waves, W = 256 -- the very wide bands of edit_distance, H ~ m, whose
-// single task is latency-bound: four times the lanes per anti-diagonal and
+// NT threads per block (64: one wave, 64 / W tasks; W = NT = DPW_NT: one task
+// per block of DPW_NT / 64 waves -- the very wide bands of edit_distance,
+// H ~ m, whose single task is latency-bound: more lanes per anti-diagonal and
 // the ring in LDS (up to DPW_LDS_H) instead of global memory, round 4).
 template <int W, bool GRING, int NT = 64>
 __global__ void __launch_bounds__(NT)
@@ -304,8 +304,15 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
             wave_sync();
     }
 }
-// widest band whose four-diagonal ring fits the LDS of k_dp<256, false, 256>
+// widest band whose four-diagonal ring fits the LDS of k_dp<DPW_NT, false, DPW_NT>
 constexpr int DPW_LDS_H = 160 * 1024 / 32 - 6;
+// lanes of the very-wide-band task (edit_distance's band, H ~ m): each lane
+// walks ceil(H/2 / DPW_NT) pairs per anti-diagonal, one dependent table /
+// ring round trip each, so the step time falls with the lanes until the
+// block barrier dominates (round 4: 256 -> 1024)
+#ifndef DPW_NT
+#define DPW_NT 1024
+#endif
 
 // ---------------------------------------------------------------------
 // k_dpr: register-resident variant of k_dp for bands up to H <= 32*NP.
@@ -563,17 +570,18 @@ __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &
 // ---------------------------------------------------------------------
 
 // FLAT (the non-lean kernels): no branch around a store -- a cell outside
-// the band goes to the sink, the final score's store to the sink when this
-// is not the final cell -- and the error flag is collected in `eflag` and
-// raised once after the loop, so every step issues the same memory
-// operations on every path (load_row_flat).
+// the band goes to the sink -- the final cell's score is kept in a register
+// (`fval` / `fset`, stored once after the loop) and the error flag is
+// collected in `eflag` and raised once after the loop, so every step issues
+// the same memory operations on every path (load_row_flat).
 template <int NP, int PAR, int LPT = 16, bool FLAT = false>
 __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool codon, bool rev,
                                          bool skew, bool trim, double (&v1)[NP], double (&v2)[NP],
                                          double (&v3)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], double *__restrict__ band,
                                          double *__restrict__ out_score, int *__restrict__ err,
-                                         double *__restrict__ sink = nullptr, int *eflag = nullptr)
+                                         double *__restrict__ sink = nullptr, int *eflag = nullptr,
+                                         double *fval = nullptr, int *fset = nullptr)
 {
     // block-edge neighbours at kappa-1 (every lane shifts: uniform control flow)
     double E1;
@@ -582,7 +590,23 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     else
         E1 = dpp_f64<TaskLanes<LPT>::FROM_R1>(v1[0]);        // (d+1) of the last pair = lane q+1's pair 0
     double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
-    if (LPT == 16 && codon) {   // codon tasks are never lean, so never 64-lane
+    if (LPT == 64 && codon) {
+        // 64-lane non-lean tasks (round 4: a few long codon tasks, e.g. the
+        // reference's DP): one or two wave shifts per neighbour
+        constexpr int L1 = TaskLanes<64>::FROM_L1, R1 = TaskLanes<64>::FROM_R1;
+        if (NP == 1) {
+            L3a = dpp_f64<L1>(v3[0]);
+            L3b = dpp_f64<L1>(L3a);
+            R3a = dpp_f64<R1>(v3[0]);
+            R3b = dpp_f64<R1>(R3a);
+        } else {
+            L3a = dpp_f64<L1>(v3[NP - 1]);
+            L3b = dpp_f64<L1>(v3[NP > 1 ? NP - 2 : 0]);
+            R3a = dpp_f64<R1>(v3[0]);
+            R3b = dpp_f64<R1>(v3[NP > 1 ? 1 : 0]);
+        }
+    }
+    if (LPT == 16 && codon) {   // (32-lane tasks are lean only)
         if (NP == 1) {
             L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
             L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
@@ -633,8 +657,9 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
         const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
         if (FLAT) {
             *eflag |= (valid && !origin && best == -RF_INF) ? 1 : 0;   // "new score is invalid"
-            const bool fin = valid && ii == T.n && jj == T.m && out_score;
-            *(fin ? out_score + T.out_idx : sink + 2 * q + 1) = v;
+            const bool fin = valid && ii == T.n && jj == T.m;
+            *fval = fin ? v : *fval;
+            *fset |= fin ? 1 : 0;
             *(stored ? orow + ((rev ? T.H - 1 - d : d) >> 1) : sink + 2 * q) = v;
         } else {
             if (valid && !origin && best == -RF_INF)
@@ -753,8 +778,11 @@ __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
 #endif
 #define DPL_SPREAD_ON(np, lpt) (DPL_SPREAD && (np) == 1 && (lpt) == 16)
+// lean flushes leave the padding pairs of line-padded rows unwritten: bit-exact
+// but measured slower (c5 DP 26.1 against 22.9-23.1 ms, profiles/r04g_ab_c5.json:
+// the rows' half-written last lines cost more than whole ones); off
 #ifndef DPL_SKIP_PAD
-#define DPL_SKIP_PAD 1   // lean flushes leave the padding pairs of line-padded rows unwritten
+#define DPL_SKIP_PAD 0
 #endif
 #ifndef DPR_WPE1
 #define DPR_WPE1 1   // minimum waves per SIMD requested for the NP = 1 kernels
@@ -857,6 +885,8 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     };
     auto lcol = [&](int jj) { return FLAT ? load_col_flat(T, rev, tbase, jj) : load_col(T, rev, tbase, jj); };
     int eflag = 0;
+    double fval = 0.0;   // FLAT: the final cell's score (the lane that computes it)
+    int fset = 0;
     double *gsink = sink + 64 * (threadIdx.x >> 4);   // 32 doubles per 16-lane row of the wave
     if (FLAT) {
         // Non-lean kernels (codon moves, skew / trim, non-finite tables; e.g. the
@@ -902,7 +932,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     col[0] = from;
                 }
                 dpr_step<NP, 0, LPT, true>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score,
-                                           err, gsink, &eflag);
+                                           err, gsink, &eflag, &fval, &fset);
                 if (k + 1 < kmax) {
                     // odd step: rows advance; lane 15 receives period k/2's row (slot j)
                     const RowRec up = row_from_above<LPT>(row[0], row_val(nq[j]), codon);
@@ -912,12 +942,14 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                     row[NP - 1] = up;
                     nq[j] = load_row_raw(T, rev, sbase, tb, top + k / 2 + 1 + QD - T.c, codon);
                     dpr_step<NP, 1, LPT, true>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
-                                               out_score, err, gsink, &eflag);
+                                               out_score, err, gsink, &eflag, &fval, &fset);
                 }
             }
         }
         if (eflag)
             set_err(err, 1);  // "new score is invalid"
+        if (fset && out_score)
+            out_score[T.out_idx] = fval;
         return;
     }
     // lean kernels: the edge row / column of the next period (one ahead)
@@ -1264,7 +1296,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             col[0] = from;
         }
         dpr_step<NP, 0, LPT, FLAT>(T, q, k, codon, rev, skew, trim, v1, v2, v3, row, col, band, out_score, err,
-                                   gsink, &eflag);
+                                   gsink, &eflag, &fval, &fset);
         if (k + 1 < kmax) {
             // odd step: rows advance; lane 15 receives the prefetched row
             const RowRec up = row_from_above<LPT>(row[0], nq[0], codon);
@@ -1277,7 +1309,7 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 nq[j] = nq[j + 1];
             nq[QD - 1] = lrow(top + (k + 2) / 2 + QD - T.c, codon);
             dpr_step<NP, 1, LPT, FLAT>(T, q, k + 1, codon, rev, skew, trim, v1, v2, v3, row, col, band,
-                                       out_score, err, gsink, &eflag);
+                                       out_score, err, gsink, &eflag, &fval, &fset);
         }
     }
     if (FLAT && eflag)
@@ -2129,9 +2161,10 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #define SEGL_MASKED_MIN 20
 #endif
 // a read's last segment with all its rows in the first 16 diagonals loads
-// half lines (64 B per kappa row)
+// half lines (64 B per kappa row): bit-exact but measured slower (c5 scoring
+// +0.6-0.9 ms, profiles/r04g_ab_c5.json); off
 #ifndef SEGL_HALF16
-#define SEGL_HALF16 1
+#define SEGL_HALF16 0
 #endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
@@ -4306,6 +4339,7 @@ struct Opts {
                             // measured slower at c5, round 4)
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
     int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
+    int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H 32..127 tasks run as 64-lane tasks
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -4365,6 +4399,7 @@ struct rf_ctx {
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
+        size_t nx = 0;         // non-lean 64-lane tasks (RF_OPT_DP_NL64)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -4636,6 +4671,7 @@ void load_env_opts(Opts &o)
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
     o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
     o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
+    o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4770,7 +4806,7 @@ int rf_create(int device, rf_ctx **out)
     // the very-wide-band DP's ring
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_dp<256, false, 256>,
+    (void)hipFuncSetAttribute((const void *)k_dp<DPW_NT, false, DPW_NT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     *out = ctx;
     return 0;
@@ -4843,6 +4879,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SEG_COLS: return &o.seg_cols;
     case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
     case RF_OPT_SYNC_BLOCK: return &o.sync_block;
+    case RF_OPT_DP_NL64: return &o.dp_nl64;
     default: return nullptr;
     }
 }
@@ -5601,6 +5638,17 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 }
             }
         }
+        // Few non-lean tasks of H 32..127 (the reference's codon DP: one long
+        // task per call) run as one 64-lane NP = 1 task per wave: a quarter /
+        // half of the 16-lane kernels' cells per lane and step, and the
+        // launch cannot fill the GPU either way (round 4)
+        std::vector<DPTask> cx;
+        if (cr[1][0].size() + cr[2][0].size() <= (size_t)std::max(ctx->opt.dp_nl64, 0)) {
+            for (int a = 1; a <= 2; ++a) {
+                cx.insert(cx.end(), cr[a][0].begin(), cr[a][0].end());
+                cr[a][0].clear();
+            }
+        }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
         std::vector<DPTask> &all = P.tasks;
         all.clear();
@@ -5618,6 +5666,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             std::stable_sort(c.begin(), c.end(), by_len);
             all.insert(all.end(), c.begin(), c.end());
         }
+        std::stable_sort(cx.begin(), cx.end(), by_len);
+        all.insert(all.end(), cx.begin(), cx.end());
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
@@ -5640,6 +5690,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 P.nrp[a][b] = cp[a][b].size();
         for (int a = 0; a < 2; ++a)
             P.nw[a] = cw[a].size();
+        P.nx = cx.size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -5659,7 +5710,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // bands), so the smaller ones run on side streams concurrently with the
     // largest: the machine stays full through every launch's tail.
     struct Launch {
-        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<64,true>,
+        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>,
+                       // 32 / 33 = lean wide tasks, 34 = non-lean 64-lane tasks,
                        // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
     };
@@ -5683,6 +5735,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 launches.push_back({32 + a, at, P.nw[a]});
                 at += P.nw[a];
             }
+        if (P.nx) {
+            launches.push_back({34, at, P.nx});
+            at += P.nx;
+        }
         if (P.n64) {
             launches.push_back({8, at, P.n64});
             at += P.n64;
@@ -5738,6 +5794,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             hipLaunchKernelGGL(kp[c], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)),
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
+        } else if (L.kind == 34) {
+            // non-lean 64-lane NP = 1 tasks (H <= 127), one per wave
+            hipLaunchKernelGGL((k_dpr<1, false, dpl_pmax(1), 64>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n,
+                               d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 32) {
             // task-width classes, both NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
             // (H <= 127)
@@ -5753,13 +5813,13 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
         } else {
-            // H > 2040: one task per 256-thread block, the ring in LDS when it fits
+            // H > 2040: one task per DPW_NT-thread block, the ring in LDS when it fits
             const int ld = P.hmaxg + 6;
             if (P.hmaxg <= DPW_LDS_H)
-                hipLaunchKernelGGL((k_dp<256, false, 256>), dim3(n), dim3(256), 4 * ld * 8, st, d_tasks + L.at, n,
+                hipLaunchKernelGGL((k_dp<DPW_NT, false, DPW_NT>), dim3(n), dim3(DPW_NT), 4 * ld * 8, st, d_tasks + L.at, n,
                                    d_bases, d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
             else
-                hipLaunchKernelGGL((k_dp<256, true, 256>), dim3(n), dim3(256), 0, st, d_tasks + L.at, n, d_bases,
+                hipLaunchKernelGGL((k_dp<DPW_NT, true, DPW_NT>), dim3(n), dim3(DPW_NT), 0, st, d_tasks + L.at, n, d_bases,
                                    d_tabs, d_bands, d_out, ctx->d_err, ld, (double *)ctx->scratch[10].p);
         }
     }

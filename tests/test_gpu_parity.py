@@ -47,12 +47,16 @@ DP_CASES = [
 
 
 @pytest.mark.parametrize("pad", [64, 1])
-@pytest.mark.parametrize("L,err,bw,jit,codon", DP_CASES)
-def test_dp_bands_bitexact(engine, opts, L, err, bw, jit, codon, pad):
+@pytest.mark.parametrize("L,err,bw,jit,codon,nl64", [c + (1024,) for c in DP_CASES] +
+                         [c + (0,) for c in DP_CASES if c[4]])
+def test_dp_bands_bitexact(engine, opts, L, err, bw, jit, codon, nl64, pad):
     """Bands, scores, backtraces and error counts vs the oracle, with the
     default row strides and with every band's rows padded to whole 128-B
-    lines (RF_OPT_BAND_PAD = 1: even strides in every DP class)."""
+    lines (RF_OPT_BAND_PAD = 1: even strides in every DP class).  The codon
+    cases run twice: a few non-lean tasks of H 32..127 as 64-lane tasks (the
+    default, RF_OPT_DP_NL64) and in the 16-lane non-lean kernels (0)."""
     opts("band_pad", pad)
+    opts("dp_nl64", nl64)
     rng = np.random.default_rng(L * 7 + bw)
     t = random_seq(L, rng)
     seqs = []
