@@ -21,6 +21,7 @@ exactly the cluster that raised it.
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 import time
 
@@ -378,10 +379,13 @@ def _native_refs(part, states, refs, params, engine, nseq, nslot):
             "cb_errors": errors}
 
 
-def _wave_native(part, params, engine):
+def _wave_native(part, params, engine, init_lock=None):
     """One wave through the native stage machine (rf_rifraf_batch), then
     (do_score) the quality pass of every cluster with three batched engine
-    calls; host setup is vectorised across the wave's reads."""
+    calls; host setup is vectorised across the wave's reads.  init_lock
+    (several engines, rifraf_batch(init_exclusive=True)): held around the
+    native stage machine, so one engine's stage machine runs while the others
+    do their host work (setup, quality pass)."""
     from . import _lib
     from .engine import RF_BWD, RF_FWD
     from .errormodel import phred_to_log_p
@@ -514,9 +518,10 @@ def _wave_native(part, params, engine):
                           int(params.batch_fixed), params.batch_size, params.batch_threshold)
     ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
     t0 = time.perf_counter()
-    res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
-                                         read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons),
-                                         cons_off, ref=ref)
+    with (init_lock if init_lock is not None else contextlib.nullcontext()):
+        res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
+                                             read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons),
+                                             cons_off, ref=ref)
     cb_errors = ref["cb_errors"] if ref is not None else {}
     STATS["native_s"] += time.perf_counter() - t0
     for s, b in zip(allseqs, bw.tolist()):
@@ -581,14 +586,18 @@ def _wave_native(part, params, engine):
     return results
 
 
-def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None, engines=None):
+def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None, engines=None,
+                 init_exclusive: bool = False):
     """rifraf() over many independent clusters, batched on one engine.
 
     engines: several engines (contexts, each with its own HIP stream, e.g.
-    on one GPU) -- the clusters are split into contiguous shards, one per
-    engine, and each shard runs on its own host thread, so one shard's host
-    work (table setup, quality pass) overlaps another's kernels.  Clusters
-    are independent, so the results equal one engine's.
+    on one GPU), one host thread each.  The clusters are cut into waves of at
+    most min(wave, ceil(len / len(engines))) clusters, and each thread takes
+    the next wave from a shared queue, so one engine's host work (table
+    setup, quality pass) overlaps another's kernels.  init_exclusive: at most
+    one engine runs its native stage machine at a time (the others meanwhile
+    do host work: a two-stage pipeline of waves).  Clusters are independent,
+    so the results equal one engine's.
 
     clusters: sequence of dicts with the keyword arguments of model.rifraf
     (`dnaseqs`, `phreds` or `error_log_ps`, optional `consensus`,
@@ -603,17 +612,31 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
     params = params or RifrafParams()
     if engines is not None and len(engines) > 1:
         E = len(engines)
-        cut = [k * len(clusters) // E for k in range(E + 1)]
-        out = [None] * E
-        errs = [None] * E
+        wv = max(1, min(wave, -(-len(clusters) // E)))
+        starts = list(range(0, len(clusters), wv))
+        out = [None] * len(starts)
+        errs = [None] * len(starts)
+        nxt = [0]
+        qlock = threading.Lock()
+        ilock = threading.Lock() if init_exclusive else None
 
-        def shard(i):
-            try:
-                out[i] = rifraf_batch(clusters[cut[i]:cut[i + 1]], params=params, engine=engines[i], wave=wave,
-                                      native=native)
-            except BaseException as e:  # noqa: BLE001 -- re-raised below in shard order
-                errs[i] = e
-        ts = [threading.Thread(target=shard, args=(i,), daemon=True) for i in range(E)]
+        def worker(i):
+            while True:
+                with qlock:
+                    w = nxt[0]
+                    nxt[0] += 1
+                if w >= len(starts):
+                    return
+                part = clusters[starts[w]:starts[w] + wv]
+                try:
+                    if ilock is not None and (native is None or native) and \
+                            native_eligible(part, params) and hasattr(engines[i], "rifraf_batch_native"):
+                        out[w] = _wave_native(part, params, engines[i], init_lock=ilock)
+                    else:
+                        out[w] = rifraf_batch(part, params=params, engine=engines[i], wave=wv, native=native)
+                except BaseException as e:  # noqa: BLE001 -- re-raised below in wave order
+                    errs[w] = e
+        ts = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(E)]
         for t in ts:
             t.start()
         for t in ts:
