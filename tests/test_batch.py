@@ -70,15 +70,19 @@ def test_batch_waves_and_errors():
         rifraf_batch(bad, params=params, engine=OracleEngine())
 
 
-def test_batch_engine_shards_oracle():
-    """rifraf_batch(engines=[...]): contiguous cluster shards on their own
-    host threads and engines give the single-engine results, in input order."""
+@pytest.mark.parametrize("wave,excl", [(1024, False), (1, True)])
+def test_batch_engine_shards_oracle(wave, excl):
+    """rifraf_batch(engines=[...]): waves of clusters taken from a shared
+    queue by one host thread per engine (one wave per engine, or one cluster
+    per wave with the exclusive-stage-machine option) give the single-engine
+    results, in input order."""
     from oracle_engine import OracleEngine
     from rifraf_amd.batch import rifraf_batch
     clusters = _clusters()
     params = _params()
     one = rifraf_batch(clusters, params=params, engine=OracleEngine())
-    three = rifraf_batch(clusters, params=params, engines=[OracleEngine() for _ in range(3)])
+    three = rifraf_batch(clusters, params=params, engines=[OracleEngine() for _ in range(3)], wave=wave,
+                         init_exclusive=excl)
     assert len(three) == len(one)
     for x, y in zip(three, one):
         assert_same_run(summary(x), summary(y))
@@ -356,11 +360,13 @@ def test_native_batch_engines_one_gpu(engine):
     engs = [Engine(0) for _ in range(3)]
     try:
         many = rifraf_batch(clusters, params=params, engines=engs, native=True)
+        piped = rifraf_batch(clusters, params=params, engines=engs[:2], native=True, wave=3, init_exclusive=True)
     finally:
         for e in engs:
             e.close()
-    for a, b in zip(many, one):
+    for a, b, c in zip(many, one, piped):
         assert_same_run(summary(a), summary(b))
+        assert_same_run(summary(c), summary(b))
 
 
 @pytest.mark.gpu
