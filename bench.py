@@ -370,8 +370,13 @@ def main():
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
     ap.add_argument("--e2e-pin-cores", type=int, default=2,
                     help="c4 only: also time the e2e run with the rank pinned to this many host cores (0: skip)")
-    ap.add_argument("--e2e-engines", type=int, default=1,
+    ap.add_argument("--e2e-engines", type=int, default=2,
                     help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
+    ap.add_argument("--e2e-wave", type=int, default=256,
+                    help="c4 only: clusters per wave of the e2e field (waves from a shared queue per engine)")
+    ap.add_argument("--e2e-init-exclusive", type=int, default=1,
+                    help="c4 only: 1 = at most one engine in its native stage machine at a time (a two-stage "
+                         "pipeline of waves: one engine's kernels, the others' host work)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     ap.add_argument("--shared-gpu", action="store_true",
@@ -501,12 +506,13 @@ def run_e2e(args, rank, world, gpu, dist, coll):
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    rifraf_batch(clusters, params=params, engines=engs)
+    bopt = dict(engines=engs, wave=max(1, args.e2e_wave), init_exclusive=bool(args.e2e_init_exclusive))
+    rifraf_batch(clusters, params=params, **bopt)
     cold = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    res = rifraf_batch(clusters, params=params, engines=engs)
+    res = rifraf_batch(clusters, params=params, **bopt)
     elapsed = time.perf_counter() - t0
     # the same steady-state run with this rank held to 2 host cores -- its
     # share at 8 ranks on the GPU box's 16 (every thread of the process pinned
@@ -522,7 +528,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                 if dist is not None:
                     dist.barrier()
                 t0 = time.perf_counter()
-                res_pin = rifraf_batch(clusters, params=params, engines=engs)
+                res_pin = rifraf_batch(clusters, params=params, **bopt)
                 pin_s = time.perf_counter() - t0
             finally:
                 unpin_threads(saved)
@@ -548,9 +554,11 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "timing": "steady state: the second full run over the clusters (the first, 'cold', also allocates "
                       "the band arena); host setup from reads included, read simulation excluded",
             "processes_per_gpu": getattr(args, "processes_per_gpu", 1),
-            "engines_per_gpu": ne,
-            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; clusters sharded "
-                      "over engines_per_gpu contexts (own HIP stream, own host thread) in one process",
+            "engines_per_gpu": ne, "wave": bopt["wave"], "init_exclusive": bopt["init_exclusive"],
+            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; waves of clusters taken "
+                      "from a shared queue by engines_per_gpu contexts (own HIP stream, own host thread) in one "
+                      "process, at most one of them in its native stage machine at a time when init_exclusive "
+                      "(scripts/e2e_pinned.py, profiles/r04l_e2e_pipeline.jsonl)",
             "params": "batch = all 50 reads, do_score (QVs), no reference",
             "consensus_equals_template": int(tot[1]), "stage_iterations": int(tot[2]),
             "consensus_misses_explained": "profiles/r04_e2e_misses.json: every miss converges at a consensus "
