@@ -415,7 +415,17 @@ def main():
         gpu = local % ndev if ndev else local      # --shared-gpu rehearsals: several ranks per GPU
         if backend == "nccl":
             torch.cuda.set_device(gpu)
-        dist.init_process_group(backend)
+        # gloo prints its connection report on stdout, which carries only the
+        # JSON line: send fd 1 to stderr while the group connects
+        sys.stdout.flush()
+        fd1 = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend)
+        finally:
+            sys.stdout.flush()
+            os.dup2(fd1, 1)
+            os.close(fd1)
         coll = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
     n_dev, per_dev = distinct_devices(dist, device_identity(torch, gpu)) if world > 1 else (1, 1)
     args.processes_per_gpu = per_dev

@@ -69,6 +69,8 @@ def test_bench_self_launches_ranks():
                        "--no-cpu", "--dry-run"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1
+    # stdout carries the JSON line only (gloo's connection report goes to stderr)
+    assert [ln for ln in p.stdout.splitlines() if ln.strip()] == [p.stdout.strip()]
     out = lines[0]
     assert out["ranks"] == 2 and out["n_gpus"] == 2
     assert out["reads_all_ranks"] == 2 * 2 * 50
