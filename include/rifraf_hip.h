@@ -335,6 +335,18 @@ void rf_batch_release(rf_ctx *ctx);
 int rf_aln_error_sums(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
                       const int32_t *tlen, const uint8_t *const *bases, const double *const *match,
                       const int32_t *seq_len, double *out);
+/* The quality pass of many groups on the device (model.jl:737-771 estimate_probs
+ * over the dense totals, normalize_log_differences :722-735, and
+ * alignment_error_probs :817-840): out_pos[(row_g + p) * 5 + s] (p < m_g; s =
+ * Sub A..T, Del at position p + 1), out_ins[(row_g + g + p) * 4 + b] (p <= m_g),
+ * out_aln[row_g + p]; score[g] = state.score; err_out = {kind, group} (kind 1:
+ * "failed to compute a valid score", 2 / 3 / 4: sub / deletion / insertion
+ * scores cannot be positive).  10^x is the device's FP64 exp10 (~1e-15
+ * relative of the host's).  Returns 1 (nothing done) when a read has no row
+ * codes. */
+int rf_qv_probs(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                const int32_t *tlen, const double *score, double *out_pos, double *out_ins, double *out_aln,
+                int32_t *err_out);
 /* Host sums of segments values[off[k]..off[k+1]): Julia 0.6 sum() order
  * (pairwise, blocks of 1024; rifrafsequences.jl:74 est_n_errors) and the
  * plain sequential order (cumsum(...)[end], util.jl:28-38 logsumexp10). */

@@ -4370,7 +4370,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[25];
+    DevBuf scratch[27];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -6620,7 +6620,8 @@ int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms, double *g
 
 // alignment_error_probs's per-column sums on the device (k_aln_sums) for
 // rf_aln_error_sums (rifraf_batch.cpp): returns 1 (nothing done) when a read
-// has no row codes -- the caller then folds the moves on the host.  A launch
+// has no row codes -- the caller then folds the moves on the host.  out NULL:
+// the sums stay on the device (scratch[19], rf_qv_probs).  A launch
 // whose largest group has more than ALN_MARKS_MIN_READS reads uses
 // k_aln_marks + k_aln_fold (RF_OPT_ALN_MARKS_MIN; tests set 0: always).
 int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
@@ -6706,7 +6707,9 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
                                (const int64_t *)ctx->scratch[23].p, (const uint32_t *)ctx->scratch[24].p,
                                (const double *)D.lut.p, (const double *)D.errlut.p, (double *)ctx->scratch[19].p, nc);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out)
+            HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost,
+                                       ctx->stream));
     } else if (ngroups > 0) {
         hipLaunchKernelGGL(k_aln_sums, dim3((unsigned)ngroups), dim3(256), 0, ctx->stream,
                            (const AlnSumGroup *)ctx->scratch[18].p, (const AlnSumRead *)ctx->scratch[17].p,
@@ -6714,7 +6717,9 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
                            (const int32_t *)ctx->scratch[4].p, (const double *)D.lut.p, (const double *)D.errlut.p,
                            (double *)ctx->scratch[19].p);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out)
+            HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost,
+                                       ctx->stream));
     }
     HIPCHK(ctx, stream_wait(ctx));
     if (ns > 0)
@@ -6727,4 +6732,188 @@ void rf_internal_arena_stats(const rf_ctx *ctx, int64_t *grows, double *secs)
 {
     *grows = ctx ? ctx->arena_grows : 0;
     *secs = ctx ? ctx->arena_grow_s : 0.0;
+}
+
+
+// ---------------------------------------------------------------------
+// k_qv: the quality pass's normalisations on the device (round 4)
+//
+// estimate_probs (model.jl:737-771, normalize_log_differences :722-735) and
+// alignment_error_probs' final step (:835-839) for one cluster per
+// workgroup, from its dense totals ((m+1) x 9, rf_score_dense's layout) and
+// its per-column base-distribution sums (m x 4, k_aln_sums): the maxima,
+// the checks and the row sums exactly as rf_host_qv_prep / rf_host_qv_finish
+// (same order), with 10^x evaluated by the device's FP64 exp10 instead of the
+// host's numpy power -- within 2 ulp of it, so the probabilities agree with
+// the host path to ~1e-15 relative (tests/test_batch.py compares them at
+// 1e-12), not bit for bit.  The consensus, scores and accepted proposals do
+// not depend on this step.
+// ---------------------------------------------------------------------
+struct alignas(16) QvGroup {
+    int64_t dense_off;   // doubles: (m + 1) x 9 dense totals
+    int64_t sums_off;    // doubles: m x 4 alignment sums
+    int64_t pos_off;     // rows of out_pos (m rows of 5)
+    int64_t ins_off;     // rows of out_ins (m + 1 rows of 4)
+    int64_t cons_off;    // bytes arena: the consensus bases
+    double score;        // state.score
+    int32_t m, pad;
+};
+
+__global__ void __launch_bounds__(256) k_qv(const QvGroup *__restrict__ groups, const double *__restrict__ dense,
+                                            const double *__restrict__ sums, const uint8_t *__restrict__ bases,
+                                            double *__restrict__ pos, double *__restrict__ ins,
+                                            double *__restrict__ aln, int32_t *__restrict__ gerr)
+{
+    __shared__ double rS[4], rD[4], rI[4];
+    __shared__ int rN[4];
+    const QvGroup G = groups[blockIdx.x];
+    const double *D = dense + G.dense_off;
+    const uint8_t *cons = bases + G.cons_off;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, m = G.m;
+    double mS = -RF_INF, mD = -RF_INF, mI = -RF_INF;
+    int nan = 0;
+    for (int p = tid; p <= m; p += 256) {
+        const double *d = D + (size_t)p * 9;
+        for (int q = 5; q < 9; ++q) {
+            nan |= d[q] != d[q];
+            mI = d[q] > mI ? d[q] : mI;
+        }
+        if (p >= 1) {
+            const int cb = cons[p - 1];
+            for (int q = 0; q < 5; ++q)
+                nan |= (q != cb && d[q] != d[q]) ? 1 : 0;
+            for (int q = 0; q < 4; ++q) {
+                const double v = q == cb ? 0.0 + G.score : d[q];
+                mS = v > mS ? v : mS;
+            }
+            mD = d[4] > mD ? d[4] : mD;
+        }
+    }
+    // maxima are exact in any order
+    for (int off = 32; off >= 1; off >>= 1) {
+        mS = fmax(mS, __shfl_xor(mS, off));
+        mD = fmax(mD, __shfl_xor(mD, off));
+        mI = fmax(mI, __shfl_xor(mI, off));
+        nan |= __shfl_xor(nan, off);
+    }
+    if (lane == 0) {
+        rS[w] = mS;
+        rD[w] = mD;
+        rI[w] = mI;
+        rN[w] = nan;
+    }
+    __syncthreads();
+    mS = fmax(fmax(rS[0], rS[1]), fmax(rS[2], rS[3]));
+    mD = fmax(fmax(rD[0], rD[1]), fmax(rD[2], rD[3]));
+    mI = fmax(fmax(rI[0], rI[1]), fmax(rI[2], rI[3]));
+    nan = rN[0] | rN[1] | rN[2] | rN[3];
+    double mx = mS;   // Python max(mxS, mxD, mxI)
+    if (mD > mx)
+        mx = mD;
+    if (mI > mx)
+        mx = mI;
+    const int e = nan ? 1 : mS - mx > 0.0 ? 2 : mD - mx > 0.0 ? 3 : mI - mx > 0.0 ? 4 : 0;
+    if (tid == 0)
+        gerr[blockIdx.x] = e;
+    if (e)
+        return;
+    const double st_pow = exp10(G.score - mx);
+    for (int p = tid; p <= m; p += 256) {
+        const double *d = D + (size_t)p * 9;
+        double ei[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            ei[q] = exp10(d[5 + q] - mx);
+        const double si = st_pow + (((ei[0] + ei[1]) + ei[2]) + ei[3]);
+        double *oi = ins + (size_t)(G.ins_off + p) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            oi[q] = ei[q] / si;
+        if (p >= 1) {
+            const int cb = cons[p - 1];
+            double ep[5];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                ep[q] = exp10((q == cb ? 0.0 + G.score : d[q]) - mx);
+            ep[4] = exp10(d[4] - mx);
+            const double sp = (((ep[0] + ep[1]) + ep[2]) + ep[3]) + ep[4];
+            double *op = pos + (size_t)(G.pos_off + p - 1) * 5;
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                op[q] = ep[q] / sp;
+            const double *a = sums + G.sums_off + (size_t)(p - 1) * 4;
+            double ea[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                ea[q] = exp10(a[q]);
+            const double t = ((ea[0] + ea[1]) + ea[2]) + ea[3];
+            double mxq = ea[0] / t;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {   // numpy max: NaN propagates
+                const double v = ea[q] / t;
+                mxq = (mxq != mxq || !(v <= mxq)) ? (mxq != mxq ? mxq : v) : mxq;
+            }
+            aln[G.pos_off + p - 1] = 1.0 - mxq;
+        }
+    }
+}
+
+extern "C" int rf_qv_probs(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
+                           const int32_t *tlen, const double *score, double *out_pos, double *out_ins,
+                           double *out_aln, int32_t *err_out)
+{
+    if (!ctx || ngroups < 0 ||
+        (ngroups > 0 && (!slot_off || !slots || !tlen || !score || !out_pos || !out_ins || !out_aln || !err_out)))
+        return fail(ctx, RF_ERR_ARG, "rf_qv_probs: bad arguments");
+    err_out[0] = err_out[1] = 0;
+    if (ngroups == 0)
+        return 0;
+    (void)hipSetDevice(ctx->device);
+    // 1. dense totals, kept on the device (scratch[15], dplan's group offsets)
+    if (int e = score_dense_impl(ctx, ngroups, slot_off, slots, nullptr, hipMemcpyDeviceToHost))
+        return e;
+    // 2. the alignment sums, kept on the device (scratch[19]); 1 = a read
+    //    without row codes: the caller takes the host path
+    if (int e = rf_internal_aln_sums_dev(ctx, ngroups, slot_off, slots, tlen, nullptr))
+        return e;
+    const auto &P = ctx->dplan;
+    std::vector<QvGroup> gq(ngroups);
+    int64_t rows = 0;
+    for (int32_t g = 0; g < ngroups; ++g) {
+        if (P.groups[g].m != tlen[g])
+            return fail(ctx, RF_ERR_ARG, "rf_qv_probs: consensus length differs from the bands'");
+        const Band &b = ctx->slots[slots[slot_off[g]]].a;
+        QvGroup &q = gq[g];
+        q.dense_off = P.groups[g].dense_off;
+        q.sums_off = rows * 4;
+        q.pos_off = rows;
+        q.ins_off = rows + g;
+        q.cons_off = ctx->tpls[b.tpl].bases.off;
+        q.score = score[g];
+        q.m = tlen[g];
+        rows += tlen[g];
+    }
+    if (int e = upload(ctx, ctx->scratch[25], gq)) return e;
+    const size_t npos = (size_t)rows * 5, nins = (size_t)(rows + ngroups) * 4, naln = (size_t)rows;
+    const size_t ob = align_up((npos + nins + naln) * 8, 256);
+    if (int e = ensure_buf(ctx, ctx->scratch[26], ob + (size_t)ngroups * 4)) return e;
+    double *d_pos = (double *)ctx->scratch[26].p, *d_ins = d_pos + npos, *d_aln = d_ins + nins;
+    int32_t *d_gerr = (int32_t *)((char *)ctx->scratch[26].p + ob);
+    hipLaunchKernelGGL(k_qv, dim3((unsigned)ngroups), dim3(256), 0, ctx->stream, (const QvGroup *)ctx->scratch[25].p,
+                       (const double *)ctx->scratch[15].p, (const double *)ctx->scratch[19].p,
+                       (const uint8_t *)ctx->bytes_arena.d, d_pos, d_ins, d_aln, d_gerr);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<int32_t> gerr(ngroups);
+    HIPCHK(ctx, hipMemcpyAsync(out_pos, d_pos, npos * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out_ins, d_ins, nins * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out_aln, d_aln, naln * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(gerr.data(), d_gerr, (size_t)ngroups * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, stream_wait(ctx));
+    for (int32_t g = 0; g < ngroups; ++g)
+        if (gerr[g]) {
+            err_out[0] = gerr[g];
+            err_out[1] = g;
+            break;
+        }
+    return 0;
 }

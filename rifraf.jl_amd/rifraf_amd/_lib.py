@@ -42,6 +42,7 @@ _SIGNATURES = {
     "rf_batch_fetch_ref": (c_int, [c_void_p, c_int32] + [c_void_p] * 6),
     "rf_batch_release": (None, [c_void_p]),
     "rf_aln_error_sums": (c_int, [c_void_p, c_int32] + [c_void_p] * 7),
+    "rf_qv_probs": (c_int, [c_void_p, c_int32] + [c_void_p] * 8),
     "rf_host_julia_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
     "rf_host_seq_sums": (c_int, [c_int64, c_void_p, c_void_p, c_void_p]),
     "rf_host_tables_from_codes": (c_int, [c_int64] + [c_void_p] * 5 + [c_double] * 3 + [c_void_p] * 6),

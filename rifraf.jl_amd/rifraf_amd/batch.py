@@ -379,17 +379,21 @@ def _native_refs(part, states, refs, params, engine, nseq, nslot):
             "cb_errors": errors}
 
 
-def _wave_native(part, params, engine, init_lock=None):
+def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     """One wave through the native stage machine (rf_rifraf_batch), then
     (do_score) the quality pass of every cluster with three batched engine
     calls; host setup is vectorised across the wave's reads.  init_lock
     (several engines, rifraf_batch(init_exclusive=True)): held around the
     native stage machine, so one engine's stage machine runs while the others
-    do their host work (setup, quality pass)."""
+    do their host work (setup, quality pass).  device_qv: the quality pass's
+    normalisations on the device (engine.qv_probs: 10^x by the GPU's exp10,
+    ~1e-15 relative of numpy's, not bit for bit) when every read is
+    row-coded; False keeps them on the host (bit-identical to the Python
+    stage machine)."""
     from . import _lib
     from .engine import RF_BWD, RF_FWD
     from .errormodel import phred_to_log_p
-    from .model import RifrafResult, Stage, check_params, initial_state, qvs_many_lib
+    from .model import EstimatedProbs, RifrafResult, Stage, check_params, initial_state, qvs_many_lib
     from .poisson import cquantile_poisson_many
     from .proposals import AmbiguousProposalsError
     from .rifrafsequences import RifrafSequence
@@ -571,9 +575,26 @@ def _wave_native(part, params, engine, init_lock=None):
                 total += v
             st_.score = total
             at += n
+        tl = [len(st_.consensus) for st_ in states]
+        qv = None
+        if device_qv and coded is not None and hasattr(engine, "qv_probs") and min(tl) > 0:
+            qv = engine.qv_probs(groups, tl, [st_.score for st_ in states])
+        if qv is not None:
+            pos, ins, aln, err = qv
+            if err[0]:
+                raise RifrafError({1: "failed to compute a valid score", 2: "sub scores cannot be positive",
+                                   3: "deletion scores cannot be positive",
+                                   4: "insertion scores cannot be positive"}[int(err[0])])
+            row = 0
+            for k, m in enumerate(tl):
+                results[k].error_probs = EstimatedProbs(pos[row:row + m, :4], pos[row:row + m, 4],
+                                                        ins[row + k:row + k + m + 1])
+                results[k].aln_error_probs = aln[row:row + m]
+                row += m
+            STATS["score_phase_s"] += time.perf_counter() - t0
+            return results
         dense = engine.score_dense(groups, rows=[len(st_.consensus) + 1 for st_ in states])
         ridx = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int64) for k, st_ in enumerate(states)])
-        tl = [len(st_.consensus) for st_ in states]
         sums = engine.aln_error_sums_ptr(groups, tl, None, None, lens[ridx]) if coded is not None else None
         if sums is None:        # host fold: the reads' bases and match scores
             ft = tabs["source"].full() if coded is not None else tabs
@@ -587,7 +608,7 @@ def _wave_native(part, params, engine, init_lock=None):
 
 
 def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None, engines=None,
-                 init_exclusive: bool = False):
+                 init_exclusive: bool = False, device_qv: bool = True):
     """rifraf() over many independent clusters, batched on one engine.
 
     engines: several engines (contexts, each with its own HIP stream, e.g.
@@ -597,7 +618,8 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
     setup, quality pass) overlaps another's kernels.  init_exclusive: at most
     one engine runs its native stage machine at a time (the others meanwhile
     do host work: a two-stage pipeline of waves).  Clusters are independent,
-    so the results equal one engine's.
+    so the results equal one engine's.  device_qv (native driver): the
+    quality pass's normalisations on the device (see _wave_native).
 
     clusters: sequence of dicts with the keyword arguments of model.rifraf
     (`dnaseqs`, `phreds` or `error_log_ps`, optional `consensus`,
@@ -631,9 +653,10 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
                 try:
                     if ilock is not None and (native is None or native) and \
                             native_eligible(part, params) and hasattr(engines[i], "rifraf_batch_native"):
-                        out[w] = _wave_native(part, params, engines[i], init_lock=ilock)
+                        out[w] = _wave_native(part, params, engines[i], init_lock=ilock, device_qv=device_qv)
                     else:
-                        out[w] = rifraf_batch(part, params=params, engine=engines[i], wave=wv, native=native)
+                        out[w] = rifraf_batch(part, params=params, engine=engines[i], wave=wv, native=native,
+                                              device_qv=device_qv)
                 except BaseException as e:  # noqa: BLE001 -- re-raised below in wave order
                     errs[w] = e
         ts = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(E)]
@@ -660,7 +683,7 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
     for w0 in range(0, len(clusters), wave):
         part = clusters[w0:w0 + wave]
         if native:
-            results[w0:w0 + len(part)] = _wave_native(part, params, engine)
+            results[w0:w0 + len(part)] = _wave_native(part, params, engine, device_qv=device_qv)
             continue
         stride = max(len(c["dnaseqs"]) for c in part) + 2
         hub = _Hub(engine, len(part), stride)

@@ -274,6 +274,30 @@ class Engine:
         self._check(rc)
         return [out[row[g]:row[g + 1]] for g in range(len(groups))]
 
+    def qv_probs(self, groups, tlens, scores):
+        """The quality pass on the device (rf_qv_probs): dense totals, the
+        alignment sums and estimate_probs' / alignment_error_probs'
+        normalisations for every group, without the totals leaving the GPU.
+        Returns (pos (M, 5), ins (M + K, 4), aln (M,), err (kind, group)) --
+        the arrays rf_host_qv_prep / rf_host_qv_finish produce, with 10^x from
+        the device's exp10 (within ~1e-15 relative, not bit for bit) -- or
+        None when a read has no row codes (the host path then runs)."""
+        off = np.zeros(len(groups) + 1, np.int32)
+        np.cumsum([len(g) for g in groups], out=off[1:])
+        slots = np.ascontiguousarray(np.concatenate([np.asarray(g, np.int32) for g in groups])
+                                     if groups else np.zeros(0, np.int32))
+        tl = np.ascontiguousarray(tlens, np.int32)
+        sc = np.ascontiguousarray(scores, np.float64)
+        M, K = int(tl.sum()), len(groups)
+        pos, ins, aln = np.empty((M, 5)), np.empty((M + K, 4)), np.empty(M)
+        err = np.zeros(2, np.int32)
+        rc = self.lib.rf_qv_probs(self.ctx, K, ptr(off), ptr(slots), ptr(tl), ptr(sc), ptr(pos), ptr(ins),
+                                  ptr(aln), ptr(err))
+        if rc == 1:
+            return None
+        self._check(rc)
+        return pos, ins, aln, err
+
     def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
         """Batched forward_moves!/backward! fill; returns A[end,end] (RF_FWD)
         or B[1,1] per job."""

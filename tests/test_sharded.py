@@ -130,7 +130,12 @@ def _w_sampled(rank, world, seed):
     return _sampled(_sharded_factory, seed)
 
 
-def assert_same_run(a, b):
+# device quality pass (rifraf_batch(device_qv=True): 10^x by the GPU's exp10)
+# against a host evaluation: relative / absolute tolerance of the QVs
+QV_RTOL, QV_ATOL = 1e-12, 1e-15
+
+
+def assert_same_run(a, b, qv_rtol=0.0):
     np.testing.assert_array_equal(a["consensus"], b["consensus"])
     assert a["score"] == b["score"]
     assert a["iters"] == b["iters"] and a["converged"] == b["converged"]
@@ -142,6 +147,8 @@ def assert_same_run(a, b):
     for k in ("sub", "dele", "ins", "aln"):
         if a[k] is None:
             assert b[k] is None
+        elif qv_rtol:
+            np.testing.assert_allclose(a[k], b[k], rtol=qv_rtol, atol=QV_ATOL, err_msg=k)
         else:
             np.testing.assert_array_equal(a[k], b[k])
 

@@ -42,7 +42,9 @@ pytestmark = pytest.mark.gpu
 NTHREADS = min(16, os.cpu_count() or 1)
 
 
-def assert_same_run(a, b):
+def assert_same_run(a, b, qv_rtol=0.0):
+    """qv_rtol > 0: the QVs within that relative tolerance (+ 1e-15
+    absolute) -- a native run's device quality pass against a host one."""
     np.testing.assert_array_equal(a.consensus, b.consensus)
     assert a.state.score == b.state.score
     assert a.state.stage_iterations == b.state.stage_iterations
@@ -55,8 +57,15 @@ def assert_same_run(a, b):
         assert b.error_probs is None
     else:
         for f in ("sub", "dele", "ins"):
-            np.testing.assert_array_equal(getattr(a.error_probs, f), getattr(b.error_probs, f), err_msg=f)
-        np.testing.assert_array_equal(a.aln_error_probs, b.aln_error_probs)
+            if qv_rtol:
+                np.testing.assert_allclose(getattr(a.error_probs, f), getattr(b.error_probs, f), rtol=qv_rtol,
+                                           atol=1e-15, err_msg=f)
+            else:
+                np.testing.assert_array_equal(getattr(a.error_probs, f), getattr(b.error_probs, f), err_msg=f)
+        if qv_rtol:
+            np.testing.assert_allclose(a.aln_error_probs, b.aln_error_probs, rtol=qv_rtol, atol=1e-15)
+        else:
+            np.testing.assert_array_equal(a.aln_error_probs, b.aln_error_probs)
 
 
 def _masked(got, ref, t):
@@ -117,7 +126,9 @@ def test_c3_throughput_frame_run_matches_oracle(engine):
     kw = dict(dnaseqs=reads, phreds=phreds, reference=ref)
     assert native_eligible([kw], params)
     n = rifraf_batch([kw], params=params, engine=engine, native=True)[0]
-    assert_same_run(n, b)
+    assert_same_run(n, b, qv_rtol=1e-12)        # device quality pass
+    n0 = rifraf_batch([kw], params=params, engine=engine, native=True, device_qv=False)[0]
+    assert_same_run(n0, b)
     assert n.state.n_ref_indel_mults == b.state.n_ref_indel_mults
 
 
@@ -158,7 +169,7 @@ def test_c4_throughput_runs_match_oracle(engine):
         a = rifraf(params=params, engine=engine, **kw)
         b = rifraf(params=params, engine=OracleEngine(), **kw)
         assert_same_run(a, b)
-        assert_same_run(n, b)
+        assert_same_run(n, b, qv_rtol=1e-12)    # device quality pass
         assert b.error_probs is not None
 
 
