@@ -370,7 +370,7 @@ def main():
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
     ap.add_argument("--e2e-pin-cores", type=int, default=2,
                     help="c4 only: also time the e2e run with the rank pinned to this many host cores (0: skip)")
-    ap.add_argument("--e2e-engines", type=int, default=2,
+    ap.add_argument("--e2e-engines", type=int, default=1,
                     help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
     ap.add_argument("--e2e-wave", type=int, default=256,
                     help="c4 only: clusters per wave of the e2e field (waves from a shared queue per engine)")
