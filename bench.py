@@ -381,6 +381,9 @@ def main():
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal only: allow several ranks on one GPU (n_gpus then counts distinct devices)")
+    ap.add_argument("--score-fwd", action="store_true",
+                    help="c4 step as the fused-step prototype: rf_realign RF_BWD only, then rf_score_dense with "
+                         "the forward band filled inside the scorer (RF_OPT_SCORE_FWD, k_fuse)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch, rendezvous, workload and device assignment only (no engine): checks the "
                          "multi-rank plumbing on a host without GPUs")
@@ -663,8 +666,14 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     from rifraf_amd.engine import pack_groups
     packed = pack_groups(groups)   # the caller's slot lists, packed once
 
+    # --score-fwd: the fused-step prototype (k_fuse fills A inside the scorer;
+    # the DP pass computes B only)
+    dp_flags = RF_BWD if args.score_fwd else RF_FWD | RF_BWD
+    if args.score_fwd:
+        eng.set_option("score_fwd", 1)
+
     def step():
-        eng.realign(slots, slots, tpl_of, bws, RF_FWD | RF_BWD)
+        eng.realign(slots, slots, tpl_of, bws, dp_flags)
         dp_ms, _, _ = eng.last_timing()
         eng.score_dense(packed, to_host=False)
         _, sc_ms, _ = eng.last_timing()
@@ -717,7 +726,8 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         "data": "synthetic (restated sample.jl simulator, seeded)",
         "config": {"workload": args.config, "description": label, "clusters_per_gpu": nclu,
                    "reads_per_cluster": nreads, "template_len": length, "error_rate": err,
-                   "bandwidth": bw, "parallelism": f"clusters sharded over {world} rank(s)"},
+                   "bandwidth": bw, "parallelism": f"clusters sharded over {world} rank(s)",
+                   "step": "B fill + fused A fill / scoring (k_fuse)" if args.score_fwd else "A/B fill + scoring"},
         "proposals_per_s": tot_props / elapsed,
         "pairs_per_s": tot_pairs / elapsed,
         "dp_ms": dp_ms,

@@ -113,6 +113,13 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H 32..127
                                    per call (codon / skew / trim) run as one
                                    64-lane task per wave (default 1024; 0 never) */
+#define RF_OPT_SCORE_FWD   25   /* 1: rf_score_dense / rf_score_dense_dev fill the
+                                   forward band inside the scorer (k_fuse, the
+                                   fused-step prototype) when every read is lean
+                                   with H <= 127: only the B bands
+                                   (rf_realign RF_BWD) are read, A is neither read
+                                   nor needed; other launches use A as usual.
+                                   align.jl:155-179 + model.jl:242-285, 389-393 */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -1891,6 +1891,215 @@ __device__ __forceinline__ void lean_chain_any(const ScoreRead &R, const LeanWin
     lean_chain(R, w, a, m, sA, sB, sT, tI, tS, tD);
 }
 
+// ---------------------------------------------------------------------
+// k_fuse: dense scoring with the forward band filled inside the scorer
+// (round 4 prototype of the fused step; RF_OPT_SCORE_FWD)
+//
+// The chain of a new column built from A column a (lean_chain) visits rows
+// d = 1 .. H of that column in order, and row d of column a is anti-diagonal
+// kappa = d + 2a: at step kappa the chain needs exactly the cell the forward
+// fill computes at that step (A(d, a)) and its insert predecessor
+// (A(d-1, a), kappa-1).  So the chains ride on the fill's wavefront: the lane
+// that computes cell (d, a) also advances column a's chain by one row, and a
+// chain moves up one lane with its column every period (DPP row_shr, -Inf
+// state entering lane 0).  A is never stored or read back; B (rf_realign
+// RF_BWD) is read once, one 128-B run per task and step.
+//
+// Per task (one read, lean tables; LPT = 16: one DPP row, 4 tasks per wave,
+// H <= 31; LPT = 64: one task per wave, H <= 127, the same moves as wave
+// shifts): lane q holds band rows {2q, 2q+1} as in k_dpr
+// (align.jl:155-179 order and sums: the cells are bit-identical), and the
+// chain rows use the same operands and FP64 ops as lean_chain
+// (model.jl:242-285, util.jl:40-48).  Rows outside a chain's range are made
+// no-ops by selecting -Inf operands (a chain row with aprev = dl = -Inf keeps
+// its -Inf state; bI = bS = -Inf leave the maxima unchanged), the peeled row
+// below column a's band is the generic row with dl = bI = -Inf.  A chain is
+// finished at d = H (lane H >> 1) and writes its read's per-position partial
+// record (the k_score_segl split layout); k_reduce folds the reads in batch
+// order (model.jl:389-393).  Inputs of QD periods ahead (row record, column
+// base, the two B cells) sit in static register slots of a loop unrolled
+// over QD periods.
+// ---------------------------------------------------------------------
+struct alignas(16) FuseTask {
+    int64_t B;      // B band offset (doubles)
+    int64_t sb, tab, tb;
+    int64_t out;    // this read's partial records (doubles from the split base), (m+1) x 9
+    int32_t n, m, H, c, vb, P, K, pad;
+};
+
+#ifndef FUSE_QD
+#define FUSE_QD 4
+#endif
+
+template <int LPT>
+__global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks, int ntasks,
+                                             const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
+                                             const double *__restrict__ bands, double *__restrict__ split)
+{
+    constexpr int QD = FUSE_QD;
+    constexpr int L1 = TaskLanes<LPT>::FROM_L1, R1 = TaskLanes<LPT>::FROM_R1;
+    static_assert(LPT == 16 || LPT == 64, "k_fuse tasks are 16 or 64 lanes");
+    const int q = threadIdx.x & (LPT - 1);
+    const int tid = blockIdx.x * (64 / LPT) + threadIdx.x / LPT;
+    FuseTask T = {};
+    const bool live = tid < ntasks;
+    if (live)
+        T = tasks[tid];
+    int kmax = T.K;
+    for (int off = 32; off >= 1; off >>= 1)
+        kmax = max(kmax, __shfl_xor(kmax, off));
+    kmax = __builtin_amdgcn_readfirstlane(kmax);
+    const int n = T.n, m = T.m, H = T.H, c = T.c, vb = T.vb, P = T.P, K = T.K;
+    const uint8_t *sq = bases + T.sb;
+    const uint8_t *tq = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    const double *Bb = bands + T.B;
+    double *out = split + T.out;
+
+    // inputs of period p: the column base of jj = p - q (both steps), the row
+    // record of ii = q + p + 1 - c (odd step of p, even step of p + 1), and
+    // B at (2p, 2q) and (2p + 1, 2q + 1).  Loaded raw at clamped indices (a
+    // padding task, T = {}, reads the arenas' first entries), masked at use.
+    struct Slot {
+        int cb, sb;
+        double mt, mm, is, ds, be, bo;
+    };
+    auto load = [&](int p, Slot &S) {
+        const int jc = min(max(p - q, 1), max(m, 1));
+        S.cb = tq[jc - 1];
+        const int ii = q + p + 1 - c;
+        const int iz = min(max(ii, 0), n);
+        const int ks = max(iz - 1, 0);
+        S.sb = sq[max(min(ii, n), 1) - 1];
+        S.mt = tb[ks];
+        S.mm = tb[n + ks];
+        S.is = tb[2 * (size_t)n + ks];
+        S.ds = tb[3 * (size_t)n + iz];
+        const int ke = min(max(K - 1 - 2 * p, 0), max(K - 1, 0));
+        const int ko = min(max(K - 2 - 2 * p, 0), max(K - 1, 0));
+        S.be = Bb[(size_t)ke * P + max((H - 1 - 2 * q) >> 1, 0)];
+        S.bo = Bb[(size_t)ko * P + max((H - 2 - 2 * q) >> 1, 0)];
+    };
+    Slot S[QD];
+#pragma unroll
+    for (int j = 0; j < QD; ++j)
+        load(j, S[j]);
+    // the row of the even step of period 0 (ii = q - c)
+    int rsb;
+    double rmt, rmm, ris, rds;
+    {
+        const int ii = q - c;
+        const int iz = min(max(ii, 0), n);
+        const int ks = max(iz - 1, 0);
+        rsb = ii >= 1 ? sq[max(min(ii, n), 1) - 1] : 4;
+        rmt = tb[ks];
+        rmm = tb[n + ks];
+        ris = tb[2 * (size_t)n + ks];
+        rds = tb[3 * (size_t)n + iz];
+    }
+    double sub[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        sub[k] = rsb == k ? rmt : rmm;
+
+    double v1 = -RF_INF, v2 = -RF_INF;   // cells at kappa-1, kappa-2 of this lane's diagonal
+    double prev[4], accI[4], accS[4], dd = -RF_INF;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        prev[k] = accI[k] = accS[k] = -RF_INF;
+    const double qnan = __builtin_nan("");
+
+    // one anti-diagonal: fill cell (d, jj), then column jj's chain row ii
+    auto step = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
+        constexpr int par = decltype(parc)::value;   // static parity
+        const int d = 2 * q + par;
+        const int jj = p - q;
+        const int ii = q + p + par - c;
+        const double E1 = dpp_f64<par == 0 ? L1 : R1>(v1);
+        const double x_ins = par ? v1 : E1;   // (d-1, kappa-1)
+        const double x_del = par ? E1 : v1;   // (d+1, kappa-1)
+        const double ms = rsb == cb ? rmt : rmm;
+        const double best = vmax(vmax(v2 + ms, x_ins + ris), x_del + rds);
+        const bool valid = live && d < H && jj >= 0 && jj <= m && ii >= 0 && ii <= n;
+        const double nv = valid ? ((ii == 0 && jj == 0) ? 0.0 : best) : -RF_INF;
+        v2 = v1;
+        v1 = nv;
+        // chain of column a = jj at row ii (lean_chain's range and peel)
+        const int a = jj;
+        const int jn = min(a + 1, m);
+        const int i0 = max(0, jn - c);
+        const int i1 = min(jn + vb, n);
+        const int ilast = min(i1, a + vb);
+        const bool cok = live && a >= 0 && a <= m;
+        const bool inrow = cok && ii >= i0 && ii <= ilast;
+        const bool peel = cok && ii == ilast + 1 && i1 > ilast;
+        const double aprev = ii < i0 ? -RF_INF : x_ins;
+        const double bSm = ((inrow || peel) && a < m) ? bS : -RF_INF;
+        const double bIm = inrow ? bI : -RF_INF;
+        const double dl = inrow ? nv + rds : -RF_INF;
+        const double dsum = inrow ? nv + bSm : -RF_INF;
+        chain_row(aprev, sub, ris, dl, bIm, bSm, prev, accI, accS);
+        dd = vmax(dd, dsum);
+        if (cok && d == H) {   // column a's chain is complete: its partial record
+            double *dst = out + (size_t)a * 9;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+            if (a < m) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                dst[13] = dd;
+            }
+            if (a == 0) {
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    dst[k] = qnan;
+            }
+        }
+    };
+    const int bve = 2 * q < H, bvo = 2 * q + 1 < H;
+    for (int p0 = 0; 2 * p0 < kmax; p0 += QD) {
+#pragma unroll
+        for (int j = 0; j < QD; ++j) {
+            const int p = p0 + j;
+            if (2 * p >= kmax)
+                break;
+            Slot &X = S[j];
+            Slot &Y = S[(j + 1) % QD];   // period p + 1
+            const int cb = (p - q >= 1 && p - q <= m) ? X.cb : 4;
+            // even step kappa = 2p: bS = B(2p + 1, 2q - 1), lane q - 1's odd cell
+            {
+                const double bI = (bve && 2 * p <= K - 1) ? X.be : -RF_INF;
+                const double bo = (bvo && 2 * p + 1 <= K - 1) ? X.bo : -RF_INF;
+                const double bS = dpp_f64<L1>(bo);
+                step(std::integral_constant<int, 0>{}, p, cb, bI, bS);
+                // odd step kappa = 2p + 1: this lane's row advances; bS = B(2p + 2, 2q)
+                const int ii = q + p + 1 - c;
+                rsb = ii >= 1 ? X.sb : 4;
+                rmt = X.mt;
+                rmm = X.mm;
+                ris = X.is;
+                rds = X.ds;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    sub[k] = rsb == k ? rmt : rmm;
+                const double bS1 = (bve && 2 * p + 2 <= K - 1) ? Y.be : -RF_INF;
+                step(std::integral_constant<int, 1>{}, p, cb, bo, bS1);
+            }
+            // the chains move up one lane with their columns; lane 0 starts a fresh one
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                prev[k] = dpp_f64<L1>(prev[k]);
+                accI[k] = dpp_f64<L1>(accI[k]);
+                accS[k] = dpp_f64<L1>(accS[k]);
+            }
+            dd = dpp_f64<L1>(dd);
+            load(p + QD, X);
+        }
+    }
+}
+
 __device__ __forceinline__ void wg_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -4340,6 +4549,7 @@ struct Opts {
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
     int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H 32..127 tasks run as 64-lane tasks
+    int score_fwd = 0;      // RF_OPT_SCORE_FWD: rf_score_dense fills A inside the scorer (k_fuse) when eligible
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -4370,7 +4580,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[27];
+    DevBuf scratch[28];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -4420,6 +4630,9 @@ struct rf_ctx {
         std::vector<ScoreGroup> groups;
         std::vector<ScoreRead> reads;
         std::vector<int64_t> gstart;
+        bool fwd = false;                 // RF_OPT_SCORE_FWD plan: k_fuse tasks (scratch[27])
+        std::vector<FuseTask> ftasks;     // the 16-lane class (H <= 31) first, then the 64-lane class
+        size_t nf16 = 0;
     } dplan;
 };
 
@@ -4672,6 +4885,7 @@ void load_env_opts(Opts &o)
     o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
     o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
+    o.score_fwd = env_int("RIFRAF_SCORE_FWD", o.score_fwd);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4880,6 +5094,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
     case RF_OPT_SYNC_BLOCK: return &o.sync_block;
     case RF_OPT_DP_NL64: return &o.dp_nl64;
+    case RF_OPT_SCORE_FWD: return &o.score_fwd;
     default: return nullptr;
     }
 }
@@ -6321,7 +6536,20 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
     (void)hipSetDevice(ctx->device);
     const int32_t nslots = ngroups > 0 ? slot_off[ngroups] : 0;
     auto &P = ctx->dplan;
-    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
+    // RF_OPT_SCORE_FWD: every read lean (finite tables), H <= 127, B computed
+    // -> k_fuse fills A in the scorer (A unused)
+    bool fwd = ctx->opt.score_fwd != 0;
+    for (int32_t k = 0; fwd && k < nslots; ++k) {
+        const int32_t sl = slots[k];
+        if (sl < 0 || sl >= (int32_t)ctx->slots.size()) {
+            fwd = false;
+            break;
+        }
+        const Band &B = ctx->slots[sl].b;
+        fwd = B.valid && B.H <= 127 && (B.flags & (RF_SKEW | RF_TRIM)) == 0 && B.seq >= 0 &&
+              ctx->seqs[B.seq].finite;
+    }
+    const bool same = P.valid && P.fwd == fwd && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
                       P.slots.size() == (size_t)nslots &&
                       !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
                       (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
@@ -6337,6 +6565,18 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             if (sl < 0 || sl >= (int32_t)ctx->slots.size())
                 return fail(ctx, RF_ERR_ARG, "rf_score_dense: unknown slot");
             const Slot &S = ctx->slots[sl];
+            if (fwd) {
+                // A is filled in the scorer: only B must be current
+                if (ctx->tpls[S.b.tpl].version != S.b.tplver)
+                    return fail(ctx, RF_ERR_STATE, "rf_score_dense: template changed since the bands were computed");
+                const SeqObj &Q = ctx->seqs[S.b.seq];
+                if (Q.ncins > 0 || Q.ncdel > 0)
+                    return fail(ctx, RF_ERR_ARG, "error model cannot allow codon indels");
+                if (tpl >= 0 && S.b.tpl != tpl)
+                    return fail(ctx, RF_ERR_ARG, "rf_score_dense: batch slots use different templates");
+                tpl = S.b.tpl;
+                continue;
+            }
             if (!S.a.valid || !S.b.valid || S.a.seq != S.b.seq || S.a.tpl != S.b.tpl ||
                 S.a.bw != S.b.bw || S.a.tplver != S.b.tplver || S.a.m != S.b.m)
                 return fail(ctx, RF_ERR_STATE, "rf_score_dense: A and B bands were computed for different alignments");
@@ -6369,12 +6609,12 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             ScoreGroup &G = groups[g];
             G.r0 = (int32_t)reads.size();
             for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
-                const Band &A = ctx->slots[slots[k]].a;
                 const Band &B = ctx->slots[slots[k]].b;
+                const Band &A = fwd ? B : ctx->slots[slots[k]].a;   // fwd: geometry from B, A unused
                 const SeqObj &S = ctx->seqs[A.seq];
                 all_finite = all_finite && S.finite;
                 ScoreRead R{};
-                R.A = A.r.off / 8;
+                R.A = fwd ? 0 : A.r.off / 8;
                 R.B = B.r.off / 8;
                 R.sb = S.bases.off;
                 R.tab = S.tabs.off / 8;
@@ -6389,7 +6629,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
                 reads.push_back(R);
             }
             G.r1 = (int32_t)reads.size();
-            const TplObj &T = ctx->tpls[ctx->slots[slots[slot_off[g]]].a.tpl];
+            const TplObj &T = ctx->tpls[ctx->slots[slots[slot_off[g]]].b.tpl];
             G.m = T.m;
             G.tb = T.bases.off;
             G.dense_off = dense_total;
@@ -6412,6 +6652,35 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         if (int e = upload(ctx, ctx->scratch[12], groups)) return e;
         if (int e = upload(ctx, ctx->scratch[13], reads)) return e;
         if (int e = upload(ctx, ctx->scratch[14], gstart)) return e;
+        P.ftasks.clear();
+        P.nf16 = 0;
+        if (fwd) {
+            P.ftasks.reserve(reads.size());
+            for (int cls = 0; cls < 2; ++cls)   // 16-lane tasks (H <= 31), then 64-lane tasks
+            for (const ScoreGroup &G : groups)
+                for (int32_t r = G.r0; r < G.r1; ++r) {
+                    if ((reads[r].H <= 31) != (cls == 0))
+                        continue;
+                    const ScoreRead &R = reads[r];
+                    FuseTask t{};
+                    t.B = R.B;
+                    t.sb = R.sb;
+                    t.tab = R.tab;
+                    t.tb = G.tb;
+                    t.out = G.split_off + (int64_t)(r - G.r0) * (G.m + 1) * 9;
+                    t.n = R.n;
+                    t.m = G.m;
+                    t.H = R.H;
+                    t.c = R.c;
+                    t.vb = R.vb;
+                    t.P = R.P;
+                    t.K = R.K;
+                    P.ftasks.push_back(t);
+                    P.nf16 += cls == 0;
+                }
+            if (int e = upload(ctx, ctx->scratch[27], P.ftasks)) return e;
+        }
+        P.fwd = fwd;
         P.valid = true;
         P.gen = ctx->layout_gen;
         P.ngroups = ngroups;
@@ -6428,6 +6697,8 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         split = false;
     else if (ctx->opt.score_mode == 2)
         split = true;
+    if (fwd)
+        split = true;   // k_fuse writes per-read partials
     if (int e = ensure_buf(ctx, ctx->scratch[15], sizeof(double) * std::max<int64_t>(P.dense_total, 1)))
         return e;
     if (split)
@@ -6435,7 +6706,22 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             return e;
     double *d_dense = (double *)ctx->scratch[15].p;
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    if (P.nitems) {
+    if (fwd && !P.ftasks.empty()) {
+        const FuseTask *ft = (const FuseTask *)ctx->scratch[27].p;
+        const size_t n64 = P.ftasks.size() - P.nf16;
+        if (n64)
+            hipLaunchKernelGGL(k_fuse<64>, dim3((unsigned)n64), dim3(64), 0, ctx->stream, ft + P.nf16, (int)n64,
+                               (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
+                               (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
+        if (P.nf16)
+            hipLaunchKernelGGL(k_fuse<16>, dim3((unsigned)((P.nf16 + 3) / 4)), dim3(64), 0, ctx->stream, ft,
+                               (int)P.nf16, (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
+                               (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
+        hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
+                           ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
+                           (const int64_t *)ctx->scratch[14].p, P.dense_total,
+                           (const double *)ctx->scratch[10].p, d_dense);
+    } else if (P.nitems) {
         dim3 grid((unsigned)P.nitems, split ? (unsigned)P.max_reads : 1u);
         launch_scorer(ctx, P.pick, grid.x, grid.y, (const WorkItem *)ctx->scratch[11].p,
                       (const ScoreGroup *)ctx->scratch[12].p, (const ScoreRead *)ctx->scratch[13].p,
