@@ -1930,6 +1930,13 @@ struct alignas(16) FuseTask {
 #ifndef FUSE_QD
 #define FUSE_QD 4
 #endif
+// interior blocks: QD periods in which every cell of every lane below H is
+// inside the matrix and every column whose chain rows lie there is interior
+// (lean_chain_fix's a >= c, a + 1 + vb <= n, a < m) run a step without range
+// checks: the per-lane masks are constants added as 0 / -Inf
+#ifndef FUSE_FAST
+#define FUSE_FAST 1
+#endif
 
 template <int LPT>
 __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks, int ntasks,
@@ -1958,7 +1965,7 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
 
     // inputs of period p: the column base of jj = p - q (both steps), the row
     // record of ii = q + p + 1 - c (odd step of p, even step of p + 1), and
-    // B at (2p, 2q) and (2p + 1, 2q + 1).  Loaded raw at clamped indices (a
+    // B at (kappa, d) = (2p, 2q) and (2p + 1, 2q + 1).  Loaded raw at clamped indices (a
     // padding task, T = {}, reads the arenas' first entries), masked at use.
     struct Slot {
         int cb, sb;
@@ -1975,10 +1982,13 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
         S.mm = tb[n + ks];
         S.is = tb[2 * (size_t)n + ks];
         S.ds = tb[3 * (size_t)n + iz];
-        const int ke = min(max(K - 1 - 2 * p, 0), max(K - 1, 0));
-        const int ko = min(max(K - 2 - 2 * p, 0), max(K - 1, 0));
-        S.be = Bb[(size_t)ke * P + max((H - 1 - 2 * q) >> 1, 0)];
-        S.bo = Bb[(size_t)ko * P + max((H - 2 - 2 * q) >> 1, 0)];
+        // B is stored in its final orientation: cell (d, jj) at kappa * P + (d >> 1)
+        const int ke = min(2 * p, max(K - 1, 0)), ko = min(2 * p + 1, max(K - 1, 0));
+        // lanes past the band read the row's last real element (a finite or
+        // -Inf cell, never an unwritten padding slot: the interior step adds
+        // its -Inf masks to these values)
+        S.be = Bb[(size_t)ke * P + min(q, max((H - 1) >> 1, 0))];
+        S.bo = Bb[(size_t)ko * P + min(q, max((H - 2) >> 1, 0))];
     };
     Slot S[QD];
 #pragma unroll
@@ -2058,12 +2068,90 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
             }
         }
     };
+    // interior step: same operands and FP64 ops; the out-of-range cases are
+    // per-lane constants (lb: cell diagonal d < H; mI: chain row 1 <= d <= H-1;
+    // mS: 1 <= d <= H, the peeled row included), added as 0 / -Inf (x + 0.0 ==
+    // x for every operand: no -0.0 among cells, B cells and table values)
+    double lbv[2], mIv[2], mSv[2];
+    bool emitv[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int d = 2 * q + par;
+        lbv[par] = (live && d < H) ? 0.0 : -RF_INF;
+        mIv[par] = (live && d >= 1 && d <= H - 1) ? 0.0 : -RF_INF;
+        mSv[par] = (live && d >= 1 && d <= H) ? 0.0 : -RF_INF;
+        emitv[par] = live && d == H;
+    }
+    auto fstep = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
+        constexpr int par = decltype(parc)::value;
+        const double E1 = dpp_f64<par == 0 ? L1 : R1>(v1);
+        const double x_ins = par ? v1 : E1;
+        const double x_del = par ? E1 : v1;
+        const double ms = rsb == cb ? rmt : rmm;
+        const double nv = vmax(vmax(v2 + ms, x_ins + ris), x_del + rds) + lbv[par];
+        v2 = v1;
+        v1 = nv;
+        const double bIm = bI + mIv[par], bSm = bS + mSv[par];
+        const double dl = (nv + rds) + mIv[par];
+        const double dsum = nv + bSm;
+        chain_row(x_ins, sub, ris, dl, bIm, bSm, prev, accI, accS);
+        dd = vmax(dd, dsum);
+        if (emitv[par]) {   // interior: 0 < a < m
+            double *dst = out + (size_t)(p - q) * 9;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
+                dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+            }
+            dst[13] = dd;
+        }
+    };
+    // the wave's interior period range [plo, phi] (see FUSE_FAST)
+    int plo = live ? c + H : 0;
+    int phi = live ? min(min(m - 1, n - 1 - vb), n + c - H - 1) : INT_MAX;
+    for (int off = 32; off >= 1; off >>= 1) {
+        plo = max(plo, __shfl_xor(plo, off));
+        phi = min(phi, __shfl_xor(phi, off));
+    }
+    plo = __builtin_amdgcn_readfirstlane(plo);
+    phi = __builtin_amdgcn_readfirstlane(phi);
+
     const int bve = 2 * q < H, bvo = 2 * q + 1 < H;
-    for (int p0 = 0; 2 * p0 < kmax; p0 += QD) {
+    // periods up to kappa = K (inclusive): column m's chain ends at d = H,
+    // kappa = 2m + H = K for even H
+    for (int p0 = 0; 2 * p0 <= kmax; p0 += QD) {
+        if (FUSE_FAST && p0 >= plo && p0 + QD - 1 <= phi) {
+#pragma unroll
+            for (int j = 0; j < QD; ++j) {
+                const int p = p0 + j;
+                Slot &X = S[j];
+                Slot &Y = S[(j + 1) % QD];
+                const int cb = X.cb;
+                fstep(std::integral_constant<int, 0>{}, p, cb, X.be, dpp_f64<L1>(X.bo));
+                rsb = X.sb;
+                rmt = X.mt;
+                rmm = X.mm;
+                ris = X.is;
+                rds = X.ds;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    sub[k] = rsb == k ? rmt : rmm;
+                fstep(std::integral_constant<int, 1>{}, p, cb, X.bo, Y.be);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    prev[k] = dpp_f64<L1>(prev[k]);
+                    accI[k] = dpp_f64<L1>(accI[k]);
+                    accS[k] = dpp_f64<L1>(accS[k]);
+                }
+                dd = dpp_f64<L1>(dd);
+                load(p + QD, X);
+            }
+            continue;
+        }
 #pragma unroll
         for (int j = 0; j < QD; ++j) {
             const int p = p0 + j;
-            if (2 * p >= kmax)
+            if (2 * p > kmax)
                 break;
             Slot &X = S[j];
             Slot &Y = S[(j + 1) % QD];   // period p + 1

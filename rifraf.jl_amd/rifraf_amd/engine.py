@@ -409,7 +409,8 @@ class Engine:
             self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), None))
             return None
         if rows is None:
-            rows = [self.geometry(int(slots[slot_off[g]]), RF_BAND_A)[1] for g in range(G)]
+            # B: computed on both paths (RF_OPT_SCORE_FWD scores without A)
+            rows = [self.geometry(int(slots[slot_off[g]]), RF_BAND_B)[1] for g in range(G)]
         out = np.empty((int(sum(rows)), 9))
         self._check(self.lib.rf_score_dense(self.ctx, G, ptr(slot_off), ptr(slots), ptr(out)))
         res, at = [], 0

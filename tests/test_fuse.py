@@ -41,7 +41,7 @@ def _clusters(rng):
         t = random_seq(300, rng)
         out.append((t, [_indel_read(t, rng, k if r % 2 == 0 else -k) for r in range(3)]))
     t = random_seq(200, rng)                              # H 61 .. 127 at bw 30 .. 40
-    out.append((t, [_indel_read(t, rng, k, bw=bw) for k, bw in ((0, 30), (5, 33), (-9, 40), (47, 40))]))
+    out.append((t, [_indel_read(t, rng, k, bw=bw) for k, bw in ((0, 30), (5, 33), (-9, 40), (46, 40))]))
     for bw in range(1, 9):                                # narrow bands
         t = random_seq(int(rng.integers(40, 120)), rng)
         out.append((t, [make_read(t, rng, 0.03, bw) for _ in range(int(rng.integers(1, 5)))]))
