@@ -1544,7 +1544,11 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
     }
 }
 
-// split mode: ordered fold over reads, one lane per (group position slot)
+// split mode: ordered fold over reads, one lane per (group position slot).
+// nan_map (k_fuse's partials): a slot other than the deletion (4) holding
+// -Inf is an empty summax and reads as NaN, as the scorers map it in-kernel
+// (lean_chain: `accI == -Inf ? NaN : accI`) -- the same values fold.
+template <bool NAN_MAP = false>
 __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
                          const int64_t *__restrict__ gstart, int64_t total,
                          const double *__restrict__ split, double *__restrict__ dense)
@@ -1569,6 +1573,9 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
     // the left fold in read order (model.jl:389-393); 16 partials are loaded
     // before they are added, so each lane keeps 16 streaming loads in flight
     double acc = 0.0;
+    const bool map = NAN_MAP && (local % 9) != 4;
+    const double qnan = __builtin_nan("");
+    auto val = [&](double v) { return (map && v == -RF_INF) ? qnan : v; };
     int r = 0;
     for (; r + 16 <= nr; r += 16) {
         double v[16];
@@ -1577,10 +1584,10 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
             v[u] = __builtin_nontemporal_load(src + (int64_t)(r + u) * stride);
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-            acc += v[u];
+            acc += val(v[u]);
     }
     for (; r < nr; ++r)
-        acc += __builtin_nontemporal_load(src + (int64_t)r * stride);
+        acc += val(__builtin_nontemporal_load(src + (int64_t)r * stride));
     dense[G.dense_off + local] = acc;
 }
 
@@ -1937,6 +1944,12 @@ struct alignas(16) FuseTask {
 #ifndef FUSE_FAST
 #define FUSE_FAST 1
 #endif
+// chain state moves with a row rotate (no `old` operand: one instruction per
+// dword instead of a constant move + DPP) and lane 0 resets the state it
+// receives at its even step by adding -Inf (lanes q > 0 add 0.0)
+#ifndef FUSE_ROT
+#define FUSE_ROT 1
+#endif
 
 template <int LPT>
 __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks, int ntasks,
@@ -1990,6 +2003,23 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
         S.be = Bb[(size_t)ke * P + min(q, max((H - 1) >> 1, 0))];
         S.bo = Bb[(size_t)ko * P + min(q, max((H - 2) >> 1, 0))];
     };
+    // interior loads (the target period inside the wave's interior range, see
+    // FUSE_FAST): no clamps; lanes past H >> 1 use lane H >> 1's indices
+    // (their rows feed only masked values)
+    const int qe = min(q, H >> 1);
+    const int eev = min(q, max((H - 1) >> 1, 0)), eod = min(q, max((H - 2) >> 1, 0));
+    const int64_t n2 = 2 * (int64_t)n, n3 = 3 * (int64_t)n;
+    auto load_fast = [&](int p, Slot &S) {
+        const int ks = qe + p - c;   // read row ii - 1
+        S.cb = tq[p - qe - 1];
+        S.sb = sq[ks];
+        S.mt = tb[ks];
+        S.mm = tb[n + ks];
+        S.is = tb[n2 + ks];
+        S.ds = tb[n3 + ks + 1];
+        S.be = Bb[(int64_t)(2 * p) * P + eev];
+        S.bo = Bb[(int64_t)(2 * p + 1) * P + eod];
+    };
     Slot S[QD];
 #pragma unroll
     for (int j = 0; j < QD; ++j)
@@ -2018,6 +2048,32 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
     for (int k = 0; k < 4; ++k)
         prev[k] = accI[k] = accS[k] = -RF_INF;
     const double qnan = __builtin_nan("");
+    const double mz = q == 0 ? -RF_INF : 0.0;   // FUSE_ROT: lane 0's fresh chain
+    auto reset0 = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            prev[k] += mz;
+            accI[k] += mz;
+            accS[k] += mz;
+        }
+        dd += mz;
+    };
+    auto shift = [&]() {   // the chains move up one lane with their columns
+        constexpr int RL1 = TaskLanes<LPT>::ROT_L1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (FUSE_ROT) {
+                prev[k] = dpp_rot_f64<RL1>(prev[k]);
+                accI[k] = dpp_rot_f64<RL1>(accI[k]);
+                accS[k] = dpp_rot_f64<RL1>(accS[k]);
+            } else {
+                prev[k] = dpp_f64<L1>(prev[k]);
+                accI[k] = dpp_f64<L1>(accI[k]);
+                accS[k] = dpp_f64<L1>(accS[k]);
+            }
+        }
+        dd = FUSE_ROT ? dpp_rot_f64<RL1>(dd) : dpp_f64<L1>(dd);
+    };
 
     // one anti-diagonal: fill cell (d, jj), then column jj's chain row ii
     auto step = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
@@ -2048,20 +2104,30 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
         const double bIm = inrow ? bI : -RF_INF;
         const double dl = inrow ? nv + rds : -RF_INF;
         const double dsum = inrow ? nv + bSm : -RF_INF;
+        if (FUSE_ROT && par == 0)
+            reset0();
         chain_row(aprev, sub, ris, dl, bIm, bSm, prev, accI, accS);
         dd = vmax(dd, dsum);
-        if (cok && d == H) {   // column a's chain is complete: its partial record
+    };
+    // After a period's odd step the chain in lane H >> 1 is complete: it
+    // reached d = H in this period (even H: at the even step; d = H + 1 at
+    // the odd step is a no-op row).  Its record is written raw; k_reduce maps
+    // an empty summax (-Inf) to NaN.
+    const bool emit_lane = live && q == (H >> 1);
+    auto emit = [&](int p, bool interior) {
+        const int a = p - q;
+        if (emit_lane && (interior || (a >= 0 && a <= m))) {
             double *dst = out + (size_t)a * 9;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
-            if (a < m) {
+                dst[5 + k] = accI[k];
+            if (interior || a < m) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
+                    dst[9 + k] = accS[k];
                 dst[13] = dd;
             }
-            if (a == 0) {
+            if (!interior && a == 0) {
 #pragma unroll
                 for (int k = 0; k < 5; ++k)
                     dst[k] = qnan;
@@ -2073,14 +2139,12 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
     // mS: 1 <= d <= H, the peeled row included), added as 0 / -Inf (x + 0.0 ==
     // x for every operand: no -0.0 among cells, B cells and table values)
     double lbv[2], mIv[2], mSv[2];
-    bool emitv[2];
 #pragma unroll
     for (int par = 0; par < 2; ++par) {
         const int d = 2 * q + par;
         lbv[par] = (live && d < H) ? 0.0 : -RF_INF;
         mIv[par] = (live && d >= 1 && d <= H - 1) ? 0.0 : -RF_INF;
         mSv[par] = (live && d >= 1 && d <= H) ? 0.0 : -RF_INF;
-        emitv[par] = live && d == H;
     }
     auto fstep = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
         constexpr int par = decltype(parc)::value;
@@ -2094,17 +2158,10 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
         const double bIm = bI + mIv[par], bSm = bS + mSv[par];
         const double dl = (nv + rds) + mIv[par];
         const double dsum = nv + bSm;
+        if (FUSE_ROT && par == 0)
+            reset0();
         chain_row(x_ins, sub, ris, dl, bIm, bSm, prev, accI, accS);
         dd = vmax(dd, dsum);
-        if (emitv[par]) {   // interior: 0 < a < m
-            double *dst = out + (size_t)(p - q) * 9;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                dst[5 + k] = accI[k] == -RF_INF ? qnan : accI[k];
-                dst[9 + k] = accS[k] == -RF_INF ? qnan : accS[k];
-            }
-            dst[13] = dd;
-        }
     };
     // the wave's interior period range [plo, phi] (see FUSE_FAST)
     int plo = live ? c + H : 0;
@@ -2120,7 +2177,7 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
     // periods up to kappa = K (inclusive): column m's chain ends at d = H,
     // kappa = 2m + H = K for even H
     for (int p0 = 0; 2 * p0 <= kmax; p0 += QD) {
-        if (FUSE_FAST && p0 >= plo && p0 + QD - 1 <= phi) {
+        if (FUSE_FAST && p0 >= plo && p0 + 2 * QD - 1 <= phi) {
 #pragma unroll
             for (int j = 0; j < QD; ++j) {
                 const int p = p0 + j;
@@ -2137,14 +2194,9 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
                 for (int k = 0; k < 4; ++k)
                     sub[k] = rsb == k ? rmt : rmm;
                 fstep(std::integral_constant<int, 1>{}, p, cb, X.bo, Y.be);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    prev[k] = dpp_f64<L1>(prev[k]);
-                    accI[k] = dpp_f64<L1>(accI[k]);
-                    accS[k] = dpp_f64<L1>(accS[k]);
-                }
-                dd = dpp_f64<L1>(dd);
-                load(p + QD, X);
+                emit(p, true);   // interior: 0 < a < m
+                shift();
+                load_fast(p + QD, X);
             }
             continue;
         }
@@ -2174,15 +2226,10 @@ __global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks,
                     sub[k] = rsb == k ? rmt : rmm;
                 const double bS1 = (bve && 2 * p + 2 <= K - 1) ? Y.be : -RF_INF;
                 step(std::integral_constant<int, 1>{}, p, cb, bo, bS1);
+                emit(p, false);
             }
             // the chains move up one lane with their columns; lane 0 starts a fresh one
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                prev[k] = dpp_f64<L1>(prev[k]);
-                accI[k] = dpp_f64<L1>(accI[k]);
-                accS[k] = dpp_f64<L1>(accS[k]);
-            }
-            dd = dpp_f64<L1>(dd);
+            shift();
             load(p + QD, X);
         }
     }
@@ -6557,7 +6604,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                       (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
                       (const ScoreRead *)ctx->scratch[2].p, d_dense, d_split);
         if (split && dense_total > 0)
-            hipLaunchKernelGGL(k_reduce, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
+            hipLaunchKernelGGL(k_reduce<false>, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[1].p, ngroups, d_gstart,
                                dense_total, d_split, d_dense);
     }
@@ -6797,15 +6844,24 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
     if (fwd && !P.ftasks.empty()) {
         const FuseTask *ft = (const FuseTask *)ctx->scratch[27].p;
         const size_t n64 = P.ftasks.size() - P.nf16;
+        // the 64-lane class on a side stream, concurrent with the 16-lane class
+        if (n64) {
+            HIPCHK(ctx, hipEventRecord(ctx->fork, ctx->stream));
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->side[0], ctx->fork, 0));
+        }
         if (n64)
-            hipLaunchKernelGGL(k_fuse<64>, dim3((unsigned)n64), dim3(64), 0, ctx->stream, ft + P.nf16, (int)n64,
+            hipLaunchKernelGGL(k_fuse<64>, dim3((unsigned)n64), dim3(64), 0, ctx->side[0], ft + P.nf16, (int)n64,
                                (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
                                (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
         if (P.nf16)
             hipLaunchKernelGGL(k_fuse<16>, dim3((unsigned)((P.nf16 + 3) / 4)), dim3(64), 0, ctx->stream, ft,
                                (int)P.nf16, (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
                                (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
-        hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
+        if (n64) {
+            HIPCHK(ctx, hipEventRecord(ctx->join[0], ctx->side[0]));
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->join[0], 0));
+        }
+        hipLaunchKernelGGL(k_reduce<true>, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
                            ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
                            (const int64_t *)ctx->scratch[14].p, P.dense_total,
                            (const double *)ctx->scratch[10].p, d_dense);
@@ -6815,7 +6871,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
                       (const ScoreGroup *)ctx->scratch[12].p, (const ScoreRead *)ctx->scratch[13].p,
                       d_dense, split ? (double *)ctx->scratch[10].p : nullptr);
         if (split)
-            hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
+            hipLaunchKernelGGL(k_reduce<false>, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
                                (const int64_t *)ctx->scratch[14].p, P.dense_total,
                                (const double *)ctx->scratch[10].p, d_dense);

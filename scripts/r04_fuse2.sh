@@ -26,7 +26,11 @@ for rep in 1 2; do
     python3 -c "import json; d=json.load(open('$D/c4_${v}_$rep.json')); print('$v $rep', 'value', round(d['value'],1), 'dp', round(d['dp_ms'],2), 'score', round(d['score_ms'],2), 'step', round(d['ms_per_step'],2), d['parity']['bitexact'])"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o fwd -- python3 bench.py --no-cpu --no-secondary \
-  --no-c3 --e2e-clusters 0 --steps 3 --warmup 1 --score-fwd > $D/prof_fwd.json 2> $D/prof_fwd.err \
-  || { echo "rocprof failed"; tail -20 $D/prof_fwd.err; exit 1; }
-find $D/prof -name "*kernel_stats.csv" | head -3
+C4F="python3 bench.py --no-cpu --no-secondary --no-c3 --e2e-clusters 0 --steps 5 --warmup 2 --score-fwd"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/stats_fwd -o p --output-format csv -- $C4F \
+  > $D/stats_fwd.log 2>&1 || { echo "rocprof stats failed"; tail -20 $D/stats_fwd.log; exit 1; }
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $D/pmc_fwd/pmc_$ctr -o p --output-format csv -- $C4F \
+    > $D/pmc_fwd_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 $D/pmc_fwd_$ctr.log; exit 1; }
+done
+find $D -name "*kernel_stats.csv" -o -name "*counter_collection.csv" | head

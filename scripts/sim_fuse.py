@@ -100,19 +100,23 @@ def sim(t, r, LPT=16, fast=False, QD=4):
                     accI[q][k] = max(accI[q][k], prev[q][k] + bIm)
                     accS[q][k] = max(accS[q][k], prev[q][k] + bSm)
                 dd[q] = max(dd[q], dsum)
-                if cok and d == H:
-                    base = a * 9
-                    for k in range(4):
-                        out[base + 5 + k] = math.nan if accI[q][k] == NINF else accI[q][k]
-                    if a < m:
-                        for k in range(4):
-                            out[base + 9 + k] = math.nan if accS[q][k] == NINF else accS[q][k]
-                        out[base + 13] = dd[q]
-                    if a == 0:
-                        out[0:5] = math.nan
             for q in L:
                 v2[q] = v1[q]
                 v1[q] = nv_all[q]
+        # after the odd step: lane H >> 1 holds a finished chain (raw maxima;
+        # k_reduce<true> maps -Inf to NaN outside the deletion slot)
+        q = H >> 1
+        a = p - q
+        if 0 <= a <= m:
+            base = a * 9
+            for k in range(4):
+                out[base + 5 + k] = math.nan if accI[q][k] == NINF else accI[q][k]
+            if a < m:
+                for k in range(4):
+                    out[base + 9 + k] = math.nan if accS[q][k] == NINF else accS[q][k]
+                out[base + 13] = dd[q]
+            if a == 0:
+                out[0:5] = math.nan
         # shift chain state up one lane
         prev = [[NINF] * 4] + [list(x) for x in prev[:-1]]
         accI = [[NINF] * 4] + [list(x) for x in accI[:-1]]
