@@ -760,6 +760,16 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
             import oracle  # test infrastructure: the parity check only
             ref = [oracle.cpu_pass(t, rs, nthreads=cpu_threads())[0] for t, rs in clusters[:2]]
         result["parity"] = parity_check(dense[:len(ref)], ref, [t for t, _ in clusters[:len(ref)]])
+    # attainable write bandwidth of the DP's store pattern on this box
+    # (diagnostic: nontemporal 16-B stores, 16-lane streams of 2.75 KB
+    # chunks; destroys the bands, so after the parity download).  The c4 DP
+    # time varies by ~12 % between boxes (8.3 / 9.3 ms) at equal read rates.
+    try:
+        eng.probe_write(4, band_bytes, 2816, 16384)
+        wms = eng.probe_write(4, band_bytes, 2816, 16384)
+        result["stream_write_gbs"] = band_bytes / (wms * 1e-3) / 1e9 if wms > 0 else None
+    except Exception:  # pragma: no cover - diagnostic only
+        result["stream_write_gbs"] = None
     eng.close()
     return result
 
