@@ -662,6 +662,14 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     # 72 B of totals per consensus position
     dp_bytes = 8 * cells
     score_bytes = 8 * cells + sum(33 * (len(r) + 1) for r in reads) + sum(72 * (len(t) + 1) for t, _ in clusters)
+    if args.score_fwd:
+        # fused-step prototype: the DP stores B only; the scorer reads B once,
+        # the tables, writes 72 B per position per read (partials) and
+        # k_reduce reads them back
+        dp_bytes = 8 * cells // 2
+        score_bytes = (8 * cells // 2 + sum(33 * (len(r) + 1) for r in reads)
+                       + 2 * 72 * sum((len(t) + 1) * len(rs) for t, rs in clusters)
+                       + sum(72 * (len(t) + 1) for t, _ in clusters))
 
     from rifraf_amd.engine import pack_groups
     packed = pack_groups(groups)   # the caller's slot lists, packed once
