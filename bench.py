@@ -718,7 +718,8 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     sc_gbs = score_bytes / (sc_ms * 1e-3) / 1e9
     dominant = "k_score" if sc_ms >= dp_ms else "k_dp"
     ach, byt, ms = (sc_gbs, score_bytes, sc_ms) if dominant == "k_score" else (dp_gbs, dp_bytes, dp_ms)
-    traffic = pmc_traffic(args.config, nclu, dominant)
+    # the committed PMC profile is the product step's (--score-fwd: profiles/r04s_fuse.json)
+    traffic = None if args.score_fwd else pmc_traffic(args.config, nclu, dominant)
     result = {
         "metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
         "value": tot_cells / elapsed / 1e9,
