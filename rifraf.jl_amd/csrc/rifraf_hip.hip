@@ -1809,6 +1809,9 @@ __device__ __forceinline__ void lean_chain(const ScoreRead &R, const LeanWin &w,
 // immediate offset from one pointer per array: the per-row index arithmetic
 // of lean_chain (about 15 of its 51 VALU ops per row) drops out.  Same
 // operands, same FP64 ops in the same order: the same values.
+#ifndef WS_UNROLL
+#define WS_UNROLL 2   // lean_chain_fix row pairs per loop iteration
+#endif
 template <int PT>
 __device__ __forceinline__ void lean_chain_fix(const ScoreRead &R, const LeanWin &w, int a, const double *sA,
                                                const double *sB, const double *sT, double tI[4], double tS[4],
@@ -1838,7 +1841,24 @@ __device__ __forceinline__ void lean_chain_fix(const ScoreRead &R, const LeanWin
         aprev = ac;
     };
     const int nrows = R.c + R.vb;   // i0 = a + 1 - c .. ilast = a + vb
-    for (int u = 0; u < (nrows >> 1); ++u) {
+    // WS_UNROLL row pairs per iteration: hipcc issues an iteration's LDS
+    // reads at its top and waits for the first ones at once, so each
+    // iteration exposes one LDS round trip; two pairs halve that per row
+    int u = 0;
+    if (WS_UNROLL > 1) {
+        for (; u + WS_UNROLL <= (nrows >> 1); u += WS_UNROLL) {
+#pragma unroll
+            for (int k = 0; k < WS_UNROLL; ++k) {    // pair k: offsets + k (2 PT + 1)
+                const int o = k * (2 * PT + 1);
+                row(o, o + PT, 12 * k);                   // d odd
+                row(o + PT + 1, o + 2 * PT, 12 * k + 6);  // d even
+            }
+            pa += WS_UNROLL * (2 * PT + 1);
+            pb += WS_UNROLL * (2 * PT + 1);
+            pt += 12 * WS_UNROLL;
+        }
+    }
+    for (; u < (nrows >> 1); ++u) {
         row(0, PT, 0);                        // d odd
         row(PT + 1, 2 * PT, 6);               // d even
         pa += 2 * PT + 1;
