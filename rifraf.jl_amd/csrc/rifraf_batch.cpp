@@ -113,7 +113,12 @@ struct Driver {
     // (stderr at the end of rf_rifraf_batch; diagnostics only)
     enum { T_FWD, T_BT, T_BWD, T_PROPS, T_SCORE, T_TPL, T_N };
     double tsum[T_N] = {};
+    double ksum[T_N] = {};   // the calls' kernel time (HIP events), seconds
     int tcnt[T_N] = {};
+    const bool timing = [] {
+        const char *tv = std::getenv("RIFRAF_BATCH_TIMING");
+        return tv && *tv && *tv != '0';
+    }();
     template <class F>
     int timed(int k, F &&call)
     {
@@ -121,6 +126,13 @@ struct Driver {
         const int e = call();
         tsum[k] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         ++tcnt[k];
+        if (timing && e == 0) {
+            double dp = 0, sc = 0, ga = 0, bt = 0;
+            rf_last_timing(ctx, &dp, &sc, &ga);
+            rf_last_backtrace_ms(ctx, &bt);
+            ksum[k] += 1e-3 * (k == T_FWD || k == T_BWD ? dp : k == T_SCORE ? sc + ga
+                               : (k == T_BT || k == T_PROPS) ? bt : 0.0);
+        }
         return e;
     }
 
@@ -950,7 +962,7 @@ extern "C" int rf_rifraf_batch_ref(rf_ctx *ctx, int32_t nclusters, const rf_batc
         std::fprintf(stderr, "rf_rifraf_batch: %d clusters, run %.4f s;", nclusters,
                      std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count());
         for (int k = 0; k < Driver::T_N; ++k) {
-            std::fprintf(stderr, " %s %.4f s / %d;", names[k], D.tsum[k], D.tcnt[k]);
+            std::fprintf(stderr, " %s %.4f s / %d (kernels %.4f s);", names[k], D.tsum[k], D.tcnt[k], D.ksum[k]);
             tot += D.tsum[k];
         }
         int64_t g1;
