@@ -3941,6 +3941,13 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 // the three others (the same strict-> order), and a codon move leaves the box
 // (|u| = 3), so the next box starts at the cell it reaches.
 // ---------------------------------------------------------------------
+// 1: moves collected in the wave's lanes and stored 64 at a time -- bit-exact
+// but slower (backtrace 19.6 -> 22.4 ms, alignment proposals 36.7 -> 40.3 ms
+// per 512 e2e clusters, profiles/r04z_btw_mvbuf.txt: the select joins the
+// walk's per-move dependency chain, which bounds it, not the stores); off
+#ifndef BTW_MVBUF
+#define BTW_MVBUF 0
+#endif
 constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
@@ -3980,6 +3987,14 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     int klo = -1, e0 = 0;                              // A window: rows [klo, klo + W), elements [e0, e0 + wd)
     int q0 = -1, r0 = -1;                              // table rows [q0, q0 + BTW_T), bases [r0, r0 + BTW_T)
     int failed = 0;
+    // BTW_MVBUF: moves collected in the wave's lanes (move cnt in lane
+    // cnt % 64) and written 64 at a time (measured slower, off)
+    int mvbuf = 0;
+    auto flush_moves = [&](int upto) {   // moves [upto & ~63, upto) -> out (forward order ends at n+m-1)
+        const int b0 = (upto - 1) & ~63;
+        if (BTW_MVBUF && lane < upto - b0)
+            out[n + m - 1 - b0 - lane] = (int8_t)mvbuf;
+    };
     while ((ii > 0 || jj > 0) && !failed) {
         // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
@@ -4135,8 +4150,14 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             const int sb = pk >> 4;
             const bool mism = pk & 8;
+            if (BTW_MVBUF) {
+                mvbuf = lane == (cnt & 63) ? mv : mvbuf;
+                if ((cnt & 63) == 63)
+                    flush_moves(cnt + 1);
+            }
             if (lane == 0) {
-                out[n + m - 1 - cnt] = (int8_t)mv;
+                if (!BTW_MVBUF)
+                    out[n + m - 1 - cnt] = (int8_t)mv;
                 if (mk) {
                     // the forward step of this move ends at (ii, jj) (k_aln_props)
                     if (mv == 1 && mism)
@@ -4167,6 +4188,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
         }
     }
+    if (cnt & 63)
+        flush_moves(cnt);
     if (lane == 0) {
         nmoves[T.idx] = cnt;
         nerr[T.idx] = errs;
