@@ -3948,6 +3948,11 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 #ifndef BTW_MVBUF
 #define BTW_MVBUF 0
 #endif
+// 1: the box's walk ranked in parallel (pointer doubling) instead of one
+// readlane step per move (round 4 experiment)
+#ifndef BTW_RANK
+#define BTW_RANK 0
+#endif
 constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
@@ -4134,6 +4139,91 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             pack = valid ? (mv | ((sb != tbb) ? 8 : 0) | (sb << 4)) : 0;
         }
+#if BTW_RANK
+        // ---- walk the box by ranking its cells in parallel: J0 = each box
+        // cell's successor lane (or the sink, lane 63: leaves the box, reaches
+        // (0, 0), or no move), J_r = J0^(2^r) by pointer doubling; lane k then
+        // finds the k-th cell of the walk from lane 1 (the current cell) by
+        // the binary digits of k, and emits the k-th move.  The same moves,
+        // marks, error counts and failure points as the sequential walk below.
+        {
+            constexpr int SINK = 63;
+            const int mv0 = pack & 7;
+            const int bu = lane % 3 - 1;
+            int ndi = bdi, nu = bu;
+            if (mv0 == 1) { ndi = bdi + 1; }
+            else if (mv0 == 2) { ndi = bdi + 1; nu = bu + 1; }
+            else if (mv0 == 3) { nu = bu - 1; }
+            const bool inbox = (mv0 >= 1 && mv0 <= 3) && ndi <= BT_DMAX && nu >= -1 && nu <= 1;
+            const int ti = ii - ndi, tj = jj - (ndi - nu);
+            int J = (blane && inbox && (ti > 0 || tj > 0)) ? ndi * 3 + nu + 1 : SINK;
+            if (lane == SINK)
+                J = SINK;
+            int Jr[6];
+            Jr[0] = J;
+#pragma unroll
+            for (int r = 1; r < 6; ++r)
+                Jr[r] = __builtin_amdgcn_ds_bpermute(Jr[r - 1] << 2, Jr[r - 1]);
+            int cell = 1;   // lane k: the k-th cell of the walk
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const int nx = __builtin_amdgcn_ds_bpermute(cell << 2, Jr[r]);
+                cell = ((lane >> r) & 1) ? nx : cell;
+            }
+            // cells reached; a cell with no move (mv 0) ends the walk in failure
+            const int pk = __builtin_amdgcn_ds_bpermute(cell << 2, pack);
+            const bool visited = cell != SINK;
+            const int nvis = __popcll(__ballot(visited));
+            const int mvk = pk & 7;
+            const bool nomove_last = __builtin_amdgcn_readlane(mvk, max(nvis - 1, 0)) == 0;
+            int nmv = nomove_last ? nvis - 1 : nvis;
+            bool fail_now = nomove_last;
+            if (cnt + nmv > n + m) {   // the sequential walk's cnt >= n + m check
+                nmv = n + m - cnt;
+                fail_now = true;
+            }
+            const bool emit = lane < nmv;
+            const int cdi = cell / 3, cdu = cell % 3 - 1;
+            const int ci = ii - cdi, cj = jj - (cdi - cdu);
+            const int ksb = pk >> 4;
+            const bool mism = pk & 8;
+            if (emit) {
+                out[n + m - 1 - (cnt + lane)] = (int8_t)mvk;
+                if (mk) {
+                    // the forward step of this move ends at (ci, cj) (k_aln_props)
+                    if (mvk == 1 && mism)
+                        mk[(size_t)cj * 9 + ksb] = 1;
+                    else if (mvk == 2 && do_indels)
+                        mk[(size_t)cj * 9 + 5 + ksb] = 1;
+                    else if (mvk == 3 && do_indels)
+                        mk[(size_t)cj * 9 + 4] = 1;
+                }
+            }
+            int e = emit ? (mvk == 1 ? (mism ? 1 : 0) : (mvk <= 3 ? 1 : 3)) : 0;
+            for (int off = 32; off >= 1; off >>= 1)
+                e += __shfl_xor(e, off);
+            errs += e;
+            if (nmv > 0) {
+                // the cell after the last move
+                int ni = ci, nj = cj;
+                switch (mvk) {
+                case 1: ni -= 1; nj -= 1; break;
+                case 2: ni -= 1; break;
+                case 3: nj -= 1; break;
+                case 4: ni -= 3; break;
+                default: nj -= 3; break;
+                }
+                ii = __builtin_amdgcn_readlane(ni, nmv - 1);
+                jj = __builtin_amdgcn_readlane(nj, nmv - 1);
+            }
+            cnt += nmv;
+            if (fail_now) {
+                if (lane == 0)
+                    set_err(err, 2);  // failed to find a move
+                failed = 1;
+            }
+        }
+#else
         // ---- walk the box (uniform control flow, one readlane per move)
         const int bi = ii, bj = jj;
         while (ii > 0 || jj > 0) {
@@ -4187,6 +4277,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                 jj -= 3;
             }
         }
+#endif
     }
     if (cnt & 63)
         flush_moves(cnt);
