@@ -3948,10 +3948,13 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 #ifndef BTW_MVBUF
 #define BTW_MVBUF 0
 #endif
-// 1: the box's walk ranked in parallel (pointer doubling) instead of one
-// readlane step per move (round 4 experiment)
+// 1 (default, round 4): the box's walk ranked in parallel (pointer
+// doubling over the 63 cells' successors) instead of one readlane step per
+// move: backtrace 19.8 -> 8.0 ms, alignment proposals 36.9 -> 12.9 ms per
+// 512 e2e clusters, bit-exact (profiles/r04ab_btw_rank.txt); 0: the
+// sequential walk
 #ifndef BTW_RANK
-#define BTW_RANK 0
+#define BTW_RANK 1
 #endif
 constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
