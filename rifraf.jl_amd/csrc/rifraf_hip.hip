@@ -3956,7 +3956,10 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 #ifndef BTW_RANK
 #define BTW_RANK 1
 #endif
-constexpr int BTW_WD = 16;     // staged elements per kappa row when P > BTW_WD
+#ifndef BTW_WD_ELEMS
+#define BTW_WD_ELEMS 16
+#endif
+constexpr int BTW_WD = BTW_WD_ELEMS;   // staged elements per kappa row when P > BTW_WD (>= 6: codon boxes)
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
 
