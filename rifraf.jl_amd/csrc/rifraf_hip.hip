@@ -3956,8 +3956,13 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 #ifndef BTW_RANK
 #define BTW_RANK 1
 #endif
+// elements staged per kappa row (the walk's box needs 3 -- 5 with codon
+// moves -- around its diagonal): 8 holds twice the kappa rows of 16 in the
+// same LDS, so windows are re-staged half as often: with the ranked walk,
+// backtrace 8.1 -> 6.9 ms and alignment proposals 12.8 -> 10.7 ms per 512
+// e2e clusters (profiles/r04ad_btw_window.txt); a 32-KB window is slower
 #ifndef BTW_WD_ELEMS
-#define BTW_WD_ELEMS 16
+#define BTW_WD_ELEMS 8
 #endif
 constexpr int BTW_WD = BTW_WD_ELEMS;   // staged elements per kappa row when P > BTW_WD (>= 6: codon boxes)
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
