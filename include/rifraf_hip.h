@@ -110,9 +110,10 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_SYNC_BLOCK  23   /* 1: host waits for the engine's stream sleep on
                                    a blocking-sync event instead of spinning
                                    (ranks held to a few host cores)             */
-#define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H 32..127
+#define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H <= 127
                                    per call (codon / skew / trim) run as one
-                                   64-lane task per wave (default 1024; 0 never) */
+                                   latency-bound task per wave, k_dpx (default
+                                   1024; 0: the 16-lane non-lean kernels)       */
 #define RF_OPT_SCORE_FWD   25   /* 1: rf_score_dense / rf_score_dense_dev fill the
                                    forward band inside the scorer (k_fuse, the
                                    fused-step prototype) when every read is lean
@@ -120,6 +121,12 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    (rf_realign RF_BWD) are read, A is neither read
                                    nor needed; other launches use A as usual.
                                    align.jl:155-179 + model.jl:242-285, 389-393 */
+#define RF_OPT_DP_LAT      26   /* latency mode: an rf_realign call with at most
+                                   this many lean tasks of H <= 127 (and no
+                                   wider lean task) runs them all as one 64-lane
+                                   task per wave (one launch; such a call cannot
+                                   fill the GPU, so a task's step latency is the
+                                   time).  Default 2048; 0 never.  align.jl:114-212 */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -1317,6 +1317,243 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------
+// k_dpx: latency-bound non-lean tasks (round 5).
+//
+// The reference's codon DP (align.jl:77-104 with codon moves; skew_matches
+// for single_indel_proposals, model.jl:538-562) is one task of ~5,000
+// anti-diagonals per call: nothing else runs beside it, so its time is the
+// step latency of one wave, i.e. the instructions one step issues.  k_dpr's
+// general step moved every row record through the lanes (7 DPP moves per
+// value and period), took the codon neighbours by two wave shifts each and
+// waited for its edge loads with vmcnt(0) -- ~900 cycles per anti-diagonal
+// (profiles/r05a_kernel_stats_c3.csv).  Here one task owns a single-wave
+// workgroup, lane q holds the diagonal pair {2q, 2q+1} (H <= 127), and
+//   - the row records {match, mismatch (x 0.99 under skew), ins, del,
+//     codon ins, codon del, base} and the template bases are staged in LDS
+//     rings of 256 rows / columns, 64 at a time, loaded a block ahead:
+//     lane q reads row P + q + par - c and column P - q at period P (one
+//     LDS read set per period instead of the systolic moves);
+//   - every anti-diagonal's values go to a 4-row LDS ring as well, so the
+//     codon neighbours (d -/+ 3 at kappa - 3) are two LDS reads at an
+//     immediate offset; only the insert / delete neighbour at kappa - 1
+//     (on the step-to-step chain) is a DPP wave shift;
+//   - interior steps (every active diagonal inside the matrix, codon moves
+//     allowed, no trim column) carry no range checks: inactive diagonals
+//     get -Inf by an additive mask, as in the lean kernels.
+// Same candidates, same FP64 sums and the same strict-'>' value (the max of
+// the candidates; no NaN, no -0.0) as k_dpr / k_dp, stored in the same
+// kappa-major positions (reverse: flipped), so bands, scores and errors are
+// bit-identical.
+// ---------------------------------------------------------------------
+constexpr int DPX_W = 72;       // doubles per LDS band row: 2 pad | 64 lanes | 6 pad (-Inf)
+constexpr int DPX_RING = 256;   // staged rows / columns: 4 blocks of 64
+struct DpxStage {
+    double mt, mm, is, ds, ci, cd;
+    int sb, col;
+};
+
+template <int PAR, bool FAST>
+__device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, int ii, int jj, double v1,
+                                           double v2, double xn, double yci, double ycd, const dvec2 &mtmm,
+                                           const dvec2 &isds, const dvec2 &cicd, int sb, int tbb, double lbv,
+                                           uint64_t actm, uint64_t &emask, int &eflag, double &fval, int &fset)
+{
+    const double ms = sb == tbb ? mtmm.x : mtmm.y;   // mismatch staged x 0.99 under skew (align.jl:70-72)
+    const double x_ins = PAR ? v1 : xn;               // (d-1, kappa-1)
+    const double x_del = PAR ? xn : v1;               // (d+1, kappa-1)
+    if (FAST) {
+        // candidates off the step-to-step chain first, the kappa-1 pair last
+        const double t = fmax(fmax(v2 + ms, yci + cicd.x), ycd + cicd.y);
+        const double best = fmax(t, fmax(x_ins + isds.x, x_del + isds.y));
+        emask |= __ballot(best == -RF_INF) & actm;   // "new score is invalid" (active diagonals)
+        return best + lbv;
+    }
+    const bool valid = d < T.H && jj >= 0 && jj <= T.m && ii >= 0 && ii <= T.n;
+    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;   // align.jl:74-76
+    const double cd = jj >= 3 ? cicd.y : -RF_INF;                         // codon delete needs j > 3
+    double best = fmax(fmax(v2 + ms, x_ins + is), x_del + isds.y);
+    best = fmax(fmax(best, yci + cicd.x), ycd + cd);   // cicd.x is -Inf unless i > 3 (staged)
+    const bool origin = ii == 0 && jj == 0;
+    const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
+    eflag |= (valid && !origin && best == -RF_INF) ? 1 : 0;
+    const bool fin = valid && ii == T.n && jj == T.m;
+    fval = fin ? v : fval;
+    fset |= fin ? 1 : 0;
+    return v;
+}
+
+__global__ void __launch_bounds__(64)
+k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
+      const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
+      int *__restrict__ err)
+{
+    __shared__ dvec2 s_mtmm[DPX_RING], s_isds[DPX_RING], s_cicd[DPX_RING];
+    __shared__ int s_sb[DPX_RING], s_col[DPX_RING];
+    __shared__ double s_band[4 * DPX_W];
+    const int q = threadIdx.x;
+    const DPTask T = tasks[blockIdx.x];   // one task per workgroup
+    const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
+    const bool codon = T.ncins > 0 || T.ncdel > 0;
+    const uint8_t *sbase = bases + T.sb;
+    const uint8_t *tbase = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    double *band = bands + T.band;
+    const int K = T.klen;
+    for (int e = q; e < 4 * DPX_W; e += 64)
+        s_band[e] = -RF_INF;
+
+    // block b: rows R = P + q + par in [64b, 64b + 64) (read row R - c) and
+    // columns J = P - q + 64 in [64b, 64b + 64) (template column J - 64)
+    auto stage_load = [&](int b) {
+        const RowRec r = load_row_flat(T, rev, sbase, tb, 64 * b + q - T.c, codon);
+        DpxStage s;
+        s.mt = r.mt;
+        s.mm = skew ? r.mm * 0.99 : r.mm;
+        s.is = r.is;
+        s.ds = r.ds;
+        s.ci = r.ci;
+        s.cd = r.cd;
+        s.sb = r.sb;
+        s.col = load_col_flat(T, rev, tbase, 64 * b + q - 64);
+        return s;
+    };
+    auto stage_put = [&](int b, const DpxStage &s) {
+        const int i = (64 * b + q) & (DPX_RING - 1);
+        s_mtmm[i] = dvec2{s.mt, s.mm};
+        s_isds[i] = dvec2{s.is, s.ds};
+        s_cicd[i] = dvec2{s.ci, s.cd};
+        s_sb[i] = s.sb;
+        s_col[i] = s.col;
+    };
+
+    // interior [klo, khi]: every diagonal with cells in the matrix has its
+    // cell inside the matrix with i, j > 3 (codon moves open) and j in
+    // 1..m-1 (trim off); the origin and the final cell lie outside it
+    double lb[2];
+    bool act[2];
+    // kappa of (0, 0) + 1, and at least H: every band diagonal has d <= kappa
+    // (stored); kappa of (n, m) - 1
+    int lo = max(T.c + 1, T.H), hi = T.n + T.c + T.m - 1;
+    bool ok = true;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int d = 2 * q + par;
+        const int mlo = max(0, T.c - d), mhi = min(T.m, T.n + T.c - d);
+        act[par] = d < T.H && mlo <= mhi;
+        lb[par] = act[par] ? 0.0 : -RF_INF;
+        if (act[par]) {
+            const int jlo = max(3, T.c + 3 - d), jhi = min(T.m - (trim ? 1 : 0), T.n + T.c - d);
+            ok = ok && jlo <= jhi;
+            lo = max(lo, d + 2 * jlo);
+            hi = min(hi, d + 2 * jhi);
+        }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        lo = max(lo, __shfl_xor(lo, off));
+        hi = min(hi, __shfl_xor(hi, off));
+    }
+    const int klo = __builtin_amdgcn_readfirstlane(__all(ok) ? lo : INT_MAX);
+    const int khi = __builtin_amdgcn_readfirstlane(hi);
+
+    stage_put(0, stage_load(0));
+    stage_put(1, stage_load(1));
+    DpxStage nxt = stage_load(2);
+    wave_sync();
+
+    // per parity: band element of this lane's diagonal (reverse: flipped) and
+    // whether the kappa row holds it
+    const int el0 = rev ? (T.H - 1 - 2 * q) >> 1 : q;
+    const int el1 = rev ? (T.H - 2 - 2 * q) >> 1 : q;
+    const uint64_t actm0 = __ballot(act[0]), actm1 = __ballot(act[1]);
+    const bool st0 = 2 * q < T.H, st1 = 2 * q + 1 < T.H;   // the band holds the diagonal
+    double v1 = -RF_INF, v2 = -RF_INF;
+    uint64_t emask = 0;
+    int eflag = 0, fset = 0;
+    double fval = 0.0;
+    // the record of row R = 2u + q (period 2u, even step), carried between pairs
+    dvec2 c_mtmm = s_mtmm[q], c_isds = s_isds[q], c_cicd = s_cicd[q];
+    int c_sb = s_sb[q];
+    // the codon neighbours of the next step, read one step ahead (kappa = 0:
+    // ring row 1, still -Inf)
+    double cy_ci = s_band[DPX_W + 2 + q - 2], cy_cd = s_band[DPX_W + 2 + q + 1];
+    const int npairs = (K + 3) >> 2;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using BT = std::integral_constant<bool, true>;
+    using BF = std::integral_constant<bool, false>;
+    for (int u = 0; u < npairs; ++u) {
+        if ((u & 31) == 0) {   // chunk t = u / 32 (64 periods): block t + 2 in, t + 3 loads
+            const int t = u >> 5;
+            stage_put(t + 2, nxt);
+            nxt = stage_load(t + 3);
+            wave_sync();
+        }
+        const int r1 = (2 * u + q + 1) & (DPX_RING - 1), r2 = (2 * u + q + 2) & (DPX_RING - 1);
+        const int j0 = (2 * u - q + 64) & (DPX_RING - 1), j1 = (2 * u - q + 65) & (DPX_RING - 1);
+        const dvec2 a_mtmm = s_mtmm[r1], a_isds = s_isds[r1], a_cicd = s_cicd[r1];
+        const int a_sb = s_sb[r1];
+        const dvec2 b_mtmm = s_mtmm[r2], b_isds = s_isds[r2], b_cicd = s_cicd[r2];
+        const int b_sb = s_sb[r2];
+        const int col0 = s_col[j0], col1 = s_col[j1];
+        // four steps kappa = 4u + s: (period, parity) = (2u, 0), (2u, 1), (2u+1, 0), (2u+1, 1)
+        auto step = [&](auto FASTC, auto PARC, auto SC, int per, const dvec2 &mtmm, const dvec2 &isds,
+                        const dvec2 &cicd, int sb, int col) {
+            constexpr bool FAST = decltype(FASTC)::value;
+            constexpr int PAR = decltype(PARC)::value, S = decltype(SC)::value;
+            const int k = 4 * u + S;
+            if (!FAST && k >= K)
+                return;
+            // the kappa - 1 neighbour by a wave rotate: lane 0 (63) receives the
+            // value of diagonal 127 (0 at kappa - 1 into diagonal 127), and
+            // diagonal 127 >= H is -Inf / masked (the host sends H <= 127 only)
+            const double xn = PAR ? dpp_rot_f64<TaskLanes<64>::ROT_R1>(v1) : dpp_rot_f64<TaskLanes<64>::ROT_L1>(v1);
+            // codon neighbours at kappa - 3: d - 3 / d + 3 = lanes q - 2 / q + 1
+            // (even), q - 1 / q + 2 (odd); this step's were read one step ago,
+            // the next step's (ring row kappa - 2, the other parity) now
+            const double yci = cy_ci, ycd = cy_cd;
+            {
+                const double *r = s_band + ((S + 2) & 3) * DPX_W + 2 + q;
+                cy_ci = r[PAR ? -2 : -1];
+                cy_cd = r[PAR ? 1 : 2];
+            }
+            const int d = 2 * q + PAR;
+            const int jj = per - q, ii = per + q + PAR - T.c;
+            const double v = dpx_cell<PAR, FAST>(T, trim, d, ii, jj, v1, v2, xn, yci, ycd, mtmm, isds, cicd, sb, col,
+                                                 lb[PAR], PAR ? actm1 : actm0, emask, eflag, fval, fset);
+            s_band[S * DPX_W + 2 + q] = v;
+            if (PAR ? st1 : st0) {
+                if (FAST || d <= k)
+                    band[(size_t)(rev ? K - 1 - k : k) * T.P + (PAR ? el1 : el0)] = v;
+            }
+            v2 = v1;
+            v1 = v;
+        };
+        if (4 * u >= klo && 4 * u + 3 <= khi) {
+            step(BT{}, I0{}, I0{}, 2 * u, c_mtmm, c_isds, c_cicd, c_sb, col0);
+            step(BT{}, I1{}, I1{}, 2 * u, a_mtmm, a_isds, a_cicd, a_sb, col0);
+            step(BT{}, I0{}, I2{}, 2 * u + 1, a_mtmm, a_isds, a_cicd, a_sb, col1);
+            step(BT{}, I1{}, I3{}, 2 * u + 1, b_mtmm, b_isds, b_cicd, b_sb, col1);
+        } else {
+            step(BF{}, I0{}, I0{}, 2 * u, c_mtmm, c_isds, c_cicd, c_sb, col0);
+            step(BF{}, I1{}, I1{}, 2 * u, a_mtmm, a_isds, a_cicd, a_sb, col0);
+            step(BF{}, I0{}, I2{}, 2 * u + 1, a_mtmm, a_isds, a_cicd, a_sb, col1);
+            step(BF{}, I1{}, I3{}, 2 * u + 1, b_mtmm, b_isds, b_cicd, b_sb, col1);
+        }
+        c_mtmm = b_mtmm;
+        c_isds = b_isds;
+        c_cicd = b_cicd;
+        c_sb = b_sb;
+    }
+    (void)ntasks;
+    if (eflag || emask)
+        set_err(err, 1);  // "new score is invalid"
+    if (fset && out_score)
+        out_score[T.out_idx] = fval;
+}
+
+// ---------------------------------------------------------------------
 // k_score: dense proposal scoring of batch reads (no codon moves)
 //
 // One lane per consensus position p in [0, m].  For a read it evaluates
@@ -4828,8 +5065,10 @@ struct Opts {
                             // measured slower at c5, round 4)
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
     int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
-    int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H 32..127 tasks run as 64-lane tasks
+    int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
     int score_fwd = 0;      // RF_OPT_SCORE_FWD: rf_score_dense fills A inside the scorer (k_fuse) when eligible
+    int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
+                            // one 64-lane NP = 1 class (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -4889,7 +5128,8 @@ struct rf_ctx {
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
-        size_t nx = 0;         // non-lean 64-lane tasks (RF_OPT_DP_NL64)
+        size_t nx = 0;         // latency-bound non-lean tasks, k_dpx (RF_OPT_DP_NL64)
+        size_t nl = 0;         // latency-mode lean tasks, one 64-lane NP = 1 class (RF_OPT_DP_LAT)
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -5165,6 +5405,7 @@ void load_env_opts(Opts &o)
     o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
     o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
+    o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_fwd = env_int("RIFRAF_SCORE_FWD", o.score_fwd);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
@@ -5374,6 +5615,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
     case RF_OPT_SYNC_BLOCK: return &o.sync_block;
     case RF_OPT_DP_NL64: return &o.dp_nl64;
+    case RF_OPT_DP_LAT: return &o.dp_lat;
     case RF_OPT_SCORE_FWD: return &o.score_fwd;
     default: return nullptr;
     }
@@ -6065,6 +6307,27 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             if (2 * n1 < nall)
                 psplit = 0;
         }
+        // latency mode (RF_OPT_DP_LAT, round 5): few lean tasks of H <= 127 --
+        // e.g. configs[2]'s 1,000 reads, or one cluster -- cannot fill the GPU
+        // whatever their class, so each runs at its own step latency; they all
+        // go to one 64-lane NP = 1 launch (one task per wave, one band pair
+        // per lane: the shortest step), on one stream
+        bool latmode = false;
+        {
+            size_t nl = 0;
+            for (int dir = 0; dir < 2; ++dir) {
+                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
+                    continue;
+                for (int32_t k = 0; k < njobs; ++k) {
+                    const SeqObj &S = ctx->seqs[seq[k]];
+                    const Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
+                    const bool ln = S.ncins == 0 && S.ncdel == 0 && S.finite && !(dir == 0 && (flags & (RF_SKEW | RF_TRIM)));
+                    nl += ln && b.H <= 127;
+                }
+            }
+            latmode = nl > 0 && nl <= (size_t)std::max(ctx->opt.dp_lat, 0);
+        }
+        std::vector<DPTask> cl;
         for (int dir = 0; dir < 2; ++dir) {
             if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
                 continue;
@@ -6106,7 +6369,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // (the 16-lane NP = 4 / 8 kernels need > 256 registers: one wave
                 // per SIMD)
                 const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
-                if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
+                if (lean && latmode && t.H <= 127) {
+                    cl.push_back(t);
+                } else if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
                 } else if (lean && ((psplit >> npi) & 1) && np8 &&
                            !(npi == 0 && DPR_PFIX && (t.P < dpr_pm(0, 0) || t.P > dpr_pm(0, 3) || !(t.P & 1)))) {
@@ -6133,13 +6398,13 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 }
             }
         }
-        // Few non-lean tasks of H 32..127 (the reference's codon DP: one long
-        // task per call) run as one 64-lane NP = 1 task per wave: a quarter /
-        // half of the 16-lane kernels' cells per lane and step, and the
-        // launch cannot fill the GPU either way (round 4)
+        // Few non-lean tasks of H <= 127 (the reference's codon DP: one long
+        // task per call) run as one latency-bound task per wave (k_dpx, round
+        // 5; round 4: k_dpr's general step in 64 lanes): such a launch cannot
+        // fill the GPU, so the step latency is the time
         std::vector<DPTask> cx;
-        if (cr[1][0].size() + cr[2][0].size() <= (size_t)std::max(ctx->opt.dp_nl64, 0)) {
-            for (int a = 1; a <= 2; ++a) {
+        if (cr[0][0].size() + cr[1][0].size() + cr[2][0].size() <= (size_t)std::max(ctx->opt.dp_nl64, 0)) {
+            for (int a = 0; a <= 2; ++a) {
                 cx.insert(cx.end(), cr[a][0].begin(), cr[a][0].end());
                 cr[a][0].clear();
             }
@@ -6163,6 +6428,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         }
         std::stable_sort(cx.begin(), cx.end(), by_len);
         all.insert(all.end(), cx.begin(), cx.end());
+        std::stable_sort(cl.begin(), cl.end(), by_len);
+        all.insert(all.end(), cl.begin(), cl.end());
         std::stable_sort(c64.begin(), c64.end(), by_len);
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
@@ -6186,6 +6453,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         for (int a = 0; a < 2; ++a)
             P.nw[a] = cw[a].size();
         P.nx = cx.size();
+        P.nl = cl.size();
         P.n64 = c64.size();
         P.ng = cg.size();
         P.hmax64 = hmax64;
@@ -6206,7 +6474,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // largest: the machine stays full through every launch's tail.
     struct Launch {
         int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>,
-                       // 32 / 33 = lean wide tasks, 34 = non-lean 64-lane tasks,
+                       // 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean), 35 = latency-mode lean,
                        // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
     };
@@ -6234,6 +6502,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             launches.push_back({34, at, P.nx});
             at += P.nx;
         }
+        if (P.nl) {
+            launches.push_back({35, at, P.nl});
+            at += P.nl;
+        }
         if (P.n64) {
             launches.push_back({8, at, P.n64});
             at += P.n64;
@@ -6247,9 +6519,17 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (int e = ensure_buf(ctx, ctx->scratch[10], P.ng * 4 * (size_t)(P.hmaxg + 6) * 8))
             return e;
     }
-    // the largest launch stays on the main stream
+    // The latency-bound classes (few long tasks: k_dpx, k_dp) go first, on
+    // the main stream: the others run beside them on the side streams, which
+    // may share hardware queues with each other (round 5: the reference's
+    // codon DP waited behind a read class on a shared queue, c3).  Otherwise
+    // the largest launch stays on the main stream.
+    std::stable_partition(launches.begin(), launches.end(),
+                          [](const Launch &L) { return L.kind == 34 || L.kind == 8 || L.kind == 9; });
     size_t big = 0;
-    for (size_t i = 1; i < launches.size(); ++i)
+    const bool lat_first = !launches.empty() &&
+                           (launches[0].kind == 34 || launches[0].kind == 8 || launches[0].kind == 9);
+    for (size_t i = 1; i < launches.size() && !lat_first; ++i)
         if (launches[i].n > launches[big].n)
             big = i;
     const bool concurrent = launches.size() > 1 && ctx->opt.dp_streams;
@@ -6290,9 +6570,14 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                                st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 34) {
-            // non-lean 64-lane NP = 1 tasks (H <= 127), one per wave
-            hipLaunchKernelGGL((k_dpr<1, false, dpl_pmax(1), 64>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n,
-                               d_bases, d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
+            // few non-lean tasks (H <= 127): one latency-bound task per wave (k_dpx)
+            hipLaunchKernelGGL(k_dpx, dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out,
+                               ctx->d_err);
+        } else if (L.kind == 35) {
+            // latency mode: lean tasks of H <= 127, one 64-lane NP = 1 task per wave
+            hipLaunchKernelGGL((k_dpr<1, true, dpl_pmax(1, 64), 64>), dim3(n), dim3(64),
+                               (size_t)dpl_task_bytes(1, dpl_pmax(1, 64), 64), st, d_tasks + L.at, n, d_bases, d_tabs,
+                               d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind >= 32) {
             // task-width classes, both NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
             // (H <= 127)

@@ -17,6 +17,10 @@ def pytest_configure(config):
 def engine():
     from rifraf_amd.engine import Engine
     e = Engine(0)
+    # small test launches would all take the latency-mode DP class
+    # (RF_OPT_DP_LAT); the shared engine keeps the throughput classes, and the
+    # DP tests parametrize latency mode explicitly (`dp_lat`)
+    e.set_option("dp_lat", 0)
     yield e
     e.close()
 

@@ -46,17 +46,21 @@ DP_CASES = [
 ]
 
 
+@pytest.mark.parametrize("lat", [0, 2048])
 @pytest.mark.parametrize("pad", [64, 1])
 @pytest.mark.parametrize("L,err,bw,jit,codon,nl64", [c + (1024,) for c in DP_CASES] +
                          [c + (0,) for c in DP_CASES if c[4]])
-def test_dp_bands_bitexact(engine, opts, L, err, bw, jit, codon, nl64, pad):
+def test_dp_bands_bitexact(engine, opts, L, err, bw, jit, codon, nl64, pad, lat):
     """Bands, scores, backtraces and error counts vs the oracle, with the
     default row strides and with every band's rows padded to whole 128-B
     lines (RF_OPT_BAND_PAD = 1: even strides in every DP class).  The codon
-    cases run twice: a few non-lean tasks of H 32..127 as 64-lane tasks (the
-    default, RF_OPT_DP_NL64) and in the 16-lane non-lean kernels (0)."""
+    cases run twice: a few non-lean tasks of H <= 127 in k_dpx (the default,
+    RF_OPT_DP_NL64) and in the 16-lane non-lean kernels (0).  Lean tasks run
+    in their throughput classes (lat 0) and in the latency-mode 64-lane class
+    (RF_OPT_DP_LAT, round 5)."""
     opts("band_pad", pad)
     opts("dp_nl64", nl64)
+    opts("dp_lat", lat)
     rng = np.random.default_rng(L * 7 + bw)
     t = random_seq(L, rng)
     seqs = []
@@ -109,14 +113,16 @@ def _check_bands(engine, t, seqs, bws):
         assert scores[k] == A_exp[d_end, L]
 
 
+@pytest.mark.parametrize("lat", [0, 2048])
 @pytest.mark.parametrize("pad", [64, 0, 1])
-def test_dp_class_boundaries(engine, opts, pad):
+def test_dp_class_boundaries(engine, opts, pad, lat):
     """H = 2bw + |n-m| + 1 on both sides of every kernel-class edge (31/32,
     63/64, 127/128), reads longer and shorter than the template, mixed in one
     launch so waves hold tasks of different geometry (lean interior bounds are
     the intersection over a wave's four tasks); default, odd-only and
-    all-padded row strides."""
+    all-padded row strides; throughput classes and latency mode (lat)."""
     opts("band_pad", pad)
+    opts("dp_lat", lat)
     rng = np.random.default_rng(77)
     t = random_seq(180, rng)
     seqs, bws = [], []
@@ -140,8 +146,8 @@ def test_dp_class_boundaries(engine, opts, pad):
     _check_bands(engine, t, seqs, bws)
 
 
-@pytest.mark.parametrize("dp_wide", [3, 1, 2, 0])
-def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide):
+@pytest.mark.parametrize("dp_wide,lat", [(3, 0), (1, 0), (2, 0), (0, 0), (3, 2048)])
+def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide, lat):
     """Regression for the round-2 64/32-lane DP task work (RF_OPT_DP_WIDE):
     one rf_realign whose lean tasks straddle every task-width class edge
     (H 62..66 -> 16 / 32 lanes, 125..131 -> 32 / 64 lanes, 250..257 -> 64
@@ -151,6 +157,7 @@ def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide):
     directions, padded and unpadded strides in the same context.  Bands and
     A[end,end] bit-exact vs oracle.forward / oracle.backward."""
     opts("dp_wide", dp_wide)
+    opts("dp_lat", lat)   # latency mode: H <= 127 in the 64-lane NP = 1 class, wider ones as before
     rng = np.random.default_rng(4242 + dp_wide)
     t = random_seq(2400, rng)
     seqs, bws = [], []
@@ -179,10 +186,12 @@ def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide):
         assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(seqs[k]) + 1, len(t) + 1, bws[k])
 
 
+@pytest.mark.parametrize("lat", [0, 2048])
 @pytest.mark.parametrize("m,n,bw", [(3, 40, 9), (8, 8, 9), (1, 1, 1), (2, 30, 2), (40, 3, 9), (25, 60, 6)])
-def test_dp_short_and_skewed_shapes(engine, m, n, bw):
+def test_dp_short_and_skewed_shapes(engine, opts, m, n, bw, lat):
     """Templates shorter than the bandwidth (c > m: no lean interior) and very
-    unequal lengths, several copies per launch."""
+    unequal lengths, several copies per launch; both lean DP modes."""
+    opts("dp_lat", lat)
     rng = np.random.default_rng(m * 100 + n)
     t = random_seq(m, rng)
     seqs = [RifrafSequence(random_seq(n, rng), np.log10(rng.uniform(0.01, 0.3, n)), bw, SEQ_SCORES)
@@ -204,6 +213,70 @@ def test_dp_skew_trim(engine, flags):
         moves, nerr = engine.backtrace([k])
         ref = oracle.backtrace(mv, len(s) + 1, 81, 5)
         np.testing.assert_array_equal(moves[0], ref)
+
+
+@pytest.mark.parametrize("flags", [0, RF_SKEW, RF_TRIM, RF_SKEW | RF_TRIM])
+@pytest.mark.parametrize("m,dn,bw", [(2600, 21, 9), (2000, -3, 9), (700, 40, 30), (1200, 5, 4), (400, 90, 18)])
+def test_dpx_long_reference_tasks(engine, opts, m, dn, bw, flags):
+    """Round 5: the latency-bound non-lean kernel (k_dpx) on reference-shaped
+    tasks -- one or two long codon alignments per call, as rf_rifraf_batch_ref
+    and has_single_indels / single_indel_proposals issue them (configs[2]:
+    2,622 x 2,601 at bw 9, H ~ 40) -- with skew_matches and trim, H from 9 to
+    127 (k_dpx takes every H <= 127), many 64-row staging blocks (ring
+    wrap-around), forward alone (flags) and forward + backward.  Bands,
+    A[end,end], backtraces and error counts bit-exact vs the oracle."""
+    rng = np.random.default_rng(m + dn + 1000 * bw + flags)
+    t = random_seq(m, rng)
+    # a mutated copy of the template, shifted in frame: codon and single indels
+    s = t.copy()
+    for _ in range(max(3, m // 200)):
+        p = int(rng.integers(0, len(s)))
+        op = int(rng.integers(0, 3))
+        if op == 0:
+            s[p] = (s[p] + 1) % 4
+        elif op == 1:
+            s = np.concatenate([s[:p], random_seq(int(rng.integers(1, 4)), rng), s[p:]])
+        else:
+            s = np.concatenate([s[:p], s[p + int(rng.integers(1, 4)):]])
+    want = m + dn
+    s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
+    ref = RifrafSequence(s, np.full(len(s), math.log10(0.1)), bw, REF_SCORES)
+    engine.set_sequences(0, [ref])
+    engine.set_templates(0, [t])
+    H = 2 * bw + abs(dn) + 1
+    assert H <= 127
+    skew, trim = bool(flags & RF_SKEW), bool(flags & RF_TRIM)
+    score = engine.realign([0], [0], 0, [bw], RF_FWD | flags)
+    A_exp, mv = oracle.forward(t, ref, moves=True, skew=skew, trim=trim)
+    assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, m + 1, bw)
+    d_end = len(s) - m + max(m - len(s), 0) + bw
+    assert score[0] == A_exp[d_end, m]
+    moves, nerr = engine.backtrace([0])
+    exp_moves = oracle.backtrace(mv, len(s) + 1, m + 1, bw)
+    np.testing.assert_array_equal(moves[0], exp_moves)
+    assert nerr[0] == oracle.count_errors(exp_moves, t, s)
+    if not flags:
+        engine.realign([0], [0], 0, [bw], RF_FWD | RF_BWD)
+        assert_band_equal(engine.download_band(0, RF_BAND_B), oracle.backward(t, ref), len(s) + 1, m + 1, bw)
+        assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, m + 1, bw)
+
+
+def test_dpx_invalid_score_is_loud(engine):
+    """A non-lean task whose band holds a cell with no finite predecessor
+    (insertions and deletions impossible: ErrorModel(1, 0, 0, 1, 1), a read
+    one base longer than the template) raises the reference's "new score is
+    invalid" (align.jl:105-107) from k_dpx, as from the other DP kernels."""
+    rng = np.random.default_rng(3)
+    t = random_seq(300, rng)
+    s = np.concatenate([t, random_seq(1, rng)])
+    sc = Scores.from_errors(ErrorModel(1.0, 0.0, 0.0, 1.0, 1.0))
+    r = RifrafSequence(s, np.full(len(s), -1.0), 9, sc)
+    engine.set_sequences(0, [r])
+    engine.set_templates(0, [t])
+    with pytest.raises(RifrafError, match="new score is invalid"):
+        engine.realign([0], [0], 0, [9], RF_FWD)
+    with pytest.raises(oracle.OracleError):
+        oracle.forward(t, r)
 
 
 def test_dp_huge_band_global_ring(engine):
