@@ -381,9 +381,6 @@ def main():
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal only: allow several ranks on one GPU (n_gpus then counts distinct devices)")
-    ap.add_argument("--score-fwd", action="store_true",
-                    help="c4 step as the fused-step prototype: rf_realign RF_BWD only, then rf_score_dense with "
-                         "the forward band filled inside the scorer (RF_OPT_SCORE_FWD, k_fuse)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch, rendezvous, workload and device assignment only (no engine): checks the "
                          "multi-rank plumbing on a host without GPUs")
@@ -662,23 +659,11 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     # 72 B of totals per consensus position
     dp_bytes = 8 * cells
     score_bytes = 8 * cells + sum(33 * (len(r) + 1) for r in reads) + sum(72 * (len(t) + 1) for t, _ in clusters)
-    if args.score_fwd:
-        # fused-step prototype: the DP stores B only; the scorer reads B once,
-        # the tables, writes 72 B per position per read (partials) and
-        # k_reduce reads them back
-        dp_bytes = 8 * cells // 2
-        score_bytes = (8 * cells // 2 + sum(33 * (len(r) + 1) for r in reads)
-                       + 2 * 72 * sum((len(t) + 1) * len(rs) for t, rs in clusters)
-                       + sum(72 * (len(t) + 1) for t, _ in clusters))
 
     from rifraf_amd.engine import pack_groups
     packed = pack_groups(groups)   # the caller's slot lists, packed once
 
-    # --score-fwd: the fused-step prototype (k_fuse fills A inside the scorer;
-    # the DP pass computes B only)
-    dp_flags = RF_BWD if args.score_fwd else RF_FWD | RF_BWD
-    if args.score_fwd:
-        eng.set_option("score_fwd", 1)
+    dp_flags = RF_FWD | RF_BWD
 
     def step():
         eng.realign(slots, slots, tpl_of, bws, dp_flags)
@@ -718,8 +703,7 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
     sc_gbs = score_bytes / (sc_ms * 1e-3) / 1e9
     dominant = "k_score" if sc_ms >= dp_ms else "k_dp"
     ach, byt, ms = (sc_gbs, score_bytes, sc_ms) if dominant == "k_score" else (dp_gbs, dp_bytes, dp_ms)
-    # the committed PMC profile is the product step's (--score-fwd: profiles/r04s_fuse.json)
-    traffic = None if args.score_fwd else pmc_traffic(args.config, nclu, dominant)
+    traffic = pmc_traffic(args.config, nclu, dominant)
     result = {
         "metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
         "value": tot_cells / elapsed / 1e9,
@@ -736,7 +720,7 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         "config": {"workload": args.config, "description": label, "clusters_per_gpu": nclu,
                    "reads_per_cluster": nreads, "template_len": length, "error_rate": err,
                    "bandwidth": bw, "parallelism": f"clusters sharded over {world} rank(s)",
-                   "step": "B fill + fused A fill / scoring (k_fuse)" if args.score_fwd else "A/B fill + scoring"},
+                   "step": "A/B fill + scoring"},
         "proposals_per_s": tot_props / elapsed,
         "pairs_per_s": tot_pairs / elapsed,
         "dp_ms": dp_ms,

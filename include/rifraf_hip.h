@@ -102,8 +102,6 @@ const char *rf_last_error(const rf_ctx *ctx);
                                     tasks (k_dpr<2,..,32>); 0 = 16-lane tasks only   */
 #define RF_OPT_ALN_SUMS_HOST 19 /* 1: rf_aln_error_sums folds the moves on host
                                     threads instead of the device (k_aln_sums)     */
-#define RF_OPT_SEG_COLS    21   /* wide-band scorer columns per work item: 64
-                                   (k_score_segl, default) or 128 (k_score_segw)  */
 #define RF_OPT_ALN_MARKS_MIN 22 /* rf_aln_error_sums on the device: groups of more
                                    than this many reads (default 128) use the
                                    per-read marks + per-column fold launches      */
@@ -114,23 +112,17 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    per call (codon / skew / trim) run as one
                                    latency-bound task per wave, k_dpx (default
                                    1024; 0: the 16-lane non-lean kernels)       */
-#define RF_OPT_SCORE_FWD   25   /* 1: rf_score_dense / rf_score_dense_dev fill the
-                                   forward band inside the scorer (k_fuse, the
-                                   fused-step prototype) when every read is lean
-                                   with H <= 127: only the B bands
-                                   (rf_realign RF_BWD) are read, A is neither read
-                                   nor needed; other launches use A as usual.
-                                   align.jl:155-179 + model.jl:242-285, 389-393 */
 #define RF_OPT_DP_LAT      26   /* latency mode: an rf_realign call with at most
-                                   this many lean tasks of H <= 127 (and no
-                                   wider lean task) runs them all as one 64-lane
-                                   task per wave (one launch; such a call cannot
-                                   fill the GPU, so a task's step latency is the
-                                   time).  Default 2048; 0 never.  align.jl:114-212 */
+                                   this many lean tasks of H <= 127 runs them all
+                                   as one latency-bound task per wave (k_dpx, one
+                                   launch; such a call cannot fill the GPU, so a
+                                   task's step latency is the time).  Default
+                                   2048; 0 never.  align.jl:114-212            */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);
-   rf_set_option rejects them. */
+   keys 21 (128-column k_score_segw) and 25 (k_fuse, the fused forward fill +
+   scoring step) in round 5.  rf_set_option rejects them. */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 

@@ -590,23 +590,9 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     else
         E1 = dpp_f64<TaskLanes<LPT>::FROM_R1>(v1[0]);        // (d+1) of the last pair = lane q+1's pair 0
     double L3a = -RF_INF, L3b = -RF_INF, R3a = -RF_INF, R3b = -RF_INF;
-    if (LPT == 64 && codon) {
-        // 64-lane non-lean tasks (round 4: a few long codon tasks, e.g. the
-        // reference's DP): one or two wave shifts per neighbour
-        constexpr int L1 = TaskLanes<64>::FROM_L1, R1 = TaskLanes<64>::FROM_R1;
-        if (NP == 1) {
-            L3a = dpp_f64<L1>(v3[0]);
-            L3b = dpp_f64<L1>(L3a);
-            R3a = dpp_f64<R1>(v3[0]);
-            R3b = dpp_f64<R1>(R3a);
-        } else {
-            L3a = dpp_f64<L1>(v3[NP - 1]);
-            L3b = dpp_f64<L1>(v3[NP > 1 ? NP - 2 : 0]);
-            R3a = dpp_f64<R1>(v3[0]);
-            R3b = dpp_f64<R1>(v3[NP > 1 ? 1 : 0]);
-        }
-    }
-    if (LPT == 16 && codon) {   // (32-lane tasks are lean only)
+    // (32- and 64-lane tasks are lean: no codon moves; few long non-lean
+    // tasks run in k_dpx, the rest as 16-lane tasks here)
+    if (LPT == 16 && codon) {
         if (NP == 1) {
             L3a = dpp_f64<DPP_FROM_L1>(v3[0]);
             L3b = dpp_f64<DPP_FROM_L2>(v3[0]);
@@ -778,12 +764,6 @@ __host__ __device__ constexpr int dpl_b(int np, int lpt = 16)
 #define DPL_SPREAD 1   // NP = 1 lean flush spread over the next block's periods
 #endif
 #define DPL_SPREAD_ON(np, lpt) (DPL_SPREAD && (np) == 1 && (lpt) == 16)
-// lean flushes leave the padding pairs of line-padded rows unwritten: bit-exact
-// but measured slower (c5 DP 26.1 against 22.9-23.1 ms, profiles/r04g_ab_c5.json:
-// the rows' half-written last lines cost more than whole ones); off
-#ifndef DPL_SKIP_PAD
-#define DPL_SKIP_PAD 0
-#endif
 #ifndef DPR_WPE1
 #define DPR_WPE1 1   // minimum waves per SIMD requested for the NP = 1 kernels
 #endif
@@ -1100,25 +1080,6 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // pipeline.  Before the first block the pending set is the sink.
             constexpr int FL = dpl_flush_stores(NP, PM, LPT);
             constexpr int FLS = DPL_SPREAD_ON(NP, LPT) ? FL : 1;
-            // line-padded rows (P % 16 == 0, the wide-band stride) of 32- and
-            // 64-lane tasks (round 4): every block is 2*DPL_B whole rows [g0, g0 + blk)
-            // with g0 a row start, so flush pair e is pair e % (P/2) of its
-            // row.  Pairs at or past vp = ceil(ceil(H/2) / 2) hold no in-band
-            // cell (d >= 4 vp >= H); a store that would write one writes its
-            // row's pair vp - 1 again instead (same line, same bytes), so the
-            // row's trailing padding sectors are never written.  The task is
-            // the whole wave: ph, vp and the reciprocal are scalars; e / ph is
-            // (e * (2^20 / ph + 1)) >> 20, exact for e < 2^11 and ph <= 64
-            // (error below 2^-9 against a fractional part of at most 1 - 1/ph).
-            // (32-lane tasks: two per wave, per-lane values)
-            const bool padrows = DPL_SKIP_PAD && LPT >= 32 && (P & 15) == 0;
-            int pk_ph = max(P >> 1, 1), pk_vq = ((((T.H + 1) >> 1) + 1) >> 1) - 1;
-            if (LPT == 64) {
-                pk_ph = __builtin_amdgcn_readfirstlane(pk_ph);
-                pk_vq = __builtin_amdgcn_readfirstlane(pk_vq);
-            }
-            const unsigned pk_m = (1u << 20) / (unsigned)pk_ph + 1u;
-            static_assert(LPT < 32 || dpl_b(NP, LPT) * PM < 2048, "pad-skip reciprocal range");
             dvec2 pv[FLS];
             dvec2 *pg = (dvec2 *)sink;
             int pnu = 0;
@@ -1242,15 +1203,9 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                             }
                         }
                     } else {
-                        // padded rows: whole-row blocks only (lo2 == g0, nu == DPL_B * P)
-                        const bool skp = padrows && real && lo2 == g0 && nu == DPL_B * P;
 #pragma unroll
                         for (int j = 0; j < FL; ++j) {
-                            int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
-                            if (skp) {
-                                const int r = e - pk_ph * (int)(((unsigned)e * pk_m) >> 20);
-                                e -= max(r - pk_vq, 0);
-                            }
+                            const int e = real ? min(q + LPT * j, nu - 1) : q + LPT * j;
                             DP_STORE(g + e, dpl_rd2<NP>(R, u2 + 2 * (real ? e : 0)));
                         }
                     }
@@ -1352,7 +1307,13 @@ struct DpxStage {
     int sb, col;
 };
 
-template <int PAR, bool FAST>
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned DPX_NOSTORE = 0x80000000u;   // buffer offset past any band: the store is dropped
+// a k_dpx task: H <= 127 (lanes hold diagonal pairs) and a band below 2 GiB
+// (32-bit buffer offsets, DPX_NOSTORE past it)
+inline bool dpx_fits(const DPTask &t) { return t.H <= 127 && (int64_t)t.klen * t.P * 8 < ((int64_t)1 << 31); }
+
+template <int PAR, bool FAST, bool CODON, bool CHECK>
 __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, int ii, int jj, double v1,
                                            double v2, double xn, double yci, double ycd, const dvec2 &mtmm,
                                            const dvec2 &isds, const dvec2 &cicd, int sb, int tbb, double lbv,
@@ -1363,16 +1324,19 @@ __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, in
     const double x_del = PAR ? xn : v1;               // (d+1, kappa-1)
     if (FAST) {
         // candidates off the step-to-step chain first, the kappa-1 pair last
-        const double t = fmax(fmax(v2 + ms, yci + cicd.x), ycd + cicd.y);
+        const double t = CODON ? fmax(fmax(v2 + ms, yci + cicd.x), ycd + cicd.y) : v2 + ms;
         const double best = fmax(t, fmax(x_ins + isds.x, x_del + isds.y));
-        emask |= __ballot(best == -RF_INF) & actm;   // "new score is invalid" (active diagonals)
+        if (CHECK)
+            emask |= __ballot(best == -RF_INF) & actm;   // "new score is invalid" (active diagonals)
         return best + lbv;
     }
     const bool valid = d < T.H && jj >= 0 && jj <= T.m && ii >= 0 && ii <= T.n;
     const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;   // align.jl:74-76
-    const double cd = jj >= 3 ? cicd.y : -RF_INF;                         // codon delete needs j > 3
     double best = fmax(fmax(v2 + ms, x_ins + is), x_del + isds.y);
-    best = fmax(fmax(best, yci + cicd.x), ycd + cd);   // cicd.x is -Inf unless i > 3 (staged)
+    if (CODON) {
+        const double cd = jj >= 3 ? cicd.y : -RF_INF;       // codon delete needs j > 3
+        best = fmax(fmax(best, yci + cicd.x), ycd + cd);   // cicd.x is -Inf unless i > 3 (staged)
+    }
     const bool origin = ii == 0 && jj == 0;
     const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
     eflag |= (valid && !origin && best == -RF_INF) ? 1 : 0;
@@ -1382,25 +1346,35 @@ __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, in
     return v;
 }
 
+// CODON: the task may have codon moves (ring of the last four anti-diagonals
+// in LDS); CHECK: the interior raises "new score is invalid" (non-finite
+// tables).  <false, false> takes the latency-mode lean tasks (finite tables,
+// no codon / skew / trim, RF_OPT_DP_LAT), <true, true> every other task.
+template <bool CODON, bool CHECK>
 __global__ void __launch_bounds__(64)
 k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
       int *__restrict__ err)
 {
-    __shared__ dvec2 s_mtmm[DPX_RING], s_isds[DPX_RING], s_cicd[DPX_RING];
+    __shared__ dvec2 s_mtmm[DPX_RING], s_isds[DPX_RING], s_cicd[CODON ? DPX_RING : 1];
     __shared__ int s_sb[DPX_RING], s_col[DPX_RING];
-    __shared__ double s_band[4 * DPX_W];
+    __shared__ double s_band[CODON ? 4 * DPX_W : 1];
     const int q = threadIdx.x;
     const DPTask T = tasks[blockIdx.x];   // one task per workgroup
     const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
-    const bool codon = T.ncins > 0 || T.ncdel > 0;
+    const bool codon = CODON && (T.ncins > 0 || T.ncdel > 0);
     const uint8_t *sbase = bases + T.sb;
     const uint8_t *tbase = bases + T.tb;
     const double *tb = tabs + T.tab;
-    double *band = bands + T.band;
     const int K = T.klen;
-    for (int e = q; e < 4 * DPX_W; e += 64)
-        s_band[e] = -RF_INF;
+    // band stores through a buffer resource: a lane that stores nothing at a
+    // step gets an offset past the band (dropped by the range check), so no
+    // step changes exec for its store (the host keeps K * P * 8 < 2^31)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc(bands + T.band, 0, (int)((int64_t)K * T.P * 8), 0x00020000);
+    if (CODON)
+        for (int e = q; e < 4 * DPX_W; e += 64)
+            s_band[e] = -RF_INF;
 
     // block b: rows R = P + q + par in [64b, 64b + 64) (read row R - c) and
     // columns J = P - q + 64 in [64b, 64b + 64) (template column J - 64)
@@ -1421,13 +1395,14 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         const int i = (64 * b + q) & (DPX_RING - 1);
         s_mtmm[i] = dvec2{s.mt, s.mm};
         s_isds[i] = dvec2{s.is, s.ds};
-        s_cicd[i] = dvec2{s.ci, s.cd};
+        if (CODON)
+            s_cicd[i] = dvec2{s.ci, s.cd};
         s_sb[i] = s.sb;
         s_col[i] = s.col;
     };
 
     // interior [klo, khi]: every diagonal with cells in the matrix has its
-    // cell inside the matrix with i, j > 3 (codon moves open) and j in
+    // cell inside the matrix (with i, j > 3: codon moves open) and j in
     // 1..m-1 (trim off); the origin and the final cell lie outside it
     double lb[2];
     bool act[2];
@@ -1442,7 +1417,8 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         act[par] = d < T.H && mlo <= mhi;
         lb[par] = act[par] ? 0.0 : -RF_INF;
         if (act[par]) {
-            const int jlo = max(3, T.c + 3 - d), jhi = min(T.m - (trim ? 1 : 0), T.n + T.c - d);
+            const int jlo = CODON ? max(3, T.c + 3 - d) : max(trim ? 1 : 0, T.c - d);
+            const int jhi = min(T.m - (trim ? 1 : 0), T.n + T.c - d);
             ok = ok && jlo <= jhi;
             lo = max(lo, d + 2 * jlo);
             hi = min(hi, d + 2 * jhi);
@@ -1460,22 +1436,29 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     DpxStage nxt = stage_load(2);
     wave_sync();
 
-    // per parity: band element of this lane's diagonal (reverse: flipped) and
-    // whether the kappa row holds it
-    const int el0 = rev ? (T.H - 1 - 2 * q) >> 1 : q;
-    const int el1 = rev ? (T.H - 2 - 2 * q) >> 1 : q;
+    // per parity: byte offset of this lane's band element in a kappa row
+    // (reverse: flipped), or past the band when the row does not hold it
+    const unsigned vo0 = 2 * q < T.H ? 8u * (unsigned)(rev ? (T.H - 1 - 2 * q) >> 1 : q) : DPX_NOSTORE;
+    const unsigned vo1 = 2 * q + 1 < T.H ? 8u * (unsigned)(rev ? (T.H - 2 - 2 * q) >> 1 : q) : DPX_NOSTORE;
+    const unsigned rowb = 8u * (unsigned)T.P;
     const uint64_t actm0 = __ballot(act[0]), actm1 = __ballot(act[1]);
-    const bool st0 = 2 * q < T.H, st1 = 2 * q + 1 < T.H;   // the band holds the diagonal
     double v1 = -RF_INF, v2 = -RF_INF;
     uint64_t emask = 0;
     int eflag = 0, fset = 0;
     double fval = 0.0;
-    // the record of row R = 2u + q (period 2u, even step), carried between pairs
-    dvec2 c_mtmm = s_mtmm[q], c_isds = s_isds[q], c_cicd = s_cicd[q];
+    // records of the current pair of periods (2u, 2u + 1), read one pair
+    // ahead: rows R = 2u + q (c_), 2u + q + 1 (a_), 2u + q + 2 (b_), columns
+    // J = 2u - q + 64 (col0), + 1 (col1)
+    dvec2 c_mtmm = s_mtmm[q], c_isds = s_isds[q], c_cicd = CODON ? s_cicd[q] : dvec2{0.0, 0.0};
     int c_sb = s_sb[q];
+    dvec2 a_mtmm = s_mtmm[q + 1], a_isds = s_isds[q + 1], a_cicd = CODON ? s_cicd[q + 1] : dvec2{0.0, 0.0};
+    int a_sb = s_sb[q + 1];
+    dvec2 b_mtmm = s_mtmm[q + 2], b_isds = s_isds[q + 2], b_cicd = CODON ? s_cicd[q + 2] : dvec2{0.0, 0.0};
+    int b_sb = s_sb[q + 2];
+    int col0 = s_col[(64 - q) & (DPX_RING - 1)], col1 = s_col[(65 - q) & (DPX_RING - 1)];
     // the codon neighbours of the next step, read one step ahead (kappa = 0:
     // ring row 1, still -Inf)
-    double cy_ci = s_band[DPX_W + 2 + q - 2], cy_cd = s_band[DPX_W + 2 + q + 1];
+    double cy_ci = CODON ? s_band[DPX_W + 2 + q - 2] : 0.0, cy_cd = CODON ? s_band[DPX_W + 2 + q + 1] : 0.0;
     const int npairs = (K + 3) >> 2;
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -1483,6 +1466,9 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     using I3 = std::integral_constant<int, 3>;
     using BT = std::integral_constant<bool, true>;
     using BF = std::integral_constant<bool, false>;
+#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
+    const long long dg_c0 = clock64(), dg_w0 = wall_clock64();   // diagnostic builds only
+#endif
     for (int u = 0; u < npairs; ++u) {
         if ((u & 31) == 0) {   // chunk t = u / 32 (64 periods): block t + 2 in, t + 3 loads
             const int t = u >> 5;
@@ -1490,13 +1476,16 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             nxt = stage_load(t + 3);
             wave_sync();
         }
-        const int r1 = (2 * u + q + 1) & (DPX_RING - 1), r2 = (2 * u + q + 2) & (DPX_RING - 1);
-        const int j0 = (2 * u - q + 64) & (DPX_RING - 1), j1 = (2 * u - q + 65) & (DPX_RING - 1);
-        const dvec2 a_mtmm = s_mtmm[r1], a_isds = s_isds[r1], a_cicd = s_cicd[r1];
-        const int a_sb = s_sb[r1];
-        const dvec2 b_mtmm = s_mtmm[r2], b_isds = s_isds[r2], b_cicd = s_cicd[r2];
-        const int b_sb = s_sb[r2];
-        const int col0 = s_col[j0], col1 = s_col[j1];
+        // the next pair's records (rows <= 2u + 67: block t + 2 at most, in LDS)
+        const int r1 = (2 * u + q + 3) & (DPX_RING - 1), r2 = (2 * u + q + 4) & (DPX_RING - 1);
+        const int j0 = (2 * u - q + 66) & (DPX_RING - 1), j1 = (2 * u - q + 67) & (DPX_RING - 1);
+        const dvec2 na_mtmm = s_mtmm[r1], na_isds = s_isds[r1];
+        const dvec2 na_cicd = CODON ? s_cicd[r1] : dvec2{0.0, 0.0};
+        const int na_sb = s_sb[r1];
+        const dvec2 nb_mtmm = s_mtmm[r2], nb_isds = s_isds[r2];
+        const dvec2 nb_cicd = CODON ? s_cicd[r2] : dvec2{0.0, 0.0};
+        const int nb_sb = s_sb[r2];
+        const int ncol0 = s_col[j0], ncol1 = s_col[j1];
         // four steps kappa = 4u + s: (period, parity) = (2u, 0), (2u, 1), (2u+1, 0), (2u+1, 1)
         auto step = [&](auto FASTC, auto PARC, auto SC, int per, const dvec2 &mtmm, const dvec2 &isds,
                         const dvec2 &cicd, int sb, int col) {
@@ -1508,25 +1497,34 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // the kappa - 1 neighbour by a wave rotate: lane 0 (63) receives the
             // value of diagonal 127 (0 at kappa - 1 into diagonal 127), and
             // diagonal 127 >= H is -Inf / masked (the host sends H <= 127 only)
+#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 2)
+            const double xn = v1;   // diagnostic builds only (wrong bands): no DPP on the chain
+#else
             const double xn = PAR ? dpp_rot_f64<TaskLanes<64>::ROT_R1>(v1) : dpp_rot_f64<TaskLanes<64>::ROT_L1>(v1);
+#endif
             // codon neighbours at kappa - 3: d - 3 / d + 3 = lanes q - 2 / q + 1
             // (even), q - 1 / q + 2 (odd); this step's were read one step ago,
             // the next step's (ring row kappa - 2, the other parity) now
             const double yci = cy_ci, ycd = cy_cd;
-            {
+            if (CODON) {
                 const double *r = s_band + ((S + 2) & 3) * DPX_W + 2 + q;
                 cy_ci = r[PAR ? -2 : -1];
                 cy_cd = r[PAR ? 1 : 2];
             }
             const int d = 2 * q + PAR;
             const int jj = per - q, ii = per + q + PAR - T.c;
-            const double v = dpx_cell<PAR, FAST>(T, trim, d, ii, jj, v1, v2, xn, yci, ycd, mtmm, isds, cicd, sb, col,
-                                                 lb[PAR], PAR ? actm1 : actm0, emask, eflag, fval, fset);
-            s_band[S * DPX_W + 2 + q] = v;
-            if (PAR ? st1 : st0) {
-                if (FAST || d <= k)
-                    band[(size_t)(rev ? K - 1 - k : k) * T.P + (PAR ? el1 : el0)] = v;
-            }
+            const double v = dpx_cell<PAR, FAST, CODON, CHECK>(T, trim, d, ii, jj, v1, v2, xn, yci, ycd, mtmm, isds,
+                                                               cicd, sb, col, lb[PAR], PAR ? actm1 : actm0, emask,
+                                                               eflag, fval, fset);
+            if (CODON)
+                s_band[S * DPX_W + 2 + q] = v;
+            const unsigned ro = rowb * (unsigned)(rev ? K - 1 - k : k);
+            const unsigned vo = PAR ? vo1 : vo0;
+#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 1)
+            if (!FAST)   // diagnostic builds only (wrong bands): no interior band stores
+#endif
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), brs,
+                                                  (FAST || d <= k) ? vo + ro : DPX_NOSTORE, 0, 0);
             v2 = v1;
             v1 = v;
         };
@@ -1545,8 +1543,23 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         c_isds = b_isds;
         c_cicd = b_cicd;
         c_sb = b_sb;
+        a_mtmm = na_mtmm;
+        a_isds = na_isds;
+        a_cicd = na_cicd;
+        a_sb = na_sb;
+        b_mtmm = nb_mtmm;
+        b_isds = nb_isds;
+        b_cicd = nb_cicd;
+        b_sb = nb_sb;
+        col0 = ncol0;
+        col1 = ncol1;
     }
     (void)ntasks;
+#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
+    if (q == 0 && blockIdx.x == 0)
+        printf("k_dpx<%d> K %d cycles %lld wall_ticks %lld cycles/step %.1f\n", (int)CODON, K, clock64() - dg_c0,
+               wall_clock64() - dg_w0, (double)(clock64() - dg_c0) / K);
+#endif
     if (eflag || emask)
         set_err(err, 1);  // "new score is invalid"
     if (fset && out_score)
@@ -1782,10 +1795,6 @@ k_score(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ group
 }
 
 // split mode: ordered fold over reads, one lane per (group position slot).
-// nan_map (k_fuse's partials): a slot other than the deletion (4) holding
-// -Inf is an empty summax and reads as NaN, as the scorers map it in-kernel
-// (lean_chain: `accI == -Inf ? NaN : accI`) -- the same values fold.
-template <bool NAN_MAP = false>
 __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
                          const int64_t *__restrict__ gstart, int64_t total,
                          const double *__restrict__ split, double *__restrict__ dense)
@@ -1810,9 +1819,6 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
     // the left fold in read order (model.jl:389-393); 16 partials are loaded
     // before they are added, so each lane keeps 16 streaming loads in flight
     double acc = 0.0;
-    const bool map = NAN_MAP && (local % 9) != 4;
-    const double qnan = __builtin_nan("");
-    auto val = [&](double v) { return (map && v == -RF_INF) ? qnan : v; };
     int r = 0;
     for (; r + 16 <= nr; r += 16) {
         double v[16];
@@ -1821,10 +1827,10 @@ __global__ void k_reduce(const ScoreGroup *__restrict__ groups, int ngroups,
             v[u] = __builtin_nontemporal_load(src + (int64_t)(r + u) * stride);
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-            acc += val(v[u]);
+            acc += v[u];
     }
     for (; r < nr; ++r)
-        acc += val(__builtin_nontemporal_load(src + (int64_t)r * stride));
+        acc += __builtin_nontemporal_load(src + (int64_t)r * stride);
     dense[G.dense_off + local] = acc;
 }
 
@@ -2155,343 +2161,6 @@ __device__ __forceinline__ void lean_chain_any(const ScoreRead &R, const LeanWin
     lean_chain(R, w, a, m, sA, sB, sT, tI, tS, tD);
 }
 
-// ---------------------------------------------------------------------
-// k_fuse: dense scoring with the forward band filled inside the scorer
-// (round 4 prototype of the fused step; RF_OPT_SCORE_FWD)
-//
-// The chain of a new column built from A column a (lean_chain) visits rows
-// d = 1 .. H of that column in order, and row d of column a is anti-diagonal
-// kappa = d + 2a: at step kappa the chain needs exactly the cell the forward
-// fill computes at that step (A(d, a)) and its insert predecessor
-// (A(d-1, a), kappa-1).  So the chains ride on the fill's wavefront: the lane
-// that computes cell (d, a) also advances column a's chain by one row, and a
-// chain moves up one lane with its column every period (DPP row_shr, -Inf
-// state entering lane 0).  A is never stored or read back; B (rf_realign
-// RF_BWD) is read once, one 128-B run per task and step.
-//
-// Per task (one read, lean tables; LPT = 16: one DPP row, 4 tasks per wave,
-// H <= 31; LPT = 64: one task per wave, H <= 127, the same moves as wave
-// shifts): lane q holds band rows {2q, 2q+1} as in k_dpr
-// (align.jl:155-179 order and sums: the cells are bit-identical), and the
-// chain rows use the same operands and FP64 ops as lean_chain
-// (model.jl:242-285, util.jl:40-48).  Rows outside a chain's range are made
-// no-ops by selecting -Inf operands (a chain row with aprev = dl = -Inf keeps
-// its -Inf state; bI = bS = -Inf leave the maxima unchanged), the peeled row
-// below column a's band is the generic row with dl = bI = -Inf.  A chain is
-// finished at d = H (lane H >> 1) and writes its read's per-position partial
-// record (the k_score_segl split layout); k_reduce folds the reads in batch
-// order (model.jl:389-393).  Inputs of QD periods ahead (row record, column
-// base, the two B cells) sit in static register slots of a loop unrolled
-// over QD periods.
-// ---------------------------------------------------------------------
-struct alignas(16) FuseTask {
-    int64_t B;      // B band offset (doubles)
-    int64_t sb, tab, tb;
-    int64_t out;    // this read's partial records (doubles from the split base), (m+1) x 9
-    int32_t n, m, H, c, vb, P, K, pad;
-};
-
-#ifndef FUSE_QD
-#define FUSE_QD 4
-#endif
-// interior blocks: QD periods in which every cell of every lane below H is
-// inside the matrix and every column whose chain rows lie there is interior
-// (lean_chain_fix's a >= c, a + 1 + vb <= n, a < m) run a step without range
-// checks: the per-lane masks are constants added as 0 / -Inf
-#ifndef FUSE_FAST
-#define FUSE_FAST 1
-#endif
-// chain state moves with a row rotate (no `old` operand: one instruction per
-// dword instead of a constant move + DPP) and lane 0 resets the state it
-// receives at its even step by adding -Inf (lanes q > 0 add 0.0)
-#ifndef FUSE_ROT
-#define FUSE_ROT 1
-#endif
-
-template <int LPT>
-__global__ void __launch_bounds__(64) k_fuse(const FuseTask *__restrict__ tasks, int ntasks,
-                                             const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
-                                             const double *__restrict__ bands, double *__restrict__ split)
-{
-    constexpr int QD = FUSE_QD;
-    constexpr int L1 = TaskLanes<LPT>::FROM_L1, R1 = TaskLanes<LPT>::FROM_R1;
-    static_assert(LPT == 16 || LPT == 64, "k_fuse tasks are 16 or 64 lanes");
-    const int q = threadIdx.x & (LPT - 1);
-    const int tid = blockIdx.x * (64 / LPT) + threadIdx.x / LPT;
-    FuseTask T = {};
-    const bool live = tid < ntasks;
-    if (live)
-        T = tasks[tid];
-    int kmax = T.K;
-    for (int off = 32; off >= 1; off >>= 1)
-        kmax = max(kmax, __shfl_xor(kmax, off));
-    kmax = __builtin_amdgcn_readfirstlane(kmax);
-    const int n = T.n, m = T.m, H = T.H, c = T.c, vb = T.vb, P = T.P, K = T.K;
-    const uint8_t *sq = bases + T.sb;
-    const uint8_t *tq = bases + T.tb;
-    const double *tb = tabs + T.tab;
-    const double *Bb = bands + T.B;
-    double *out = split + T.out;
-
-    // inputs of period p: the column base of jj = p - q (both steps), the row
-    // record of ii = q + p + 1 - c (odd step of p, even step of p + 1), and
-    // B at (kappa, d) = (2p, 2q) and (2p + 1, 2q + 1).  Loaded raw at clamped indices (a
-    // padding task, T = {}, reads the arenas' first entries), masked at use.
-    struct Slot {
-        int cb, sb;
-        double mt, mm, is, ds, be, bo;
-    };
-    auto load = [&](int p, Slot &S) {
-        const int jc = min(max(p - q, 1), max(m, 1));
-        S.cb = tq[jc - 1];
-        const int ii = q + p + 1 - c;
-        const int iz = min(max(ii, 0), n);
-        const int ks = max(iz - 1, 0);
-        S.sb = sq[max(min(ii, n), 1) - 1];
-        S.mt = tb[ks];
-        S.mm = tb[n + ks];
-        S.is = tb[2 * (size_t)n + ks];
-        S.ds = tb[3 * (size_t)n + iz];
-        // B is stored in its final orientation: cell (d, jj) at kappa * P + (d >> 1)
-        const int ke = min(2 * p, max(K - 1, 0)), ko = min(2 * p + 1, max(K - 1, 0));
-        // lanes past the band read the row's last real element (a finite or
-        // -Inf cell, never an unwritten padding slot: the interior step adds
-        // its -Inf masks to these values)
-        S.be = Bb[(size_t)ke * P + min(q, max((H - 1) >> 1, 0))];
-        S.bo = Bb[(size_t)ko * P + min(q, max((H - 2) >> 1, 0))];
-    };
-    // interior loads (the target period inside the wave's interior range, see
-    // FUSE_FAST): no clamps; lanes past H >> 1 use lane H >> 1's indices
-    // (their rows feed only masked values)
-    const int qe = min(q, H >> 1);
-    const int eev = min(q, max((H - 1) >> 1, 0)), eod = min(q, max((H - 2) >> 1, 0));
-    const int64_t n2 = 2 * (int64_t)n, n3 = 3 * (int64_t)n;
-    auto load_fast = [&](int p, Slot &S) {
-        const int ks = qe + p - c;   // read row ii - 1
-        S.cb = tq[p - qe - 1];
-        S.sb = sq[ks];
-        S.mt = tb[ks];
-        S.mm = tb[n + ks];
-        S.is = tb[n2 + ks];
-        S.ds = tb[n3 + ks + 1];
-        S.be = Bb[(int64_t)(2 * p) * P + eev];
-        S.bo = Bb[(int64_t)(2 * p + 1) * P + eod];
-    };
-    Slot S[QD];
-#pragma unroll
-    for (int j = 0; j < QD; ++j)
-        load(j, S[j]);
-    // the row of the even step of period 0 (ii = q - c)
-    int rsb;
-    double rmt, rmm, ris, rds;
-    {
-        const int ii = q - c;
-        const int iz = min(max(ii, 0), n);
-        const int ks = max(iz - 1, 0);
-        rsb = ii >= 1 ? sq[max(min(ii, n), 1) - 1] : 4;
-        rmt = tb[ks];
-        rmm = tb[n + ks];
-        ris = tb[2 * (size_t)n + ks];
-        rds = tb[3 * (size_t)n + iz];
-    }
-    double sub[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        sub[k] = rsb == k ? rmt : rmm;
-
-    double v1 = -RF_INF, v2 = -RF_INF;   // cells at kappa-1, kappa-2 of this lane's diagonal
-    double prev[4], accI[4], accS[4], dd = -RF_INF;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        prev[k] = accI[k] = accS[k] = -RF_INF;
-    const double qnan = __builtin_nan("");
-    const double mz = q == 0 ? -RF_INF : 0.0;   // FUSE_ROT: lane 0's fresh chain
-    auto reset0 = [&]() {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            prev[k] += mz;
-            accI[k] += mz;
-            accS[k] += mz;
-        }
-        dd += mz;
-    };
-    auto shift = [&]() {   // the chains move up one lane with their columns
-        constexpr int RL1 = TaskLanes<LPT>::ROT_L1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (FUSE_ROT) {
-                prev[k] = dpp_rot_f64<RL1>(prev[k]);
-                accI[k] = dpp_rot_f64<RL1>(accI[k]);
-                accS[k] = dpp_rot_f64<RL1>(accS[k]);
-            } else {
-                prev[k] = dpp_f64<L1>(prev[k]);
-                accI[k] = dpp_f64<L1>(accI[k]);
-                accS[k] = dpp_f64<L1>(accS[k]);
-            }
-        }
-        dd = FUSE_ROT ? dpp_rot_f64<RL1>(dd) : dpp_f64<L1>(dd);
-    };
-
-    // one anti-diagonal: fill cell (d, jj), then column jj's chain row ii
-    auto step = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
-        constexpr int par = decltype(parc)::value;   // static parity
-        const int d = 2 * q + par;
-        const int jj = p - q;
-        const int ii = q + p + par - c;
-        const double E1 = dpp_f64<par == 0 ? L1 : R1>(v1);
-        const double x_ins = par ? v1 : E1;   // (d-1, kappa-1)
-        const double x_del = par ? E1 : v1;   // (d+1, kappa-1)
-        const double ms = rsb == cb ? rmt : rmm;
-        const double best = vmax(vmax(v2 + ms, x_ins + ris), x_del + rds);
-        const bool valid = live && d < H && jj >= 0 && jj <= m && ii >= 0 && ii <= n;
-        const double nv = valid ? ((ii == 0 && jj == 0) ? 0.0 : best) : -RF_INF;
-        v2 = v1;
-        v1 = nv;
-        // chain of column a = jj at row ii (lean_chain's range and peel)
-        const int a = jj;
-        const int jn = min(a + 1, m);
-        const int i0 = max(0, jn - c);
-        const int i1 = min(jn + vb, n);
-        const int ilast = min(i1, a + vb);
-        const bool cok = live && a >= 0 && a <= m;
-        const bool inrow = cok && ii >= i0 && ii <= ilast;
-        const bool peel = cok && ii == ilast + 1 && i1 > ilast;
-        const double aprev = ii < i0 ? -RF_INF : x_ins;
-        const double bSm = ((inrow || peel) && a < m) ? bS : -RF_INF;
-        const double bIm = inrow ? bI : -RF_INF;
-        const double dl = inrow ? nv + rds : -RF_INF;
-        const double dsum = inrow ? nv + bSm : -RF_INF;
-        if (FUSE_ROT && par == 0)
-            reset0();
-        chain_row(aprev, sub, ris, dl, bIm, bSm, prev, accI, accS);
-        dd = vmax(dd, dsum);
-    };
-    // After a period's odd step the chain in lane H >> 1 is complete: it
-    // reached d = H in this period (even H: at the even step; d = H + 1 at
-    // the odd step is a no-op row).  Its record is written raw; k_reduce maps
-    // an empty summax (-Inf) to NaN.
-    const bool emit_lane = live && q == (H >> 1);
-    auto emit = [&](int p, bool interior) {
-        const int a = p - q;
-        if (emit_lane && (interior || (a >= 0 && a <= m))) {
-            double *dst = out + (size_t)a * 9;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                dst[5 + k] = accI[k];
-            if (interior || a < m) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    dst[9 + k] = accS[k];
-                dst[13] = dd;
-            }
-            if (!interior && a == 0) {
-#pragma unroll
-                for (int k = 0; k < 5; ++k)
-                    dst[k] = qnan;
-            }
-        }
-    };
-    // interior step: same operands and FP64 ops; the out-of-range cases are
-    // per-lane constants (lb: cell diagonal d < H; mI: chain row 1 <= d <= H-1;
-    // mS: 1 <= d <= H, the peeled row included), added as 0 / -Inf (x + 0.0 ==
-    // x for every operand: no -0.0 among cells, B cells and table values)
-    double lbv[2], mIv[2], mSv[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-        const int d = 2 * q + par;
-        lbv[par] = (live && d < H) ? 0.0 : -RF_INF;
-        mIv[par] = (live && d >= 1 && d <= H - 1) ? 0.0 : -RF_INF;
-        mSv[par] = (live && d >= 1 && d <= H) ? 0.0 : -RF_INF;
-    }
-    auto fstep = [&](auto parc, const int p, const int cb, const double bI, const double bS) {
-        constexpr int par = decltype(parc)::value;
-        const double E1 = dpp_f64<par == 0 ? L1 : R1>(v1);
-        const double x_ins = par ? v1 : E1;
-        const double x_del = par ? E1 : v1;
-        const double ms = rsb == cb ? rmt : rmm;
-        const double nv = vmax(vmax(v2 + ms, x_ins + ris), x_del + rds) + lbv[par];
-        v2 = v1;
-        v1 = nv;
-        const double bIm = bI + mIv[par], bSm = bS + mSv[par];
-        const double dl = (nv + rds) + mIv[par];
-        const double dsum = nv + bSm;
-        if (FUSE_ROT && par == 0)
-            reset0();
-        chain_row(x_ins, sub, ris, dl, bIm, bSm, prev, accI, accS);
-        dd = vmax(dd, dsum);
-    };
-    // the wave's interior period range [plo, phi] (see FUSE_FAST)
-    int plo = live ? c + H : 0;
-    int phi = live ? min(min(m - 1, n - 1 - vb), n + c - H - 1) : INT_MAX;
-    for (int off = 32; off >= 1; off >>= 1) {
-        plo = max(plo, __shfl_xor(plo, off));
-        phi = min(phi, __shfl_xor(phi, off));
-    }
-    plo = __builtin_amdgcn_readfirstlane(plo);
-    phi = __builtin_amdgcn_readfirstlane(phi);
-
-    const int bve = 2 * q < H, bvo = 2 * q + 1 < H;
-    // periods up to kappa = K (inclusive): column m's chain ends at d = H,
-    // kappa = 2m + H = K for even H
-    for (int p0 = 0; 2 * p0 <= kmax; p0 += QD) {
-        if (FUSE_FAST && p0 >= plo && p0 + 2 * QD - 1 <= phi) {
-#pragma unroll
-            for (int j = 0; j < QD; ++j) {
-                const int p = p0 + j;
-                Slot &X = S[j];
-                Slot &Y = S[(j + 1) % QD];
-                const int cb = X.cb;
-                fstep(std::integral_constant<int, 0>{}, p, cb, X.be, dpp_f64<L1>(X.bo));
-                rsb = X.sb;
-                rmt = X.mt;
-                rmm = X.mm;
-                ris = X.is;
-                rds = X.ds;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    sub[k] = rsb == k ? rmt : rmm;
-                fstep(std::integral_constant<int, 1>{}, p, cb, X.bo, Y.be);
-                emit(p, true);   // interior: 0 < a < m
-                shift();
-                load_fast(p + QD, X);
-            }
-            continue;
-        }
-#pragma unroll
-        for (int j = 0; j < QD; ++j) {
-            const int p = p0 + j;
-            if (2 * p > kmax)
-                break;
-            Slot &X = S[j];
-            Slot &Y = S[(j + 1) % QD];   // period p + 1
-            const int cb = (p - q >= 1 && p - q <= m) ? X.cb : 4;
-            // even step kappa = 2p: bS = B(2p + 1, 2q - 1), lane q - 1's odd cell
-            {
-                const double bI = (bve && 2 * p <= K - 1) ? X.be : -RF_INF;
-                const double bo = (bvo && 2 * p + 1 <= K - 1) ? X.bo : -RF_INF;
-                const double bS = dpp_f64<L1>(bo);
-                step(std::integral_constant<int, 0>{}, p, cb, bI, bS);
-                // odd step kappa = 2p + 1: this lane's row advances; bS = B(2p + 2, 2q)
-                const int ii = q + p + 1 - c;
-                rsb = ii >= 1 ? X.sb : 4;
-                rmt = X.mt;
-                rmm = X.mm;
-                ris = X.is;
-                rds = X.ds;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    sub[k] = rsb == k ? rmt : rmm;
-                const double bS1 = (bve && 2 * p + 2 <= K - 1) ? Y.be : -RF_INF;
-                step(std::integral_constant<int, 1>{}, p, cb, bo, bS1);
-                emit(p, false);
-            }
-            // the chains move up one lane with their columns; lane 0 starts a fresh one
-            shift();
-            load(p + QD, X);
-        }
-    }
-}
-
 __device__ __forceinline__ void wg_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2761,12 +2430,6 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
 #ifndef SEGL_MASKED_MIN
 #define SEGL_MASKED_MIN 20
 #endif
-// a read's last segment with all its rows in the first 16 diagonals loads
-// half lines (64 B per kappa row): bit-exact but measured slower (c5 scoring
-// +0.6-0.9 ms, profiles/r04g_ab_c5.json); off
-#ifndef SEGL_HALF16
-#define SEGL_HALF16 0
-#endif
 #define SEGL_FENCE() __builtin_amdgcn_sched_barrier(0)
 // A kappa row's piece of a segment is one 128-B line.  (Half-line segments
 // of 16 diagonals -- 55 % of the LDS, two waves per SIMD -- were bit-exact but
@@ -2894,20 +2557,12 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
     auto load_seg = [&](SegSet &X, const RG &g, int D, bool first) {
         const int kb = D + 2 * a0, eh = D >> 1;
         if ((g.P & 15) == 0) {
-            // a read's last segment whose rows (chain rows and the peel row,
-            // up to dhi) all lie in its first 16 diagonals reads half lines
-            // (round 4): the lanes of the upper 16 leave their registers as
-            // they are -- those LDS rows are never read (generic steps stop
-            // at dhi, the masked steps overwrite them with -Inf)
-            const bool lo16 = SEGL_HALF16 && D + 16 > g.dhi;
 #pragma unroll
             for (int j = 0; j < NUA; ++j) {
                 const int kap = min(kb + r8 + RPI * j, g.K - 1);
                 const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
-                if (!lo16 || cc8 < 4) {
-                    X.ra[j] = *(const dvec2 *)(g.gA + o);
-                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
-                }
+                X.ra[j] = *(const dvec2 *)(g.gA + o);
+                X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
             }
         }
         if (first && D > 0) {
@@ -3254,546 +2909,6 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
 #pragma unroll
         for (int k = 0; k < 5; ++k)
             dst[k] = qnan;
-    }
-}
-
-// ---------------------------------------------------------------------
-// k_score_segw: k_score_segl over 128-column work items (round 4, default)
-//
-// A segment of k_score_segl's 64-column item reads 160 kappa rows for 128
-// rows' worth of cells: its first and last 32 rows are shared with the
-// neighbouring items (1.25x the algorithmic bytes, PMC 1.23-1.27x fetched).
-// Here one wave owns 128 columns [a0, a0 + 128) and scores each segment in
-// two halves of 64 columns, one after the other, through the same 39 KB LDS
-// slice: half 0 loads kappa rows [kb, kb + 160), half 1 needs
-// [kb + 128, kb + 288), whose first 32 rows are half 0's last 32 -- they
-// stay in the prefetch registers (rows j in [NUA - 4, NUA) move to j in
-// [0, 4)) and only 128 rows are loaded.  288 rows per 256 rows of cells:
-// 1.125x.  Each lane carries the chain state of two columns (a0 + tid and
-// a0 + 64 + tid); LDS row 0 (diagonal D - 1) of each half is the half's own
-// previous segment, kept in registers while the other half uses the slice.
-// Same chains, operands, FP64 order and fold as k_score_segl: identical
-// results.  SPLIT selects the per-read partial output (k_reduce folds) at
-// compile time, so the fused kernel carries no partial-write code and the
-// split kernel no running totals.
-// ---------------------------------------------------------------------
-template <int SEGS, bool SPLIT>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
-k_score_segw(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ groups,
-             const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
-             const double *__restrict__ tabs, const double *__restrict__ bands,
-             double *__restrict__ dense, double *__restrict__ split, int diag_mode, int rchunk)
-{
-    using Gm = SeglGeo<SEGS>;
-    constexpr int S = Gm::S, LS = Gm::LS, NUA = Gm::NUA, NUG = Gm::NUG, NT = Gm::NT;
-    constexpr int CPR = Gm::CPR, RPI = Gm::RPI, NC = Gm::NC;
-    constexpr int NCAR = S / RPI;   // prefetch rows carried from half 0 to half 1
-    static_assert(NUA * RPI == 128 + S && NCAR * RPI == S, "segment geometry");
-
-    constexpr int SL = (Gm::NRW * LS + 1) & ~1;   // doubles per band slice (16-B multiple)
-    __shared__ __attribute__((aligned(16))) double sA[SL];
-    __shared__ __attribute__((aligned(16))) double sB[SL];
-    __shared__ __attribute__((aligned(16))) dvec2 sT0[NT], sT1[NT], sT2[NT];
-    const int nx = gridDim.x;
-    const int lin = blockIdx.x + nx * blockIdx.y, ncell = nx * gridDim.y;
-    const int xq = ncell >> 3, xr = ncell & 7, x = lin & 7;
-    const int cell = x * xq + min(x, xr) + (lin >> 3);
-    const int bx = cell % nx, by = cell / nx;
-    const WorkItem wi = items[bx];
-    const ScoreGroup G = groups[wi.group];
-    const int m = G.m;
-    const int a0 = wi.p0;
-    const int tid = threadIdx.x;
-    int r0 = G.r0, r1 = G.r1;
-    if (SPLIT) {
-        r0 = G.r0 + by * rchunk;
-        if (r0 >= G.r1)
-            return;
-        r1 = min(r0 + rchunk, G.r1);
-    }
-    // the lane's two columns
-    struct Lane {
-        int a;
-        bool active, hasS, all_act;
-        double smask;
-    };
-    Lane hl[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        hl[h].a = a0 + 64 * h + tid;
-        hl[h].active = hl[h].a <= m;
-        hl[h].hasS = hl[h].a < m;
-        hl[h].smask = hl[h].hasS ? 0.0 : -RF_INF;
-        hl[h].all_act = __all(hl[h].active) && __all(hl[h].hasS);
-    }
-    // a wave with no column writes nothing; half 1 is skipped when it has none
-    if (!__any(hl[0].active))
-        return;
-    const int NH = __any(hl[1].active) ? 2 : 1;
-    // aligned-row loader lane roles: row r8 + RPI j, 16-B chunk cc8 of the row piece
-    const int r8 = tid / CPR, cc8 = tid % CPR, p8 = r8 & 1;
-    struct RG {
-        const double *gA;
-        const double *tm;
-        const uint8_t *sq;
-        int64_t dB;
-        int c, P, K, n;
-        int dfirst[2], dlast[2];   // this lane's chain rows (band diagonals) per half
-        bool peel[2];
-        int dlo, dhi;              // wave-wide over both halves
-        int dfmax[2], dlmin[2];    // wave-wide per half
-        bool uni[2];               // interior half: same [dfirst, dlast] and a peel in every lane
-    };
-    auto setup = [&](int r, RG &g) {
-        const ScoreRead R = reads[r];
-        g.c = R.c;
-        g.P = R.P;
-        g.K = R.K;
-        g.n = R.n;
-        g.gA = bands + R.A;
-        g.dB = R.B - R.A;
-        g.tm = tabs + R.tab;
-        g.sq = bases + R.sb;
-        int dlo = INT_MAX, dhi = -1;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int a = hl[h].a;
-            const int jn = min(a + 1, m);
-            const int i0 = max(0, jn - g.c);
-            const int i1 = min(jn + R.vb, g.n);
-            const int ilast = min(i1, a + R.vb);
-            g.dfirst[h] = i0 - a + g.c;
-            g.dlast[h] = ilast - a + g.c;
-            g.peel[h] = i1 > ilast;
-            const bool act = hl[h].active && h < NH;
-            dlo = min(dlo, act ? g.dfirst[h] : INT_MAX);
-            dhi = max(dhi, act ? g.dlast[h] + (g.peel[h] ? 1 : 0) : -1);
-            int dfmax = act ? g.dfirst[h] : INT_MAX, dlmin = act ? g.dlast[h] : -1;
-            for (int off = 32; off >= 1; off >>= 1) {
-                dfmax = max(dfmax, __shfl_xor(dfmax, off));
-                dlmin = min(dlmin, __shfl_xor(dlmin, off));
-            }
-            g.dfmax[h] = __builtin_amdgcn_readfirstlane(dfmax);
-            g.dlmin[h] = __builtin_amdgcn_readfirstlane(dlmin);
-            g.uni[h] = hl[h].all_act && h < NH &&
-                       __all(g.dfirst[h] == g.dfmax[h] && g.dlast[h] == g.dlmin[h] && g.peel[h]);
-        }
-        for (int off = 32; off >= 1; off >>= 1) {
-            dlo = min(dlo, __shfl_xor(dlo, off));
-            dhi = max(dhi, __shfl_xor(dhi, off));
-        }
-        g.dlo = __builtin_amdgcn_readfirstlane(dlo);
-        g.dhi = __builtin_amdgcn_readfirstlane(dhi);
-    };
-    struct SegSet {
-        dvec2 ra[NUA], rb[NUA];
-        double tmt[2], tmm[2], tin[2], tdl[2];
-        int tsb[2];
-        double z0a, z0b, z1a, z1b;
-    };
-    // loads of half h of segment D of read g (registers only); half 1 takes
-    // its first NCAR row groups from half 0's last, already in X
-    auto load_seg = [&](SegSet &X, const RG &g, int D, int h, bool first) {
-        const int a0h = a0 + 64 * h;
-        const int kb = D + 2 * a0h, eh = D >> 1;
-        if ((g.P & 15) == 0) {
-            if (h == 0) {
-#pragma unroll
-                for (int j = 0; j < NUA; ++j) {
-                    const int kap = min(kb + r8 + RPI * j, g.K - 1);
-                    const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
-                    X.ra[j] = *(const dvec2 *)(g.gA + o);
-                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < NCAR; ++j) {
-                    X.ra[j] = X.ra[j + NUA - NCAR];
-                    X.rb[j] = X.rb[j + NUA - NCAR];
-                }
-#pragma unroll
-                for (int j = NCAR; j < NUA; ++j) {
-                    const int kap = min(kb + r8 + RPI * j, g.K - 1);
-                    const int64_t o = (int64_t)kap * g.P + eh + 2 * cc8;
-                    X.ra[j] = *(const dvec2 *)(g.gA + o);
-                    X.rb[j] = *(const dvec2 *)(g.gA + g.dB + o);
-                }
-            }
-        }
-        if (first && D > 0) {
-            // diagonal D-1 of columns a0h .. a0h+64 (the previous segment's last row)
-            const int kap = min(D - 1 + 2 * (a0h + tid), g.K - 1);
-            const int64_t o = (int64_t)kap * g.P + ((D - 1) >> 1);
-            X.z0a = g.gA[o];
-            X.z0b = g.gA[g.dB + o];
-            if (tid == 0) {
-                const int kap1 = min(D - 1 + 2 * (a0h + 64), g.K - 1);
-                const int64_t o1 = (int64_t)kap1 * g.P + ((D - 1) >> 1);
-                X.z1a = g.gA[o1];
-                X.z1b = g.gA[g.dB + o1];
-            }
-        }
-        const int ib = a0h - g.c + D;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = min(max(ib + tid + 64 * u, 0), g.n);
-            const int ks = max(i - 1, 0);
-            X.tsb[u] = g.sq[ks];   // read row 0 (the gap) is selected at the store
-            X.tmt[u] = g.tm[ks];
-            X.tmm[u] = g.tm[g.n + ks];
-            X.tin[u] = g.tm[2 * (size_t)g.n + ks];
-            X.tdl[u] = g.tm[3 * (size_t)g.n + i];
-        }
-    };
-    auto store_seg = [&](const SegSet &X, const RG &g, int D, int h) {
-        const int a0h = a0 + 64 * h;
-        if ((g.P & 15) == 0) {
-            // an interior half's last segment: rows past the peel row read -Inf
-            // (k_score_segl's store_seg)
-            const bool un = h ? g.uni[1] : g.uni[0];
-            const int dl = h ? g.dlmin[1] : g.dlmin[0];
-            const int dm = (un && D > 0 && dl + 1 < D + S && dl + 1 - D >= SEGL_MASKED_MIN) ? dl + 1 - D : INT_MAX;
-#pragma unroll
-            for (int j = 0; j < NUA; ++j) {
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int ddl = 4 * cc8 + 2 * hh + p8;      // d - D
-                    const int col = (r8 + RPI * j - ddl) >> 1;  // a - a0h
-                    const double v = hh ? X.ra[j].y : X.ra[j].x, w = hh ? X.rb[j].y : X.rb[j].x;
-                    const int l = (ddl + 1) * LS + col;
-                    if ((j * RPI >= S && (j + 1) * RPI <= 128) || (col >= 0 && col <= 64)) {
-                        sA[l] = v;
-                        sB[l] = w;
-                    }
-                }
-            }
-            if (dm != INT_MAX) {
-                for (int e = tid; e < (S - dm) * LS; e += 64) {
-                    const int l = (dm + 1) * LS + e;
-                    sA[l] = -RF_INF;
-                    sB[l] = -RF_INF;
-                }
-            }
-        } else {
-            // odd-stride rows: NC pair-aligned chunks per row, loaded here
-            const int kb = D + 2 * a0h, eh = D >> 1;
-#pragma unroll 1
-            for (int j0 = 0; j0 < NUG; j0 += 4) {
-                dvec2 ga[4], gb[4];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int t = min(tid + 64 * (j0 + jj), Gm::NROW * NC - 1);
-                    const int rr = t / NC, cc = t - NC * rr;
-                    const int kap = min(kb + rr, g.K - 1);
-                    const int o = ((kap * g.P + eh) & ~1) + 2 * cc;
-                    ga[jj] = *(const dvec2 *)(g.gA + o);
-                    gb[jj] = *(const dvec2 *)(g.gA + g.dB + o);
-                }
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int t = tid + 64 * (j0 + jj);
-                    const int rr = t / NC, cc = t - NC * rr;
-                    const int sh = (kb + rr + eh) & 1;   // P odd
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const int xl = 2 * cc + hh - sh;
-                        const int ddl = 2 * xl + (rr & 1);
-                        const int col = (rr - ddl) >> 1;
-                        if (t < Gm::NROW * NC && xl >= 0 && xl < S / 2 && col >= 0 && col <= 64) {
-                            const int l = (ddl + 1) * LS + col;
-                            sA[l] = hh ? ga[jj].y : ga[jj].x;
-                            sB[l] = hh ? gb[jj].y : gb[jj].x;
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0);
-        }
-        const int ib = a0h - g.c + D;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int t = tid + 64 * u;
-            if (t < NT) {
-                const int sb = ib + t >= 1 ? X.tsb[u] : 4;
-                const double mt = X.tmt[u], mm = X.tmm[u];
-                sT0[t] = dvec2{sb == 0 ? mt : mm, sb == 1 ? mt : mm};
-                sT1[t] = dvec2{sb == 2 ? mt : mm, sb == 3 ? mt : mm};
-                sT2[t] = dvec2{X.tin[u], X.tdl[u]};
-            }
-        }
-    };
-    const bool do_load = !(diag_mode & 4);
-    double prev[2][4], accI[2][4], accS[2][4], dd[2];
-    double tI[2][4], tS[2][4], tD[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        dd[h] = -RF_INF;
-        tD[h] = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            prev[h][k] = accI[h][k] = accS[h][k] = -RF_INF;
-            tI[h][k] = tS[h][k] = 0.0;
-        }
-    }
-    // the chains of half H of segment D of read g (operands from LDS)
-    // The chains of the unit's half always run on state slot 0: the halves'
-    // states are swapped after every unit of a two-half item (unit), so the
-    // unrolled body exists once (instruction cache).
-    auto chains = [&](int h, const RG &g, int D) {
-        const Lane L = h ? hl[1] : hl[0];
-        const int a = L.a;
-        const int c = g.c, dfirst = h ? g.dfirst[1] : g.dfirst[0], dlast = h ? g.dlast[1] : g.dlast[0];
-        const int dfmax = h ? g.dfmax[1] : g.dfmax[0], dlmin = h ? g.dlmin[1] : g.dlmin[0];
-        const bool peel = h ? g.peel[1] : g.peel[0];
-        const bool uni = h ? g.uni[1] : g.uni[0];
-        double(&pv)[4] = prev[0];
-        double(&aI)[4] = accI[0];
-        double(&aS)[4] = accS[0];
-        double &ddh = dd[0];
-        if (L.active && !(diag_mode & 2)) {
-            const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
-            const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];
-            double aprev = (lo <= hi && lo >= 1 && a - c + lo >= 1) ? a0v : -RF_INF;
-            const double *pA = sA + LS + tid;
-            const double *pB = sB + LS + tid;
-            const double *pS = sB + tid + 1;
-            const dvec2 *q0 = sT0 + tid, *q1 = sT1 + tid, *q2 = sT2 + tid;
-            struct Ops {
-                double ac, bI, bs;
-                dvec2 u0, u1, u2;
-            };
-            auto ld = [&](int s) {
-                Ops o;
-                o.ac = pA[s * LS];
-                o.bI = pB[s * LS];
-                o.bs = pS[s * LS];
-                o.u0 = q0[s];
-                o.u1 = q1[s];
-                o.u2 = q2[s];
-                return o;
-            };
-            auto stp = [&](const Ops &o, auto alls) {
-                const double bS = ((decltype(alls)::value || L.hasS) ? o.bs : o.bI) + L.smask;
-                const double sub[4] = {o.u0.x, o.u0.y, o.u1.x, o.u1.y};
-                const double dl = o.ac + o.u2.y;
-                const double dsum = o.ac + bS;
-                chain_row(aprev, sub, o.u2.x, dl, o.bI, bS, pv, aI, aS);
-                ddh = vmax(ddh, dsum);
-                aprev = o.ac;
-            };
-            // one copy of the unrolled body per half (k_score_segl's run)
-            auto run = [&](bool skip0) {
-                Ops cur = ld(0);
-#pragma unroll SEGL_UNROLL
-                for (int s = 0; s < S; ++s) {
-                    const Ops nxt = ld(s + 1 < S ? s + 1 : s);
-                    SEGL_FENCE();
-                    if (s == 0 && skip0)
-                        aprev = a - c >= 0 ? cur.ac : -RF_INF;
-                    else
-                        stp(cur, std::true_type{});
-                    cur = nxt;
-                }
-            };
-            const bool full = L.all_act && dfmax <= D && dlmin >= D + S - 1;
-            const bool first_u = uni && D == 0 && dfirst == 1 && dlast + 1 >= S && (g.P & 15) == 0;
-            const bool last_u = uni && D > 0 && dlast + 1 < D + S && dlast + 1 - D >= SEGL_MASKED_MIN &&
-                                (g.P & 15) == 0;
-            if (full || first_u || last_u) {
-                run(__builtin_amdgcn_readfirstlane((int)first_u) != 0);
-            } else {
-                const int slo = max(lo - D, 0), shi = hi - D;
-                if (slo <= shi) {
-                    Ops cur = ld(slo);
-                    for (int s = slo; s <= shi; ++s) {
-                        const Ops nxt = ld(s < shi ? s + 1 : s);
-                        SEGL_FENCE();
-                        stp(cur, std::false_type{});
-                        cur = nxt;
-                    }
-                }
-                const int dp = dlast + 1;
-                if (peel && dp >= D && dp < D + S) {
-                    const int sp = dp - D;
-                    const double ap = sA[sp * LS + tid];
-                    const double bSr = sB[sp * LS + tid + 1];
-                    const dvec2 u0 = sT0[tid + sp], u1 = sT1[tid + sp], u2 = sT2[tid + sp];
-                    const double sub[4] = {u0.x, u0.y, u1.x, u1.y};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        aS[k] = vmax(aS[k], vmax(ap + sub[k], pv[k] + u2.x) + bSr);
-                }
-            }
-        }
-    };
-    // read r's totals (after its last segment) and fresh chain state.  Called
-    // after the read's last unit, before the swap: half NH-1 is in slot 0, and
-    // with two halves half 0 is in slot 1 -- swap first so that slot h holds
-    // half h
-    auto swap_slots = [&]() {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const double p0 = prev[0][k], i0 = accI[0][k], s0 = accS[0][k];
-            prev[0][k] = prev[1][k];
-            accI[0][k] = accI[1][k];
-            accS[0][k] = accS[1][k];
-            prev[1][k] = p0;
-            accI[1][k] = i0;
-            accS[1][k] = s0;
-        }
-        const double d0 = dd[0];
-        dd[0] = dd[1];
-        dd[1] = d0;
-    };
-    auto finish = [&](int r) {
-        const double qnan = __builtin_nan("");
-        if (NH == 2)
-            swap_slots();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (h < NH && hl[h].active) {
-                const int a = hl[h].a;
-                if (SPLIT) {
-                    double *dst = split + G.split_off + ((size_t)(r - G.r0) * (m + 1) + a) * 9;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        dst[5 + k] = accI[h][k] == -RF_INF ? qnan : accI[h][k];
-                    if (a < m) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            dst[9 + k] = accS[h][k] == -RF_INF ? qnan : accS[h][k];
-                        dst[13] = dd[h];
-                    }
-                    if (a == 0) {
-#pragma unroll
-                        for (int k = 0; k < 5; ++k)
-                            dst[k] = qnan;
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        tI[h][k] += accI[h][k] == -RF_INF ? qnan : accI[h][k];
-                        tS[h][k] += accS[h][k] == -RF_INF ? qnan : accS[h][k];
-                    }
-                    tD[h] += dd[h];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                prev[h][k] = accI[h][k] = accS[h][k] = -RF_INF;
-            dd[h] = -RF_INF;
-        }
-    };
-    // units (read, segment, half) as one stream: the register prefetch
-    // always holds the next unit
-    struct Pos {
-        int r, D, h;
-        RG g;
-    };
-    auto first_of = [&](const RG &g) { return g.dlo & ~(S - 1); };
-    auto adv = [&](Pos &p) {
-        if (p.h + 1 < NH) {
-            ++p.h;
-        } else {
-            p.h = 0;
-            if (p.D + S > p.g.dhi) {
-                ++p.r;
-                if (p.r < r1) {
-                    setup(p.r, p.g);
-                    p.D = first_of(p.g);
-                }
-            } else {
-                p.D += S;
-            }
-        }
-    };
-    // LDS row S of each half's last scored segment (its next segment's row 0)
-    double svA[2] = {0.0, 0.0}, svB[2] = {0.0, 0.0}, svA6[2] = {0.0, 0.0}, svB6[2] = {0.0, 0.0};
-    int held = -1;   // half whose segment the LDS slice holds
-    auto unit = [&](SegSet &X, Pos &cur) {
-        const int D = cur.D, h = cur.h;
-        const bool first = D == first_of(cur.g);
-        wave_sync();   // previous unit's chains are done with LDS
-        if (held >= 0) {
-            const double va = sA[S * LS + tid], vb = sB[S * LS + tid];
-            const double va6 = sA[S * LS + 64], vb6 = sB[S * LS + 64];
-            if (held == 0) {
-                svA[0] = va; svB[0] = vb; svA6[0] = va6; svB6[0] = vb6;
-            } else {
-                svA[1] = va; svB[1] = vb; svA6[1] = va6; svB6[1] = vb6;
-            }
-        }
-        // LDS row 0 = diagonal D-1: prefetched for a read's first segment, else
-        // the half's previous segment's row S
-        if (first) {
-            if (D > 0) {
-                sA[tid] = X.z0a;
-                sB[tid] = X.z0b;
-                if (tid == 0) {
-                    sA[64] = X.z1a;
-                    sB[64] = X.z1b;
-                }
-            }
-        } else {
-            const double va = h ? svA[1] : svA[0], vb = h ? svB[1] : svB[0];
-            const double va6 = h ? svA6[1] : svA6[0], vb6 = h ? svB6[1] : svB6[0];
-            sA[tid] = va;
-            sB[tid] = vb;
-            if (tid == 0) {
-                sA[64] = va6;
-                sB[64] = vb6;
-            }
-        }
-        store_seg(X, cur.g, D, h);
-        wave_sync();
-        held = h;
-        Pos ahead = cur;
-        if (ahead.r < r1)
-            adv(ahead);
-        if (do_load && ahead.r < r1)
-            load_seg(X, ahead.g, ahead.D, ahead.h, ahead.D == first_of(ahead.g));
-        chains(h, cur.g, D);
-        if (h + 1 == NH && D + S > cur.g.dhi)
-            finish(cur.r);            // leaves slot h = half h, fresh: the next unit is half 0
-        else if (NH == 2)
-            swap_slots();             // slot 0 = the next unit's half
-        cur = ahead;
-    };
-    Pos cur;
-    cur.r = r0;
-    cur.h = 0;
-    if (r0 < r1) {
-        setup(r0, cur.g);
-        cur.D = first_of(cur.g);
-    }
-    SegSet X0;
-    if (r0 < r1 && do_load)
-        load_seg(X0, cur.g, cur.D, 0, true);
-    while (cur.r < r1)
-        unit(X0, cur);
-    if (SPLIT)
-        return;
-    const double qnan = __builtin_nan("");
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (h < NH && hl[h].active) {
-            const int a = hl[h].a;
-            double *dst = dense + G.dense_off + (size_t)a * 9;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                dst[5 + k] = tI[h][k];
-            if (a < m) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    dst[9 + k] = tS[h][k];
-                dst[13] = tD[h];
-            }
-            if (a == 0) {
-#pragma unroll
-                for (int k = 0; k < 5; ++k)
-                    dst[k] = qnan;
-            }
-        }
     }
 }
 
@@ -4178,13 +3293,6 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 // the three others (the same strict-> order), and a codon move leaves the box
 // (|u| = 3), so the next box starts at the cell it reaches.
 // ---------------------------------------------------------------------
-// 1: moves collected in the wave's lanes and stored 64 at a time -- bit-exact
-// but slower (backtrace 19.6 -> 22.4 ms, alignment proposals 36.7 -> 40.3 ms
-// per 512 e2e clusters, profiles/r04z_btw_mvbuf.txt: the select joins the
-// walk's per-move dependency chain, which bounds it, not the stores); off
-#ifndef BTW_MVBUF
-#define BTW_MVBUF 0
-#endif
 // 1 (default, round 4): the box's walk ranked in parallel (pointer
 // doubling over the 63 cells' successors) instead of one readlane step per
 // move: backtrace 19.8 -> 8.0 ms, alignment proposals 36.9 -> 12.9 ms per
@@ -4240,14 +3348,6 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     int klo = -1, e0 = 0;                              // A window: rows [klo, klo + W), elements [e0, e0 + wd)
     int q0 = -1, r0 = -1;                              // table rows [q0, q0 + BTW_T), bases [r0, r0 + BTW_T)
     int failed = 0;
-    // BTW_MVBUF: moves collected in the wave's lanes (move cnt in lane
-    // cnt % 64) and written 64 at a time (measured slower, off)
-    int mvbuf = 0;
-    auto flush_moves = [&](int upto) {   // moves [upto & ~63, upto) -> out (forward order ends at n+m-1)
-        const int b0 = (upto - 1) & ~63;
-        if (BTW_MVBUF && lane < upto - b0)
-            out[n + m - 1 - b0 - lane] = (int8_t)mvbuf;
-    };
     while ((ii > 0 || jj > 0) && !failed) {
         // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
@@ -4488,14 +3588,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             const int sb = pk >> 4;
             const bool mism = pk & 8;
-            if (BTW_MVBUF) {
-                mvbuf = lane == (cnt & 63) ? mv : mvbuf;
-                if ((cnt & 63) == 63)
-                    flush_moves(cnt + 1);
-            }
             if (lane == 0) {
-                if (!BTW_MVBUF)
-                    out[n + m - 1 - cnt] = (int8_t)mv;
+                out[n + m - 1 - cnt] = (int8_t)mv;
                 if (mk) {
                     // the forward step of this move ends at (ii, jj) (k_aln_props)
                     if (mv == 1 && mism)
@@ -4527,8 +3621,6 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         }
 #endif
     }
-    if (cnt & 63)
-        flush_moves(cnt);
     if (lane == 0) {
         nmoves[T.idx] = cnt;
         nerr[T.idx] = errs;
@@ -4898,12 +3990,11 @@ struct Slot {
 // Choice of dense scorer for one launch.
 struct ScorePick {
     bool lean = false;
-    bool seg = false;   // k_score_segl / k_score_segw: wide bands (window too large for LDS), finite tables
-    int segq = 64;      // seg: columns per work item (64: k_score_segl, 128: k_score_segw)
+    bool seg = false;   // k_score_segl: wide bands (window too large for LDS), finite tables
     int lds = 0;    // lean: doubles of dynamic LDS; general: doubles per staged band
     int q() const { return 256; }   // k_score_ws chain columns per work item
     // columns per work item of the chosen scorer (k_score: 64)
-    int cols() const { return lean ? q() : seg ? segq : 64; }
+    int cols() const { return lean ? q() : 64; }
 };
 
 struct DevBuf {
@@ -5061,14 +4152,11 @@ struct Opts {
     int dp_np8_lean = 1;    // RF_OPT_DP_NP8_LEAN: lean k_dpr<8> path
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
-    int seg_cols = 64;      // RF_OPT_SEG_COLS: wide-band scorer columns per work item (64 segl, 128 segw:
-                            // measured slower at c5, round 4)
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
     int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
-    int score_fwd = 0;      // RF_OPT_SCORE_FWD: rf_score_dense fills A inside the scorer (k_fuse) when eligible
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
-                            // one 64-lane NP = 1 class (latency mode: the launch cannot fill the GPU)
+                            // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
     int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
     int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
@@ -5150,9 +4238,6 @@ struct rf_ctx {
         std::vector<ScoreGroup> groups;
         std::vector<ScoreRead> reads;
         std::vector<int64_t> gstart;
-        bool fwd = false;                 // RF_OPT_SCORE_FWD plan: k_fuse tasks (scratch[27])
-        std::vector<FuseTask> ftasks;     // the 16-lane class (H <= 31) first, then the 64-lane class
-        size_t nf16 = 0;
     } dplan;
 };
 
@@ -5402,11 +4487,9 @@ void load_env_opts(Opts &o)
     o.band_pad_h = env_int("RIFRAF_BAND_PAD", o.band_pad_h);
     o.dp_wide = env_int("RIFRAF_DP_WIDE", o.dp_wide);
     o.aln_sums_host = env_int("RIFRAF_ALN_SUMS_HOST", o.aln_sums_host);
-    o.seg_cols = env_int("RIFRAF_SEG_COLS", o.seg_cols);
     o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
-    o.score_fwd = env_int("RIFRAF_SCORE_FWD", o.score_fwd);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -5435,7 +4518,6 @@ ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool a
     // wide bands: the row-segment scorer (same chains, H-independent LDS)
     if (all_finite && !force_general && !reads.empty()) {
         p.seg = true;
-        p.segq = o.seg_cols == 128 ? 128 : 64;
         return p;
     }
     p.lds = score_lds_elems(reads);
@@ -5477,15 +4559,8 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
             rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
-        if (pk.segq == 64)
-            hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases,
-                               d_tabs, d_bands, dense, split, sm, rchunk);
-        else if (split)
-            hipLaunchKernelGGL((k_score_segw<32, true>), grid, dim3(64), 0, ctx->stream, items, groups, reads,
-                               d_bases, d_tabs, d_bands, dense, split, sm, rchunk);
-        else
-            hipLaunchKernelGGL((k_score_segw<32, false>), grid, dim3(64), 0, ctx->stream, items, groups, reads,
-                               d_bases, d_tabs, d_bands, dense, split, sm, rchunk);
+        hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
+                           d_bands, dense, split, sm, rchunk);
     } else if (!pk.lean) {
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
@@ -5611,12 +4686,10 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_BAND_PAD: return &o.band_pad_h;
     case RF_OPT_DP_WIDE: return &o.dp_wide;
     case RF_OPT_ALN_SUMS_HOST: return &o.aln_sums_host;
-    case RF_OPT_SEG_COLS: return &o.seg_cols;
     case RF_OPT_ALN_MARKS_MIN: return &o.aln_marks_min;
     case RF_OPT_SYNC_BLOCK: return &o.sync_block;
     case RF_OPT_DP_NL64: return &o.dp_nl64;
     case RF_OPT_DP_LAT: return &o.dp_lat;
-    case RF_OPT_SCORE_FWD: return &o.score_fwd;
     default: return nullptr;
     }
 }
@@ -6369,7 +5442,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 // (the 16-lane NP = 4 / 8 kernels need > 256 registers: one wave
                 // per SIMD)
                 const int wide = npi == 3 && t.H <= 255 ? 0 : (npi == 2 ? 1 : -1);
-                if (lean && latmode && t.H <= 127) {
+                if (lean && latmode && t.H <= 127 && dpx_fits(t)) {
                     cl.push_back(t);
                 } else if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
@@ -6405,8 +5478,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         std::vector<DPTask> cx;
         if (cr[0][0].size() + cr[1][0].size() + cr[2][0].size() <= (size_t)std::max(ctx->opt.dp_nl64, 0)) {
             for (int a = 0; a <= 2; ++a) {
-                cx.insert(cx.end(), cr[a][0].begin(), cr[a][0].end());
-                cr[a][0].clear();
+                std::vector<DPTask> keep;
+                for (const DPTask &t : cr[a][0])
+                    (dpx_fits(t) ? cx : keep).push_back(t);
+                cr[a][0].swap(keep);
             }
         }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
@@ -6571,13 +5646,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 34) {
             // few non-lean tasks (H <= 127): one latency-bound task per wave (k_dpx)
-            hipLaunchKernelGGL(k_dpx, dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out,
-                               ctx->d_err);
+            hipLaunchKernelGGL((k_dpx<true, true>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
+                               d_bands, d_out, ctx->d_err);
         } else if (L.kind == 35) {
-            // latency mode: lean tasks of H <= 127, one 64-lane NP = 1 task per wave
-            hipLaunchKernelGGL((k_dpr<1, true, dpl_pmax(1, 64), 64>), dim3(n), dim3(64),
-                               (size_t)dpl_task_bytes(1, dpl_pmax(1, 64), 64), st, d_tasks + L.at, n, d_bases, d_tabs,
-                               d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
+            // latency mode: lean tasks of H <= 127, one latency-bound task per wave
+            hipLaunchKernelGGL((k_dpx<false, false>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
+                               d_bands, d_out, ctx->d_err);
         } else if (L.kind >= 32) {
             // task-width classes, both NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
             // (H <= 127)
@@ -7034,7 +6108,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                       (const WorkItem *)ctx->scratch[0].p, (const ScoreGroup *)ctx->scratch[1].p,
                       (const ScoreRead *)ctx->scratch[2].p, d_dense, d_split);
         if (split && dense_total > 0)
-            hipLaunchKernelGGL(k_reduce<false>, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
+            hipLaunchKernelGGL(k_reduce, dim3((unsigned)((dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[1].p, ngroups, d_gstart,
                                dense_total, d_split, d_dense);
     }
@@ -7101,20 +6175,7 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
     (void)hipSetDevice(ctx->device);
     const int32_t nslots = ngroups > 0 ? slot_off[ngroups] : 0;
     auto &P = ctx->dplan;
-    // RF_OPT_SCORE_FWD: every read lean (finite tables), H <= 127, B computed
-    // -> k_fuse fills A in the scorer (A unused)
-    bool fwd = ctx->opt.score_fwd != 0;
-    for (int32_t k = 0; fwd && k < nslots; ++k) {
-        const int32_t sl = slots[k];
-        if (sl < 0 || sl >= (int32_t)ctx->slots.size()) {
-            fwd = false;
-            break;
-        }
-        const Band &B = ctx->slots[sl].b;
-        fwd = B.valid && B.H <= 127 && (B.flags & (RF_SKEW | RF_TRIM)) == 0 && B.seq >= 0 &&
-              ctx->seqs[B.seq].finite;
-    }
-    const bool same = P.valid && P.fwd == fwd && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
+    const bool same = P.valid && P.gen == ctx->layout_gen && P.ngroups == ngroups && P.opt_gen == ctx->opt_gen &&
                       P.slots.size() == (size_t)nslots &&
                       !std::memcmp(P.slot_off.data(), slot_off, sizeof(int32_t) * (ngroups + 1)) &&
                       (nslots == 0 || !std::memcmp(P.slots.data(), slots, sizeof(int32_t) * nslots));
@@ -7130,18 +6191,6 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             if (sl < 0 || sl >= (int32_t)ctx->slots.size())
                 return fail(ctx, RF_ERR_ARG, "rf_score_dense: unknown slot");
             const Slot &S = ctx->slots[sl];
-            if (fwd) {
-                // A is filled in the scorer: only B must be current
-                if (ctx->tpls[S.b.tpl].version != S.b.tplver)
-                    return fail(ctx, RF_ERR_STATE, "rf_score_dense: template changed since the bands were computed");
-                const SeqObj &Q = ctx->seqs[S.b.seq];
-                if (Q.ncins > 0 || Q.ncdel > 0)
-                    return fail(ctx, RF_ERR_ARG, "error model cannot allow codon indels");
-                if (tpl >= 0 && S.b.tpl != tpl)
-                    return fail(ctx, RF_ERR_ARG, "rf_score_dense: batch slots use different templates");
-                tpl = S.b.tpl;
-                continue;
-            }
             if (!S.a.valid || !S.b.valid || S.a.seq != S.b.seq || S.a.tpl != S.b.tpl ||
                 S.a.bw != S.b.bw || S.a.tplver != S.b.tplver || S.a.m != S.b.m)
                 return fail(ctx, RF_ERR_STATE, "rf_score_dense: A and B bands were computed for different alignments");
@@ -7175,11 +6224,11 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             G.r0 = (int32_t)reads.size();
             for (int32_t k = slot_off[g]; k < slot_off[g + 1]; ++k) {
                 const Band &B = ctx->slots[slots[k]].b;
-                const Band &A = fwd ? B : ctx->slots[slots[k]].a;   // fwd: geometry from B, A unused
+                const Band &A = ctx->slots[slots[k]].a;
                 const SeqObj &S = ctx->seqs[A.seq];
                 all_finite = all_finite && S.finite;
                 ScoreRead R{};
-                R.A = fwd ? 0 : A.r.off / 8;
+                R.A = A.r.off / 8;
                 R.B = B.r.off / 8;
                 R.sb = S.bases.off;
                 R.tab = S.tabs.off / 8;
@@ -7217,35 +6266,6 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         if (int e = upload(ctx, ctx->scratch[12], groups)) return e;
         if (int e = upload(ctx, ctx->scratch[13], reads)) return e;
         if (int e = upload(ctx, ctx->scratch[14], gstart)) return e;
-        P.ftasks.clear();
-        P.nf16 = 0;
-        if (fwd) {
-            P.ftasks.reserve(reads.size());
-            for (int cls = 0; cls < 2; ++cls)   // 16-lane tasks (H <= 31), then 64-lane tasks
-            for (const ScoreGroup &G : groups)
-                for (int32_t r = G.r0; r < G.r1; ++r) {
-                    if ((reads[r].H <= 31) != (cls == 0))
-                        continue;
-                    const ScoreRead &R = reads[r];
-                    FuseTask t{};
-                    t.B = R.B;
-                    t.sb = R.sb;
-                    t.tab = R.tab;
-                    t.tb = G.tb;
-                    t.out = G.split_off + (int64_t)(r - G.r0) * (G.m + 1) * 9;
-                    t.n = R.n;
-                    t.m = G.m;
-                    t.H = R.H;
-                    t.c = R.c;
-                    t.vb = R.vb;
-                    t.P = R.P;
-                    t.K = R.K;
-                    P.ftasks.push_back(t);
-                    P.nf16 += cls == 0;
-                }
-            if (int e = upload(ctx, ctx->scratch[27], P.ftasks)) return e;
-        }
-        P.fwd = fwd;
         P.valid = true;
         P.gen = ctx->layout_gen;
         P.ngroups = ngroups;
@@ -7262,8 +6282,6 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
         split = false;
     else if (ctx->opt.score_mode == 2)
         split = true;
-    if (fwd)
-        split = true;   // k_fuse writes per-read partials
     if (int e = ensure_buf(ctx, ctx->scratch[15], sizeof(double) * std::max<int64_t>(P.dense_total, 1)))
         return e;
     if (split)
@@ -7271,37 +6289,13 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
             return e;
     double *d_dense = (double *)ctx->scratch[15].p;
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    if (fwd && !P.ftasks.empty()) {
-        const FuseTask *ft = (const FuseTask *)ctx->scratch[27].p;
-        const size_t n64 = P.ftasks.size() - P.nf16;
-        // the 64-lane class on a side stream, concurrent with the 16-lane class
-        if (n64) {
-            HIPCHK(ctx, hipEventRecord(ctx->fork, ctx->stream));
-            HIPCHK(ctx, hipStreamWaitEvent(ctx->side[0], ctx->fork, 0));
-        }
-        if (n64)
-            hipLaunchKernelGGL(k_fuse<64>, dim3((unsigned)n64), dim3(64), 0, ctx->side[0], ft + P.nf16, (int)n64,
-                               (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
-                               (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
-        if (P.nf16)
-            hipLaunchKernelGGL(k_fuse<16>, dim3((unsigned)((P.nf16 + 3) / 4)), dim3(64), 0, ctx->stream, ft,
-                               (int)P.nf16, (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
-                               (const double *)ctx->band_arena.d, (double *)ctx->scratch[10].p);
-        if (n64) {
-            HIPCHK(ctx, hipEventRecord(ctx->join[0], ctx->side[0]));
-            HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->join[0], 0));
-        }
-        hipLaunchKernelGGL(k_reduce<true>, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
-                           ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
-                           (const int64_t *)ctx->scratch[14].p, P.dense_total,
-                           (const double *)ctx->scratch[10].p, d_dense);
-    } else if (P.nitems) {
+    if (P.nitems) {
         dim3 grid((unsigned)P.nitems, split ? (unsigned)P.max_reads : 1u);
         launch_scorer(ctx, P.pick, grid.x, grid.y, (const WorkItem *)ctx->scratch[11].p,
                       (const ScoreGroup *)ctx->scratch[12].p, (const ScoreRead *)ctx->scratch[13].p,
                       d_dense, split ? (double *)ctx->scratch[10].p : nullptr);
         if (split)
-            hipLaunchKernelGGL(k_reduce<false>, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
+            hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P.dense_total + 255) / 256)), dim3(256), 0,
                                ctx->stream, (const ScoreGroup *)ctx->scratch[12].p, ngroups,
                                (const int64_t *)ctx->scratch[14].p, P.dense_total,
                                (const double *)ctx->scratch[10].p, d_dense);

@@ -5,9 +5,8 @@ holding 1/E of the clusters, free-running K steps.  Whether the DP fill of
 one context overlaps another's scoring on the GPU (different limiters:
 the DP is issue/latency-bound at ~20 % VALU busy, the scorer LDS/VALU-bound).
 Prints one JSON line per E: wall ms per step (all contexts), GCUPS.
-SCORE_FWD=1: the fused-step prototype instead (rf_realign RF_BWD, then
-rf_score_dense with RF_OPT_SCORE_FWD: the VALU-bound k_fuse of one context
-beside the store-bound B fill of another)."""
+(Round 4 also ran the fused-step prototype k_fuse here, SCORE_FWD=1; it was
+removed in round 5, profiles/r04v_exp_overlap_fused.jsonl keeps the record.)"""
 import json
 import os
 import sys
@@ -42,10 +41,7 @@ def setup(clusters):
         at += len(rs)
     packed = pack_groups(groups)
 
-    fwd = os.environ.get("SCORE_FWD", "0") == "1"
-    if fwd:
-        eng.set_option("score_fwd", 1)
-    flags = RF_BWD if fwd else RF_FWD | RF_BWD
+    flags = RF_FWD | RF_BWD
 
     def step():
         eng.realign(slots, slots, tpl_of, bws, flags)
@@ -79,7 +75,7 @@ def main():
             t.join()
         wall = time.perf_counter() - t0
         cells = sum(c for _, _, c in ctx)
-        print(json.dumps({"engines": E, "score_fwd": os.environ.get("SCORE_FWD", "0") == "1", "clusters": nclu, "steps": steps, "ms_per_step": wall / steps * 1e3,
+        print(json.dumps({"engines": E, "clusters": nclu, "steps": steps, "ms_per_step": wall / steps * 1e3,
                           "gcups": cells * steps / wall / 1e9}), flush=True)
         for e, _, _ in ctx:
             e.close()

@@ -1,4 +1,4 @@
-"""bench.py's multi-rank path on CPU (gloo, world_size 2).
+"""bench.py's multi-rank path on CPU (gloo, world sizes 2 and 8).
 
 The benchmark shards clusters over ranks with no data-path collective; the
 only cross-rank step is the whole-job reduction (max time, summed units).
@@ -35,11 +35,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_aggregate_two_ranks():
+@pytest.mark.parametrize("world", [2, 8])
+def test_aggregate_ranks(world):
+    """Max-over-ranks time and summed units, at 2 ranks and at the 8 of a
+    node (the only world size north_star scores)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in procs]
@@ -47,8 +50,9 @@ def test_aggregate_two_ranks():
         p.join(60)
         assert p.exitcode == 0
     for _, el, units in got:
-        assert el == 2.0                       # slowest rank
-        assert units == [30.0, 6.0, 11.0]      # whole-job units
+        assert el == float(world)              # slowest rank
+        assert units == [10.0 * world * (world + 1) / 2, 3.0 * world,
+                         5.0 * world + world * (world - 1) / 2]   # whole-job units
 
 
 def _bench(args, env=None, timeout=300):
@@ -62,20 +66,22 @@ def _bench(args, env=None, timeout=300):
     return p, [json.loads(ln) for ln in lines]
 
 
-def test_bench_self_launches_ranks():
-    """`bench.py --gpus 2` with no launcher starts two ranks itself: one JSON
-    line (rank 0) whose reduction covers both ranks' shards."""
-    p, lines = _bench(["--gpus", "2", "--backend", "gloo", "--config", "c4", "--clusters", "2",
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_self_launches_ranks(world):
+    """`bench.py --gpus N` with no launcher starts N ranks itself: one JSON
+    line (rank 0) whose reduction covers every rank's shard (N = 8: the
+    driver's scaling run on one node, rehearsed with gloo)."""
+    p, lines = _bench(["--gpus", str(world), "--backend", "gloo", "--config", "c4", "--clusters", "2",
                        "--no-cpu", "--dry-run"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1
     # stdout carries the JSON line only (gloo's connection report goes to stderr)
     assert [ln for ln in p.stdout.splitlines() if ln.strip()] == [p.stdout.strip()]
     out = lines[0]
-    assert out["ranks"] == 2 and out["n_gpus"] == 2
-    assert out["reads_all_ranks"] == 2 * 2 * 50
+    assert out["ranks"] == world and out["n_gpus"] == world
+    assert out["reads_all_ranks"] == world * 2 * 50
     cells = sum(2 * bench.band_cells(len(r), len(t), r.bandwidth)
-                for rank in range(2)
+                for rank in range(world)
                 for t, rs in bench.make_workload(2, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, rank))
                 for r in rs)
     assert out["cells_per_step_all_ranks"] == cells

@@ -554,9 +554,6 @@ SCORER_CONFIGS = [
     ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segl (64 columns)
     ("seglodd", None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
     ("seglpad", None),   # k_score_segl with every band line-padded (band_pad 1)
-    ("seg64", None),     # the same three on 128-column items: k_score_segw (RF_OPT_SEG_COLS 128)
-    ("seglodd64", None),
-    ("seglpad64", None),
     (None, None),        # k_score_ws (the default for these shapes)
     (None, "8"),         # windows exceed the budget: sub-passes over fewer lanes
     (None, "12"),
@@ -569,13 +566,10 @@ SCORER_CONFIGS = [
 @pytest.mark.parametrize("kern,lds", SCORER_CONFIGS)
 @pytest.mark.parametrize("mode", ["fused", "split"])
 def test_score_dense_kernels(engine, opts, kern, lds, mode):
-    """The dense scorers (general, k_score_ws, k_score_segw, k_score_segl) over
-    ragged clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs
-    the oracle."""
+    """The dense scorers (general, k_score_ws, k_score_segl) over ragged
+    clusters: n << m, n >> m, wide bands, 1-read groups; bit-exact vs the
+    oracle."""
     pad = 64
-    if kern and kern.endswith("64"):
-        opts("seg_cols", 128)   # the "...64" variants: the non-default item width
-        kern = kern[:-2]
     if kern in ("seglodd", "seglpad"):
         pad = 0 if kern == "seglodd" else 1
         kern = "seg"
@@ -650,19 +644,14 @@ def test_score_lean_ineligible_tables(engine):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "general",
-                                  "segl64", "seglodd64", "seglmix64"])
+@pytest.mark.parametrize("kern", [None, "seglodd", "seglpad", "seglmix", "general"])
 def test_score_wide_bands(engine, opts, mode, kern):
     """Bands whose kappa-row window exceeds LDS (H ~ 90-260, reads longer and
     shorter than the template, plus a narrow read in the same launch): the
-    line-aligned row-segment scorers k_score_segl (default, 64-column items)
-    and k_score_segw (128-column items, the "...64" variants) on line-padded rows,
+    line-aligned row-segment scorer k_score_segl on line-padded rows,
     odd-stride rows and both in one launch, and the in-place k_score
     ("general"), are bit-exact against the oracle."""
     opts("band_pad", 64)
-    if kern and kern.endswith("64"):
-        opts("seg_cols", 128)   # the "...64" variants: the non-default item width
-        kern = None if kern == "segl64" else kern[:-2]
     if kern in (None, "seglmix"):
         opts("score_kernel", "auto")
     elif kern in ("seglodd", "seglpad"):
@@ -1016,10 +1005,10 @@ def test_set_sequences_staged_in_chunks(engine, opts, stage_kb):
 
 
 def test_removed_option_keys_rejected(engine):
-    """Scorer-variant keys removed in round 3 (include/rifraf_hip.h) are
-    refused with an error, not silently accepted."""
+    """Scorer-variant keys removed in rounds 3 and 5 (include/rifraf_hip.h)
+    are refused with an error, not silently accepted."""
     from rifraf_amd.engine import RifrafError
-    for key in (3, 5, 6, 7, 8, 14, 20):
+    for key in (3, 5, 6, 7, 8, 14, 20, 21, 25):
         assert engine.lib.rf_set_option(engine.ctx, key, 1) != 0
         assert "unknown option" in engine.lib.rf_last_error(engine.ctx).decode()
     with pytest.raises(KeyError):

@@ -1,5 +1,6 @@
 """Read-sharded rifraf() (rifraf_amd.sharded) on CPU with
-gloo: world sizes 2 and 3, every rank wrapping the oracle engine.
+gloo: world sizes 2, 3 and 8 (one node's GPUs), every rank wrapping the
+oracle engine.
 
 * whole rifraf() runs through ShardedEngine give the same consensus at every
   iteration, the same final score and the same quality estimates as one
@@ -153,10 +154,11 @@ def assert_same_run(a, b, qv_rtol=0.0):
             np.testing.assert_array_equal(a[k], b[k])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_config1_with_reference(world):
     """Reference-informed run (FRAME stage, codon scoring on the last rank's
-    reference slot) with quality scores: identical to one engine."""
+    reference slot) with quality scores: identical to one engine.  At world
+    8 the 3 reads leave five ranks without a read slot."""
     f = "input-reads-1.fastq"
     refmap = dict(line.split() for line in open(os.path.join(G1, "ref-map.tsv")) if line.strip())
     refid = refmap[f]
@@ -170,7 +172,7 @@ def _w_grown(rank, world, seed):
     return _grown(_sharded_factory, seed)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_batch_growth(world):
     """check_score! grows the batch from 3 reads towards all 12: the sharded
     run equals one engine bit for bit, and the grown batch's bands stay
@@ -217,7 +219,7 @@ def _w_dense(rank, world, seed):
     return e.score_dense(groups), tpls, reads
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_dense_exchange(world):
     import oracle
     got = _spawn(_w_dense, world, 17)
