@@ -169,6 +169,19 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq,
 int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
                            const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
                            double s_ins, double s_del);
+/* rf_set_sequences_codes plus the native driver's per-read setup values,
+ * computed on the device from the same staged codes (k_code_prep, round 5;
+ * bit-identical to rf_host_code_prep, which it replaces on the driver's
+ * path): est[k] = est_n_errors (Julia-order sum of p10_t[code],
+ * rifrafsequences.jl:74), ucode[k] = the code of the first maximal match
+ * score, tsum[k] = the sequential sum of grid[ucode * 256 + code] --
+ * logsumexp10 of the match scores is log10(tsum) + match_t[ucode]
+ * (rf_host_lse_finish; util.jl:28-38, model.jl:575-579).  p10_t: 256 values
+ * 10^lp; grid: 256 x 256, grid[u * 256 + x] = 10^(match_t[x] - match_t[u]). */
+int rf_set_sequences_codes_prep(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
+                                const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
+                                double s_ins, double s_del, const double *p10_t, const double *grid, double *est,
+                                int32_t *ucode, double *tsum);
 
 /* Templates (consensus sequences, one per cluster): ids [first, first+n). */
 int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl,
@@ -374,6 +387,10 @@ int rf_host_code_seq_sums(int64_t nseg, const uint8_t *codes, const int64_t *off
  * (util.jl:28-38 with grid[u * 256 + x] = 10^(match_t[x] - match_t[u])). */
 int rf_host_code_prep(int64_t nseg, const uint8_t *codes, const int64_t *off, const double *p10_t,
                       const double *match_t, const double *grid, double *est, int32_t *ucode, double *lse);
+/* logsumexp10 from rf_set_sequences_codes_prep's outputs: lse[k] =
+ * log10(tsum[k]) + match_t[ucode[k]] (libm log10), or match_t[ucode[k]] when
+ * that is infinite -- the values rf_host_code_prep writes. */
+int rf_host_lse_finish(int64_t nseg, const double *tsum, const int32_t *ucode, const double *match_t, double *lse);
 /* estimate_probs (model.jl:742-800) and alignment_error_probs's
  * normalisation (model.jl:835-839) for K clusters, around the caller's 10^x:
  * prep checks the stacked dense totals D ((m_k+1) x 9 per cluster) and

@@ -1360,6 +1360,20 @@ extern "C" int rf_host_code_prep(int64_t nseg, const uint8_t *codes, const int64
     return 0;
 }
 
+extern "C" int rf_host_lse_finish(int64_t nseg, const double *tsum, const int32_t *ucode, const double *match_t,
+                                  double *lse)
+{
+    if (nseg < 0 || (nseg > 0 && (!tsum || !ucode || !match_t || !lse)))
+        return RF_ERR_ARG;
+    for (int64_t k = 0; k < nseg; ++k) {
+        if (ucode[k] < 0 || ucode[k] > 255)
+            return RF_ERR_ARG;
+        const double u = match_t[ucode[k]];
+        lse[k] = std::isinf(u) ? u : std::log10(tsum[k]) + u;   // as rf_host_code_prep
+    }
+    return 0;
+}
+
 // estimate_probs (model.jl:742-800 via the dense totals) and the final
 // normalisation of alignment_error_probs (model.jl:835-839) for K clusters at
 // once, in two passes around the caller's 10^x (numpy's power, so the values

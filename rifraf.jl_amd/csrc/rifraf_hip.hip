@@ -3938,6 +3938,98 @@ __global__ void __launch_bounds__(256) k_tables(const CodeSeq *__restrict__ seqs
     }
 }
 
+// Per-read setup values of the native driver from the staged Phred codes
+// (round 5: formerly rf_host_code_prep's per-position host pass, which
+// bounded a rank held to 2 host cores): one thread per sequence,
+//   est[k]   = est_n_errors = sum(10^lp) in Julia 0.6's order
+//              (rifrafsequences.jl:19-82, base/reduce.jl mapreduce_impl:
+//              sequential below 1,024 elements, else pairwise halves);
+//   ucode[k] = the code of the first maximal match score;
+//   tsum[k]  = sum_i 10^(match[c_i] - match[ucode]) sequentially -- the
+//              host finishes logsumexp10 = log10(tsum) + max with libm
+//              (rf_host_lse_finish), so the initial consensus (model.jl:
+//              575-579) is the one the host pass picks.
+// The same table entries and the same FP64 additions in the same order as
+// rf_host_code_prep: bit-identical.
+constexpr int PREP_STACK = 40;
+__device__ double prep_julia_sum(const uint8_t *c, const double *p10, int64_t lo0, int64_t hi0)
+{
+    // explicit-stack post-order of the pairwise split (no device recursion)
+    int64_t slo[PREP_STACK], shi[PREP_STACK];
+    double sleft[PREP_STACK];
+    int sst[PREP_STACK];
+    int sp = 0;
+    slo[0] = lo0;
+    shi[0] = hi0;
+    sst[0] = 0;
+    double ret = 0.0;
+    while (true) {
+        const int64_t lo = slo[sp], hi = shi[sp];
+        if (lo + 1024 > hi) {   // leaf: sequential
+            double a = p10[c[lo]];
+            for (int64_t i = lo + 1; i <= hi; ++i)
+                a += p10[c[i]];
+            ret = a;
+            if (--sp < 0)
+                return ret;
+            continue;
+        }
+        const int64_t mid = (lo + hi) >> 1;
+        if (sst[sp] == 0) {
+            sst[sp] = 1;
+            ++sp;
+            slo[sp] = lo;
+            shi[sp] = mid;
+            sst[sp] = 0;
+        } else if (sst[sp] == 1) {
+            sleft[sp] = ret;
+            sst[sp] = 2;
+            ++sp;
+            slo[sp] = mid + 1;
+            shi[sp] = hi;
+            sst[sp] = 0;
+        } else {
+            ret = sleft[sp] + ret;
+            if (--sp < 0)
+                return ret;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_code_prep(const CodeSeq *__restrict__ seqs, int nseq,
+                                                   const uint8_t *__restrict__ codes, const double *__restrict__ tabs3,
+                                                   const double *__restrict__ grid, double *__restrict__ est,
+                                                   int32_t *__restrict__ ucode, double *__restrict__ tsum)
+{
+    __shared__ double p10[256], mt[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        p10[i] = tabs3[i];
+        mt[i] = tabs3[256 + i];
+    }
+    __syncthreads();
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nseq)
+        return;
+    const CodeSeq S = seqs[k];
+    const int64_t n = S.n;
+    const uint8_t *c = codes + S.src;
+    int uc = c[0];
+    double s = p10[c[0]];
+    for (int64_t i = 1; i < n; ++i) {   // the sequential leg (n < 16, or n <= 1,024)
+        const int ci = c[i];
+        s += p10[ci];
+        if (mt[ci] > mt[uc])
+            uc = ci;
+    }
+    est[k] = n <= 1024 ? s : prep_julia_sum(c, p10, 0, n - 1);
+    ucode[k] = uc;
+    const double *g = grid + (size_t)uc * 256;
+    double t = g[c[0]];
+    for (int64_t i = 1; i < n; ++i)
+        t += g[c[i]];
+    tsum[k] = t;
+}
+
 // ---------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------
@@ -5017,10 +5109,13 @@ int rf_set_sequences(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *ba
     return 0;
 }
 
-int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
-                           const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
-                           double s_ins, double s_del)
+static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases,
+                                    const int64_t *off, const uint8_t *codes, const double *lp_t,
+                                    const double *match_t, double s_mis, double s_ins, double s_del,
+                                    const double *p10_t, const double *grid, double *est, int32_t *ucode,
+                                    double *tsum)
 {
+    const bool prep = p10_t != nullptr;
     if (!ctx || first < 0 || nseq < 0 || (nseq > 0 && (!bases || !off || !codes || !lp_t || !match_t)))
         return fail(ctx, RF_ERR_ARG, "rf_set_sequences_codes: bad arguments");
     (void)hipSetDevice(ctx->device);
@@ -5141,6 +5236,20 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
         D.up1 = n1;
     }
     if (int e = upload(ctx, ctx->scratch[20], lut)) return e;
+    // prep (rf_set_sequences_codes_prep): p10 | match tables, the 256 x 256
+    // grid, then est / tsum (nseq doubles each) and ucode (nseq ints)
+    const size_t prep_tab = 512 * 8, prep_grid = 65536 * 8, prep_out = (size_t)std::max(nseq, 1) * 20;
+    if (prep) {
+        if (int e = ensure_buf(ctx, ctx->scratch[27], prep_tab + prep_grid + prep_out)) return e;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[27].p, p10_t, 256 * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + 256 * 8, match_t, 256 * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + prep_tab, grid, prep_grid, hipMemcpyHostToDevice,
+                                   ctx->stream));
+    }
+    double *d_est = (double *)((char *)ctx->scratch[27].p + prep_tab + prep_grid);
+    double *d_tsum = d_est + std::max(nseq, 1);
+    int32_t *d_ucode = (int32_t *)(d_tsum + std::max(nseq, 1));
     // chunks of sequences: codes + bases staged in pinned memory, one H2D,
     // the bases scattered to their regions, the tables built in place
     int32_t k0 = 0;
@@ -5180,6 +5289,11 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
         hipLaunchKernelGGL(k_tables, dim3(k1 - k0), dim3(256), 0, ctx->stream, (const CodeSeq *)ctx->scratch[6].p,
                            (const uint8_t *)ctx->scratch[7].p + nb, (const uint8_t *)ctx->scratch[7].p,
                            (const CodeLut *)ctx->scratch[20].p, s_mis, s_ins, s_del, (double *)ctx->tab_arena.d);
+        if (prep)
+            hipLaunchKernelGGL(k_code_prep, dim3((k1 - k0 + 255) / 256), dim3(256), 0, ctx->stream,
+                               (const CodeSeq *)ctx->scratch[6].p, k1 - k0, (const uint8_t *)ctx->scratch[7].p + nb,
+                               (const double *)ctx->scratch[27].p, (const double *)((char *)ctx->scratch[27].p + prep_tab),
+                               d_est + k0, d_ucode + k0, d_tsum + k0);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, stream_wait(ctx));   // staging and descriptors are reused
         k0 = k1;
@@ -5201,7 +5315,32 @@ int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8
         ctx->seqs[first + k].valid = true;
     }
     ++ctx->layout_gen;
+    if (prep && nseq > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(est, d_est, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(tsum, d_tsum, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ucode, d_ucode, (size_t)nseq * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, stream_wait(ctx));
+    }
     return 0;
+}
+
+int rf_set_sequences_codes(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
+                           const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
+                           double s_ins, double s_del)
+{
+    return set_sequences_codes_impl(ctx, first, nseq, bases, off, codes, lp_t, match_t, s_mis, s_ins, s_del, nullptr,
+                                    nullptr, nullptr, nullptr, nullptr);
+}
+
+int rf_set_sequences_codes_prep(rf_ctx *ctx, int32_t first, int32_t nseq, const uint8_t *bases, const int64_t *off,
+                                const uint8_t *codes, const double *lp_t, const double *match_t, double s_mis,
+                                double s_ins, double s_del, const double *p10_t, const double *grid, double *est,
+                                int32_t *ucode, double *tsum)
+{
+    if (!ctx || (nseq > 0 && (!p10_t || !grid || !est || !ucode || !tsum)))
+        return fail(ctx, RF_ERR_ARG, "rf_set_sequences_codes_prep: bad arguments");
+    return set_sequences_codes_impl(ctx, first, nseq, bases, off, codes, lp_t, match_t, s_mis, s_ins, s_del, p10_t,
+                                    grid, est, ucode, tsum);
 }
 
 int rf_set_templates(rf_ctx *ctx, int32_t first, int32_t ntpl, const uint8_t *bases,
@@ -6736,13 +6875,12 @@ extern "C" int rf_qv_probs(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     for (int32_t g = 0; g < ngroups; ++g) {
         if (P.groups[g].m != tlen[g])
             return fail(ctx, RF_ERR_ARG, "rf_qv_probs: consensus length differs from the bands'");
-        const Band &b = ctx->slots[slots[slot_off[g]]].a;
         QvGroup &q = gq[g];
         q.dense_off = P.groups[g].dense_off;
         q.sums_off = rows * 4;
         q.pos_off = rows;
         q.ins_off = rows + g;
-        q.cons_off = ctx->tpls[b.tpl].bases.off;
+        q.cons_off = P.groups[g].tb;   // the consensus the dense totals were scored against
         q.score = score[g];
         q.m = tlen[g];
         rows += tlen[g];

@@ -31,6 +31,8 @@ _SIGNATURES = {
     "rf_device_bytes": (c_int64, [c_void_p]),
     "rf_set_sequences_codes": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_double, c_double, c_double]),
+    "rf_set_sequences_codes_prep": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_double, c_double, c_double] + [c_void_p] * 5),
     "rf_code_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "rf_set_sequences": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -48,6 +50,7 @@ _SIGNATURES = {
     "rf_host_tables_from_codes": (c_int, [c_int64] + [c_void_p] * 5 + [c_double] * 3 + [c_void_p] * 6),
     "rf_host_code_seq_sums": (c_int, [c_int64] + [c_void_p] * 5),
     "rf_host_code_prep": (c_int, [c_int64] + [c_void_p] * 8),
+    "rf_host_lse_finish": (c_int, [c_int64] + [c_void_p] * 4),
     "rf_host_qv_prep": (c_int, [c_int64] + [c_void_p] * 8),
     "rf_host_qv_finish": (c_int, [c_int64] + [c_void_p] * 6),
     "rf_realign": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),

@@ -225,6 +225,12 @@ class _Hub:
 
 STATS = {"launches": 0, "engine_s": 0.0, "native_s": 0.0, "score_phase_s": 0.0, "setup_native_s": 0.0,
          "upload_s": 0.0}
+_STATS_LOCK = threading.Lock()   # waves of several engines update STATS from their own threads
+
+
+def _stat(key, value):
+    with _STATS_LOCK:
+        STATS[key] += value
 
 
 def native_eligible(clusters, params) -> bool:
@@ -424,9 +430,23 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     # tables (est_n_errors and the initial consensus's logsumexp10 in one C++
     # pass; RifrafSequence.many_coded), else the concatenated host tables
     coded = None
+    allb = None
     if (phred_in and cat_lp is not None and cat_lp.dtype.kind in "iu" and len(cat_lp)
             and int(cat_lp.max()) <= 127):
-        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8), soff, params.bandwidth, params.scores)
+        device = None
+        if hasattr(engine, "set_sequences_codes"):
+            # the reads go to the device first, and the per-read setup sums
+            # (est_n_errors, logsumexp10) come back from it (round 5: no
+            # per-position host pass; rf_set_sequences_codes_prep)
+            if hasattr(engine, "release_bands"):
+                engine.release_bands()
+            allb = np.concatenate(all_s)
+
+            def device(code, lp_t, match_t, p10, grid):
+                r = engine.set_sequences_codes(0, allb, soff, code, lp_t, match_t, params.scores, prep=(p10, grid))
+                return r if r is not False else None
+        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8), soff, params.bandwidth, params.scores,
+                                          device=device)
     if coded is not None:
         allseqs, tabs, lse_all = coded
     else:
@@ -490,20 +510,24 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
             est_bytes += (He + 2 * m) * band_stride(He, pad_h=1) * 8
     # a new wave rewrites every slot it uses: the previous wave's bands are
     # dropped and the arena is reused (sized once for a steady stream of waves)
-    if hasattr(engine, "release_bands"):
+    uploaded = coded is not None and tabs["uploaded"]
+    if hasattr(engine, "release_bands") and not uploaded:
         engine.release_bands()
     engine.reserve(int(est_bytes * 1.5) + (64 << 20))
-    STATS["setup_native_s"] += time.perf_counter() - t_setup
-    allb = np.concatenate(all_s)
+    _stat("setup_native_s", time.perf_counter() - t_setup)
+    if allb is None:
+        allb = np.concatenate(all_s)
     # Phred-coded reads: 2 B per position to the device, tables built there
-    # (rf_set_sequences_codes; the same bits); else the host tables
-    if not (phred_in and hasattr(engine, "set_sequences_codes") and
+    # (rf_set_sequences_codes; the same bits; already done with the setup
+    # sums above when `uploaded`); else the host tables
+    if not uploaded and not (
+            phred_in and hasattr(engine, "set_sequences_codes") and
             engine.set_sequences_codes(0, allb, soff, tabs["code"], tabs["lp_table"], tabs["match_table"],
                                        params.scores)):
         ft = tabs["source"].full() if coded is not None else tabs
         engine.set_sequences_concat(0, allb, soff, ft["match"], ft["mismatch"], ft["ins"], ft["del"])
     engine.set_templates(0, [st_.consensus for st_ in states])
-    STATS["upload_s"] += time.perf_counter() - t_setup
+    _stat("upload_s", time.perf_counter() - t_setup)
     read_seq = np.arange(len(all_s), dtype=np.int32)
     read_len = lens.astype(np.int32)
     est = np.array([s.est_n_errors for s in allseqs])
@@ -521,13 +545,13 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
                           int(params.batch_fixed), params.batch_size, params.batch_threshold)
     ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
-    t0 = time.perf_counter()
     with (init_lock if init_lock is not None else contextlib.nullcontext()):
+        t0 = time.perf_counter()   # the stage machine's own time, not the wait for the lock
         res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
                                              read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons),
                                              cons_off, ref=ref)
+        _stat("native_s", time.perf_counter() - t0)
     cb_errors = ref["cb_errors"] if ref is not None else {}
-    STATS["native_s"] += time.perf_counter() - t0
     for s, b in zip(allseqs, bw.tolist()):
         s.bandwidth = abs(b)
         s.bandwidth_fixed = b < 0
@@ -591,7 +615,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
                                                         ins[row + k:row + k + m + 1])
                 results[k].aln_error_probs = aln[row:row + m]
                 row += m
-            STATS["score_phase_s"] += time.perf_counter() - t0
+            _stat("score_phase_s", time.perf_counter() - t0)
             return results
         dense = engine.score_dense(groups, rows=[len(st_.consensus) + 1 for st_ in states])
         ridx = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int64) for k, st_ in enumerate(states)])
@@ -603,7 +627,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
         for k, (ep, ap) in enumerate(qvs_many_lib(states, dense, sums)):
             results[k].error_probs = ep
             results[k].aln_error_probs = ap
-        STATS["score_phase_s"] += time.perf_counter() - t0
+        _stat("score_phase_s", time.perf_counter() - t0)
     return results
 
 
@@ -713,8 +737,8 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
         hub.serve()
         for t in threads:
             t.join()
-        STATS["launches"] += hub.launches
-        STATS["engine_s"] += hub.engine_s
+        _stat("launches", hub.launches)
+        _stat("engine_s", hub.engine_s)
         for e in errors:
             if e is not None:
                 raise e

@@ -148,10 +148,13 @@ class Engine:
         self._check(self.lib.rf_set_sequences(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off),
                                               *[ptr(x) for x in a], None, None, None, None))
 
-    def set_sequences_codes(self, first: int, bases, off, codes, lp_table, match_table, scores) -> bool:
+    def set_sequences_codes(self, first: int, bases, off, codes, lp_table, match_table, scores, prep=None):
         """rf_set_sequences_codes: Phred-coded reads (no codon moves) with
         their tables built on the device from one byte per position.  False
-        when the row-code dictionary is full (upload host tables instead)."""
+        when the row-code dictionary is full (upload host tables instead).
+        prep = (p10_table, grid): rf_set_sequences_codes_prep -- returns
+        (est, ucode, tsum) per sequence (the native driver's setup values,
+        computed on the device; rifrafsequences.RifrafSequence.many_coded)."""
         off = np.ascontiguousarray(off, np.int64)
         bases = np.ascontiguousarray(bases, np.uint8)
         codes = np.ascontiguousarray(codes, np.uint8)
@@ -159,13 +162,26 @@ class Engine:
         mt = np.ascontiguousarray(match_table, np.float64)
         if lp_t.shape != (256,) or mt.shape != (256,) or len(codes) != len(bases):
             raise ValueError("set_sequences_codes: 256-entry tables and one code per base")
-        rc = self.lib.rf_set_sequences_codes(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off), ptr(codes),
-                                             ptr(lp_t), ptr(mt), float(scores.mismatch), float(scores.insertion),
-                                             float(scores.deletion))
+        sc = (float(scores.mismatch), float(scores.insertion), float(scores.deletion))
+        if prep is None:
+            rc = self.lib.rf_set_sequences_codes(self.ctx, int(first), len(off) - 1, ptr(bases), ptr(off),
+                                                 ptr(codes), ptr(lp_t), ptr(mt), *sc)
+            out = True
+        else:
+            p10 = np.ascontiguousarray(prep[0], np.float64)
+            grid = np.ascontiguousarray(prep[1], np.float64)
+            if p10.shape != (256,) or grid.shape != (256, 256):
+                raise ValueError("set_sequences_codes: prep = (256 values of 10^lp, 256 x 256 grid)")
+            n = len(off) - 1
+            est, tsum, ucode = np.empty(n), np.empty(n), np.empty(n, np.int32)
+            rc = self.lib.rf_set_sequences_codes_prep(self.ctx, int(first), n, ptr(bases), ptr(off), ptr(codes),
+                                                      ptr(lp_t), ptr(mt), *sc, ptr(p10), ptr(grid), ptr(est),
+                                                      ptr(ucode), ptr(tsum))
+            out = (est, ucode, tsum)
         if rc == -4:
             return False
         self._check(rc)
-        return True
+        return out
 
     def set_templates(self, first: int, tpls):
         if not tpls:

@@ -236,16 +236,22 @@ class RifrafSequence:
             {"match": match, "mismatch": mism, "ins": ins, "del": dele, **extra}
 
     @classmethod
-    def many_coded(cls, seqs, phreds, off, bandwidth: int, scores: Scores):
+    def many_coded(cls, seqs, phreds, off, bandwidth: int, scores: Scores, device=None):
         """The native driver's setup (batch._wave_native) from concatenated
-        int8 Phred scores, without building host tables: one C++ pass
-        (rf_host_code_prep) gives est_n_errors (the same Julia-order sum as
-        many_concat) and logsumexp10 of every sequence's match scores (the
-        values batch._logsumexp10_many returns).  The objects build their
+        int8 Phred scores, without building host tables: est_n_errors (the
+        same Julia-order sum as many_concat) and logsumexp10 of every
+        sequence's match scores (the values batch._logsumexp10_many returns)
+        from one C++ pass (rf_host_code_prep) -- or, with `device` (a
+        callable (codes, lp_table, match_table, p10_table, grid) -> (est,
+        ucode, tsum) or None: the
+        engine's rf_set_sequences_codes_prep, which uploads the reads and
+        sums on the GPU, round 5), from the device's sums and the host's
+        log10 (rf_host_lse_finish): the same bits.  The objects build their
         tables from the codes on first access (CodedRifrafSequence: the same
         gathers, adds and maxima as many_concat, so the same bits).  Returns
         (objects, tables-dict with the codes and per-code tables, lse), or
-        None when the library is absent."""
+        None when the library is absent; tables-dict["uploaded"] says whether
+        `device` uploaded the reads."""
         try:
             from . import _lib
             lib = _lib.load()
@@ -263,11 +269,19 @@ class RifrafSequence:
             raise ValueError("a log error probability is out of range")
         K = len(off) - 1
         off64 = np.ascontiguousarray(off, np.int64)
-        est, lse = np.empty(K), np.empty(K)
-        ucode = np.empty(K, np.int32)
         P = _lib.ptr
-        if lib.rf_host_code_prep(K, P(code), P(off64), P(tp10), P(tmatch), P(grid), P(est), P(ucode), P(lse)) != 0:
-            raise ValueError("rf_host_code_prep: invalid segments (empty sequence?)")
+        dev = device(code, vals, tmatch, tp10, grid) if device is not None else None
+        if dev is not None:
+            est, ucode, tsum = dev
+            lse = np.empty(K)
+            if lib.rf_host_lse_finish(K, P(tsum), P(ucode), P(tmatch), P(lse)) != 0:
+                raise ValueError("rf_host_lse_finish: invalid codes")
+        else:
+            est, lse = np.empty(K), np.empty(K)
+            ucode = np.empty(K, np.int32)
+            if lib.rf_host_code_prep(K, P(code), P(off64), P(tp10), P(tmatch), P(grid), P(est), P(ucode),
+                                     P(lse)) != 0:
+                raise ValueError("rf_host_code_prep: invalid segments (empty sequence?)")
         src = _CodeSource(code, off64, vals, tmatch, scores)
         out = []
         new = object.__new__
@@ -284,7 +298,7 @@ class RifrafSequence:
             r.bandwidth = bw
             r.bandwidth_fixed = False
             out.append(r)
-        tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src}
+        tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src, "uploaded": dev is not None}
         return out, tabs, lse
 
     @classmethod

@@ -63,7 +63,9 @@ class ShardedEngine:
         self.dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
                     else torch.device("cpu"))
         self.last_dense = None
-        self.tlen, self.slot_tpl = {}, {}    # template lengths, slot -> template (replicated)
+        # template lengths, and the template length each slot's bands were
+        # last filled against (replicated: every rank sees every call)
+        self.tlen, self.slot_m = {}, {}
         self.exchange_s, self.exchanges = 0.0, 0   # time in (and number of) collectives
 
     @classmethod
@@ -161,8 +163,14 @@ class ShardedEngine:
 
     def _rows(self, slot: int) -> int:
         """m + 1 for the template the slot's bands were last filled against
-        (replicated bookkeeping: every rank sees every realign call)."""
-        return self.tlen[self.slot_tpl[int(slot)]] + 1
+        (replicated bookkeeping: every rank sees every realign call).  The
+        length is recorded at realign time, so a later set_templates of a
+        different length cannot mis-shape the result buffer."""
+        m = self.slot_m.get(int(slot))
+        if m is None:
+            raise RifrafError(f"slot {int(slot)} has no bands filled through this ShardedEngine "
+                              "(realign it through the sharded engine first)")
+        return m + 1
 
     # ------------------------------------------------------------------
     # replicated state
@@ -191,7 +199,9 @@ class ShardedEngine:
         tpls = np.broadcast_to(np.asarray(tpls, np.int32), (n,))
         bws = np.broadcast_to(np.asarray(bws, np.int32), (n,))
         for sl, tp in zip(slots.tolist(), tpls.tolist()):
-            self.slot_tpl[sl] = tp
+            if tp not in self.tlen:
+                raise RifrafError(f"rf_realign: unknown template {tp}")
+            self.slot_m[sl] = self.tlen[tp]
         mine = np.flatnonzero(self.owned(slots))
         err = None
         buf = np.zeros(n + 1)

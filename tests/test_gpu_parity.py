@@ -1016,6 +1016,54 @@ def test_removed_option_keys_rejected(engine):
     assert RifrafError is not None
 
 
+def test_set_sequences_codes_prep_matches_host(engine):
+    """Round 5: the native driver's per-read setup values computed on the
+    device while uploading (rf_set_sequences_codes_prep, k_code_prep) --
+    est_n_errors in Julia 0.6's pairwise order and the initial consensus's
+    logsumexp10 (rifrafsequences.jl:19-82, util.jl:28-38) -- equal
+    rf_host_code_prep's bit for bit, over lengths on both sides of every
+    pairwise-sum edge (16, 1,024, 2,048, 4,096), all-Phred-0 reads (an
+    infinite maximum match score), and 5,000 reads in one call (two staging
+    chunks at 256 KB); the reads' bands equal a plain upload's."""
+    rng = np.random.default_rng(2525)
+    lens = [1, 2, 15, 16, 17, 1023, 1024, 1025, 1500, 2047, 2048, 2049, 4095, 4096, 4097, 10000, 3, 3]
+    reads = [rng.integers(0, 4, L).astype(np.uint8) for L in lens]
+    phreds = [rng.integers(0, 61, L).astype(np.int8) for L in lens]
+    phreds[-1][:] = 0                      # every code infinite: lse = match = -Inf
+    phreds[-2][1] = 0
+    reads += [rng.integers(0, 4, 300).astype(np.uint8) for _ in range(5000)]
+    phreds += [rng.integers(5, 45, 300).astype(np.int8) for _ in range(5000)]
+    off = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum([len(r) for r in reads], out=off[1:])
+    cat = np.concatenate(phreds)
+    allb = np.concatenate(reads)
+    host = RifrafSequence.many_coded(reads, cat, off, 9, SEQ_SCORES)
+    got = {}
+
+    def dev(code, lp_t, match_t, p10, grid):
+        got["r"] = engine.set_sequences_codes(0, allb, off, code, lp_t, match_t, SEQ_SCORES, prep=(p10, grid))
+        return got["r"]
+    try:
+        engine.set_option("stage_kb", 256)
+        devr = RifrafSequence.many_coded(reads, cat, off, 9, SEQ_SCORES, device=dev)
+    finally:
+        engine.set_option("stage_kb", 262144)
+    assert devr[1]["uploaded"] and got["r"] is not False
+    est_h = np.array([r.est_n_errors for r in host[0]])
+    est_d = np.array([r.est_n_errors for r in devr[0]])
+    assert est_h.view(np.int64).tolist() == est_d.view(np.int64).tolist()
+    assert host[2].view(np.int64).tolist() == devr[2].view(np.int64).tolist()   # lse, -Inf included
+    # the upload itself: bands of a few reads equal a plain rf_set_sequences_codes upload's
+    t = reads[20]
+    engine.set_templates(0, [t])
+    sl = np.arange(18, 24)
+    a1 = engine.realign(sl, sl, 0, [9] * 6, RF_FWD)
+    tabs = host[1]
+    assert engine.set_sequences_codes(0, allb, off, tabs["code"], tabs["lp_table"], tabs["match_table"], SEQ_SCORES)
+    a2 = engine.realign(sl, sl, 0, [9] * 6, RF_FWD)
+    np.testing.assert_array_equal(a1, a2)
+
+
 @pytest.mark.parametrize("scores", ["seq", "other"])
 def test_set_sequences_codes_matches_host_tables(engine, scores):
     """rf_set_sequences_codes (tables built on the device from Phred codes)

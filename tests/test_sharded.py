@@ -271,3 +271,42 @@ def test_sharded_slot_balance():
         assert c[(20, 7)][:2] == ([4, 3], [4, 3])
         for v in c.values():
             assert v[2] == v[3] == 1
+
+
+def _w_unfilled(rank, world):
+    """results of a slot whose bands were never filled through the
+    sharded engine, or of an unknown template, raise the engine's error (on
+    every rank, before any collective) instead of a KeyError."""
+    from _util import make_read
+    from oracle_engine import OracleEngine
+    from rifraf_amd.engine import RF_BWD, RF_FWD, RifrafError
+    from rifraf_amd.sample import random_seq
+    from rifraf_amd.sharded import ShardedEngine
+    rng = np.random.default_rng(3)
+    t = random_seq(50, rng)
+    reads = [make_read(t, rng, 0.03, 6) for _ in range(4)]
+    e = ShardedEngine(OracleEngine(), len(reads))
+    e.set_sequences(0, reads)
+    e.set_templates(0, [t])
+    msgs = []
+    for call in (lambda: e.score_dense([np.arange(4)]),
+                 lambda: e.realign(np.arange(4), np.arange(4), 3, [6] * 4, RF_FWD)):
+        try:
+            call()
+        except RifrafError as err:
+            msgs.append(str(err))
+    e.realign(np.arange(4), np.arange(4), 0, [6] * 4, RF_FWD | RF_BWD)
+    shapes = [e.score_dense([np.arange(4)])[0].shape]   # m = 50
+    e.set_templates(0, [random_seq(40, rng)])
+    e.realign(np.arange(4), np.arange(4), 0, [6] * 4, RF_FWD | RF_BWD)
+    shapes.append(e.score_dense([np.arange(4)])[0].shape)   # refilled: m = 40
+    return msgs, shapes
+
+
+def test_sharded_unfilled_slot_and_unknown_template():
+    got = _spawn(_w_unfilled, 2)
+    for r in range(2):
+        msgs, shapes = got[r]
+        assert len(msgs) == 2
+        assert "no bands filled" in msgs[0] and "unknown template" in msgs[1]
+        assert shapes == [(51, 9), (41, 9)]
