@@ -118,6 +118,10 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    launch; such a call cannot fill the GPU, so a
                                    task's step latency is the time).  Default
                                    2048; 0 never.  align.jl:114-212            */
+#define RF_OPT_SCORE_WGS   27   /* split-mode k_score_ws: reads per workgroup chosen
+                                   so that about this many workgroups remain
+                                   (default 2048; small values: many reads per
+                                   workgroup, partials written per read)        */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -2195,7 +2195,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
            const ScoreRead *__restrict__ reads, const uint8_t *__restrict__ bases,
            const double *__restrict__ tabs, const double *__restrict__ bands,
            double *__restrict__ dense, double *__restrict__ split, int split_mode, int lds_elems,
-           const double *__restrict__ lut)
+           const double *__restrict__ lut, int rchunk)
 {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int nb = gridDim.x, b = blockIdx.x;
@@ -2208,10 +2208,14 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
     const int la1f = min(a0 + Q - 1, m);
     int r0 = G.r0, r1 = G.r1;
     if (split_mode & 1) {
-        r0 = G.r0 + blockIdx.y;
+        // split mode: rchunk consecutive reads per workgroup (round 5: one
+        // read per workgroup left a small cluster's launch -- configs[2]'s
+        // 1,000 reads x 11 items -- without the loaders' prefetch overlap),
+        // each read's own partial written, k_reduce folds them in order
+        r0 = G.r0 + blockIdx.y * rchunk;
         if (r0 >= G.r1)
             return;
-        r1 = r0 + 1;
+        r1 = min(r0 + rchunk, G.r1);
     }
     // same decision in both roles (block-uniform)
     auto fast = [&](const ScoreRead &R, const LeanWin &w) {
@@ -2370,34 +2374,48 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
         tI[k] = 0.0;
         tS[k] = 0.0;
     }
-    for (Unit u = unit_first(r0); u.r < r1; u = unit_next(u)) {
+    const double qnan = __builtin_nan("");
+    // one position's 9 totals (fused: the group's fold; split: read r's
+    // partial, 0.0 + its own sums, and the running values restart at 0.0)
+    auto emit = [&](double *base) {
+        double *dst = base + (size_t)a * 9;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[5 + k] = tI[k];
+        if (a < m) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                dst[9 + k] = tS[k];
+            dst[13] = tD;
+        }
+        if (a == 0) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                dst[k] = qnan;
+        }
+    };
+    for (Unit u = unit_first(r0); u.r < r1;) {
         const ScoreRead R = reads[u.r];
         const LeanWin w = unit_win(R, u);
         wg_barrier();                                // unit ready
         if (tid >= u.s0 && tid < u.s0 + u.L && a <= m && !(split_mode & 2))
             lean_chain_any(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
         wg_barrier();                                // chains of the unit done
+        const Unit nx = unit_next(u);
+        if ((split_mode & 1) && nx.r != u.r && a <= m) {
+            emit(split + G.split_off + (size_t)(u.r - G.r0) * (m + 1) * 9);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                tI[k] = 0.0;
+                tS[k] = 0.0;
+            }
+            tD = 0.0;
+        }
+        u = nx;
     }
-    if (a > m)
+    if (a > m || (split_mode & 1))
         return;
-    const double qnan = __builtin_nan("");
-    double *base = (split_mode & 1) ? split + G.split_off + (size_t)blockIdx.y * (m + 1) * 9
-                                    : dense + G.dense_off;
-    double *dst = base + (size_t)a * 9;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        dst[5 + k] = tI[k];
-    if (a < m) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dst[9 + k] = tS[k];
-        dst[13] = tD;
-    }
-    if (a == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            dst[k] = qnan;
-    }
+    emit(dense + G.dense_off);
 }
 
 // ---------------------------------------------------------------------
@@ -4247,6 +4265,8 @@ struct Opts {
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
     int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
+    int score_wgs = 2048;   // RF_OPT_SCORE_WGS: split-mode k_score_ws takes reads in chunks so that about
+                            // this many workgroups remain
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
@@ -4582,6 +4602,7 @@ void load_env_opts(Opts &o)
     o.sync_block = env_int("RIFRAF_SYNC_BLOCK", o.sync_block);
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
+    o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4657,9 +4678,16 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
         hipLaunchKernelGGL(k_score, grid, dim3(128), 2 * pk.lds * 8, ctx->stream, items, groups, reads,
                            d_bases, d_tabs, d_bands, dense, split, sm, pk.lds);
     } else {
+        // split: enough reads per workgroup for the loaders' prefetch to
+        // overlap the chains, still >= 2,048 workgroups (one per CU at a time)
+        int rchunk = 1;
+        if (split) {
+            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy) / std::max(ctx->opt.score_wgs, 1));
+            grid.y = (gy + rchunk - 1) / rchunk;
+        }
         hipLaunchKernelGGL((k_score_ws<WS_NPF, 256>), grid, dim3(512), pk.lds * 8, ctx->stream, items,
                            groups, reads, d_bases, d_tabs, d_bands, dense, split, sm, pk.lds,
-                           WS_CODES ? (const double *)ctx->codes.lut.p : nullptr);
+                           WS_CODES ? (const double *)ctx->codes.lut.p : nullptr, rchunk);
     }
 }
 
@@ -4782,6 +4810,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SYNC_BLOCK: return &o.sync_block;
     case RF_OPT_DP_NL64: return &o.dp_nl64;
     case RF_OPT_DP_LAT: return &o.dp_lat;
+    case RF_OPT_SCORE_WGS: return &o.score_wgs;
     default: return nullptr;
     }
 }

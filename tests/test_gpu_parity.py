@@ -563,6 +563,34 @@ SCORER_CONFIGS = [
 ]
 
 
+@pytest.mark.parametrize("wgs", [2048, 1])
+def test_score_ws_split_read_chunks(engine, opts, wgs):
+    """Round 5: split-mode k_score_ws takes several reads per workgroup
+    (RF_OPT_SCORE_WGS 1: every read of a group in one workgroup per item,
+    sub-window units included), writing each read's partial, so k_reduce's
+    ordered fold equals the one-read-per-workgroup launch and the oracle."""
+    import oracle
+    opts("score_mode", "split")
+    opts("score_wgs", wgs)
+    rng = np.random.default_rng(77)
+    tpls = [random_seq(L, rng) for L in (700, 300)]
+    groups, seqs, tpl_of, bws = [], [], [], []
+    for c, t in enumerate(tpls):
+        rs = [make_read(t, rng, 0.03, 9 if k % 3 else 20) for k in range(9 + 4 * c)]
+        groups.append(np.arange(len(seqs), len(seqs) + len(rs)))
+        seqs += rs
+        tpl_of += [c] * len(rs)
+        bws += [r.bandwidth for r in rs]
+    engine.set_sequences(0, seqs)
+    engine.set_templates(0, tpls)
+    n = len(seqs)
+    engine.realign(np.arange(n), np.arange(n), np.array(tpl_of), bws, RF_FWD | RF_BWD)
+    dense = engine.score_dense(groups)
+    for c, t in enumerate(tpls):
+        exp, _ = oracle.cpu_pass(t, [seqs[i] for i in groups[c]], nthreads=2)
+        np.testing.assert_array_equal(dense[c], exp)
+
+
 @pytest.mark.parametrize("kern,lds", SCORER_CONFIGS)
 @pytest.mark.parametrize("mode", ["fused", "split"])
 def test_score_dense_kernels(engine, opts, kern, lds, mode):
