@@ -1272,6 +1272,134 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------
+// k_dpw: k_dp<DPW_NT> for very wide bands without codon moves (round 5;
+// edit_distance's band, align.jl:253-260: bw = ceil(min(m, n) / 2), H ~ m,
+// configs[2]: H = 2,624, one task per call).  k_dp's step loads each cell's
+// table entries and bases from global memory right before their use: a
+// dependent round trip per anti-diagonal, ~1 us per step (7.9 ms per call,
+// profiles/r05a_kernel_stats_c3.csv).  Here the row records {match, mismatch
+// (x 0.99 under skew), ins, del, base} and the template bases are staged in
+// LDS rings of DPW_RR rows / columns, 64 at a time one chunk (64 periods)
+// ahead: pair pp at period P reads row R = P + pp + par (read row R - c) and
+// column J = P - pp + JOFF (template column J - JOFF), both sliding windows.
+// Without codon moves the value ring needs only kappa-1 and kappa-2: three
+// rows.  Same candidates, FP64 sums, strict-'>' value and stored positions as
+// k_dp: bit-identical.
+// ---------------------------------------------------------------------
+constexpr int DPW_RR = 2048;   // staged rows / columns (32 blocks of 64)
+// widest band k_dpw takes: npairs + 128 staged rows, and a three-row value ring
+// beside the static rings in 160 KB of LDS
+constexpr int DPW_MAXH = 3600;
+
+template <int NT>
+__global__ void __launch_bounds__(NT)
+k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
+      const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
+      int *__restrict__ err, int ring_ld)
+{
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // value ring: 3 rows of ring_ld
+    __shared__ dvec2 s_mtmm[DPW_RR], s_isds[DPW_RR];
+    __shared__ uint8_t s_sb[DPW_RR], s_col[DPW_RR];
+    const int q = threadIdx.x;
+    const DPTask T = tasks[blockIdx.x];   // one task per workgroup
+    (void)ntasks;
+    const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
+    const uint8_t *sbase = bases + T.sb;
+    const uint8_t *tbase = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    double *band = bands + T.band;
+    const int K = T.klen, H = T.H;
+    const int npairs = (H + 1) >> 1;
+    const int JOFF = (npairs + 63) & ~63;
+    for (int e = q; e < 3 * ring_ld; e += NT)
+        smem[e] = -RF_INF;
+    // block b of rows: R in [64b, 64b + 64) -> read row R - c; of columns:
+    // J in [64b, 64b + 64) -> template column J - JOFF
+    struct Rec {
+        double mt, mm, is, ds;
+        int sb;
+    };
+    auto row_load = [&](int b, int l) {
+        const RowRec r = load_row_flat(T, rev, sbase, tb, 64 * b + l - T.c, false);
+        return Rec{r.mt, skew ? r.mm * 0.99 : r.mm, r.is, r.ds, r.sb};
+    };
+    auto row_put = [&](int b, int l, const Rec &x) {
+        const int i = (64 * b + l) & (DPW_RR - 1);
+        s_mtmm[i] = dvec2{x.mt, x.mm};
+        s_isds[i] = dvec2{x.is, x.ds};
+        s_sb[i] = (uint8_t)x.sb;
+    };
+    auto col_load = [&](int b, int l) { return load_col_flat(T, rev, tbase, 64 * b + l - JOFF); };
+    auto col_put = [&](int b, int l, int v) { s_col[(64 * b + l) & (DPW_RR - 1)] = (uint8_t)v; };
+    // newest blocks chunk t needs: rows up to 64t + 63 + npairs, columns up to 64t + 63 + JOFF
+    auto brow = [&](int t) { return (64 * t + 63 + npairs) >> 6; };
+    auto bcol = [&](int t) { return t + (JOFF >> 6); };
+    for (int e = q; e < 64 * (brow(0) + 1); e += NT)
+        row_put(e >> 6, e & 63, row_load(e >> 6, e & 63));
+    for (int e = q; e < 64 * (bcol(0) + 1); e += NT)
+        col_put(e >> 6, e & 63, col_load(e >> 6, e & 63));
+    // one chunk ahead: wave 0 holds the next row block, wave 1 the next column block
+    const int l = q & 63, wv = q >> 6;
+    Rec nrow{};
+    int ncol = 4;
+    if (wv == 0)
+        nrow = row_load(brow(1), l);
+    else if (wv == 1)
+        ncol = col_load(bcol(1), l);
+    __syncthreads();
+
+    int eflag = 0;
+    for (int k = 0; k < K; ++k) {
+        const int par = k & 1, P = k >> 1;
+        if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
+            const int t = k >> 7;
+            if (wv == 0) {
+                row_put(brow(t), l, nrow);
+                nrow = row_load(brow(t + 1), l);
+            } else if (wv == 1) {
+                col_put(bcol(t), l, ncol);
+                ncol = col_load(bcol(t + 1), l);
+            }
+            __syncthreads();
+        }
+        double *r0 = smem + (k % 3) * ring_ld + 1;
+        const double *r1 = smem + ((k + 2) % 3) * ring_ld + 1;
+        const double *r2 = smem + ((k + 1) % 3) * ring_ld + 1;
+        double *row = band + (size_t)(rev ? K - 1 - k : k) * T.P;
+        for (int pp = q;; pp += NT) {
+            const int d = 2 * pp + par;
+            if (d >= H || d > k)
+                break;
+            const int jj = P - pp;
+            const int ii = d + jj - T.c;
+            double v = -RF_INF;
+            if (jj <= T.m && ii >= 0 && ii <= T.n) {
+                if (ii == 0 && jj == 0) {
+                    v = 0.0;
+                } else {
+                    const int R = (P + pp + par) & (DPW_RR - 1);
+                    const dvec2 mtmm = s_mtmm[R], isds = s_isds[R];
+                    const int sb = s_sb[R], tbb = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
+                    const double ms = sb == tbb ? mtmm.x : mtmm.y;
+                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;
+                    // align.jl:77-104: the maximum of the candidates
+                    double best = fmax(fmax(r2[d] + ms, r1[d - 1] + is), r1[d + 1] + isds.y);
+                    eflag |= best == -RF_INF ? 1 : 0;   // "new score is invalid"
+                    v = best;
+                }
+                if (ii == T.n && jj == T.m && out_score)
+                    out_score[T.out_idx] = v;
+            }
+            row[(rev ? H - 1 - d : d) >> 1] = v;
+            r0[d] = v;
+        }
+        __syncthreads();
+    }
+    if (eflag)
+        set_err(err, 1);
+}
+
+// ---------------------------------------------------------------------
 // k_dpx: latency-bound non-lean tasks (round 5).
 //
 // The reference's codon DP (align.jl:77-104 with codon moves; skew_matches
@@ -4330,6 +4458,8 @@ struct rf_ctx {
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
         size_t nx = 0;         // latency-bound non-lean tasks, k_dpx (RF_OPT_DP_NL64)
         size_t nl = 0;         // latency-mode lean tasks, one 64-lane NP = 1 class (RF_OPT_DP_LAT)
+        size_t nww = 0;        // very wide bands without codon moves (k_dpw)
+        int hmaxw = 0;
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -4738,6 +4868,8 @@ int rf_create(int device, rf_ctx **out)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_dp<DPW_NT, false, DPW_NT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_dpw<DPW_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - DPW_RR * 34);
     *out = ctx;
     return 0;
 }
@@ -5527,8 +5659,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2];
-        int hmax64 = 0, hmaxg = 0;
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cww;
+        int hmax64 = 0, hmaxg = 0, hmaxw = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
         // of the tasks -- measured: c4 DP -5..9 %; splitting the wide classes,
@@ -5633,6 +5765,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
+                } else if (S.ncins == 0 && S.ncdel == 0 && t.H <= DPW_MAXH) {
+                    cww.push_back(t);   // k_dpw: staged rows, no codon moves (edit_distance's band)
+                    hmaxw = std::max(hmaxw, t.H);
                 } else {
                     cg.push_back(t);
                     hmaxg = std::max(hmaxg, t.H);
@@ -5677,6 +5812,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
         all.insert(all.end(), cg.begin(), cg.end());
+        all.insert(all.end(), cww.begin(), cww.end());
         if (int e = upload(ctx, ctx->scratch[8], all))
             return e;
         P.valid = true;
@@ -5699,6 +5835,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         P.nl = cl.size();
         P.n64 = c64.size();
         P.ng = cg.size();
+        P.nww = cww.size();
+        P.hmaxw = hmaxw;
         P.hmax64 = hmax64;
         P.hmaxg = hmaxg;
     }
@@ -5717,7 +5855,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // largest: the machine stays full through every launch's tail.
     struct Launch {
         int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>,
-                       // 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean), 35 = latency-mode lean,
+                       // 10 = k_dpw, 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean),
+                       // 35 = latency-mode lean,
                        // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
     };
@@ -5753,8 +5892,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             launches.push_back({8, at, P.n64});
             at += P.n64;
         }
-        if (P.ng)
+        if (P.ng) {
             launches.push_back({9, at, P.ng});
+            at += P.ng;
+        }
+        if (P.nww)
+            launches.push_back({10, at, P.nww});
     }
     if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))  // lean padding-task sink
         return e;
@@ -5768,10 +5911,10 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     // codon DP waited behind a read class on a shared queue, c3).  Otherwise
     // the largest launch stays on the main stream.
     std::stable_partition(launches.begin(), launches.end(),
-                          [](const Launch &L) { return L.kind == 34 || L.kind == 8 || L.kind == 9; });
+                          [](const Launch &L) { return L.kind == 34 || (L.kind >= 8 && L.kind <= 10); });
     size_t big = 0;
     const bool lat_first = !launches.empty() &&
-                           (launches[0].kind == 34 || launches[0].kind == 8 || launches[0].kind == 9);
+                           (launches[0].kind == 34 || (launches[0].kind >= 8 && launches[0].kind <= 10));
     for (size_t i = 1; i < launches.size() && !lat_first; ++i)
         if (launches[i].n > launches[big].n)
             big = i;
@@ -5834,6 +5977,11 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
+        } else if (L.kind == 10) {
+            // H > 2040 without codon moves: staged rows (k_dpw), a three-row value ring
+            const int ld = P.hmaxw + 4;
+            hipLaunchKernelGGL(k_dpw<DPW_NT>, dim3(n), dim3(DPW_NT), 3 * ld * 8, st, d_tasks + L.at, n, d_bases, d_tabs,
+                               d_bands, d_out, ctx->d_err, ld);
         } else {
             // H > 2040: one task per DPW_NT-thread block, the ring in LDS when it fits
             const int ld = P.hmaxg + 6;

@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Summarise the round-3 PMC passes (scripts/pmc_r03.sh) into profiles/.
+"""Summarise the FP64 PMC passes (scripts/pmc_fp64.sh; round 3: pmc_r03.sh)
+into profiles/.
 
   pmc_fp64.json   FP64 VALU instruction counts (SQ_INSTS_VALU_{ADD,MUL,FMA,
                   TRANS}_F64) per kernel at c4 and c5, the issued FP64 lane-op
@@ -14,7 +15,7 @@ an upper bound for partially active waves).  v_max_f64 is counted in the
 ADD_F64 class (the DP's 3 adds + 2 maxima per cell give ~5/64 wave
 instructions per cell; measured 5.5/64 at c4).
 
-usage: scripts/pmc_fp64_summary.py [gpurun_out/r03pmc]
+usage: scripts/pmc_fp64_summary.py [gpurun_out/r05pmc]
 """
 import collections
 import csv
@@ -77,12 +78,14 @@ def fp64_pass(d, name):
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "r03pmc")
-    out = {"source": "scripts/pmc_r03.sh passes c4_F / c5_F (rocprofv3 --kernel-trace --pmc, one pass each); "
-                     "scripts/pmc_fp64_summary.py",
+    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "r05pmc")
+    out = {"source": f"scripts/pmc_fp64.sh passes c4_F / c5_F / c3_F in {os.path.relpath(d, REPO)} "
+                     "(rocprofv3 --kernel-trace --pmc, one pass each); scripts/pmc_fp64_summary.py",
            "fp64_lane_ops_peak_per_s": FP64_LANE_OPS_PEAK,
            "note": "SQ_INSTS_* are wave instructions; lane-ops = x64 (full exec mask). v_max_f64 counts as ADD_F64."}
-    for cfg, name in (("c4", "c4_F"), ("c5", "c5_F")):
+    for cfg, name in (("c4", "c4_F"), ("c5", "c5_F"), ("c3", "c3_F")):
+        if not os.path.exists(os.path.join(d, name, "p_counter_collection.csv")):
+            continue
         ks = fp64_pass(d, name)
         b = bench_line(os.path.join(d, name + ".log"))
         ent = {"kernels": ks}
@@ -97,7 +100,7 @@ def main():
     p = os.path.join(REPO, "profiles", "pmc_fp64.json")
     json.dump(out, open(p, "w"), indent=1)
     print("wrote", p)
-    for cfg in ("c4", "c5"):
+    for cfg in [c for c in ("c4", "c5", "c3") if c in out]:
         for k, v in out[cfg]["kernels"].items():
             print(cfg, k, v["launches"], "%.3g" % v["f64_wave_insts"], "share %.3f" % v["f64_share_of_valu"],
                   "longest frac %.3f" % v["longest_launch"]["frac_of_fp64_peak"])

@@ -279,6 +279,40 @@ def test_dpx_invalid_score_is_loud(engine):
         oracle.forward(t, r)
 
 
+@pytest.mark.parametrize("m,dn,flags", [(2601, 21, RF_SKEW), (3000, -40, 0), (3400, 180, RF_SKEW | RF_TRIM),
+                                         (2300, 0, RF_TRIM)])
+def test_dpw_edit_distance_bands(engine, m, dn, flags):
+    """Round 5: very wide bands without codon moves (edit_distance,
+    align.jl:253-260: bw = ceil(min(m, n) / 2), skew_matches) run in k_dpw
+    (staged row / column rings, three-row value ring): configs[2]'s shape
+    (2,622 x 2,601), H up to ~3,600 (the k_dpw limit), skew and trim,
+    forward and (no flags) backward; bands, A[end,end], backtraces and error
+    counts bit-exact vs the oracle."""
+    rng = np.random.default_rng(m + dn)
+    t = random_seq(m, rng)
+    s = make_read(t, rng, 0.1, 9).seq
+    want = m + dn
+    s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
+    bw = int(math.ceil(min(m, len(s)) * 0.5))
+    r = RifrafSequence(s, np.full(len(s), -1.0), bw, Scores.from_errors(ErrorModel(1.0, 1.0, 1.0)))
+    H = 2 * bw + abs(len(s) - m) + 1
+    assert 2040 < H <= 3600
+    engine.set_sequences(0, [r])
+    engine.set_templates(0, [t])
+    score = engine.realign([0], [0], 0, [bw], RF_FWD | flags)
+    A_exp, mv = oracle.forward(t, r, moves=True, skew=bool(flags & RF_SKEW), trim=bool(flags & RF_TRIM))
+    assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, m + 1, bw)
+    d_end = len(s) - m + max(m - len(s), 0) + bw
+    assert score[0] == A_exp[d_end, m]
+    moves, nerr = engine.backtrace([0])
+    exp_moves = oracle.backtrace(mv, len(s) + 1, m + 1, bw)
+    np.testing.assert_array_equal(moves[0], exp_moves)
+    assert nerr[0] == oracle.count_errors(exp_moves, t, s)
+    if not flags:
+        engine.realign([0], [0], 0, [bw], RF_BWD)
+        assert_band_equal(engine.download_band(0, RF_BAND_B), oracle.backward(t, r), len(s) + 1, m + 1, bw)
+
+
 def test_dp_huge_band_global_ring(engine):
     """H > 2040 (edit_distance-sized bands) takes the one-task-per-block path
     (k_dp<256, false, 256>: 256 lanes per anti-diagonal, the ring in LDS)."""
