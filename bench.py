@@ -307,6 +307,18 @@ def aggregate(elapsed: float, units, device="cpu"):
     return float(t.item()), [float(x) for x in c.tolist()]
 
 
+def spread(x: float, device="cpu"):
+    """(min, max) of a per-rank figure over all ranks (load balance of the
+    static cluster shards; one all-gather, outside any timed region)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    v = [float(o.item()) for o in out]
+    return min(v), max(v)
+
+
 def pmc_traffic(config, size, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_<config>.json, scripts/pmc_summary.py), when it was taken at
@@ -477,13 +489,16 @@ def run_dry(args, rank, world, gpu, dist, coll, n_dev):
     cells = sum(2 * band_cells(len(r), len(t), r.bandwidth) for t, rs in clusters for r in rs)
     units = [float(cells), float(sum(len(rs) for _, rs in clusters))]
     elapsed = 0.0
+    cspread = None
     if dist is not None:
         elapsed, units = aggregate(elapsed, units, coll)
+        cspread = spread(float(cells), coll)
     return {"metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
             "value": None, "unit": "GCUPS", "dry_run": True, "steps": args.steps, "warmup": args.warmup,
             "higher_is_better": True, "scaling": "strong" if args.config == "c5" else "weak",
             "config": {"workload": args.config, "description": label},
-            "cells_per_step_all_ranks": int(units[0]), "reads_all_ranks": int(units[1])}
+            "cells_per_step_all_ranks": int(units[0]), "reads_all_ranks": int(units[1]),
+            "rank_cells_min_max": None if cspread is None else [int(x) for x in cspread]}
 
 
 def run_e2e(args, rank, world, gpu, dist, coll):
@@ -685,13 +700,19 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
         dps.append(a)
         scs.append(b)
     sync()
+    work_s = time.perf_counter() - t0   # this rank's own time, before waiting for the others
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # per-step units of this rank; the timed region ran args.steps steps
     tot_cells, tot_props, tot_pairs = cells * args.steps, nprops * args.steps, npairs * args.steps
+    balance = None
     if dist is not None:
         elapsed, (tot_cells, tot_props, tot_pairs) = aggregate(elapsed, [tot_cells, tot_props, tot_pairs], coll)
+        lo, hi = spread(work_s, coll)
+        balance = {"rank_work_s_min": lo, "rank_work_s_max": hi, "imbalance": hi / lo - 1.0 if lo > 0 else None,
+                   "note": "each rank's own timed-region time before the closing barrier: the spread of the "
+                           "static per-rank cluster shards (equal shapes, seeded per rank)"}
 
     # attainable streaming-read bandwidth over the same band arena (diagnostic)
     probe_ms = eng.probe_stream(band_bytes, 3)
@@ -721,6 +742,7 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
                    "reads_per_cluster": nreads, "template_len": length, "error_rate": err,
                    "bandwidth": bw, "parallelism": f"clusters sharded over {world} rank(s)",
                    "step": "A/B fill + scoring"},
+        "rank_balance": balance,
         "proposals_per_s": tot_props / elapsed,
         "pairs_per_s": tot_pairs / elapsed,
         "dp_ms": dp_ms,

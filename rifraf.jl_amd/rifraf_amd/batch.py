@@ -746,3 +746,74 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
 
 
 __all__ = ["rifraf_batch", "ClusterEngine"]
+
+
+class ClusterQueue:
+    """Waves of cluster indices [0, n) handed out to whichever rank asks next
+    -- the reference's `pmap` over files (scripts/rifraf.jl:190: an idle
+    worker takes the next file) across the GPUs of a node.  The counter lives
+    in the process group's key-value store (torch.distributed's TCPStore:
+    `add` is atomic), so no data-path collective is involved.  Every rank
+    must create its queues in the same order (the key carries a generation
+    number).  Without a store (one process) the counter is local."""
+
+    _gen = 0
+
+    def __init__(self, n: int, wave: int, store=None, prefix: str = "rifraf_cluster_queue"):
+        ClusterQueue._gen += 1
+        self.n, self.wave = int(n), max(1, int(wave))
+        self.store = store
+        self.key = f"{prefix}/{ClusterQueue._gen}"
+        self._local = 0
+        self._lock = threading.Lock()
+
+    @classmethod
+    def for_process_group(cls, n: int, wave: int):
+        """A queue on the default process group's store (every rank calls
+        this in the same order), or a local one when no group is up."""
+        store = None
+        try:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                from torch.distributed import distributed_c10d
+                store = distributed_c10d._get_default_store()
+        except Exception:  # noqa: BLE001 -- no process group: one process takes every wave
+            store = None
+        return cls(n, wave, store)
+
+    def take(self):
+        """The next wave's cluster indices (a range), or None when the queue
+        is empty."""
+        if self.store is not None:
+            hi = int(self.store.add(self.key, self.wave))
+        else:
+            with self._lock:
+                self._local += self.wave
+                hi = self._local
+        lo = hi - self.wave
+        if lo >= self.n:
+            return None
+        return range(lo, min(hi, self.n))
+
+
+def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=None, **kw):
+    """rifraf_batch over the waves this process takes from `queue` (a
+    ClusterQueue shared by the ranks of a node): `get_cluster(i)` gives
+    cluster i's keyword dict (e.g. read from its FASTQ file, as each `pmap`
+    worker does).  Returns {cluster index: RifrafResult} for the clusters
+    this rank ran; over all ranks every cluster runs exactly once, with the
+    result rifraf() gives it alone (clusters are independent).  With a
+    store-backed queue every rank waits at a barrier once the queue is empty:
+    rank 0 hosts the store, so it must not tear the group down while another
+    rank still takes waves."""
+    out = {}
+    while True:
+        r = queue.take()
+        if r is None:
+            break
+        res = rifraf_batch([get_cluster(i) for i in r], params=params, engine=engine, wave=len(r), **kw)
+        out.update(zip(r, res))
+    if queue.store is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    return out

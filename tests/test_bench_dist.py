@@ -85,6 +85,11 @@ def test_bench_self_launches_ranks(world):
                 for t, rs in bench.make_workload(2, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, rank))
                 for r in rs)
     assert out["cells_per_step_all_ranks"] == cells
+    # the per-rank spread of the static shards (bench `rank_balance` measures their time)
+    per_rank = [sum(2 * bench.band_cells(len(r), len(t), r.bandwidth)
+                    for t, rs in bench.make_workload(2, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, rank))
+                    for r in rs) for rank in range(world)]
+    assert out["rank_cells_min_max"] == [min(per_rank), max(per_rank)]
 
 
 def test_bench_rejects_world_mismatch():

@@ -310,3 +310,51 @@ def test_sharded_unfilled_slot_and_unknown_template():
         assert len(msgs) == 2
         assert "no bands filled" in msgs[0] and "unknown template" in msgs[1]
         assert shapes == [(51, 9), (41, 9)]
+
+
+def _w_queue(rank, world, n, wave):
+    """Each rank takes waves from the store-backed queue and runs them on the
+    oracle engine (the Python stage machine)."""
+    import time
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import ClusterQueue, rifraf_batch_queue
+    from rifraf_amd.model import RifrafParams
+    q = ClusterQueue.for_process_group(n, wave)
+    params = RifrafParams(max_iters=20)
+
+    def get(i):
+        if rank == 0:
+            time.sleep(0.05)   # a slow rank: the others take more waves
+        return _queue_cluster(i)
+    res = rifraf_batch_queue(get, q, params=params, engine=OracleEngine())
+    return {i: np.asarray(r.consensus).tolist() for i, r in res.items()}
+
+
+def _queue_cluster(i):
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng([99, i])
+    _, _, _, reads, _, phreds, _, _ = sample_sequences(4, 40, error_rate=0.03, rng=rng)
+    return dict(dnaseqs=reads, phreds=phreds)
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_cluster_queue_across_ranks(world):
+    """The cross-rank cluster queue (pmap's dynamic hand-out,
+    scripts/rifraf.jl:190): every cluster runs on exactly one rank, a slow
+    rank takes fewer waves, and each result equals one process's run."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    n, wave = 13, 2
+    got = _spawn(_w_queue, world, n, wave)
+    seen = {}
+    for r in range(world):
+        for i, c in got[r].items():
+            assert i not in seen
+            seen[i] = c
+    assert sorted(seen) == list(range(n))
+    assert len(got[0]) <= min(len(got[r]) for r in range(1, world)) + wave
+    single = rifraf_batch([_queue_cluster(i) for i in range(n)], params=RifrafParams(max_iters=20),
+                          engine=OracleEngine())
+    for i in range(n):
+        assert seen[i] == np.asarray(single[i].consensus).tolist()
