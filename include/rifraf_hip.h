@@ -204,6 +204,13 @@ int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids,
 int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot,
                const int32_t *seq, const int32_t *tpl, const int32_t *bw,
                int32_t flags, double *out_score);
+/* rf_realign with flags per job (round 5): independent fills of one stage
+ * machine step -- e.g. the reads' backward! and the reference's skewed
+ * forward_moves! of single_indel_proposals (model.jl:538-562) -- share one
+ * launch set, so a latency-bound task runs beside the others. */
+int rf_realign_jobs(rf_ctx *ctx, int32_t njobs, const int32_t *slot,
+                    const int32_t *seq, const int32_t *tpl, const int32_t *bw,
+                    const int32_t *flags, double *out_score);
 
 /* Backtrace of the A band of each slot (align.jl:229-238), moves in
  * alignment order written at moves[moves_off[k] ...] (capacity n+m each);

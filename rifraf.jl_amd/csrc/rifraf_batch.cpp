@@ -97,6 +97,9 @@ struct Clu {
     double ref_score = -INF;
     int32_t n_ref_indel_mults = 0;
     std::vector<Prop> seeds;                    // FRAME indel seeds
+    // the scratch slot already holds single_indel_proposals' skewed fill of
+    // the reference against this consensus (filled beside the B realign)
+    bool sip_pre = false;
 };
 
 struct Driver {
@@ -269,9 +272,18 @@ struct Driver {
         return 0;
     }
 
+    // backward! of every batch read (and the reference in FRAME); round 5:
+    // in FRAME with seeded indels also single_indel_proposals' skewed
+    // forward fill of the reference against the same consensus
+    // (model.jl:538-562, align_moves(skew_matches=true)) into the scratch
+    // slot, in the same launch set: the reference's long latency-bound fill
+    // runs beside the reads' instead of after them.  The stage machine's
+    // order is unchanged (the fill reads only the consensus and the
+    // reference, which do not change before single_indel_proposals).
     int realign_B(const std::vector<int> &cs)
     {
-        std::vector<int32_t> sl, sq, tp, bw;
+        std::vector<int32_t> sl, sq, tp, bw, fl;
+        std::vector<int> pre;
         for (int c : cs) {
             const Clu &C = clu[c];
             for (int k = 0; k < (int)C.batch.size(); ++k) {
@@ -280,6 +292,7 @@ struct Driver {
                 sq.push_back(R.seq);
                 tp.push_back(C.tpl);
                 bw.push_back(R.bw);
+                fl.push_back(RF_BWD);
             }
             if (ref_on(C)) {   // model.jl:710-712
                 const Read &R = reads[C.ref_read];
@@ -287,11 +300,25 @@ struct Driver {
                 sq.push_back(R.seq);
                 tp.push_back(C.tpl);
                 bw.push_back(R.bw);
+                fl.push_back(RF_BWD);
+                if (RP.seed_indels) {
+                    sl.push_back(C.scratch_slot);
+                    sq.push_back(R.seq);
+                    tp.push_back(C.tpl);
+                    bw.push_back(R.bw);
+                    fl.push_back(RF_FWD | RF_SKEW);
+                    pre.push_back(c);
+                }
             }
         }
-        return timed(T_BWD, [&] {
-            return rf_realign(ctx, (int32_t)sl.size(), sl.data(), sq.data(), tp.data(), bw.data(), RF_BWD, nullptr);
+        const int e = timed(T_BWD, [&] {
+            return rf_realign_jobs(ctx, (int32_t)sl.size(), sl.data(), sq.data(), tp.data(), bw.data(), fl.data(),
+                                   nullptr);
         });
+        if (e == 0)
+            for (int c : pre)
+                clu[c].sip_pre = true;
+        return e;
     }
 
     // ---------------- realign! + rescore! (model.jl:630-719), no reference
@@ -388,7 +415,8 @@ struct Driver {
     // align.jl:337-344; model.jl:532-562): forward fill of the reference
     // (rows) against the consensus in the cluster's scratch slot with the
     // reference's bandwidth, then the backtrace moves
-    int ref_moves(const std::vector<int> &cs, bool skew, std::vector<std::vector<int8_t>> &mv)
+    int ref_moves(const std::vector<int> &cs, bool skew, std::vector<std::vector<int8_t>> &mv,
+                  bool filled = false)
     {
         std::vector<int32_t> sl, sq, tp, bw, nm(cs.size());
         std::vector<int64_t> moff{0};
@@ -401,11 +429,12 @@ struct Driver {
             bw.push_back(R.bw);
             moff.push_back(moff.back() + R.len + (int64_t)C.cons.size());
         }
-        if (int e = timed(T_FWD, [&] {
-                return rf_realign(ctx, (int32_t)cs.size(), sl.data(), sq.data(), tp.data(), bw.data(),
-                                  RF_FWD | (skew ? RF_SKEW : 0), nullptr);
-            }))
-            return e;
+        if (!filled)   // (filled: the scratch slot holds this fill already, realign_B)
+            if (int e = timed(T_FWD, [&] {
+                    return rf_realign(ctx, (int32_t)cs.size(), sl.data(), sq.data(), tp.data(), bw.data(),
+                                      RF_FWD | (skew ? RF_SKEW : 0), nullptr);
+                }))
+                return e;
         std::vector<int8_t> moves((size_t)std::max<int64_t>(moff.back(), 1));
         if (int e = timed(T_BT, [&] {
                 return rf_backtrace(ctx, (int32_t)cs.size(), sl.data(), moves.data(), moff.data(), nm.data(), nullptr);
@@ -432,12 +461,23 @@ struct Driver {
         });
     }
 
-    // single_indel_proposals (model.jl:538-562) -> clu[c].seeds
+    // single_indel_proposals (model.jl:538-562) -> clu[c].seeds; clusters whose
+    // skewed fill ran beside their B realign (sip_pre) take only the walk
     void single_indel_proposals(std::vector<int> &cs)
+    {
+        std::vector<int> pre, rest;
+        for (int c : cs)
+            (clu[c].sip_pre ? pre : rest).push_back(c);
+        single_indel_proposals_(pre, true);
+        single_indel_proposals_(rest, false);
+        cs = pre;
+        cs.insert(cs.end(), rest.begin(), rest.end());
+    }
+    void single_indel_proposals_(std::vector<int> &cs, bool filled)
     {
         batched(cs, [&](const std::vector<int> &s) {
             std::vector<std::vector<int8_t>> mv;
-            if (int e = ref_moves(s, true, mv))
+            if (int e = ref_moves(s, true, mv, filled))
                 return e;
             for (size_t i = 0; i < s.size(); ++i) {
                 Clu &C = clu[s[i]];
@@ -825,6 +865,8 @@ struct Driver {
                     C.seeds.clear();
             }
             single_indel_proposals(sd);
+            for (int c : act)
+                clu[c].sip_pre = false;   // the scratch slot is refilled from here on (has_single_indels)
             for (int c : gc)
                 cands[c].clear();
             get_candidates(gc, cands);

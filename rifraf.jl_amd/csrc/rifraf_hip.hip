@@ -4451,19 +4451,19 @@ struct rf_ctx {
         bool valid = false;
         uint64_t gen = 0;
         uint64_t val_epoch = 0;   // state_epoch at which the job list was last validated
-        int32_t flags = 0;
-        std::vector<int32_t> slot, seq, tpl, bw;
+        std::vector<int32_t> slot, seq, tpl, bw, flags;   // flags: per job (rf_realign_jobs)
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
         size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
         size_t nx = 0;         // latency-bound non-lean tasks, k_dpx (RF_OPT_DP_NL64)
-        size_t nl = 0;         // latency-mode lean tasks, one 64-lane NP = 1 class (RF_OPT_DP_LAT)
+        size_t nl = 0;         // latency-mode lean tasks, one k_dpx<false, false> class (RF_OPT_DP_LAT)
         size_t nww = 0;        // very wide bands without codon moves (k_dpw)
         int hmaxw = 0;
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
     } rplan;
+    std::vector<int32_t> jflags;   // rf_realign: the call's flags for every job
     struct {
         bool valid = false;
         uint64_t gen = 0;
@@ -5560,20 +5560,22 @@ int rf_set_templates_ids(rf_ctx *ctx, int32_t ntpl, const int32_t *ids, const ui
     return 0;
 }
 
-int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *seq,
-               const int32_t *tpl, const int32_t *bw, int32_t flags, double *out_score)
+static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *seq, const int32_t *tpl,
+                        const int32_t *bw, const int32_t *jf, double *out_score)
 {
-    if (!ctx || njobs < 0 || (njobs > 0 && (!slot || !seq || !tpl || !bw)))
+    if (!ctx || njobs < 0 || (njobs > 0 && (!slot || !seq || !tpl || !bw || !jf)))
         return fail(ctx, RF_ERR_ARG, "rf_realign: bad arguments");
-    if (!(flags & (RF_FWD | RF_BWD)))
-        return fail(ctx, RF_ERR_ARG, "rf_realign: need RF_FWD and/or RF_BWD");
+    for (int32_t k = 0; k < njobs; ++k)
+        if (!(jf[k] & (RF_FWD | RF_BWD)))
+            return fail(ctx, RF_ERR_ARG, "rf_realign: need RF_FWD and/or RF_BWD");
     (void)hipSetDevice(ctx->device);
     auto &P = ctx->rplan;
     const size_t nb = sizeof(int32_t) * (size_t)njobs;
-    const bool same = P.valid && P.gen == ctx->layout_gen && P.flags == flags &&
+    const bool same = P.valid && P.gen == ctx->layout_gen &&
                       P.slot.size() == (size_t)njobs && (njobs == 0 ||
                       (!std::memcmp(P.slot.data(), slot, nb) && !std::memcmp(P.seq.data(), seq, nb) &&
-                       !std::memcmp(P.tpl.data(), tpl, nb) && !std::memcmp(P.bw.data(), bw, nb)));
+                       !std::memcmp(P.tpl.data(), tpl, nb) && !std::memcmp(P.bw.data(), bw, nb) &&
+                       !std::memcmp(P.flags.data(), jf, nb)));
     // the same job list, validated with nothing changed since: its checks and
     // its band bookkeeping would come out the same
     const bool fresh = same && P.val_epoch == ctx->state_epoch;
@@ -5591,9 +5593,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (!fresh) {
             bool changed = false;
             for (int dir = 0; dir < 2; ++dir) {
-                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                    continue;
                 for (int32_t k = 0; k < njobs; ++k) {
+                    if (!(jf[k] & (dir == 0 ? RF_FWD : RF_BWD)))
+                        continue;
                     Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
                     const uint64_t v = ctx->tpls[tpl[k]].version;
                     changed = changed || b.tplver != v;
@@ -5622,9 +5624,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
             hmax_call = std::max(hmax_call, band_rows(ctx->seqs[seq[k]].n + 1, ctx->tpls[tpl[k]].m + 1, bw[k]));
         const bool pad_call = ctx->opt.band_pad_h > 0 && hmax_call >= ctx->opt.band_pad_h;
         for (int dir = 0; dir < 2; ++dir) {
-            if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                continue;
             for (int32_t k = 0; k < njobs; ++k) {
+                if (!(jf[k] & (dir == 0 ? RF_FWD : RF_BWD)))
+                    continue;
                 const SeqObj &S = ctx->seqs[seq[k]];
                 const TplObj &T = ctx->tpls[tpl[k]];
                 Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
@@ -5649,7 +5651,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 b.n = S.n;
                 b.m = T.m;
                 b.H = H;
-                b.flags = dir == 0 ? (flags & (RF_SKEW | RF_TRIM)) : 0;
+                b.flags = dir == 0 ? (jf[k] & (RF_SKEW | RF_TRIM)) : 0;
                 b.tplver = T.version;
             }
         }
@@ -5669,9 +5671,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         if (ctx->opt.dp_psplit < 0) {
             size_t n1 = 0, nall = 0;
             for (int dir = 0; dir < 2; ++dir) {
-                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                    continue;
                 for (int32_t k = 0; k < njobs; ++k) {
+                    if (!(jf[k] & (dir == 0 ? RF_FWD : RF_BWD)))
+                        continue;
                     const Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
                     n1 += b.H <= 31;
                     ++nall;
@@ -5689,12 +5691,12 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         {
             size_t nl = 0;
             for (int dir = 0; dir < 2; ++dir) {
-                if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                    continue;
                 for (int32_t k = 0; k < njobs; ++k) {
+                    if (!(jf[k] & (dir == 0 ? RF_FWD : RF_BWD)))
+                        continue;
                     const SeqObj &S = ctx->seqs[seq[k]];
                     const Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
-                    const bool ln = S.ncins == 0 && S.ncdel == 0 && S.finite && !(dir == 0 && (flags & (RF_SKEW | RF_TRIM)));
+                    const bool ln = S.ncins == 0 && S.ncdel == 0 && S.finite && !(dir == 0 && (jf[k] & (RF_SKEW | RF_TRIM)));
                     nl += ln && b.H <= 127;
                 }
             }
@@ -5702,9 +5704,9 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         }
         std::vector<DPTask> cl;
         for (int dir = 0; dir < 2; ++dir) {
-            if (!(flags & (dir == 0 ? RF_FWD : RF_BWD)))
-                continue;
             for (int32_t k = 0; k < njobs; ++k) {
+                if (!(jf[k] & (dir == 0 ? RF_FWD : RF_BWD)))
+                    continue;
                 const SeqObj &S = ctx->seqs[seq[k]];
                 const TplObj &T = ctx->tpls[tpl[k]];
                 const Band &b = dir == 0 ? ctx->slots[slot[k]].a : ctx->slots[slot[k]].b;
@@ -5720,8 +5722,8 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                 t.c = std::max(T.m - S.n, 0) + bw[k];
                 t.ncins = S.ncins;
                 t.ncdel = S.ncdel;
-                t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (flags & RF_SKEW) ? 2 : 0) |
-                          (dir == 0 && (flags & RF_TRIM) ? 4 : 0) | (S.coded ? RF_TASK_CODED : 0);
+                t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (jf[k] & RF_SKEW) ? 2 : 0) |
+                          (dir == 0 && (jf[k] & RF_TRIM) ? 4 : 0) | (S.coded ? RF_TASK_CODED : 0);
 #ifdef RIFRAF_DIAG
                 // RIFRAF_DP_SINK=1 (diagnostic builds only): the blocked interior's
                 // band stores all go to one small sink buffer (bands are then invalid)
@@ -5729,7 +5731,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
                     t.flags |= 512;
 #endif
                 // out_score: forward scores win when both directions run
-                t.out_idx = (dir == 0 || !(flags & RF_FWD)) ? k : njobs + k;
+                t.out_idx = (dir == 0 || !(jf[k] & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
                 t.P = b.P;
                 // classes: k_dpr<NP> for H <= 32*NP-1 (NP = 1, 2, 4, 8), lean when
@@ -5818,7 +5820,7 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
         P.valid = true;
         P.gen = ctx->layout_gen;
         P.val_epoch = ctx->state_epoch;
-        P.flags = flags;
+        P.flags.assign(jf, jf + njobs);
         P.slot.assign(slot, slot + njobs);
         P.seq.assign(seq, seq + njobs);
         P.tpl.assign(tpl, tpl + njobs);
@@ -6013,6 +6015,21 @@ int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *s
     (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
     ctx->dp_ms = ms;
     return check_err_landed(ctx);
+}
+
+int rf_realign(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *seq,
+               const int32_t *tpl, const int32_t *bw, int32_t flags, double *out_score)
+{
+    if (!ctx || njobs < 0)
+        return fail(ctx, RF_ERR_ARG, "rf_realign: bad arguments");
+    ctx->jflags.assign((size_t)njobs, flags);
+    return realign_impl(ctx, njobs, slot, seq, tpl, bw, ctx->jflags.data(), out_score);
+}
+
+int rf_realign_jobs(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32_t *seq, const int32_t *tpl,
+                    const int32_t *bw, const int32_t *flags, double *out_score)
+{
+    return realign_impl(ctx, njobs, slot, seq, tpl, bw, flags, out_score);
 }
 
 // Every walk runs in k_bt_win (round 4: codon alignments and bands of any

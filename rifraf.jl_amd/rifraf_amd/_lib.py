@@ -54,6 +54,7 @@ _SIGNATURES = {
     "rf_host_qv_prep": (c_int, [c_int64] + [c_void_p] * 8),
     "rf_host_qv_finish": (c_int, [c_int64] + [c_void_p] * 6),
     "rf_realign": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "rf_realign_jobs": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_backtrace": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rf_score": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p]),

@@ -314,17 +314,24 @@ class Engine:
         self._check(rc)
         return pos, ins, aln, err
 
-    def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
+    def realign(self, slots, seqs, tpls, bws, flags) -> np.ndarray:
         """Batched forward_moves!/backward! fill; returns A[end,end] (RF_FWD)
-        or B[1,1] per job."""
+        or B[1,1] per job.  flags: one int for every job (rf_realign) or one
+        per job (rf_realign_jobs: e.g. backward fills beside a skewed forward
+        fill in one launch set)."""
         slots = np.ascontiguousarray(slots, np.int32)
         n = slots.shape[0]
         seqs = np.ascontiguousarray(np.broadcast_to(seqs, (n,)), np.int32)
         tpls = np.ascontiguousarray(np.broadcast_to(tpls, (n,)), np.int32)
         bws = np.ascontiguousarray(np.broadcast_to(bws, (n,)), np.int32)
         out = np.empty(max(n, 1))
-        self._check(self.lib.rf_realign(self.ctx, n, ptr(slots), ptr(seqs), ptr(tpls), ptr(bws),
-                                        int(flags), ptr(out)))
+        if np.ndim(flags) == 0:
+            self._check(self.lib.rf_realign(self.ctx, n, ptr(slots), ptr(seqs), ptr(tpls), ptr(bws),
+                                            int(flags), ptr(out)))
+        else:
+            fl = np.ascontiguousarray(np.broadcast_to(flags, (n,)), np.int32)
+            self._check(self.lib.rf_realign_jobs(self.ctx, n, ptr(slots), ptr(seqs), ptr(tpls), ptr(bws),
+                                                 ptr(fl), ptr(out)))
         return out[:n]
 
     def backtrace(self, slots, want_moves: bool = True):

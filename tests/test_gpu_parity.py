@@ -261,6 +261,38 @@ def test_dpx_long_reference_tasks(engine, opts, m, dn, bw, flags):
         assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, m + 1, bw)
 
 
+def test_realign_jobs_per_job_flags(engine):
+    """rf_realign_jobs (round 5): flags per job in one launch set -- reads'
+    backward fills beside the reference's skewed forward fill and a trimmed
+    one (the native driver's realign_B + single_indel_proposals) -- give the
+    bands, scores and walks of separate rf_realign calls."""
+    rng = np.random.default_rng(606)
+    t = random_seq(900, rng)
+    reads = [make_read(t, rng, 0.02, 9) for _ in range(5)]
+    ref = RifrafSequence(np.concatenate([t[:400], t[401:]]), np.full(len(t) - 1, math.log10(0.1)), 9, REF_SCORES)
+    engine.set_sequences(0, reads + [ref])
+    engine.set_templates(0, [t])
+    slots = [0, 1, 2, 3, 4, 5, 6, 7]
+    seqs = [0, 1, 2, 3, 4, 5, 5, 5]
+    flags = [RF_BWD] * 5 + [RF_BWD, RF_FWD | RF_SKEW, RF_FWD | RF_TRIM]
+    got = engine.realign(slots, seqs, 0, [9] * 8, flags)
+    bands = [engine.download_band(s, RF_BAND_B).data.copy() for s in range(6)]
+    bands += [engine.download_band(s, RF_BAND_A).data.copy() for s in (6, 7)]
+    mv_got = engine.backtrace([6, 7])[0]
+    sep = list(engine.realign(slots[:6], seqs[:6], 0, [9] * 6, RF_BWD))
+    sep += list(engine.realign([6], [5], 0, [9], RF_FWD | RF_SKEW))
+    sep += list(engine.realign([7], [5], 0, [9], RF_FWD | RF_TRIM))
+    np.testing.assert_array_equal(got, np.array(sep))
+    for s, b in zip(range(6), bands):
+        np.testing.assert_array_equal(engine.download_band(s, RF_BAND_B).data, b)
+    for s, b in zip((6, 7), bands[6:]):
+        np.testing.assert_array_equal(engine.download_band(s, RF_BAND_A).data, b)
+    for a, b in zip(mv_got, engine.backtrace([6, 7])[0]):
+        np.testing.assert_array_equal(a, b)
+    A_exp, _ = oracle.forward(t, ref, skew=True)
+    assert_band_equal(engine.download_band(6, RF_BAND_A), A_exp, len(ref.seq) + 1, len(t) + 1, 9)
+
+
 def test_dpx_invalid_score_is_loud(engine):
     """A non-lean task whose band holds a cell with no finite predecessor
     (insertions and deletions impossible: ErrorModel(1, 0, 0, 1, 1), a read
@@ -622,7 +654,11 @@ def test_score_ws_split_read_chunks(engine, opts, wgs):
     dense = engine.score_dense(groups)
     for c, t in enumerate(tpls):
         exp, _ = oracle.cpu_pass(t, [seqs[i] for i in groups[c]], nthreads=2)
-        np.testing.assert_array_equal(dense[c], exp)
+        mask = np.ones_like(exp, bool)
+        mask[0, :5] = False                       # p = 0 has no sub/del
+        for j in range(1, len(t) + 1):
+            mask[j, t[j - 1]] = False             # not a proposal
+        np.testing.assert_array_equal(dense[c][mask], exp[mask])
 
 
 @pytest.mark.parametrize("kern,lds", SCORER_CONFIGS)
