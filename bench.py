@@ -846,8 +846,9 @@ class _StageTimer:
         tp = np.broadcast_to(tpls, (n,))
         bw = np.broadcast_to(bws, (n,))
         from rifraf_amd.engine import RF_BWD, RF_FWD
-        dirs = int(bool(flags & RF_FWD)) + int(bool(flags & RF_BWD))
-        cells = dirs * sum(band_cells(self.lens[int(a)], self.tlen[int(b)], int(c)) for a, b, c in zip(sq, tp, bw))
+        fl = np.broadcast_to(np.asarray(flags), (n,))   # one value or one per job
+        cells = sum((int(bool(f & RF_FWD)) + int(bool(f & RF_BWD))) * band_cells(self.lens[int(a)], self.tlen[int(b)], int(c))
+                    for a, b, c, f in zip(sq, tp, bw, fl.tolist()))
         self._add(dp_ms=self.e.last_timing()[0], dp_cells=cells, realign_calls=1)
         return out
 

@@ -56,7 +56,19 @@ class ClusterEngine:
         return self.hub.call(self.k, "set_templates", first, tpls)
 
     def realign(self, slots, seqs, tpls, bws, flags):
-        return self.hub.call(self.k, "realign", slots, seqs, tpls, bws, flags)
+        if np.ndim(flags) == 0:
+            return self.hub.call(self.k, "realign", slots, seqs, tpls, bws, flags)
+        # flags per job: the hub batches requests by flags, so one request
+        # per distinct value (the results in job order)
+        slots = np.atleast_1d(np.asarray(slots, np.int32))
+        n = len(slots)
+        fl = np.broadcast_to(np.asarray(flags), (n,))
+        seqs, tpls, bws = (np.broadcast_to(np.asarray(x), (n,)) for x in (seqs, tpls, bws))
+        out = np.empty(n)
+        for f in dict.fromkeys(fl.tolist()):
+            idx = np.flatnonzero(fl == f)
+            out[idx] = self.hub.call(self.k, "realign", slots[idx], seqs[idx], tpls[idx], bws[idx], int(f))
+        return out
 
     def backtrace(self, slots, want_moves=True):
         return self.hub.call(self.k, "backtrace", slots, want_moves)

@@ -120,9 +120,19 @@ class _Run:
         self.REF = nseqs
         self.SCRATCH = nseqs + 1
         self.tpl_version = None
+        # the scratch slot holds single_indel_proposals' skewed fill of the
+        # current reference against the current consensus (filled beside the
+        # B realign, realign()); cleared by every consensus / reference upload
+        # and by has_single_indels' own fill
+        self.sip_ready = False
 
     def set_consensus(self, cons):
+        self.sip_ready = False
         self.e.set_templates(0, [cons])
+
+    def set_ref(self, ref):
+        self.sip_ready = False
+        self.e.set_sequences(self.REF, [ref])
 
 
 def log(params, level, msg):
@@ -260,23 +270,43 @@ def realign(state: RifrafState, run: _Run, params: RifrafParams):   # :679-714
         state.slot_scores.append(0.0)                # A[end,end] of a fresh (zero) BandedArray
         state.n_slots += 1
     ref_on = use_ref(state.reference, state.stage, params.use_ref_for_qvs)
+    # the reads' and the reference's fills are independent jobs of one engine
+    # call each (round 5: the reference's long latency-bound fill runs beside
+    # the reads' instead of after them; the same bands and scores)
     if state.realign_As:
         log(params, 2, "    realigning As")
         jobs = [(k, i) for k, i in enumerate(state.batch_seqs)]
-        sc = smart_forward_moves(run, jobs, seqs, len(state.consensus), params.bandwidth_pvalue)
-        for k in range(len(jobs)):
+        jseqs = list(seqs)
+        if ref_on:
+            jobs.append((run.REF, run.REF))
+            jseqs.append(state.reference)
+        sc = smart_forward_moves(run, jobs, jseqs, len(state.consensus), params.bandwidth_pvalue)
+        for k in range(len(seqs)):
             state.slot_scores[k] = float(sc[k])
         if ref_on:
-            sc = smart_forward_moves(run, [(run.REF, run.REF)], [state.reference], len(state.consensus),
-                                     params.bandwidth_pvalue)
-            state.ref_score = float(sc[0])
+            state.ref_score = float(sc[len(seqs)])
     if state.realign_Bs:
         log(params, 2, "    realigning Bs")
-        slots = np.arange(len(seqs), dtype=np.int32)
-        run.e.realign(slots, np.array(state.batch_seqs, np.int32), 0,
-                      np.array([s.bandwidth for s in seqs], np.int32), RF_BWD)
+        slots = list(range(len(seqs)))
+        ids = list(state.batch_seqs)
+        bws = [s.bandwidth for s in seqs]
+        flags = [RF_BWD] * len(seqs)
         if ref_on:
-            run.e.realign([run.REF], [run.REF], 0, [state.reference.bandwidth], RF_BWD)
+            slots.append(run.REF)
+            ids.append(run.REF)
+            bws.append(state.reference.bandwidth)
+            flags.append(RF_BWD)
+        # FRAME with seeded indels: single_indel_proposals' skewed fill of the
+        # reference against this consensus (model.jl:538-562) in the same call
+        sip = state.stage == Stage.FRAME and params.seed_indels and len(state.reference) > 0
+        if sip:
+            slots.append(run.SCRATCH)
+            ids.append(run.REF)
+            bws.append(state.reference.bandwidth)
+            flags.append(RF_FWD | RF_SKEW)
+        run.e.realign(np.array(slots, np.int32), np.array(ids, np.int32), 0, np.array(bws, np.int32),
+                      np.array(flags, np.int32) if sip else RF_BWD)
+        run.sip_ready = sip
 
 
 def realign_rescore(state, run, params):       # :716-719
@@ -352,10 +382,13 @@ def mask_to_proposals(mask):
 def _align_ref_moves(state: RifrafState, run: _Run, skew: bool):
     """align_moves(consensus, reference; skew_matches) on the engine
     (align.jl:337-344): forward_moves! of the reference (rows) against the
-    consensus with the reference's own bandwidth, then backtrace."""
+    consensus with the reference's own bandwidth, then backtrace.  The
+    skewed fill may already be in the scratch slot (realign's B call)."""
     ref = state.reference
-    run.e.set_sequences(run.REF, [ref])
-    run.e.realign([run.SCRATCH], [run.REF], 0, [ref.bandwidth], RF_FWD | (RF_SKEW if skew else 0))
+    if not (skew and run.sip_ready):
+        run.set_ref(ref)
+        run.e.realign([run.SCRATCH], [run.REF], 0, [ref.bandwidth], RF_FWD | (RF_SKEW if skew else 0))
+    run.sip_ready = False
     moves, _ = run.e.backtrace([run.SCRATCH])
     return moves[0]
 
@@ -454,7 +487,7 @@ def finish_stage(state: RifrafState, run: _Run, params: RifrafParams):   # :937-
             ref_error_log_p = np.full(len(state.reference), math.log10(state.ref_error_rate))
             state.reference = RifrafSequence(state.reference.seq, ref_error_log_p, params.bandwidth,
                                              state.ref_scores)
-            run.e.set_sequences(run.REF, [state.reference])
+            run.set_ref(state.reference)
             if not has_single_indels(state, run):
                 state.converged = True
     elif state.stage == Stage.FRAME:
@@ -474,7 +507,7 @@ def finish_stage(state: RifrafState, run: _Run, params: RifrafParams):   # :937-
             state.ref_scores = Scores(rs.mismatch, rs.insertion * mult, rs.deletion * mult,
                                       rs.codon_insertion, rs.codon_deletion)
             state.reference = RifrafSequence.rescored(state.reference, state.ref_scores)
-            run.e.set_sequences(run.REF, [state.reference])
+            run.set_ref(state.reference)
             log(params, 2, "    NOTE: alignment to reference had single indels. increasing penalty.")
     elif state.stage == Stage.REFINE:
         state.converged = True

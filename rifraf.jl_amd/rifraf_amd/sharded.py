@@ -189,7 +189,7 @@ class ShardedEngine:
         self.e.close()
 
     # ------------------------------------------------------------------
-    def realign(self, slots, seqs, tpls, bws, flags: int) -> np.ndarray:
+    def realign(self, slots, seqs, tpls, bws, flags) -> np.ndarray:
         """Each rank fills the bands of its own slots; per-job scores travel
         in one all-gather of n + 1 doubles (verbatim, so rescore!'s fold is
         exact)."""
@@ -207,7 +207,8 @@ class ShardedEngine:
         buf = np.zeros(n + 1)
         if len(mine):
             try:
-                buf[mine] = self.e.realign(slots[mine], seqs[mine], tpls[mine], bws[mine], flags)
+                fl = flags if np.ndim(flags) == 0 else np.broadcast_to(np.asarray(flags), (n,))[mine]
+                buf[mine] = self.e.realign(slots[mine], seqs[mine], tpls[mine], bws[mine], fl)
             except RifrafError as e:
                 err = str(e)
         buf[n] = 0.0 if err is None else 1.0

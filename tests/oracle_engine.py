@@ -44,12 +44,14 @@ class OracleEngine:
         seqs = np.broadcast_to(seqs, (n,))
         tpls = np.broadcast_to(tpls, (n,))
         bws = np.broadcast_to(bws, (n,))
+        fl = np.broadcast_to(np.asarray(flags, np.int64), (n,))   # one value, or one per job (rf_realign_jobs)
         out = np.empty(n)
         for k in range(n):
             if int(bws[k]) < 1:
                 raise RifrafError("bandwidth must be positive")
 
         def one(k):
+            flags = int(fl[k])
             s = self.seqs[int(seqs[k])]
             t, ver = self.tpls[int(tpls[k])]
             bw = int(bws[k])
@@ -80,6 +82,7 @@ class OracleEngine:
             if B is not None:
                 ent["B"] = (B, None, key, ns, nt)
             bw = key[3]
+            flags = int(fl[k])
             data = ent["A"][0] if flags & RF_FWD else ent["B"][0]
             if flags & RF_FWD:
                 out[k] = data[ns - nt + max(nt - ns, 0) + bw, nt]
