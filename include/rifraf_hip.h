@@ -87,7 +87,7 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_SCORE_MODE   1   /* 0 auto, 1 fused in-kernel fold, 2 split + k_reduce  */
 #define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_segl           */
 #define RF_OPT_LEAN_LDS_KB  4   /* k_score_ws LDS budget in KB (0 = default 160)       */
-#define RF_OPT_BT_GLOBAL    9   /* 1: every backtrace walk in k_backtrace              */
+/* key 9 (RF_OPT_BT_GLOBAL: every walk in the one-lane k_backtrace) removed in round 5 */
 #define RF_OPT_DP_PSPLIT   10   /* lean DP stride-class split mask (-1 auto)           */
 #define RF_OPT_DP_NP8      11   /* 0: H 128..255 bands in k_dp<64> instead of k_dpr<8> */
 #define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
@@ -122,11 +122,16 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    so that about this many workgroups remain
                                    (default 2048; small values: many reads per
                                    workgroup, partials written per read)        */
+#define RF_OPT_DP_SCHED    28   /* DP class launches of one rf_realign call: 0 =
+                                   the largest on the engine stream, the others
+                                   round robin over three side streams; 1 = all
+                                   balanced over the engine stream and two side
+                                   streams by their band stores, largest first */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);
-   keys 21 (128-column k_score_segw) and 25 (k_fuse, the fused forward fill +
-   scoring step) in round 5.  rf_set_option rejects them. */
+   keys 9 (the one-lane k_backtrace walk), 21 (128-column k_score_segw) and 25
+   (k_fuse, the fused forward fill + scoring step) in round 5.  rf_set_option rejects them. */
 int rf_set_option(rf_ctx *ctx, int32_t key, int32_t value);
 int rf_get_option(rf_ctx *ctx, int32_t key, int32_t *value);
 
@@ -440,7 +445,7 @@ int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes
 int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms,
                    double *gather_ms);
 /* Kernel time of the walks of the last rf_backtrace / rf_alignment_proposals
- * call (k_bt_win / k_backtrace / k_aln_props), milliseconds. */
+ * call (k_bt_win), milliseconds. */
 int rf_last_backtrace_ms(const rf_ctx *ctx, double *ms);
 /* Kernel time of the reference's codon score_proposal (k_codon,
  * model.jl:287-383) in the last rf_score call, milliseconds (0 when the call

@@ -2,10 +2,15 @@
 //
 // Kernels (all FP64 max-plus, bit-exact with the reference's evaluation
 // order; no MFMA: the path has no dense contraction):
-//   k_dp        banded forward / reverse Viterbi fill (forward_moves!,
-//               forward!, backward! = reverse forward + flip!)
+//   k_dpr       banded forward / reverse Viterbi fill (forward_moves!,
+//               forward!, backward! = reverse forward + flip!), many tasks
+//               per launch: 16-, 32- or 64-lane tasks, systolic DPP lanes
 //               src/align.jl:50-112 (update), :114-179, :196-202
-//   k_score     dense per-position proposal scoring of every batch read,
+//   k_dpx       the same fill for a few long tasks (H <= 127), one
+//               latency-bound task per wave (the reference's codon DP)
+//   k_dpw / k_dp  very wide bands (edit_distance, align.jl:253-260)
+//   k_score_ws / k_score_segl / k_score
+//               dense per-position proposal scoring of every batch read,
 //               left-folded over the batch in batch order
 //               src/model.jl:227-285 (seq_score_deletion, score_nocodon),
 //               :385-399 (fold)
@@ -13,8 +18,10 @@
 //               proposal  src/model.jl:287-383
 //   k_reduce    ordered fold of per-read partials (split mode)
 //   k_gather    proposal list -> totals (+ reference score, last)
-//   k_backtrace trace recomputed from the stored A band, backtrace +
-//               count_errors  src/align.jl:229-245
+//   k_bt_win    moves recomputed from the stored A band, backtrace +
+//               count_errors (+ alignment_proposals' mask)
+//               src/align.jl:229-245, src/model.jl:458-497
+//   k_tables / k_code_prep / k_aln_* / k_qv  device setup and QV pass
 //
 // Host side: device arenas (sequences, templates, bands), descriptor
 // upload, the C-ABI of include/rifraf_hip.h.
@@ -565,7 +572,7 @@ __device__ __forceinline__ RowRec row_from_above(const RowRec &x, const RowRec &
 // static.  The cell value of the reference's strict-'>' candidate chain
 // (align.jl:43, :77-104) is the maximum of the candidates, and FP64 max of
 // the same sums is exact (no NaN, no signed zero among candidates), so
-// fmax yields bit-identical cells; the move is recomputed in k_backtrace
+// fmax yields bit-identical cells; the move is recomputed in k_bt_win
 // with the strict order.
 // ---------------------------------------------------------------------
 
@@ -702,12 +709,6 @@ __device__ __forceinline__ dvec2 dpl_rd2(const double *R, int u)   // u even
     return *(const dvec2 *)(R + u);
 }
 
-#ifndef DPL_REORDER
-#define DPL_REORDER 0
-#endif
-#ifndef DPL_MASKIN
-#define DPL_MASKIN 0
-#endif
 template <int NP, int PAR, int LPT = 16>
 __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], const RowRec (&row)[NP],
                                          const int (&col)[NP], const double (&lb)[NP],
@@ -722,17 +723,9 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         const double ms = (R.sb == col[r]) ? R.mt : R.mm;
         const double x_ins = PAR ? v1[r] : (r > 0 ? v1[r > 0 ? r - 1 : 0] : E1);
         const double x_del = PAR ? (r < NP - 1 ? v1[r < NP - 1 ? r + 1 : 0] : E1) : v1[r];
-        // DPL_MASKIN: the inactive-diagonal mask on the insert / delete inputs
-        // (off the step-to-step chain) instead of on the cell; an inactive
-        // diagonal then stays -Inf by induction (its own v2 is -Inf)
-        const double is = DPL_MASKIN ? R.is + lb[r] : R.is;
-        const double ds = DPL_MASKIN ? R.ds + lb[r] : R.ds;
-        double raw;
-        if (DPL_REORDER && PAR == 0 && r == 0)   // the exchanged value (E1) enters the max last
-            raw = fmax(fmax(v2[r] + ms, x_del + ds), x_ins + is);
-        else
-            raw = fmax(fmax(v2[r] + ms, x_ins + is), x_del + ds);
-        nv[r] = DPL_MASKIN ? raw : raw + lb[r];
+        // (round 3: the mask on the insert / delete inputs instead of the cell,
+        // and the exchanged value entering the max last, were no faster)
+        nv[r] = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds) + lb[r];
         if (st[r] && !DPL_NO_LDS_OUT)
             Rb[u0 + r * ostep] = nv[r];
     }
@@ -795,11 +788,6 @@ __host__ __device__ constexpr int dpr_pm(int npi, int pmi)
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
-#ifdef DPR_WAVES
-#define DPR_ATTR __attribute__((amdgpu_waves_per_eu(DPR_WAVES)))
-#else
-#define DPR_ATTR
-#endif
 // PM: the largest band row stride P of the launch's tasks (default: the
 // class maximum).  The lean flush issues a fixed dpl_flush_stores(NP, PM)
 // 16-B stores per lane (a static count, so hipcc's wait for the next edge
@@ -817,7 +805,7 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 #define DPR_PFIX 1
 #endif
 template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16, bool PFIX = false>
-__global__ void __launch_bounds__(64) DPR_ATTR
+__global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(LPT >= 32 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
 k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands,
@@ -3324,91 +3312,6 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 }
 
 // ---------------------------------------------------------------------
-// k_backtrace: trace recomputed from the A band (the forward pass's move
-// at (i,j) is the first strictly-best candidate over the stored A values,
-// so re-evaluating the same FP64 sums yields the same move), then
-// backtrace + count_errors (align.jl:229-245).
-// ---------------------------------------------------------------------
-
-__global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
-                            const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
-                            const double *__restrict__ bands, int8_t *__restrict__ moves,
-                            int32_t *__restrict__ nmoves, int32_t *__restrict__ nerr,
-                            int *__restrict__ err)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntasks)
-        return;
-    const BTTask T = tasks[t];
-    const double *A = bands + T.A;
-    const uint8_t *s = bases + T.sb;
-    const uint8_t *tt = bases + T.tb;
-    const double *tb = tabs + T.tab;
-    const int n = T.n, m = T.m;
-    Geo g;
-    g.n = n;
-    g.m = m;
-    g.bw = T.bw;
-    g.H = T.H;
-    g.P = T.P;
-    g.c = max(m - n, 0) + T.bw;
-    const double *t_cins = tb + 4 * (size_t)n + 1;
-    const double *t_cdel = t_cins + T.ncins;
-    const bool skew = T.flags & 2, trim = T.flags & 4;
-    int8_t *out = moves + T.out;
-    int ii = n, jj = m, cnt = 0, errs = 0;
-    while (ii > 0 || jj > 0) {
-        const int sb = ii >= 1 ? s[ii - 1] : 4;
-        const int tbb = jj >= 1 ? tt[jj - 1] : 4;
-        const int ks = max(ii - 1, 0);
-        double ms = (sb == tbb) ? tb[ks] : tb[n + ks];
-        double is = tb[2 * (size_t)n + ks];
-        const double ds = tb[3 * (size_t)n + ii];
-        if (skew && sb != tbb)
-            ms *= 0.99;
-        if (trim && (jj == 0 || jj == m))
-            is = 0.0;
-        double best = -RF_INF, x;
-        int mv = 0;
-        if (g.inband(ii - 1, jj - 1)) {
-            x = g.get(A, ii - 1, jj - 1) + ms;
-            if (x > best) { best = x; mv = 1; }
-        }
-        if (g.inband(ii - 1, jj)) {
-            x = g.get(A, ii - 1, jj) + is;
-            if (x > best) { best = x; mv = 2; }
-        }
-        if (g.inband(ii, jj - 1)) {
-            x = g.get(A, ii, jj - 1) + ds;
-            if (x > best) { best = x; mv = 3; }
-        }
-        if (T.ncins > 0 && ii >= 3 && g.inband(ii - 3, jj)) {
-            x = g.get(A, ii - 3, jj) + t_cins[ii - 3];
-            if (x > best) { best = x; mv = 4; }
-        }
-        if (T.ncdel > 0 && jj >= 3 && g.inband(ii, jj - 3)) {
-            x = g.get(A, ii, jj - 3) + t_cdel[ii];
-            if (x > best) { best = x; mv = 5; }
-        }
-        if (mv == 0 || cnt >= n + m) {
-            set_err(err, 2);  // failed to find a move
-            break;
-        }
-        out[n + m - 1 - cnt] = (int8_t)mv;   // forward order ends at slot n+m-1
-        ++cnt;
-        switch (mv) {
-        case 1: errs += (sb != tbb); ii -= 1; jj -= 1; break;
-        case 2: errs += 1; ii -= 1; break;
-        case 3: errs += 1; jj -= 1; break;
-        case 4: errs += 3; ii -= 3; break;
-        default: errs += 3; jj -= 3; break;
-        }
-    }
-    nmoves[T.idx] = cnt;
-    nerr[T.idx] = errs;
-}
-
-// ---------------------------------------------------------------------
 // k_bt_win: backtrace + count_errors (align.jl:229-245), one wave per
 // alignment, from LDS windows (round 4: codon moves and any band height too --
 // the reference's codon alignment and edit_distance's wide bands).
@@ -3431,8 +3334,8 @@ __global__ void k_backtrace(const BTTask *__restrict__ tasks, int ntasks,
 // box would leave it.  Staging issues every load of a window before the
 // first LDS write (one memory latency per window, not one per element).
 // With a mask, the walk also marks the proposals its alignment implies
-// (moves_to_proposals, model.jl:458-480; k_aln_props fused into the walk --
-// the set union does not depend on the walk direction).
+// (moves_to_proposals, model.jl:458-480; the set union does not depend on
+// the walk direction).
 // Codon moves (align.jl:77-104, TRACE_CODON_INSERT / _DELETE) reach cells
 // 3 diagonals off the walk's: the windows then extend 2 more kappa rows,
 // diagonals and table rows, the box evaluates the two codon candidates after
@@ -3684,7 +3587,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             if (emit) {
                 out[n + m - 1 - (cnt + lane)] = (int8_t)mvk;
                 if (mk) {
-                    // the forward step of this move ends at (ci, cj) (k_aln_props)
+                    // the forward step of this move ends at (ci, cj) (moves_to_proposals)
                     if (mvk == 1 && mism)
                         mk[(size_t)cj * 9 + ksb] = 1;
                     else if (mvk == 2 && do_indels)
@@ -3737,7 +3640,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             if (lane == 0) {
                 out[n + m - 1 - cnt] = (int8_t)mv;
                 if (mk) {
-                    // the forward step of this move ends at (ii, jj) (k_aln_props)
+                    // the forward step of this move ends at (ii, jj) (moves_to_proposals)
                     if (mv == 1 && mism)
                         mk[(size_t)jj * 9 + sb] = 1;
                     else if (mv == 2 && do_indels)
@@ -3757,7 +3660,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             } else if (mv == 3) {
                 errs += 1;
                 --jj;
-            } else if (mv == 4) {   // codon moves propose nothing (k_aln_props)
+            } else if (mv == 4) {   // codon moves propose nothing (model.jl:469-476)
                 errs += 3;
                 ii -= 3;
             } else {
@@ -3774,60 +3677,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
 }
 
 // ---------------------------------------------------------------------
-// k_aln_props: alignment_proposals / moves_to_proposals (model.jl:458-497)
-// on the device.  One lane per batch read walks its forward move list (left
-// by k_backtrace) and marks every proposal the alignment implies in its
-// cluster's dense mask [(m+1) x 9] (slots as rf_score_dense: 0-3 Sub A..T,
-// 4 Del, 5-8 Ins A..T).  The mask is the reference's Set union over the
-// batch; reading it position-major gives the (pos, kind, base) order.
-// ---------------------------------------------------------------------
-struct alignas(16) PropTask {
-    int64_t sb, tb, mv, mask;   // read bases, template bases, moves, mask offset (bytes)
-    int32_t n, m, idx, pad;
-};
-
-__global__ void k_aln_props(const PropTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
-                            const int8_t *__restrict__ moves, const int32_t *__restrict__ nmoves,
-                            uint8_t *__restrict__ mask, int do_indels)
-{
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ntasks)
-        return;
-    const PropTask T = tasks[k];
-    const uint8_t *s = bases + T.sb;
-    const uint8_t *t = bases + T.tb;
-    const int cnt = nmoves[T.idx];
-    const int8_t *mv = moves + T.mv + (T.n + T.m - cnt);   // end-aligned in the n+m slot
-    uint8_t *out = mask + T.mask;
-    int i = 0, j = 0;
-    for (int e = 0; e < cnt; ++e) {
-        switch (mv[e]) {
-        case 1:   // TRACE_MATCH: Substitution(j, s[i]) where the bases differ
-            ++i;
-            ++j;
-            if (s[i - 1] != t[j - 1])
-                out[(size_t)j * 9 + s[i - 1]] = 1;
-            break;
-        case 2:   // TRACE_INSERT: Insertion(j, s[i])
-            ++i;
-            if (do_indels)
-                out[(size_t)j * 9 + 5 + s[i - 1]] = 1;
-            break;
-        case 3:   // TRACE_DELETE: Deletion(j)
-            ++j;
-            if (do_indels)
-                out[(size_t)j * 9 + 4] = 1;
-            break;
-        case 4: i += 3; break;   // codon moves propose nothing (model.jl:469-476)
-        default: j += 3; break;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------
 // k_aln_sums: alignment_error_probs's per-column sums (model.jl:817-840)
-// on the device, from the backtrace moves already there (k_bt_win /
-// k_backtrace).  One workgroup per group (cluster); its reads are walked in
+// on the device, from the backtrace moves already there (k_bt_win).  One workgroup per group (cluster); its reads are walked in
 // batch order, one read at a time: the 256 threads take 256 consecutive
 // moves, a block prefix sum of the (read, consensus) steps gives each move's
 // (i, j), and a MATCH move adds base_distribution(s[i], match[i]) to column
@@ -4382,7 +4233,6 @@ struct Opts {
                                      // bit 1: H 64..127 in 32 lanes)
     int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
                             // 128-B-line rows for all its bands (0: never, 1: always)
-    int bt_global = 0;      // RF_OPT_BT_GLOBAL: 1 = every walk in k_backtrace
     int bt_win_kb = 16;     // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS)
     int stage_kb = 262144;  // RF_OPT_STAGE_KB: rf_set_sequences staging chunk (KB of tables)
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
@@ -4395,6 +4245,7 @@ struct Opts {
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
     int score_wgs = 2048;   // RF_OPT_SCORE_WGS: split-mode k_score_ws takes reads in chunks so that about
                             // this many workgroups remain
+    int dp_sched = 0;       // RF_OPT_DP_SCHED: 1 = DP classes balanced over three streams by their stores
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
@@ -4444,7 +4295,7 @@ struct rf_ctx {
     hipEvent_t ev_block = nullptr;   // blocking-sync event (RF_OPT_SYNC_BLOCK)
     Opts opt;
     uint64_t opt_gen = 0;      // bumped by rf_set_option (scorer plan key)
-    std::vector<BTTask> bt_win, bt_old;   // backtrace descriptors of the last launch
+    std::vector<BTTask> bt_win;   // backtrace descriptors of the last launch
     // host-side plan caches: a repeated call with identical arguments and an
     // unchanged layout reuses the uploaded descriptors (steady-state loops)
     struct {
@@ -4720,7 +4571,6 @@ void load_env_opts(Opts &o)
     if (const char *m = std::getenv("RIFRAF_SCORE_MODE"))
         o.score_mode = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "split") ? 2 : 0;
     o.lean_lds_kb = env_int("RIFRAF_LEAN_LDS_KB", o.lean_lds_kb);
-    o.bt_global = env_int("RIFRAF_BT_GLOBAL", o.bt_global);
     o.dp_psplit = env_int("RIFRAF_DP_PSPLIT", o.dp_psplit);
     o.dp_np8 = env_int("RIFRAF_DP_NO_NP8", 0) ? 0 : 1;
     o.dp_np8_lean = env_int("RIFRAF_DP_NP8_LEAN", o.dp_np8_lean);
@@ -4733,6 +4583,7 @@ void load_env_opts(Opts &o)
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
+    o.dp_sched = env_int("RIFRAF_DP_SCHED", o.dp_sched);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4928,7 +4779,6 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SCORE_MODE: return &o.score_mode;
     case RF_OPT_SCORE_KERNEL: return &o.score_kernel;
     case RF_OPT_LEAN_LDS_KB: return &o.lean_lds_kb;
-    case RF_OPT_BT_GLOBAL: return &o.bt_global;
     case RF_OPT_DP_PSPLIT: return &o.dp_psplit;
     case RF_OPT_DP_NP8: return &o.dp_np8;
     case RF_OPT_DP_NP8_LEAN: return &o.dp_np8_lean;
@@ -4943,6 +4793,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NL64: return &o.dp_nl64;
     case RF_OPT_DP_LAT: return &o.dp_lat;
     case RF_OPT_SCORE_WGS: return &o.score_wgs;
+    case RF_OPT_DP_SCHED: return &o.dp_sched;
     default: return nullptr;
     }
 }
@@ -5921,17 +5772,56 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (launches[i].n > launches[big].n)
             big = i;
     const bool concurrent = launches.size() > 1 && ctx->opt.dp_streams;
+    // stream of each launch: -1 = the main stream, else a side stream
+    std::vector<int> lstream(launches.size(), -1);
+    if (concurrent && ctx->opt.dp_sched == 1 && !lat_first) {
+        // RF_OPT_DP_SCHED 1: the classes balanced over the main stream and two
+        // side streams by their stores (klen * P per task), largest first, so
+        // that each stream's kernels run back to back and the three streams
+        // end together (three streams: the hardware queues a process gets)
+        std::vector<double> w(launches.size(), 0.0);
+        for (size_t i = 0; i < launches.size(); ++i)
+            for (size_t t = launches[i].at; t < launches[i].at + launches[i].n; ++t)
+                w[i] += (double)P.tasks[t].klen * P.tasks[t].P;
+        std::vector<size_t> ord(launches.size());
+        for (size_t i = 0; i < ord.size(); ++i)
+            ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return w[a] > w[b]; });
+        double load[3] = {0.0, 0.0, 0.0};
+        std::vector<int> sof(launches.size());
+        for (size_t i : ord) {
+            int s = 0;
+            for (int k = 1; k < 3; ++k)
+                if (load[k] < load[s])
+                    s = k;
+            load[s] += w[i];
+            sof[i] = s - 1;
+        }
+        // each stream runs its classes smallest first: a class too small to
+        // fill the GPU runs beside the large ones, not alone in the tail
+        std::reverse(ord.begin(), ord.end());
+        std::vector<Launch> sorted;
+        for (size_t i : ord) {
+            lstream[sorted.size()] = sof[i];
+            sorted.push_back(launches[i]);
+        }
+        launches.swap(sorted);
+    } else if (concurrent) {
+        int nside = 0;
+        for (size_t i = 0; i < launches.size(); ++i)
+            if (i != big)
+                lstream[i] = nside++ % 3;
+    }
     if (concurrent)
         HIPCHK(ctx, hipEventRecord(ctx->fork, ctx->stream));
-    int nside = 0;
     std::vector<int> used_side;
     for (size_t i = 0; i < launches.size(); ++i) {
         const Launch &L = launches[i];
         hipStream_t st = ctx->stream;
-        if (concurrent && i != big) {
-            const int si = nside++ % 3;
+        if (lstream[i] >= 0) {
+            const int si = lstream[i];
             st = ctx->side[si];
-            if (nside <= 3) {
+            if (std::find(used_side.begin(), used_side.end(), si) == used_side.end()) {
                 HIPCHK(ctx, hipStreamWaitEvent(st, ctx->fork, 0));
                 used_side.push_back(si);
             }
@@ -6032,35 +5922,16 @@ int rf_realign_jobs(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const int32
     return realign_impl(ctx, njobs, slot, seq, tpl, bw, flags, out_score);
 }
 
-// Every walk runs in k_bt_win (round 4: codon alignments and bands of any
-// height too); RF_OPT_BT_GLOBAL = 1 sends them all to k_backtrace instead
-static bool bt_windowed(const BTTask &) { return true; }
-
 // Launch the backtraces of `tasks` (moves into scratch[3] at t.out, counts in
-// scratch[4]); with d_mask, the windowed walks also mark alignment proposals.
+// scratch[4]) in k_bt_win (round 4: codon alignments and bands of any height
+// too); with d_mask, the walks also mark alignment proposals.
 static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d_mask, int do_indels)
 {
     const int32_t nslots = (int32_t)tasks.size();
-    std::vector<BTTask> &win = ctx->bt_win, &old = ctx->bt_old;   // alive until the caller's sync
-    win.clear();
-    old.clear();
-    for (const auto &t : tasks)
-        (bt_windowed(t) ? win : old).push_back(t);
-    if (ctx->opt.bt_global && !d_mask) {   // RF_OPT_BT_GLOBAL: every walk in k_backtrace
-        old = tasks;
-        win.clear();
-    }
+    std::vector<BTTask> &win = ctx->bt_win;   // alive until the caller's sync
+    win = tasks;
     int32_t *d_cnt = (int32_t *)ctx->scratch[4].p;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
-    if (!old.empty()) {
-        if (int e = upload(ctx, ctx->scratch[0], old))
-            return e;
-        hipLaunchKernelGGL(k_backtrace, dim3((unsigned)((old.size() + 63) / 64)), dim3(64), 0, ctx->stream,
-                           (const BTTask *)ctx->scratch[0].p, (int)old.size(),
-                           (const uint8_t *)ctx->bytes_arena.d, (const double *)ctx->tab_arena.d,
-                           (const double *)ctx->band_arena.d, (int8_t *)ctx->scratch[3].p, d_cnt,
-                           d_cnt + nslots, ctx->d_err);
-    }
     if (!win.empty()) {
         if (int e = upload(ctx, ctx->scratch[16], win))
             return e;
@@ -6179,7 +6050,6 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     std::vector<int64_t> offs;
     if (int e = build_bt_tasks(ctx, nslots, slots, tasks, offs))
         return e;
-    std::vector<PropTask> ptasks;   // reads whose walk runs in k_backtrace (then k_aln_props)
     int64_t mask_total = 0;
     for (int32_t g = 0; g < ngroups; ++g) {
         int32_t tpl = -1, m = 0;
@@ -6190,17 +6060,6 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
             tpl = b.tpl;
             m = b.m;
             tasks[k].mask = mask_total;
-            if (!bt_windowed(tasks[k])) {
-                PropTask t{};
-                t.sb = ctx->seqs[b.seq].bases.off;
-                t.tb = ctx->tpls[b.tpl].bases.off;
-                t.mv = offs[k];
-                t.mask = mask_total;
-                t.n = b.n;
-                t.m = b.m;
-                t.idx = k;
-                ptasks.push_back(t);
-            }
         }
         if (slot_off[g + 1] > slot_off[g])
             mask_total += (int64_t)(m + 1) * 9;
@@ -6210,17 +6069,9 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     if (int e = ensure_buf(ctx, ctx->scratch[2], std::max<int64_t>(mask_total, 16)))
         return e;
     HIPCHK(ctx, hipMemsetAsync(ctx->scratch[2].p, 0, mask_total, ctx->stream));
-    // 2. the walks; windowed ones mark the mask as they go (k_aln_props fused)
+    // 2. the walks mark the mask as they go
     if (int e = launch_backtraces(ctx, tasks, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0))
         return e;
-    if (!ptasks.empty()) {
-        if (int e = upload(ctx, ctx->scratch[1], ptasks))
-            return e;
-        hipLaunchKernelGGL(k_aln_props, dim3((unsigned)((ptasks.size() + 63) / 64)), dim3(64), 0, ctx->stream,
-                           (const PropTask *)ctx->scratch[1].p, (int)ptasks.size(),
-                           (const uint8_t *)ctx->bytes_arena.d, (const int8_t *)ctx->scratch[3].p,
-                           (const int32_t *)ctx->scratch[4].p, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0);
-    }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, stream_wait(ctx));

@@ -1,7 +1,9 @@
 #!/usr/bin/env python
 """DP fill time alone at the c4 shape (bench.make_workload: clusters of 50
 reads x 1.5 kb, bw 9; default 1250 clusters), for A/B-timing library builds
-(RIFRAF_HIP_LIB).  Prints one JSON line: per-call realign(FWD|BWD) ms."""
+(RIFRAF_HIP_LIB), or of option settings in one process, interleaved
+(argv[2], e.g. "dp_sched=0/1").  Prints one JSON line: per-call
+realign(FWD|BWD) ms per setting."""
 import json, os, sys
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [REPO, os.path.join(REPO, "rifraf.jl_amd")]
@@ -19,9 +21,16 @@ for a in range(0, len(reads), 4096):
 e.set_templates(0, [t for t, _ in clusters])
 sl = np.arange(len(reads), dtype=np.int32)
 bws = np.full(len(reads), 9, np.int32)
-ms = []
-for _ in range(8):
-    e.realign(sl, sl, tpl, bws, RF_FWD | RF_BWD)
-    ms.append(e.last_timing()[0])
-print(json.dumps({"clusters": nclu, "dp_ms": [round(x, 3) for x in ms[2:]], "median": float(np.median(ms[2:])),
+opt, vals = (sys.argv[2].split("=") if len(sys.argv) > 2 else ("dp_sched", "0"))
+vals = [int(v) for v in vals.split("/")]
+ms = {v: [] for v in vals}
+for rnd in range(3):
+    for v in vals:
+        e.set_option(opt, v)
+        for _ in range(5):
+            e.realign(sl, sl, tpl, bws, RF_FWD | RF_BWD)
+            ms[v].append(e.last_timing()[0])
+print(json.dumps({"clusters": nclu, "option": opt,
+                  "dp_ms": {v: [round(x, 3) for x in ms[v]] for v in vals},
+                  "median": {v: float(np.median([x for k, x in enumerate(ms[v]) if k % 5])) for v in vals},
                   "lib": os.environ.get("RIFRAF_HIP_LIB", "default")}), flush=True)

@@ -888,8 +888,7 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     walk leaves them) against the oracle's backtrace and count_errors, and the
     fused proposal marking against the host moves_to_proposals union, on long
     reads (many windows), wide bands (small windows: P up to 129) and reads
-    longer / shorter than the template; option bt_global=1 (k_backtrace for
-    every walk) gives the same moves."""
+    longer / shorter than the template."""
     from rifraf_amd.align import moves_to_proposals_np
     rng = np.random.default_rng(L + bw)
     t = random_seq(L, rng)
@@ -910,18 +909,13 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
     opts("bt_win_kb", win_kb)
-    opts("bt_global", 0)
     got, nerr = engine.backtrace(np.arange(n))
-    opts("bt_global", 1)
-    legacy, nerr_l = engine.backtrace(np.arange(n))
-    opts("bt_global", 0)
     exp_mask = np.zeros((L + 1, 9), np.uint8)
     for k, s in enumerate(seqs):
         _, mv = oracle.forward(t, s, moves=True, bandwidth=bw)
         ref = oracle.backtrace(mv, len(s) + 1, L + 1, bw)
         np.testing.assert_array_equal(got[k], ref)
-        np.testing.assert_array_equal(legacy[k], ref)
-        assert nerr[k] == nerr_l[k] == oracle.count_errors(ref, t, s.seq)
+        assert nerr[k] == oracle.count_errors(ref, t, s.seq)
         kk, p, b = moves_to_proposals_np(ref, t, s.seq)
         exp_mask[p, np.where(kk == 0, b, np.where(kk == 2, 4, 5 + b))] = 1
     np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
@@ -933,7 +927,7 @@ def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
     TRACE_CODON_INSERT / _DELETE leave the box, the windows cover the +-3
     predecessors) and bands of any height (H = 301 .. 281 here, above the old
     255 limit): moves and error counts against the oracle's trace band, and
-    the same moves as k_backtrace (bt_global = 1); alignment_proposals' fused
+    alignment_proposals' fused
     marking against the host union (codon moves propose nothing)."""
     from rifraf_amd.align import moves_to_proposals_np
     rng = np.random.default_rng(L * 3 + bw)
@@ -954,11 +948,7 @@ def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
-    opts("bt_global", 0)
     got, nerr = engine.backtrace(np.arange(n))
-    opts("bt_global", 1)
-    legacy, nerr_l = engine.backtrace(np.arange(n))
-    opts("bt_global", 0)
     exp_mask = np.zeros((L + 1, 9), np.uint8)
     ncod = 0
     for k, s in enumerate(seqs):
@@ -966,8 +956,7 @@ def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
         ref = oracle.backtrace(mv, len(s) + 1, L + 1, bw)
         ncod += int(np.sum(ref >= 4))
         np.testing.assert_array_equal(got[k], ref)
-        np.testing.assert_array_equal(legacy[k], ref)
-        assert nerr[k] == nerr_l[k] == oracle.count_errors(ref, t, s.seq)
+        assert nerr[k] == oracle.count_errors(ref, t, s.seq)
         kk, p, b = moves_to_proposals_np(ref, t, s.seq)
         exp_mask[p, np.where(kk == 0, b, np.where(kk == 2, 4, 5 + b))] = 1
     if codon:
@@ -1106,7 +1095,7 @@ def test_removed_option_keys_rejected(engine):
     """Scorer-variant keys removed in rounds 3 and 5 (include/rifraf_hip.h)
     are refused with an error, not silently accepted."""
     from rifraf_amd.engine import RifrafError
-    for key in (3, 5, 6, 7, 8, 14, 20, 21, 25):
+    for key in (3, 5, 6, 7, 8, 9, 14, 20, 21, 25):
         assert engine.lib.rf_set_option(engine.ctx, key, 1) != 0
         assert "unknown option" in engine.lib.rf_last_error(engine.ctx).decode()
     with pytest.raises(KeyError):
