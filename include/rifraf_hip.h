@@ -122,11 +122,6 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    so that about this many workgroups remain
                                    (default 2048; small values: many reads per
                                    workgroup, partials written per read)        */
-#define RF_OPT_DP_SCHED    28   /* DP class launches of one rf_realign call: 0 =
-                                   the largest on the engine stream, the others
-                                   round robin over three side streams; 1 = all
-                                   balanced over the engine stream and two side
-                                   streams by their band stores, largest first */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -4245,7 +4245,6 @@ struct Opts {
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
     int score_wgs = 2048;   // RF_OPT_SCORE_WGS: split-mode k_score_ws takes reads in chunks so that about
                             // this many workgroups remain
-    int dp_sched = 0;       // RF_OPT_DP_SCHED: 1 = DP classes balanced over three streams by their stores
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
@@ -4583,7 +4582,6 @@ void load_env_opts(Opts &o)
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
-    o.dp_sched = env_int("RIFRAF_DP_SCHED", o.dp_sched);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4793,7 +4791,6 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NL64: return &o.dp_nl64;
     case RF_OPT_DP_LAT: return &o.dp_lat;
     case RF_OPT_SCORE_WGS: return &o.score_wgs;
-    case RF_OPT_DP_SCHED: return &o.dp_sched;
     default: return nullptr;
     }
 }
@@ -5772,41 +5769,12 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (launches[i].n > launches[big].n)
             big = i;
     const bool concurrent = launches.size() > 1 && ctx->opt.dp_streams;
-    // stream of each launch: -1 = the main stream, else a side stream
+    // stream of each launch: -1 = the main stream, else a side stream.  (Round
+    // 5: balancing the classes over the main stream and two side streams by
+    // their stores, largest or smallest first, was slower at c4: 8.42-8.48
+    // against 8.25 ms, profiles/r05l_exp_dp_sched.jsonl.)
     std::vector<int> lstream(launches.size(), -1);
-    if (concurrent && ctx->opt.dp_sched == 1 && !lat_first) {
-        // RF_OPT_DP_SCHED 1: the classes balanced over the main stream and two
-        // side streams by their stores (klen * P per task), largest first, so
-        // that each stream's kernels run back to back and the three streams
-        // end together (three streams: the hardware queues a process gets)
-        std::vector<double> w(launches.size(), 0.0);
-        for (size_t i = 0; i < launches.size(); ++i)
-            for (size_t t = launches[i].at; t < launches[i].at + launches[i].n; ++t)
-                w[i] += (double)P.tasks[t].klen * P.tasks[t].P;
-        std::vector<size_t> ord(launches.size());
-        for (size_t i = 0; i < ord.size(); ++i)
-            ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return w[a] > w[b]; });
-        double load[3] = {0.0, 0.0, 0.0};
-        std::vector<int> sof(launches.size());
-        for (size_t i : ord) {
-            int s = 0;
-            for (int k = 1; k < 3; ++k)
-                if (load[k] < load[s])
-                    s = k;
-            load[s] += w[i];
-            sof[i] = s - 1;
-        }
-        // each stream runs its classes smallest first: a class too small to
-        // fill the GPU runs beside the large ones, not alone in the tail
-        std::reverse(ord.begin(), ord.end());
-        std::vector<Launch> sorted;
-        for (size_t i : ord) {
-            lstream[sorted.size()] = sof[i];
-            sorted.push_back(launches[i]);
-        }
-        launches.swap(sorted);
-    } else if (concurrent) {
+    if (concurrent) {
         int nside = 0;
         for (size_t i = 0; i < launches.size(); ++i)
             if (i != big)
