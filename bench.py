@@ -534,31 +534,39 @@ def run_e2e(args, rank, world, gpu, dist, coll):
     bopt = dict(engines=engs, wave=max(1, args.e2e_wave), init_exclusive=bool(args.e2e_init_exclusive))
     rifraf_batch(clusters, params=params, **bopt)
     cold = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    res = rifraf_batch(clusters, params=params, **bopt)
-    elapsed = time.perf_counter() - t0
-    # the same steady-state run with this rank held to 2 host cores -- its
-    # share at 8 ranks on the GPU box's 16 (every thread of the process pinned
-    # in place, no relaunch); the library's worker pools follow the mask
+    # steady state: three rounds of (unpinned run, run with this rank held to
+    # 2 host cores -- its share at 8 ranks on the GPU box's 16; every thread
+    # of the process pinned in place, no relaunch; the library's worker pools
+    # follow the mask), medians of each (one run of either varies by ~10 %
+    # between rounds on one box, profiles/r05l_e2e_pinned.jsonl)
     pin = pin_rate = None
-    if args.e2e_pin_cores > 0:
-        allowed = sorted(os.sched_getaffinity(0))
-        if len(allowed) > args.e2e_pin_cores:
-            k = args.e2e_pin_cores
-            pin = allowed[(rank * k) % len(allowed):][:k] or allowed[:k]
+    allowed = sorted(os.sched_getaffinity(0))
+    if args.e2e_pin_cores > 0 and len(allowed) > args.e2e_pin_cores:
+        k = args.e2e_pin_cores
+        pin = allowed[(rank * k) % len(allowed):][:k] or allowed[:k]
+    runs, pin_runs, same_pin = [], [], True
+    res = None
+    for _ in range(3 if pin else 1):
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        r_ = rifraf_batch(clusters, params=params, **bopt)
+        runs.append(time.perf_counter() - t0)
+        res = res or r_
+        if pin:
             saved = pin_threads(pin)
             try:
                 if dist is not None:
                     dist.barrier()
                 t0 = time.perf_counter()
                 res_pin = rifraf_batch(clusters, params=params, **bopt)
-                pin_s = time.perf_counter() - t0
+                pin_runs.append(time.perf_counter() - t0)
             finally:
                 unpin_threads(saved)
-            same_pin = all(np.array_equal(a.consensus, b.consensus) for a, b in zip(res, res_pin))
-            pin_rate = (pin_s, same_pin)
+            same_pin = same_pin and all(np.array_equal(a.consensus, b.consensus) for a, b in zip(res, res_pin))
+    elapsed = float(np.median(runs))
+    if pin:
+        pin_rate = (float(np.median(pin_runs)), same_pin)
     ref = rifraf_batch(clusters[:2], params=params, engine=engs[0], native=False)
     same = all(np.array_equal(a.consensus, b.consensus) and a.state.score == b.state.score and
                qv_close(a, b) for a, b in zip(res[:2], ref))
@@ -576,8 +584,9 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "clusters_per_s_per_gpu": tot[0] / elapsed / max(world, 1), "ranks": world,
             "clusters": int(tot[0]), "seconds": elapsed,
             "cold_clusters_per_s": tot[0] / cold,
-            "timing": "steady state: the second full run over the clusters (the first, 'cold', also allocates "
-                      "the band arena); host setup from reads included, read simulation excluded",
+            "timing": "steady state: the median of three full runs over the clusters after the first ('cold', "
+                      "which also allocates the band arena), alternating with the pinned runs; host setup from "
+                      "reads included, read simulation excluded",
             "processes_per_gpu": getattr(args, "processes_per_gpu", 1),
             "engines_per_gpu": ne, "wave": bopt["wave"], "init_exclusive": bopt["init_exclusive"],
             "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; waves of clusters taken "
@@ -591,6 +600,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "same_as_python_stage_machine": tot[3] == world,
             "same_as_python_stage_machine_note": "consensus and score bit-identical; QVs (device quality pass) "
                                                  "within 1e-12 relative + 1e-15 absolute",
+            "runs_s": runs, "pinned_runs_s": pin_runs,
             "pinned": None if pin_rate is None else {
                 "cores": len(pin), "clusters_per_s": tot[0] / pin_s, "ratio_to_unpinned": elapsed / pin_s,
                 "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(pin_rate[1]),

@@ -804,17 +804,16 @@ extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 #ifndef DPR_PFIX
 #define DPR_PFIX 1
 #endif
-template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16, bool PFIX = false>
-__global__ void __launch_bounds__(64)
-__attribute__((amdgpu_waves_per_eu(LPT >= 32 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
-k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
-      const double *__restrict__ tabs, double *__restrict__ bands,
-      double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink,
-      const double *__restrict__ lut)
+template <int NP, bool LEAN, int PM, int LPT, bool PFIX>
+__device__ __forceinline__ void dpr_body(const int blk, const DPTask *__restrict__ tasks, int ntasks,
+                                         const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
+                                         double *__restrict__ bands, double *__restrict__ out_score,
+                                         int *__restrict__ err, double *__restrict__ sink,
+                                         const double *__restrict__ lut)
 {
     constexpr int DPL_B = dpl_b(NP, LPT);
     const int q = threadIdx.x & (LPT - 1);
-    const int tid = blockIdx.x * (64 / LPT) + threadIdx.x / LPT;
+    const int tid = blk * (64 / LPT) + threadIdx.x / LPT;
     DPTask T = {};
     if (tid < ntasks)
         T = tasks[tid];
@@ -1257,6 +1256,17 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     }
     if (FLAT && eflag)
         set_err(err, 1);  // "new score is invalid"
+}
+
+template <int NP, bool LEAN, int PM = dpl_pmax(NP), int LPT = 16, bool PFIX = false>
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(LPT >= 32 ? DPR_WPE64 : (NP == 1 ? DPR_WPE1 : 1))))
+k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
+      const double *__restrict__ tabs, double *__restrict__ bands,
+      double *__restrict__ out_score, int *__restrict__ err, double *__restrict__ sink,
+      const double *__restrict__ lut)
+{
+    dpr_body<NP, LEAN, PM, LPT, PFIX>(blockIdx.x, tasks, ntasks, bases, tabs, bands, out_score, err, sink, lut);
 }
 
 // ---------------------------------------------------------------------
@@ -5749,6 +5759,13 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (P.nww)
             launches.push_back({10, at, P.nww});
     }
+    // (Round 5: the lean 16-lane classes as ONE launch -- a kernel choosing the
+    // class body per block, dynamic LDS of the largest class -- was slower:
+    // c4 DP 9.86 against 8.75 ms, profiles/r05p_exp_dp_merge.jsonl; splitting
+    // the lean NP = 2 class by stride too: 9.61 against 8.72 ms,
+    // r05o_exp_dp_psplit.jsonl.  Concurrent launches pack workgroups of
+    // different LDS sizes on a CU; one launch holds every workgroup to the
+    // largest.)
     if (int e = ensure_buf(ctx, ctx->scratch[7], 4 * (size_t)dpl_task_bytes(4)))  // lean padding-task sink
         return e;
     if (P.ng) {
