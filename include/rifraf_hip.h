@@ -85,7 +85,7 @@ const char *rf_last_error(const rf_ctx *ctx);
  * are read once from the RIFRAF_* environment at rf_create.  No reference
  * counterpart (the reference has one code path). */
 #define RF_OPT_SCORE_MODE   1   /* 0 auto, 1 fused in-kernel fold, 2 split + k_reduce  */
-#define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_segl           */
+#define RF_OPT_SCORE_KERNEL 2   /* 0 auto, 1 general k_score, 2 k_score_segl, 3 k_score_ws whenever it fits */
 #define RF_OPT_LEAN_LDS_KB  4   /* k_score_ws LDS budget in KB (0 = default 160)       */
 /* key 9 (RF_OPT_BT_GLOBAL: every walk in the one-lane k_backtrace) removed in round 5 */
 #define RF_OPT_DP_PSPLIT   10   /* lean DP stride-class split mask (-1 auto)           */

@@ -4237,7 +4237,7 @@ struct CodeDict {
 #endif
 struct Opts {
     int score_mode = 0;     // RF_OPT_SCORE_MODE: 0 auto, 1 fused, 2 split
-    int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg
+    int score_kernel = 0;   // RF_OPT_SCORE_KERNEL: 0 auto, 1 general, 2 seg, 3 ws (k_score_ws when it fits)
     int lean_lds_kb = 0;    // RF_OPT_LEAN_LDS_KB: k_score_ws LDS budget (0 = default 160 KB)
     int dp_wide = DP_WIDE_DEFAULT;   // RF_OPT_DP_WIDE: wide lean tasks (bit 0: H 128..255 in 64 lanes,
                                      // bit 1: H 64..127 in 32 lanes)
@@ -4576,7 +4576,7 @@ int env_int(const char *name, int dflt)
 void load_env_opts(Opts &o)
 {
     if (const char *k = std::getenv("RIFRAF_SCORE_KERNEL"))
-        o.score_kernel = !std::strcmp(k, "general") ? 1 : !std::strcmp(k, "seg") ? 2 : 0;
+        o.score_kernel = !std::strcmp(k, "general") ? 1 : !std::strcmp(k, "seg") ? 2 : !std::strcmp(k, "ws") ? 3 : 0;
     if (const char *m = std::getenv("RIFRAF_SCORE_MODE"))
         o.score_mode = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "split") ? 2 : 0;
     o.lean_lds_kb = env_int("RIFRAF_LEAN_LDS_KB", o.lean_lds_kb);
@@ -4611,7 +4611,20 @@ ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool a
         // (measured at c4: 128 chain lanes (two workgroups per CU) +14 %,
         // 320 / 384 chain lanes +50 % scoring time)
         const int lds = std::max((o.lean_lds_kb > 0 ? o.lean_lds_kb : 160) * 1024 / 8, need1);
-        if (lds <= 160 * 1024 / 8) {
+        // Round 5: a read whose 256-column window exceeds LDS runs in sub-
+        // windows over a half (or less) of the chain lanes, the others idle;
+        // when such reads hold most of the launch's cells, the segment scorer
+        // (LDS independent of H) is faster -- configs[2]'s doubled bands
+        // (bw 18, H ~ 37-51): 1.50 -> 0.65 ms per dense pass,
+        // profiles/r05q_c3_score_kernel.jsonl
+        double wide = 0.0, all = 0.0;
+        for (const auto &R : reads) {
+            const double w = (double)R.n * R.H;
+            all += w;
+            if (lean_need(256, R.H, R.P) > lds)
+                wide += w;
+        }
+        if (lds <= 160 * 1024 / 8 && (o.score_kernel == 3 || !(2.0 * wide > all))) {
             p.lean = true;
             p.lds = lds;
             return p;

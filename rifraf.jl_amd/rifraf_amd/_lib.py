@@ -81,7 +81,7 @@ OPTIONS = {"score_mode": 1, "score_kernel": 2, "lean_lds_kb": 4, "dp_psplit": 10
            "score_wgs": 27}
 # symbolic values of the enum-like options
 OPTION_VALUES = {"score_mode": {"auto": 0, "fused": 1, "split": 2},
-                 "score_kernel": {"auto": 0, "general": 1, "seg": 2}}
+                 "score_kernel": {"auto": 0, "general": 1, "seg": 2, "ws": 3}}
 
 
 

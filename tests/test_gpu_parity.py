@@ -620,12 +620,14 @@ SCORER_CONFIGS = [
     ("seg", None),       # row-segment scorer (wide bands) on every shape: k_score_segl (64 columns)
     ("seglodd", None),   # k_score_segl over odd-stride rows only (band_pad 0: 9-chunk loader)
     ("seglpad", None),   # k_score_segl with every band line-padded (band_pad 1)
-    (None, None),        # k_score_ws (the default for these shapes)
-    (None, "8"),         # windows exceed the budget: sub-passes over fewer lanes
-    (None, "12"),
-    (None, "24"),
-    (None, "40"),
-    (None, "60"),
+    (None, None),        # auto: k_score_ws, or k_score_segl when most cells need sub-windows
+    ("ws", None),        # k_score_ws whenever it fits
+    ("ws", "8"),         # windows exceed the budget: sub-passes over fewer lanes
+    ("ws", "12"),
+    ("ws", "24"),
+    ("ws", "40"),
+    ("ws", "60"),
+    (None, "24"),        # auto under a small budget: k_score_segl
 ]
 
 
@@ -637,6 +639,7 @@ def test_score_ws_split_read_chunks(engine, opts, wgs):
     ordered fold equals the one-read-per-workgroup launch and the oracle."""
     import oracle
     opts("score_mode", "split")
+    opts("score_kernel", "ws")
     opts("score_wgs", wgs)
     rng = np.random.default_rng(77)
     tpls = [random_seq(L, rng) for L in (700, 300)]
