@@ -179,6 +179,16 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier ordering LDS only: the fences name the local address
+// space, so the wait before s_barrier is lgkmcnt(0) -- a wave's global
+// stores in flight are not drained (vmcnt counts loads and stores alike).
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---------------------------------------------------------------------
 // k_dp: anti-diagonal wavefront DP fill
 //
@@ -1429,8 +1439,9 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 constexpr int DPX_W = 72;       // doubles per LDS band row: 2 pad | 64 lanes | 6 pad (-Inf)
 constexpr int DPX_RING = 256;   // staged rows / columns: 4 blocks of 64
 struct DpxStage {
-    double mt, mm, is, ds, ci, cd;
-    int sb, col;
+    RawRow r;
+    int col;
+    bool colok;
 };
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1477,7 +1488,7 @@ __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, in
 // tables).  <false, false> takes the latency-mode lean tasks (finite tables,
 // no codon / skew / trim, RF_OPT_DP_LAT), <true, true> every other task.
 template <bool CODON, bool CHECK>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(128)
 k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
       int *__restrict__ err)
@@ -1485,7 +1496,11 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     __shared__ dvec2 s_mtmm[DPX_RING], s_isds[DPX_RING], s_cicd[CODON ? DPX_RING : 1];
     __shared__ int s_sb[DPX_RING], s_col[DPX_RING];
     __shared__ double s_band[CODON ? 4 * DPX_W : 1];
-    const int q = threadIdx.x;
+    // wave 0 fills the band; wave 1 stages the edge records (round 5: its
+    // loads' waits are its own, so the filling wave never waits on vmcnt,
+    // which would drain its band stores too)
+    const int q = threadIdx.x & 63;
+    const bool loader = threadIdx.x >= 64;
     const DPTask T = tasks[blockIdx.x];   // one task per workgroup
     const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
     const bool codon = CODON && (T.ncins > 0 || T.ncdel > 0);
@@ -1498,33 +1513,34 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     // step changes exec for its store (the host keeps K * P * 8 < 2^31)
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc(bands + T.band, 0, (int)((int64_t)K * T.P * 8), 0x00020000);
-    if (CODON)
+    if (CODON && !loader)
         for (int e = q; e < 4 * DPX_W; e += 64)
             s_band[e] = -RF_INF;
 
     // block b: rows R = P + q + par in [64b, 64b + 64) (read row R - c) and
     // columns J = P - q + 64 in [64b, 64b + 64) (template column J - 64)
+    // A block's loads are held raw (load_row_raw) until the block is put in
+    // LDS a chunk later, and their range selects (and the skew factor) are
+    // applied there: a select right after the loads made hipcc wait for them
+    // at once, draining every band store in flight (vmcnt counts both).
     auto stage_load = [&](int b) {
-        const RowRec r = load_row_flat(T, rev, sbase, tb, 64 * b + q - T.c, codon);
         DpxStage s;
-        s.mt = r.mt;
-        s.mm = skew ? r.mm * 0.99 : r.mm;
-        s.is = r.is;
-        s.ds = r.ds;
-        s.ci = r.ci;
-        s.cd = r.cd;
-        s.sb = r.sb;
-        s.col = load_col_flat(T, rev, tbase, 64 * b + q - 64);
+        s.r = load_row_raw(T, rev, sbase, tb, 64 * b + q - T.c, codon);
+        const int jj = 64 * b + q - 64;
+        const int jc = min(max(jj, 1), max(T.m, 1));
+        s.col = tbase[rev ? max(T.m - jc, 0) : jc - 1];
+        s.colok = jj >= 1 && jj <= T.m;
         return s;
     };
     auto stage_put = [&](int b, const DpxStage &s) {
         const int i = (64 * b + q) & (DPX_RING - 1);
-        s_mtmm[i] = dvec2{s.mt, s.mm};
-        s_isds[i] = dvec2{s.is, s.ds};
+        const RowRec r = row_val(s.r);
+        s_mtmm[i] = dvec2{r.mt, skew ? r.mm * 0.99 : r.mm};
+        s_isds[i] = dvec2{r.is, r.ds};
         if (CODON)
-            s_cicd[i] = dvec2{s.ci, s.cd};
-        s_sb[i] = s.sb;
-        s_col[i] = s.col;
+            s_cicd[i] = dvec2{r.ci, r.cd};
+        s_sb[i] = r.sb;
+        s_col[i] = s.colok ? s.col : 4;
     };
 
     // interior [klo, khi]: every diagonal with cells in the matrix has its
@@ -1557,10 +1573,23 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     const int klo = __builtin_amdgcn_readfirstlane(__all(ok) ? lo : INT_MAX);
     const int khi = __builtin_amdgcn_readfirstlane(hi);
 
-    stage_put(0, stage_load(0));
-    stage_put(1, stage_load(1));
-    DpxStage nxt = stage_load(2);
-    wave_sync();
+    const int npairs = (K + 3) >> 2;
+    if (loader) {
+        // blocks 0-2 before the fill starts; block t + 3 during chunk t (ring
+        // slot of block t - 1, which chunk t no longer reads), one barrier
+        // per chunk boundary 1 .. nch - 1
+        stage_put(0, stage_load(0));
+        stage_put(1, stage_load(1));
+        stage_put(2, stage_load(2));
+        lds_barrier();
+        const int nch = (npairs + 31) >> 5;
+        for (int t = 0; t + 1 < nch; ++t) {
+            stage_put(t + 3, stage_load(t + 3));
+            lds_barrier();
+        }
+        return;
+    }
+    lds_barrier();
 
     // per parity: byte offset of this lane's band element in a kappa row
     // (reverse: flipped), or past the band when the row does not hold it
@@ -1585,7 +1614,6 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     // the codon neighbours of the next step, read one step ahead (kappa = 0:
     // ring row 1, still -Inf)
     double cy_ci = CODON ? s_band[DPX_W + 2 + q - 2] : 0.0, cy_cd = CODON ? s_band[DPX_W + 2 + q + 1] : 0.0;
-    const int npairs = (K + 3) >> 2;
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
@@ -1595,13 +1623,13 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
     const long long dg_c0 = clock64(), dg_w0 = wall_clock64();   // diagnostic builds only
 #endif
+    // byte offset of kappa row 4u (reverse: K - 1 - 4u), advanced once per
+    // pair of periods (the per-step select and multiply off the loop)
+    const int drow = rev ? -(int)rowb : (int)rowb;
+    unsigned rob = rev ? rowb * (unsigned)(K - 1) : 0u;
     for (int u = 0; u < npairs; ++u) {
-        if ((u & 31) == 0) {   // chunk t = u / 32 (64 periods): block t + 2 in, t + 3 loads
-            const int t = u >> 5;
-            stage_put(t + 2, nxt);
-            nxt = stage_load(t + 3);
-            wave_sync();
-        }
+        if ((u & 31) == 0 && u > 0)   // chunk t = u / 32 (64 periods): block t + 2 is in
+            lds_barrier();
         // the next pair's records (rows <= 2u + 67: block t + 2 at most, in LDS)
         const int r1 = (2 * u + q + 3) & (DPX_RING - 1), r2 = (2 * u + q + 4) & (DPX_RING - 1);
         const int j0 = (2 * u - q + 66) & (DPX_RING - 1), j1 = (2 * u - q + 67) & (DPX_RING - 1);
@@ -1644,7 +1672,7 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                                                                eflag, fval, fset);
             if (CODON)
                 s_band[S * DPX_W + 2 + q] = v;
-            const unsigned ro = rowb * (unsigned)(rev ? K - 1 - k : k);
+            const unsigned ro = rob + (unsigned)(S * drow);   // = rowb * (rev ? K - 1 - k : k)
             const unsigned vo = PAR ? vo1 : vo0;
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 1)
             if (!FAST)   // diagnostic builds only (wrong bands): no interior band stores
@@ -1679,6 +1707,7 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         b_sb = nb_sb;
         col0 = ncol0;
         col1 = ncol1;
+        rob += (unsigned)(4 * drow);
     }
     (void)ntasks;
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
@@ -5847,11 +5876,11 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                                (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 34) {
             // few non-lean tasks (H <= 127): one latency-bound task per wave (k_dpx)
-            hipLaunchKernelGGL((k_dpx<true, true>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
+            hipLaunchKernelGGL((k_dpx<true, true>), dim3(n), dim3(128), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
                                d_bands, d_out, ctx->d_err);
         } else if (L.kind == 35) {
             // latency mode: lean tasks of H <= 127, one latency-bound task per wave
-            hipLaunchKernelGGL((k_dpx<false, false>), dim3(n), dim3(64), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
+            hipLaunchKernelGGL((k_dpx<false, false>), dim3(n), dim3(128), 0, st, d_tasks + L.at, n, d_bases, d_tabs,
                                d_bands, d_out, ctx->d_err);
         } else if (L.kind >= 32) {
             // task-width classes, both NP 2: 32 = 64 lanes (H <= 255), 33 = 32 lanes
