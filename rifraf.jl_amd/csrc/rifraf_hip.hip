@@ -1305,6 +1305,7 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
       const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
       int *__restrict__ err, int ring_ld)
 {
+    constexpr int DPW_PPL = (DPW_MAXH / 2 + NT) / NT;   // band pairs per lane and step (at most)
     extern __shared__ __attribute__((aligned(16))) double smem[];   // value ring: 3 rows of ring_ld
     __shared__ dvec2 s_mtmm[DPW_RR], s_isds[DPW_RR];
     __shared__ uint8_t s_sb[DPW_RR], s_col[DPW_RR];
@@ -1374,10 +1375,34 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
         const double *r1 = smem + ((k + 2) % 3) * ring_ld + 1;
         const double *r2 = smem + ((k + 1) % 3) * ring_ld + 1;
         double *row = band + (size_t)(rev ? K - 1 - k : k) * T.P;
-        for (int pp = q;; pp += NT) {
+        // DPW_PPL pairs per lane (H <= DPW_MAXH), straight-line: every pair's
+        // LDS reads at clamped indices first, then the cells (round 5: a loop
+        // with a break per pair waited for each pair's reads in turn)
+        dvec2 mtmm[DPW_PPL], isds[DPW_PPL];
+        int sb[DPW_PPL], tbb[DPW_PPL];
+        double a2[DPW_PPL], a1l[DPW_PPL], a1r[DPW_PPL];
+        bool on[DPW_PPL];
+#pragma unroll
+        for (int it = 0; it < DPW_PPL; ++it) {
+            const int pp = q + it * NT;
             const int d = 2 * pp + par;
-            if (d >= H || d > k)
-                break;
+            on[it] = d < H && d <= k;
+            const int dc = min(d, H);   // ring rows hold H + 2 entries from -1
+            const int R = (P + pp + par) & (DPW_RR - 1);
+            mtmm[it] = s_mtmm[R];
+            isds[it] = s_isds[R];
+            sb[it] = s_sb[R];
+            tbb[it] = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
+            a2[it] = r2[dc];
+            a1l[it] = r1[dc - 1];
+            a1r[it] = r1[dc + 1];
+        }
+#pragma unroll
+        for (int it = 0; it < DPW_PPL; ++it) {
+            if (!on[it])
+                continue;
+            const int pp = q + it * NT;
+            const int d = 2 * pp + par;
             const int jj = P - pp;
             const int ii = d + jj - T.c;
             double v = -RF_INF;
@@ -1385,13 +1410,10 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 if (ii == 0 && jj == 0) {
                     v = 0.0;
                 } else {
-                    const int R = (P + pp + par) & (DPW_RR - 1);
-                    const dvec2 mtmm = s_mtmm[R], isds = s_isds[R];
-                    const int sb = s_sb[R], tbb = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
-                    const double ms = sb == tbb ? mtmm.x : mtmm.y;
-                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;
+                    const double ms = sb[it] == tbb[it] ? mtmm[it].x : mtmm[it].y;
+                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds[it].x;
                     // align.jl:77-104: the maximum of the candidates
-                    double best = fmax(fmax(r2[d] + ms, r1[d - 1] + is), r1[d + 1] + isds.y);
+                    double best = fmax(fmax(a2[it] + ms, a1l[it] + is), a1r[it] + isds[it].y);
                     eflag |= best == -RF_INF ? 1 : 0;   // "new score is invalid"
                     v = best;
                 }
