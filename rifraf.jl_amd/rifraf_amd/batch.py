@@ -280,9 +280,9 @@ def native_eligible(clusters, params) -> bool:
             quals = kw.get("phreds")
         if quals is None or len(quals) != n:
             return False
-        for s, q in zip(kw["dnaseqs"], quals):
-            if len(s) == 0 or len(q) != len(s):
-                return False
+        ls = list(map(len, kw["dnaseqs"]))
+        if 0 in ls or ls != list(map(len, quals)):
+            return False
     return True
 
 
@@ -433,8 +433,9 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
     if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
         raise RifrafError("phred score cannot be negative")
-    lens = np.array([len(x) for x in all_s], np.int64)
-    if (lens == 0).any() or any(len(x) != len(y) for x, y in zip(all_s, all_lp)):
+    lens = np.fromiter(map(len, all_s), np.int64, len(all_s))
+    if (lens == 0).any() or len(all_lp) != len(all_s) or \
+            (lens != np.fromiter(map(len, all_lp), np.int64, len(all_lp))).any():
         raise RifrafError("empty read or length mismatch")
     soff = np.zeros(len(all_s) + 1, np.int64)
     np.cumsum(lens, out=soff[1:])
@@ -494,9 +495,11 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     states = []
     refs_in = [DNASeq(kw["reference"]) if kw.get("reference") is not None and len(kw["reference"]) > 0
                else np.zeros(0, np.uint8) for kw in part]
+    maxlen = np.maximum.reduceat(lens, read_off[:-1]) if K > 0 else lens
     for k, kw in enumerate(part):
         cons = first[k] if k in first else DNASeq(kw["consensus"])
-        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], refs_in[k], params))
+        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], refs_in[k], params,
+                                    maxlen=int(maxlen[k])))
     # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
     # The bands of every batch read in one arena reservation (growing it in
     # steps would re-allocate and compact tens of GB several times): A and B
@@ -542,7 +545,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     _stat("upload_s", time.perf_counter() - t_setup)
     read_seq = np.arange(len(all_s), dtype=np.int32)
     read_len = lens.astype(np.int32)
-    est = np.array([s.est_n_errors for s in allseqs])
+    est = tabs["est"] if coded is not None else np.array([s.est_n_errors for s in allseqs])
     thr = cquantile_poisson_many(est, params.bandwidth_pvalue)
     fixed_off = fixed = None
     if params.batch_fixed:

@@ -189,7 +189,7 @@ def logsumexp10(x):                            # util.jl:28-38
     return math.log10(s) + u
 
 
-def initial_state(consensus, sequences, reference, params: RifrafParams) -> RifrafState:  # :564-615
+def initial_state(consensus, sequences, reference, params: RifrafParams, maxlen=None) -> RifrafState:  # :564-615
     batch_size = params.batch_size if params.batch_size > 1 else len(sequences)
     batch_size = min(batch_size, len(sequences))
     batch_fixed_size = min(params.batch_fixed_size, len(sequences))
@@ -197,7 +197,8 @@ def initial_state(consensus, sequences, reference, params: RifrafParams) -> Rifr
         scores = [logsumexp10(s.match_scores) for s in sequences]
         idx = int(np.argmax(scores))              # indmax: first maximum
         consensus = sequences[idx].seq.copy()
-    maxlen = max(len(s) for s in sequences)
+    if maxlen is None:                            # (callers with the lengths at hand pass it)
+        maxlen = max(len(s) for s in sequences)
     ref_error_log_p = np.zeros(len(reference))    # placeholder, :601-603
     refseq = RifrafSequence(reference, ref_error_log_p, params.bandwidth, params.ref_scores) \
         if len(reference) > 0 else RifrafSequence()

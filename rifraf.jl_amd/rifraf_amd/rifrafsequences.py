@@ -298,7 +298,8 @@ class RifrafSequence:
             r.bandwidth = bw
             r.bandwidth_fixed = False
             out.append(r)
-        tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src, "uploaded": dev is not None}
+        tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src, "uploaded": dev is not None,
+                "est": np.asarray(est, np.float64)}
         return out, tabs, lse
 
     @classmethod
