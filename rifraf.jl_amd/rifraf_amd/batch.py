@@ -505,13 +505,18 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     # steps would re-allocate and compact tens of GB several times): A and B
     # at the initial bandwidth, x1.5 for band doubling
     nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
-    est_bytes = 0
+    # every read's A/B band (upper bound: padded rows), one vector pass; a
+    # cluster whose batch is smaller than its reads counts its largest bands
+    mcons = np.fromiter((len(st_.consensus) for st_ in states), np.int64, K)
+    mrd = np.repeat(mcons, nread)
+    Hs = 2 * params.bandwidth + np.abs(lens - mrd) + 1
+    band = (Hs + 2 * mrd) * band_stride(Hs, pad_h=1) * 8
+    est_bytes = 2 * int(band.sum())
+    for k in np.flatnonzero(nb < nread):
+        bk = band[read_off[k]:read_off[k + 1]]
+        est_bytes -= 2 * int(bk.sum() - np.sort(bk)[::-1][:nb[k]].sum())
     for k, st_ in enumerate(states):
         m = len(st_.consensus)
-        ln = lens[read_off[k]:read_off[k + 1]]
-        H = 2 * params.bandwidth + np.abs(ln - m) + 1
-        band = (H + 2 * m) * band_stride(H, pad_h=1) * 8   # upper bound: padded rows
-        est_bytes += int(np.sort(band)[::-1][:nb[k]].sum()) * 2
         L = len(refs_in[k])
         if L > 0:
             # reference-guided cluster (_native_refs): the reference's A and B
@@ -602,7 +607,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
         groups = [read_off[k] + np.arange(len(st_.batch_seqs), dtype=np.int32) for k, st_ in enumerate(states)]
         sq = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int32) for k, st_ in enumerate(states)])
         tp = np.concatenate([np.full(len(g), k, np.int32) for k, g in enumerate(groups)])
-        bws = np.array([st_.sequences[i].bandwidth for st_ in states for i in st_.batch_seqs], np.int32)
+        bws = np.abs(np.asarray(bw, np.int64))[sq].astype(np.int32)   # = the reads' .bandwidth set above
         engine.set_templates(0, [st_.consensus for st_ in states])
         sc = engine.realign(np.concatenate(groups), sq, tp, bws, RF_FWD | RF_BWD)
         at = 0
