@@ -572,9 +572,15 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
                                              cons_off, ref=ref)
         _stat("native_s", time.perf_counter() - t0)
     cb_errors = ref["cb_errors"] if ref is not None else {}
-    for s, b in zip(allseqs, bw.tolist()):
-        s.bandwidth = abs(b)
-        s.bandwidth_fixed = b < 0
+    if coded is not None:                  # CodedRifrafSequence: the shared arrays
+        src = tabs["source"]
+        bwa = np.asarray(bw, np.int64)
+        src.bw[:] = np.abs(bwa)
+        src.bwf[:] = bwa < 0
+    else:
+        for s, b in zip(allseqs, bw.tolist()):
+            s.bandwidth = abs(b)
+            s.bandwidth_fixed = b < 0
     results, errors = [], [None] * K
     for k, (st_, r) in enumerate(zip(states, res)):
         if r["status"] == 2:

@@ -283,20 +283,19 @@ class RifrafSequence:
                                      P(lse)) != 0:
                 raise ValueError("rf_host_code_prep: invalid segments (empty sequence?)")
         src = _CodeSource(code, off64, vals, tmatch, scores)
+        # per-sequence est / bandwidth live in the source's arrays (the
+        # objects read and write them through properties), so neither this
+        # loop nor a caller's bulk bandwidth update touches every object
+        src.est = np.asarray(est, np.float64)
+        src.bw = np.full(K, int(bandwidth), np.int64)
+        src.bwf = np.zeros(K, bool)
         out = []
         new = object.__new__
-        bw = int(bandwidth)
-        estl = est.tolist()
         for k, sq in enumerate(seqs):
             r = new(CodedRifrafSequence)
             r.seq = sq
             r._src = src
             r._k = k
-            r.codon_ins_scores = _EMPTY
-            r.codon_del_scores = _EMPTY
-            r.est_n_errors = estl[k]
-            r.bandwidth = bw
-            r.bandwidth_fixed = False
             out.append(r)
         tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src, "uploaded": dev is not None,
                 "est": np.asarray(est, np.float64)}
@@ -381,9 +380,32 @@ def _coded_table(name, idx):
 class CodedRifrafSequence(RifrafSequence):
     """A RifrafSequence of RifrafSequence.many_coded: its tables are built
     from the Phred codes on first access (the same values as the eager
-    constructor's)."""
+    constructor's); est_n_errors and the bandwidth fields are entries of the
+    shared source's arrays."""
 
     __slots__ = ("_src", "_k")
+    codon_ins_scores = _EMPTY     # reads have no codon tables
+    codon_del_scores = _EMPTY
+
+    @property
+    def est_n_errors(self):
+        return float(self._src.est[self._k])
+
+    @property
+    def bandwidth(self):
+        return int(self._src.bw[self._k])
+
+    @bandwidth.setter
+    def bandwidth(self, v):
+        self._src.bw[self._k] = v
+
+    @property
+    def bandwidth_fixed(self):
+        return bool(self._src.bwf[self._k])
+
+    @bandwidth_fixed.setter
+    def bandwidth_fixed(self, v):
+        self._src.bwf[self._k] = v
 
 
 for _i, _n in enumerate(_TABLES):
