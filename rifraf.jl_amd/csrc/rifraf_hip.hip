@@ -1487,7 +1487,12 @@ __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, in
         const double best = fmax(t, fmax(x_ins + isds.x, x_del + isds.y));
         if (CHECK)
             emask |= __ballot(best == -RF_INF) & actm;   // "new score is invalid" (active diagonals)
+#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 8)
+        (void)lbv;
+        return best;   // diagnostic builds only (wrong bands): one FP64 op less on the chain
+#else
         return best + lbv;
+#endif
     }
     const bool valid = d < T.H && jj >= 0 && jj <= T.m && ii >= 0 && ii <= T.n;
     const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;   // align.jl:74-76
