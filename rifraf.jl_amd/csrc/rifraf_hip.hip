@@ -4059,38 +4059,59 @@ __device__ double prep_julia_sum(const uint8_t *c, const double *p10, int64_t lo
     }
 }
 
-__global__ void __launch_bounds__(256) k_code_prep(const CodeSeq *__restrict__ seqs, int nseq,
-                                                   const uint8_t *__restrict__ codes, const double *__restrict__ tabs3,
-                                                   const double *__restrict__ grid, double *__restrict__ est,
-                                                   int32_t *__restrict__ ucode, double *__restrict__ tsum)
+// One wave per sequence (round 5): the wave stages the sequence's codes in
+// LDS with coalesced loads, and lane 0 runs the sequential sums from LDS (a
+// thread per sequence read its codes one byte load at a time, dependent
+// chains of global loads: 1.2 ms for configs[2]'s 1,000 reads).  The sums
+// and their order are unchanged.
+constexpr int CP_MAX = 32768;   // codes staged in LDS (longer sequences: read in place)
+__global__ void __launch_bounds__(64) k_code_prep(const CodeSeq *__restrict__ seqs, int nseq,
+                                                  const uint8_t *__restrict__ codes, const double *__restrict__ tabs3,
+                                                  const double *__restrict__ grid, double *__restrict__ est,
+                                                  int32_t *__restrict__ ucode, double *__restrict__ tsum)
 {
-    __shared__ double p10[256], mt[256];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    __shared__ double p10[256], mt[256], gr[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sc[CP_MAX];
+    __shared__ int s_uc;
+    for (int i = threadIdx.x; i < 256; i += 64) {
         p10[i] = tabs3[i];
         mt[i] = tabs3[256 + i];
     }
-    __syncthreads();
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.x;
     if (k >= nseq)
         return;
     const CodeSeq S = seqs[k];
     const int64_t n = S.n;
-    const uint8_t *c = codes + S.src;
-    int uc = c[0];
-    double s = p10[c[0]];
-    for (int64_t i = 1; i < n; ++i) {   // the sequential leg (n < 16, or n <= 1,024)
-        const int ci = c[i];
-        s += p10[ci];
-        if (mt[ci] > mt[uc])
-            uc = ci;
+    const uint8_t *cg = codes + S.src;
+    if (n <= CP_MAX)
+        for (int64_t i = threadIdx.x; i < n; i += 64)
+            sc[i] = cg[i];
+    __syncthreads();
+    const uint8_t *c = n <= CP_MAX ? (const uint8_t *)sc : cg;
+    if (threadIdx.x == 0) {
+        int uc = c[0];
+        double s = p10[c[0]];
+        for (int64_t i = 1; i < n; ++i) {   // the sequential leg (n < 16, or n <= 1,024)
+            const int ci = c[i];
+            s += p10[ci];
+            if (mt[ci] > mt[uc])
+                uc = ci;
+        }
+        est[k] = n <= 1024 ? s : prep_julia_sum(c, p10, 0, n - 1);
+        ucode[k] = uc;
+        s_uc = uc;
     }
-    est[k] = n <= 1024 ? s : prep_julia_sum(c, p10, 0, n - 1);
-    ucode[k] = uc;
-    const double *g = grid + (size_t)uc * 256;
-    double t = g[c[0]];
-    for (int64_t i = 1; i < n; ++i)
-        t += g[c[i]];
-    tsum[k] = t;
+    __syncthreads();
+    const int uc = s_uc;
+    for (int i = threadIdx.x; i < 256; i += 64)
+        gr[i] = grid[(size_t)uc * 256 + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = gr[c[0]];
+        for (int64_t i = 1; i < n; ++i)
+            t += gr[c[i]];
+        tsum[k] = t;
+    }
 }
 
 // ---------------------------------------------------------------------
@@ -5378,7 +5399,7 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
                            (const uint8_t *)ctx->scratch[7].p + nb, (const uint8_t *)ctx->scratch[7].p,
                            (const CodeLut *)ctx->scratch[20].p, s_mis, s_ins, s_del, (double *)ctx->tab_arena.d);
         if (prep)
-            hipLaunchKernelGGL(k_code_prep, dim3((k1 - k0 + 255) / 256), dim3(256), 0, ctx->stream,
+            hipLaunchKernelGGL(k_code_prep, dim3(k1 - k0), dim3(64), 0, ctx->stream,
                                (const CodeSeq *)ctx->scratch[6].p, k1 - k0, (const uint8_t *)ctx->scratch[7].p + nb,
                                (const double *)ctx->scratch[27].p, (const double *)((char *)ctx->scratch[27].p + prep_tab),
                                d_est + k0, d_ucode + k0, d_tsum + k0);
