@@ -382,11 +382,13 @@ def main():
                     help="c4 only: whole rifraf() runs per rank for the e2e field (0: skip)")
     ap.add_argument("--e2e-pin-cores", type=int, default=2,
                     help="c4 only: also time the e2e run with the rank pinned to this many host cores (0: skip)")
-    ap.add_argument("--e2e-engines", type=int, default=1,
-                    help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each")
+    ap.add_argument("--e2e-engines", type=int, default=2,
+                    help="c4 only: contexts (HIP streams) per GPU for the e2e field, one host thread each "
+                         "(round 5: two engines, so one wave's host setup runs beside the other's kernels; "
+                         "profiles/r05aj_e2e_engines.jsonl)")
     ap.add_argument("--e2e-wave", type=int, default=256,
                     help="c4 only: clusters per wave of the e2e field (waves from a shared queue per engine)")
-    ap.add_argument("--e2e-init-exclusive", type=int, default=1,
+    ap.add_argument("--e2e-init-exclusive", type=int, default=0,
                     help="c4 only: 1 = at most one engine in its native stage machine at a time (a two-stage "
                          "pipeline of waves: one engine's kernels, the others' host work)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
