@@ -391,6 +391,8 @@ def main():
     ap.add_argument("--e2e-init-exclusive", type=int, default=0,
                     help="c4 only: 1 = at most one engine in its native stage machine at a time (a two-stage "
                          "pipeline of waves: one engine's kernels, the others' host work)")
+    ap.add_argument("--e2e-pin-exclusive", type=int, default=-1,
+                    help="c4 only: init_exclusive for the pinned e2e run (-1: as the unpinned run)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process group for N > 1 (auto: nccl = RCCL when GPUs are visible)")
     ap.add_argument("--shared-gpu", action="store_true",
@@ -536,19 +538,21 @@ def run_e2e(args, rank, world, gpu, dist, coll):
     bopt = dict(engines=engs, wave=max(1, args.e2e_wave), init_exclusive=bool(args.e2e_init_exclusive))
     rifraf_batch(clusters, params=params, **bopt)
     cold = time.perf_counter() - t0
-    # steady state: three rounds of (unpinned run, run with this rank held to
+    # steady state: five rounds of (unpinned run, run with this rank held to
     # 2 host cores -- its share at 8 ranks on the GPU box's 16; every thread
     # of the process pinned in place, no relaunch; the library's worker pools
     # follow the mask), medians of each (one run of either varies by ~10 %
-    # between rounds on one box, profiles/r05l_e2e_pinned.jsonl)
+    # between rounds on one box, profiles/r05l_e2e_pinned.jsonl, r05al_bench.json)
     pin = pin_rate = None
     allowed = sorted(os.sched_getaffinity(0))
     if args.e2e_pin_cores > 0 and len(allowed) > args.e2e_pin_cores:
         k = args.e2e_pin_cores
         pin = allowed[(rank * k) % len(allowed):][:k] or allowed[:k]
+    pin_opt = dict(bopt, init_exclusive=bool(args.e2e_pin_exclusive) if ne > 1 and args.e2e_pin_exclusive >= 0
+                   else bopt["init_exclusive"])
     runs, pin_runs, same_pin = [], [], True
     res = None
-    for _ in range(3 if pin else 1):
+    for _ in range(5 if pin else 3):
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
@@ -561,7 +565,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                 if dist is not None:
                     dist.barrier()
                 t0 = time.perf_counter()
-                res_pin = rifraf_batch(clusters, params=params, **bopt)
+                res_pin = rifraf_batch(clusters, params=params, **pin_opt)
                 pin_runs.append(time.perf_counter() - t0)
             finally:
                 unpin_threads(saved)
@@ -586,7 +590,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "clusters_per_s_per_gpu": tot[0] / elapsed / max(world, 1), "ranks": world,
             "clusters": int(tot[0]), "seconds": elapsed,
             "cold_clusters_per_s": tot[0] / cold,
-            "timing": "steady state: the median of three full runs over the clusters after the first ('cold', "
+            "timing": "steady state: the median of five full runs over the clusters after the first ('cold', "
                       "which also allocates the band arena), alternating with the pinned runs; host setup from "
                       "reads included, read simulation excluded",
             "processes_per_gpu": getattr(args, "processes_per_gpu", 1),
@@ -605,6 +609,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "runs_s": runs, "pinned_runs_s": pin_runs,
             "pinned": None if pin_rate is None else {
                 "cores": len(pin), "clusters_per_s": tot[0] / pin_s, "ratio_to_unpinned": elapsed / pin_s,
+                "init_exclusive": pin_opt["init_exclusive"],
                 "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(pin_rate[1]),
                 "note": "the same steady-state run with every thread of the rank pinned to this many cores "
                         "(a rank's share of the box's 16 at 8 ranks)"}}
