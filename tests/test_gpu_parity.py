@@ -1112,11 +1112,14 @@ def test_set_sequences_codes_prep_matches_host(engine):
     est_n_errors in Julia 0.6's pairwise order and the initial consensus's
     logsumexp10 (rifrafsequences.jl:19-82, util.jl:28-38) -- equal
     rf_host_code_prep's bit for bit, over lengths on both sides of every
-    pairwise-sum edge (16, 1,024, 2,048, 4,096), all-Phred-0 reads (an
+    pairwise-sum edge (16, 1,024, 2,048, 4,096) and of the LDS staging limit
+    (32,768), all-Phred-0 reads (an
     infinite maximum match score), and 5,000 reads in one call (two staging
     chunks at 256 KB); the reads' bands equal a plain upload's."""
     rng = np.random.default_rng(2525)
-    lens = [1, 2, 15, 16, 17, 1023, 1024, 1025, 1500, 2047, 2048, 2049, 4095, 4096, 4097, 10000, 3, 3]
+    # (32,768 / 32,769 / 40,000: both sides of k_code_prep's LDS staging limit)
+    lens = [1, 2, 15, 16, 17, 1023, 1024, 1025, 1500, 2047, 2048, 2049, 4095, 4096, 4097, 10000, 32768, 32769,
+            40000, 3, 3]
     reads = [rng.integers(0, 4, L).astype(np.uint8) for L in lens]
     phreds = [rng.integers(0, 61, L).astype(np.int8) for L in lens]
     phreds[-1][:] = 0                      # every code infinite: lse = match = -Inf
@@ -1144,9 +1147,9 @@ def test_set_sequences_codes_prep_matches_host(engine):
     assert est_h.view(np.int64).tolist() == est_d.view(np.int64).tolist()
     assert host[2].view(np.int64).tolist() == devr[2].view(np.int64).tolist()   # lse, -Inf included
     # the upload itself: bands of a few reads equal a plain rf_set_sequences_codes upload's
-    t = reads[20]
+    t = reads[len(lens) + 2]
     engine.set_templates(0, [t])
-    sl = np.arange(18, 24)
+    sl = np.arange(len(lens), len(lens) + 6)     # 300-base reads
     a1 = engine.realign(sl, sl, 0, [9] * 6, RF_FWD)
     tabs = host[1]
     assert engine.set_sequences_codes(0, allb, off, tabs["code"], tabs["lp_table"], tabs["match_table"], SEQ_SCORES)
