@@ -4332,6 +4332,8 @@ struct Opts {
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
     int score_wgs = 2048;   // RF_OPT_SCORE_WGS: split-mode k_score_ws takes reads in chunks so that about
                             // this many workgroups remain
+    int seg_wgs = 262144;   // RF_OPT_SEG_WGS: split-mode k_score_segl takes reads in chunks so that about
+                            // this many workgroups remain
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 #ifdef RIFRAF_DIAG
@@ -4669,6 +4671,7 @@ void load_env_opts(Opts &o)
     o.dp_nl64 = env_int("RIFRAF_DP_NL64", o.dp_nl64);
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
+    o.seg_wgs = env_int("RIFRAF_SEG_WGS", o.seg_wgs);
 #ifdef RIFRAF_DIAG
     o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
     o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
@@ -4748,7 +4751,8 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     if (pk.seg) {
         int rchunk = 1;
         if (split) {
-            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + 32767) / 32768);
+            const int64_t tgt = std::max(ctx->opt.seg_wgs, 1);
+            rchunk = (int)std::max<int64_t>(1, ((int64_t)nitems * gy + tgt - 1) / tgt);
             grid.y = (gy + rchunk - 1) / rchunk;
         }
         hipLaunchKernelGGL(k_score_segl<32>, grid, dim3(64), 0, ctx->stream, items, groups, reads, d_bases, d_tabs,
@@ -4891,6 +4895,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_NL64: return &o.dp_nl64;
     case RF_OPT_DP_LAT: return &o.dp_lat;
     case RF_OPT_SCORE_WGS: return &o.score_wgs;
+    case RF_OPT_SEG_WGS: return &o.seg_wgs;
     default: return nullptr;
     }
 }
