@@ -1628,16 +1628,33 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     uint64_t emask = 0;
     int eflag = 0, fset = 0;
     double fval = 0.0;
-    // records of the current pair of periods (2u, 2u + 1), read one pair
-    // ahead: rows R = 2u + q (c_), 2u + q + 1 (a_), 2u + q + 2 (b_), columns
-    // J = 2u - q + 64 (col0), + 1 (col1)
-    dvec2 c_mtmm = s_mtmm[q], c_isds = s_isds[q], c_cicd = CODON ? s_cicd[q] : dvec2{0.0, 0.0};
-    int c_sb = s_sb[q];
-    dvec2 a_mtmm = s_mtmm[q + 1], a_isds = s_isds[q + 1], a_cicd = CODON ? s_cicd[q + 1] : dvec2{0.0, 0.0};
-    int a_sb = s_sb[q + 1];
-    dvec2 b_mtmm = s_mtmm[q + 2], b_isds = s_isds[q + 2], b_cicd = CODON ? s_cicd[q + 2] : dvec2{0.0, 0.0};
-    int b_sb = s_sb[q + 2];
-    int col0 = s_col[(64 - q) & (DPX_RING - 1)], col1 = s_col[(65 - q) & (DPX_RING - 1)];
+    // Records of a pair of periods (2u, 2u + 1): rows R = 2u + q (c), 2u + q + 1
+    // (a), 2u + q + 2 (b) and columns J = 2u - q + 64, + 1.  Pair u reads the
+    // records of pair u + 1 (rows 2u + q + 3, + 4 and the next columns) into
+    // set u mod 3; its own a / b are set u - 1 and its c is the b of set u - 2.
+    // The loop runs three pairs per iteration with the sets rotated by name,
+    // so no record moves between registers (round 5: the one-pair loop copied
+    // 17 registers per pair at its end, ~4 of the ~22 instructions per step).
+    struct Rec {
+        dvec2 mtmm, isds, cicd;
+        int sb;
+    };
+    auto rec_ld = [&](int r) {
+        Rec x;
+        x.mtmm = s_mtmm[r];
+        x.isds = s_isds[r];
+        x.cicd = CODON ? s_cicd[r] : dvec2{0.0, 0.0};
+        x.sb = s_sb[r];
+        return x;
+    };
+    Rec A0, B0, A1, B1, A2, B2;
+    int C00 = 0, C01 = 0, C10 = 0, C11 = 0, C20, C21;
+    B1 = rec_ld(q);              // set -2: b = row q
+    A2 = rec_ld(q + 1);          // set -1: rows q + 1, q + 2, columns 64 - q, 65 - q
+    B2 = rec_ld(q + 2);
+    C20 = s_col[(64 - q) & (DPX_RING - 1)];
+    C21 = s_col[(65 - q) & (DPX_RING - 1)];
+    A0 = A1 = B0 = A2;           // (defined before their first load)
     // the codon neighbours of the next step, read one step ahead (kappa = 0:
     // ring row 1, still -Inf)
     double cy_ci = CODON ? s_band[DPX_W + 2 + q - 2] : 0.0, cy_cd = CODON ? s_band[DPX_W + 2 + q + 1] : 0.0;
@@ -1654,22 +1671,17 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     // pair of periods (the per-step select and multiply off the loop)
     const int drow = rev ? -(int)rowb : (int)rowb;
     unsigned rob = rev ? rowb * (unsigned)(K - 1) : 0u;
-    for (int u = 0; u < npairs; ++u) {
+    auto pair = [&](const int u, const Rec &c, const Rec &a, const Rec &b, const int col0, const int col1, Rec &na,
+                    Rec &nb, int &ncol0, int &ncol1) {
         if ((u & 31) == 0 && u > 0)   // chunk t = u / 32 (64 periods): block t + 2 is in
             lds_barrier();
         // the next pair's records (rows <= 2u + 67: block t + 2 at most, in LDS)
-        const int r1 = (2 * u + q + 3) & (DPX_RING - 1), r2 = (2 * u + q + 4) & (DPX_RING - 1);
-        const int j0 = (2 * u - q + 66) & (DPX_RING - 1), j1 = (2 * u - q + 67) & (DPX_RING - 1);
-        const dvec2 na_mtmm = s_mtmm[r1], na_isds = s_isds[r1];
-        const dvec2 na_cicd = CODON ? s_cicd[r1] : dvec2{0.0, 0.0};
-        const int na_sb = s_sb[r1];
-        const dvec2 nb_mtmm = s_mtmm[r2], nb_isds = s_isds[r2];
-        const dvec2 nb_cicd = CODON ? s_cicd[r2] : dvec2{0.0, 0.0};
-        const int nb_sb = s_sb[r2];
-        const int ncol0 = s_col[j0], ncol1 = s_col[j1];
+        na = rec_ld((2 * u + q + 3) & (DPX_RING - 1));
+        nb = rec_ld((2 * u + q + 4) & (DPX_RING - 1));
+        ncol0 = s_col[(2 * u - q + 66) & (DPX_RING - 1)];
+        ncol1 = s_col[(2 * u - q + 67) & (DPX_RING - 1)];
         // four steps kappa = 4u + s: (period, parity) = (2u, 0), (2u, 1), (2u+1, 0), (2u+1, 1)
-        auto step = [&](auto FASTC, auto PARC, auto SC, int per, const dvec2 &mtmm, const dvec2 &isds,
-                        const dvec2 &cicd, int sb, int col) {
+        auto step = [&](auto FASTC, auto PARC, auto SC, int per, const Rec &r, int col) {
             constexpr bool FAST = decltype(FASTC)::value;
             constexpr int PAR = decltype(PARC)::value, S = decltype(SC)::value;
             const int k = 4 * u + S;
@@ -1688,17 +1700,22 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // the next step's (ring row kappa - 2, the other parity) now
             const double yci = cy_ci, ycd = cy_cd;
             if (CODON) {
-                const double *r = s_band + ((S + 2) & 3) * DPX_W + 2 + q;
-                cy_ci = r[PAR ? -2 : -1];
-                cy_cd = r[PAR ? 1 : 2];
+                const double *rr = s_band + ((S + 2) & 3) * DPX_W + 2 + q;
+                cy_ci = rr[PAR ? -2 : -1];
+                cy_cd = rr[PAR ? 1 : 2];
             }
             const int d = 2 * q + PAR;
             const int jj = per - q, ii = per + q + PAR - T.c;
-            const double v = dpx_cell<PAR, FAST, CODON, CHECK>(T, trim, d, ii, jj, v1, v2, xn, yci, ycd, mtmm, isds,
-                                                               cicd, sb, col, lb[PAR], PAR ? actm1 : actm0, emask,
-                                                               eflag, fval, fset);
-            if (CODON)
+            const double v = dpx_cell<PAR, FAST, CODON, CHECK>(T, trim, d, ii, jj, v1, v2, xn, yci, ycd, r.mtmm,
+                                                               r.isds, r.cicd, r.sb, col, lb[PAR],
+                                                               PAR ? actm1 : actm0, emask, eflag, fval, fset);
+            if (CODON) {
                 s_band[S * DPX_W + 2 + q] = v;
+                // other lanes read this row two and three steps on: keep hipcc
+                // from hoisting those reads above the write (the three-pair loop
+                // body gives it the room; LDS is in order within the wave)
+                wave_sync();
+            }
             const unsigned ro = rob + (unsigned)(S * drow);   // = rowb * (rev ? K - 1 - k : k)
             const unsigned vo = PAR ? vo1 : vo0;
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 1)
@@ -1710,32 +1727,28 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             v1 = v;
         };
         if (4 * u >= klo && 4 * u + 3 <= khi) {
-            step(BT{}, I0{}, I0{}, 2 * u, c_mtmm, c_isds, c_cicd, c_sb, col0);
-            step(BT{}, I1{}, I1{}, 2 * u, a_mtmm, a_isds, a_cicd, a_sb, col0);
-            step(BT{}, I0{}, I2{}, 2 * u + 1, a_mtmm, a_isds, a_cicd, a_sb, col1);
-            step(BT{}, I1{}, I3{}, 2 * u + 1, b_mtmm, b_isds, b_cicd, b_sb, col1);
+            step(BT{}, I0{}, I0{}, 2 * u, c, col0);
+            step(BT{}, I1{}, I1{}, 2 * u, a, col0);
+            step(BT{}, I0{}, I2{}, 2 * u + 1, a, col1);
+            step(BT{}, I1{}, I3{}, 2 * u + 1, b, col1);
         } else {
-            step(BF{}, I0{}, I0{}, 2 * u, c_mtmm, c_isds, c_cicd, c_sb, col0);
-            step(BF{}, I1{}, I1{}, 2 * u, a_mtmm, a_isds, a_cicd, a_sb, col0);
-            step(BF{}, I0{}, I2{}, 2 * u + 1, a_mtmm, a_isds, a_cicd, a_sb, col1);
-            step(BF{}, I1{}, I3{}, 2 * u + 1, b_mtmm, b_isds, b_cicd, b_sb, col1);
+            step(BF{}, I0{}, I0{}, 2 * u, c, col0);
+            step(BF{}, I1{}, I1{}, 2 * u, a, col0);
+            step(BF{}, I0{}, I2{}, 2 * u + 1, a, col1);
+            step(BF{}, I1{}, I3{}, 2 * u + 1, b, col1);
         }
-        c_mtmm = b_mtmm;
-        c_isds = b_isds;
-        c_cicd = b_cicd;
-        c_sb = b_sb;
-        a_mtmm = na_mtmm;
-        a_isds = na_isds;
-        a_cicd = na_cicd;
-        a_sb = na_sb;
-        b_mtmm = nb_mtmm;
-        b_isds = nb_isds;
-        b_cicd = nb_cicd;
-        b_sb = nb_sb;
-        col0 = ncol0;
-        col1 = ncol1;
         rob += (unsigned)(4 * drow);
+    };
+    int u = 0;
+    for (; u + 3 <= npairs; u += 3) {
+        pair(u, B1, A2, B2, C20, C21, A0, B0, C00, C01);
+        pair(u + 1, B2, A0, B0, C00, C01, A1, B1, C10, C11);
+        pair(u + 2, B0, A1, B1, C10, C11, A2, B2, C20, C21);
     }
+    if (u < npairs)
+        pair(u, B1, A2, B2, C20, C21, A0, B0, C00, C01);
+    if (u + 1 < npairs)
+        pair(u + 1, B2, A0, B0, C00, C01, A1, B1, C10, C11);
     (void)ntasks;
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
     if (q == 0 && blockIdx.x == 0)
@@ -5241,7 +5254,9 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
     // codes present, per-code values and finiteness
     bool present[256] = {};
     {
-        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 22) + 1));
+        // one byte store per position (~0.5 ns): threads from 512 K positions
+        // (c3's 2.6 M: 1.3 ms on one thread)
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 19) + 1));
         std::vector<std::array<uint8_t, 256>> pr(nth);
         parallel_for(nth, [&](int t) {
             pr[t].fill(0);
@@ -5412,9 +5427,16 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
         HIPCHK(ctx, stream_wait(ctx));   // staging and descriptors are reused
         k0 = k1;
     }
-    // finiteness per sequence (lean DP / scorer eligibility)
-    {
-        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 22) + 1));
+    // finiteness per sequence (lean DP / scorer eligibility): every sequence
+    // is finite when every code present is; else one pass per sequence
+    bool all_fin = true;
+    for (int c = 0; c < 256; ++c)
+        all_fin = all_fin && (!present[c] || fin[c]);
+    if (all_fin) {
+        for (int32_t k = 0; k < nseq; ++k)
+            ctx->seqs[first + k].finite = true;
+    } else {
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (N >> 19) + 1));
         parallel_for(nth, [&](int t) {
             for (int32_t k = (int32_t)((int64_t)nseq * t / nth); k < (int32_t)((int64_t)nseq * (t + 1) / nth); ++k) {
                 bool f = true;

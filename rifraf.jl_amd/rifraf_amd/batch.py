@@ -503,14 +503,20 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
     # The bands of every batch read in one arena reservation (growing it in
     # steps would re-allocate and compact tens of GB several times): A and B
-    # at the initial bandwidth, x1.5 for band doubling
+    # at the initial bandwidth plus the doubled bandwidth's regions, which a
+    # band-doubling realign allocates above them (the arena bump-allocates; a
+    # reservation of 1.5x the initial bands grew, and compacted every band,
+    # in each c3 run: 1,999 regions, ~1.8 ms of a 45 ms run, r05am trace)
     nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
     # every read's A/B band (upper bound: padded rows), one vector pass; a
     # cluster whose batch is smaller than its reads counts its largest bands
     mcons = np.fromiter((len(st_.consensus) for st_ in states), np.int64, K)
     mrd = np.repeat(mcons, nread)
-    Hs = 2 * params.bandwidth + np.abs(lens - mrd) + 1
-    band = (Hs + 2 * mrd) * band_stride(Hs, pad_h=1) * 8
+    dn = np.abs(lens - mrd)
+    band = np.zeros(len(lens), np.int64)
+    for bw_ in (params.bandwidth, 2 * params.bandwidth):
+        Hs = 2 * bw_ + dn + 1
+        band += (Hs + 2 * mrd) * band_stride(Hs, pad_h=1) * 8
     est_bytes = 2 * int(band.sum())
     for k in np.flatnonzero(nb < nread):
         bk = band[read_off[k]:read_off[k + 1]]
@@ -523,8 +529,9 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
             # at the read bandwidth, and the scratch slot's forward band, which
             # at FRAME entry holds edit_distance's band at bw = ceil(min / 2)
             # (align.jl:253-260) -- it grows with the square of the length
-            Hr = 2 * params.bandwidth + abs(L - m) + 1
-            est_bytes += 2 * (Hr + 2 * m) * band_stride(Hr, pad_h=1) * 8
+            for bw_ in (params.bandwidth, 2 * params.bandwidth):
+                Hr = 2 * bw_ + abs(L - m) + 1
+                est_bytes += 2 * (Hr + 2 * m) * band_stride(Hr, pad_h=1) * 8
             bwe = -(-min(L, m) // 2)
             He = 2 * bwe + abs(L - m) + 1
             est_bytes += (He + 2 * m) * band_stride(He, pad_h=1) * 8
@@ -533,7 +540,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     uploaded = coded is not None and tabs["uploaded"]
     if hasattr(engine, "release_bands") and not uploaded:
         engine.release_bands()
-    engine.reserve(int(est_bytes * 1.5) + (64 << 20))
+    engine.reserve(int(est_bytes * 1.1) + (64 << 20))
     _stat("setup_native_s", time.perf_counter() - t_setup)
     if allb is None:
         allb = np.concatenate(all_s)
