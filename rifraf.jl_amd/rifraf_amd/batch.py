@@ -428,7 +428,9 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
         else:
             elp = kw.get("error_log_ps")
             all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
-        all_s += [DNASeq(x) for x in kw["dnaseqs"]]
+        # code arrays pass as they are (DNASeq would only re-wrap them)
+        all_s += [x if type(x) is np.ndarray and x.dtype == np.uint8 and x.flags.c_contiguous else DNASeq(x)
+                  for x in kw["dnaseqs"]]
         nread.append(len(kw["dnaseqs"]))
     cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
     if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
@@ -458,7 +460,8 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
             def device(code, lp_t, match_t, p10, grid):
                 r = engine.set_sequences_codes(0, allb, soff, code, lp_t, match_t, params.scores, prep=(p10, grid))
                 return r if r is not False else None
-        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8), soff, params.bandwidth, params.scores,
+        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8, copy=False), soff, params.bandwidth,
+                                          params.scores,
                                           device=device)
     if coded is not None:
         allseqs, tabs, lse_all = coded
