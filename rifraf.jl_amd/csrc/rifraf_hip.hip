@@ -1306,7 +1306,7 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
       int *__restrict__ err, int ring_ld)
 {
     constexpr int DPW_PPL = (DPW_MAXH / 2 + NT) / NT;   // band pairs per lane and step (at most)
-    extern __shared__ __attribute__((aligned(16))) double smem[];   // value ring: 3 rows of ring_ld
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // value ring: rows of ring_ld (2 used)
     __shared__ dvec2 s_mtmm[DPW_RR], s_isds[DPW_RR];
     __shared__ uint8_t s_sb[DPW_RR], s_col[DPW_RR];
     const int q = threadIdx.x;
@@ -1358,6 +1358,11 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     __syncthreads();
 
     int eflag = 0;
+    // the last value of each of this lane's diagonals (2pp: vev, 2pp + 1: vod)
+    double vev[DPW_PPL], vod[DPW_PPL];
+#pragma unroll
+    for (int it = 0; it < DPW_PPL; ++it)
+        vev[it] = vod[it] = -RF_INF;
     for (int k = 0; k < K; ++k) {
         const int par = k & 1, P = k >> 1;
         if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
@@ -1371,9 +1376,11 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             }
             __syncthreads();
         }
-        double *r0 = smem + (k % 3) * ring_ld + 1;
-        const double *r1 = smem + ((k + 2) % 3) * ring_ld + 1;
-        const double *r2 = smem + ((k + 1) % 3) * ring_ld + 1;
+        // the neighbour pair's kappa - 1 value from LDS (two rows: this step's
+        // and the last); the lane's own kappa - 1 and kappa - 2 values are in
+        // registers (round 5: one LDS value read per cell instead of three)
+        double *r0 = smem + (k & 1) * ring_ld + 1;
+        const double *r1 = smem + ((k + 1) & 1) * ring_ld + 1;
         double *row = band + (size_t)(rev ? K - 1 - k : k) * T.P;
         // DPW_PPL pairs per lane (H <= DPW_MAXH), straight-line: every pair's
         // LDS reads at clamped indices first, then the cells (round 5: a loop
@@ -1393,9 +1400,12 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             isds[it] = s_isds[R];
             sb[it] = s_sb[R];
             tbb[it] = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
-            a2[it] = r2[dc];
-            a1l[it] = r1[dc - 1];
-            a1r[it] = r1[dc + 1];
+            // (d, kappa - 2): this parity's last value; (d -/+ 1, kappa - 1):
+            // the other parity's (own pair) and the neighbour pair's (LDS)
+            const double nb = r1[par ? dc + 1 : dc - 1];
+            a2[it] = par ? vod[it] : vev[it];
+            a1l[it] = par ? vev[it] : nb;
+            a1r[it] = par ? nb : vod[it];
         }
 #pragma unroll
         for (int it = 0; it < DPW_PPL; ++it) {
@@ -1422,6 +1432,10 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             }
             row[(rev ? H - 1 - d : d) >> 1] = v;
             r0[d] = v;
+            if (par)
+                vod[it] = v;
+            else
+                vev[it] = v;
         }
         __syncthreads();
     }
