@@ -1360,33 +1360,33 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     int eflag = 0;
     // the last value of each of this lane's diagonals (2pp: vev, 2pp + 1: vod)
     double vev[DPW_PPL], vod[DPW_PPL];
+    // a pair's row record changes at odd steps (R = P + pp + 1) and its
+    // template column at even steps (J = P - pp + JOFF): each is read from
+    // LDS once and used by two consecutive anti-diagonals
+    dvec2 mtmm[DPW_PPL], isds[DPW_PPL];
+    int sb[DPW_PPL], tbb[DPW_PPL];
 #pragma unroll
-    for (int it = 0; it < DPW_PPL; ++it)
+    for (int it = 0; it < DPW_PPL; ++it) {
+        const int pp = q + it * NT;
         vev[it] = vod[it] = -RF_INF;
-    for (int k = 0; k < K; ++k) {
-        const int par = k & 1, P = k >> 1;
-        if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
-            const int t = k >> 7;
-            if (wv == 0) {
-                row_put(brow(t), l, nrow);
-                nrow = row_load(brow(t + 1), l);
-            } else if (wv == 1) {
-                col_put(bcol(t), l, ncol);
-                ncol = col_load(bcol(t + 1), l);
-            }
-            __syncthreads();
-        }
+        const int R = pp & (DPW_RR - 1);   // step 0's row
+        mtmm[it] = s_mtmm[R];
+        isds[it] = s_isds[R];
+        sb[it] = s_sb[R];
+        tbb[it] = 4;
+    }
+    auto step = [&](auto PARC, const int k) {
+        constexpr int par = decltype(PARC)::value;
+        const int P = k >> 1;
         // the neighbour pair's kappa - 1 value from LDS (two rows: this step's
         // and the last); the lane's own kappa - 1 and kappa - 2 values are in
         // registers (round 5: one LDS value read per cell instead of three)
-        double *r0 = smem + (k & 1) * ring_ld + 1;
-        const double *r1 = smem + ((k + 1) & 1) * ring_ld + 1;
+        double *r0 = smem + par * ring_ld + 1;
+        const double *r1 = smem + (1 - par) * ring_ld + 1;
         double *row = band + (size_t)(rev ? K - 1 - k : k) * T.P;
         // DPW_PPL pairs per lane (H <= DPW_MAXH), straight-line: every pair's
         // LDS reads at clamped indices first, then the cells (round 5: a loop
         // with a break per pair waited for each pair's reads in turn)
-        dvec2 mtmm[DPW_PPL], isds[DPW_PPL];
-        int sb[DPW_PPL], tbb[DPW_PPL];
         double a2[DPW_PPL], a1l[DPW_PPL], a1r[DPW_PPL];
         bool on[DPW_PPL];
 #pragma unroll
@@ -1395,11 +1395,14 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             const int d = 2 * pp + par;
             on[it] = d < H && d <= k;
             const int dc = min(d, H);   // ring rows hold H + 2 entries from -1
-            const int R = (P + pp + par) & (DPW_RR - 1);
-            mtmm[it] = s_mtmm[R];
-            isds[it] = s_isds[R];
-            sb[it] = s_sb[R];
-            tbb[it] = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
+            if (par) {
+                const int R = (P + pp + 1) & (DPW_RR - 1);
+                mtmm[it] = s_mtmm[R];
+                isds[it] = s_isds[R];
+                sb[it] = s_sb[R];
+            } else {
+                tbb[it] = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
+            }
             // (d, kappa - 2): this parity's last value; (d -/+ 1, kappa - 1):
             // the other parity's (own pair) and the neighbour pair's (LDS)
             const double nb = r1[par ? dc + 1 : dc - 1];
@@ -1438,6 +1441,22 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 vev[it] = v;
         }
         __syncthreads();
+    };
+    for (int k = 0; k < K; k += 2) {
+        if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
+            const int t = k >> 7;
+            if (wv == 0) {
+                row_put(brow(t), l, nrow);
+                nrow = row_load(brow(t + 1), l);
+            } else if (wv == 1) {
+                col_put(bcol(t), l, ncol);
+                ncol = col_load(bcol(t + 1), l);
+            }
+            __syncthreads();
+        }
+        step(std::integral_constant<int, 0>{}, k);
+        if (k + 1 < K)
+            step(std::integral_constant<int, 1>{}, k + 1);
     }
     if (eflag)
         set_err(err, 1);
