@@ -1492,6 +1492,9 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 // bit-identical.
 // ---------------------------------------------------------------------
 constexpr int DPX_W = 72;       // doubles per LDS band row: 2 pad | 64 lanes | 6 pad (-Inf)
+#ifndef DPX_STAGE
+#define DPX_STAGE 1   // interior rows staged in LDS, four per contiguous flush
+#endif
 constexpr int DPX_RING = 256;   // staged rows / columns: 4 blocks of 64
 struct DpxStage {
     RawRow r;
@@ -1556,6 +1559,13 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     __shared__ dvec2 s_mtmm[DPX_RING], s_isds[DPX_RING], s_cicd[CODON ? DPX_RING : 1];
     __shared__ int s_sb[DPX_RING], s_col[DPX_RING];
     __shared__ double s_band[CODON ? 4 * DPX_W : 1];
+    // DPX_STAGE: the interior's four rows of a pair of periods, staged here
+    // and written as one contiguous run (P <= 65)
+    // (lean tasks only: the reference's single codon task, latency-bound on
+    // one wave, ran 0.43 -> 0.61 ms with it; 1,000 lean reads 0.52 -> 0.49 ms,
+    // profiles/r05bt_exp_dpx_stage.jsonl)
+    constexpr bool STAGE = DPX_STAGE && !CODON;
+    __shared__ __attribute__((aligned(16))) double s_out[STAGE ? 4 * 72 : 1];
     // wave 0 fills the band; wave 1 stages the edge records (round 5: its
     // loads' waits are its own, so the filling wave never waits on vmcnt,
     // which would drain its band stores too)
@@ -1754,8 +1764,13 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 #if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 1)
             if (!FAST)   // diagnostic builds only (wrong bands): no interior band stores
 #endif
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), brs,
-                                                  (FAST || d <= k) ? vo + ro : DPX_NOSTORE, 0, 0);
+            if (STAGE && FAST) {
+                if (vo != DPX_NOSTORE)
+                    s_out[(rev ? 3 - S : S) * T.P + (int)(vo >> 3)] = v;
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), brs,
+                                                      (FAST || d <= k) ? vo + ro : DPX_NOSTORE, 0, 0);
+            }
             v2 = v1;
             v1 = v;
         };
@@ -1764,6 +1779,17 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             step(BT{}, I1{}, I1{}, 2 * u, a, col0);
             step(BT{}, I0{}, I2{}, 2 * u + 1, a, col1);
             step(BT{}, I1{}, I3{}, 2 * u + 1, b, col1);
+            if (STAGE) {
+                // rows 4u .. 4u + 3 (reverse: K - 4 - 4u .. K - 1 - 4u) are one
+                // run of 4P doubles: 8-B stores of consecutive lanes
+                wave_sync();
+                const unsigned base = rev ? rob - 3u * rowb : rob;
+                const int n = 4 * T.P;
+                for (int t = q; t < n; t += 64)
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, s_out[t]), brs,
+                                                          base + 8u * (unsigned)t, 0, 0);
+                wave_sync();
+            }
         } else {
             step(BF{}, I0{}, I0{}, 2 * u, c, col0);
             step(BF{}, I1{}, I1{}, 2 * u, a, col0);
