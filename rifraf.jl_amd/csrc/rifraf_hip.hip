@@ -4087,6 +4087,27 @@ __global__ void __launch_bounds__(256) k_tables(const CodeSeq *__restrict__ seqs
 // The same table entries and the same FP64 additions in the same order as
 // rf_host_code_prep: bit-identical.
 constexpr int PREP_STACK = 40;
+// sum_{i = lo..hi} tab[c[i]] left to right (the same additions in the same
+// order as one loop), with eight entries loaded ahead of their additions:
+// from LDS each element was two dependent round trips on lane 0's chain
+__device__ __forceinline__ double prep_seq_sum(const uint8_t *c, const double *tab, int64_t lo, int64_t hi)
+{
+    double a = tab[c[lo]];
+    int64_t i = lo + 1;
+    for (; i + 8 <= hi + 1; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = tab[c[i + u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            a += v[u];
+    }
+    for (; i <= hi; ++i)
+        a += tab[c[i]];
+    return a;
+}
+
 __device__ double prep_julia_sum(const uint8_t *c, const double *p10, int64_t lo0, int64_t hi0)
 {
     // explicit-stack post-order of the pairwise split (no device recursion)
@@ -4101,10 +4122,7 @@ __device__ double prep_julia_sum(const uint8_t *c, const double *p10, int64_t lo
     while (true) {
         const int64_t lo = slo[sp], hi = shi[sp];
         if (lo + 1024 > hi) {   // leaf: sequential
-            double a = p10[c[lo]];
-            for (int64_t i = lo + 1; i <= hi; ++i)
-                a += p10[c[i]];
-            ret = a;
+            ret = prep_seq_sum(c, p10, lo, hi);
             if (--sp < 0)
                 return ret;
             continue;
@@ -4160,30 +4178,41 @@ __global__ void __launch_bounds__(64) k_code_prep(const CodeSeq *__restrict__ se
             sc[i] = cg[i];
     __syncthreads();
     const uint8_t *c = n <= CP_MAX ? (const uint8_t *)sc : cg;
-    if (threadIdx.x == 0) {
-        int uc = c[0];
-        double s = p10[c[0]];
-        for (int64_t i = 1; i < n; ++i) {   // the sequential leg (n < 16, or n <= 1,024)
-            const int ci = c[i];
-            s += p10[ci];
-            if (mt[ci] > mt[uc])
-                uc = ci;
+    // ucode: the code at the first position whose match score is maximal
+    // (the sequential `if (mt[c_i] > mt[uc]) uc = c_i` scan), by a wave
+    // reduction of (maximum, first position)
+    {
+        double best = -RF_INF;
+        int64_t at = INT64_MAX;
+        for (int64_t i = threadIdx.x; i < n; i += 64) {
+            const double v = mt[c[i]];
+            if (v > best) {   // strided: a lane's first maximum is its smallest position
+                best = v;
+                at = i;
+            }
         }
-        est[k] = n <= 1024 ? s : prep_julia_sum(c, p10, 0, n - 1);
-        ucode[k] = uc;
-        s_uc = uc;
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ob = __shfl_xor(best, off);
+            const int64_t oa = __shfl_xor(at, off);
+            if (ob > best || (ob == best && oa < at)) {
+                best = ob;
+                at = oa;
+            }
+        }
+        if (threadIdx.x == 0) {
+            const int uc = c[at == INT64_MAX ? 0 : at];
+            est[k] = n <= 1024 ? prep_seq_sum(c, p10, 0, n - 1) : prep_julia_sum(c, p10, 0, n - 1);
+            ucode[k] = uc;
+            s_uc = uc;
+        }
     }
     __syncthreads();
     const int uc = s_uc;
     for (int i = threadIdx.x; i < 256; i += 64)
         gr[i] = grid[(size_t)uc * 256 + i];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = gr[c[0]];
-        for (int64_t i = 1; i < n; ++i)
-            t += gr[c[i]];
-        tsum[k] = t;
-    }
+    if (threadIdx.x == 0)
+        tsum[k] = prep_seq_sum(c, gr, 0, n - 1);
 }
 
 // ---------------------------------------------------------------------
