@@ -373,6 +373,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="c4 only: skip the secondary c5 (10 kb, band doubling) workload")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="c4 only: skip the c2 field (configs[1]: whole runs of 100 reads x 1 kb, seeds 1..5)")
     ap.add_argument("--no-c3", action="store_true",
                     help="c4 only: skip the c3 field (configs[2] run with the reference's codon moves)")
     ap.add_argument("--no-sharded-rifraf", action="store_true",
@@ -454,6 +456,10 @@ def main():
         result = run_clusters(args, rank, world, gpu, dist, torch, coll)
         if args.config == "c4" and args.e2e_clusters > 0:
             result["e2e"] = run_e2e(args, rank, world, gpu, dist, coll)
+        if args.config == "c4" and not args.no_c2 and rank == 0:
+            # configs[1] beside the headline line: whole runs of the 1 kb
+            # cluster, latency mode, checked against the oracle's runs
+            result["c2"] = run_c2(args, gpu)
         if args.config == "c4" and not args.no_c3 and rank == 0:
             # configs[2] beside the headline line: the reference-informed path
             # (FRAME, codon moves) end to end, rank 0 only (one cluster)
@@ -497,108 +503,265 @@ def run_dry(args, rank, world, gpu, dist, coll, n_dev):
     if dist is not None:
         elapsed, units = aggregate(elapsed, units, coll)
         cspread = spread(float(cells), coll)
+    hand_out = None
+    if args.config == "c4" and args.e2e_clusters > 0:
+        hand_out = dry_hand_out(args, rank, world, dist)
     return {"metric": "banded fwd/bwd GCUPS + candidate proposals scored/sec, 1/2/4/8 MI355X",
             "value": None, "unit": "GCUPS", "dry_run": True, "steps": args.steps, "warmup": args.warmup,
+            "e2e_hand_out": hand_out,
             "higher_is_better": True, "scaling": "strong" if args.config == "c5" else "weak",
             "config": {"workload": args.config, "description": label},
             "cells_per_step_all_ranks": int(units[0]), "reads_all_ranks": int(units[1]),
             "rank_cells_min_max": None if cspread is None else [int(x) for x in cspread]}
 
 
+E2E_SHAPE = (50, 1500, 0.01)     # SURVEY.md §8(d) config 4's cluster shape
+
+
+def e2e_cluster(seed, k):
+    """Global e2e cluster k: sample_sequences(50, 1500; error_rate=0.01)
+    seeded by (seed, 77, 0, k) -> (template, rifraf keyword dict)."""
+    from rifraf_amd.sample import sample_sequences
+    nr, ln, er = E2E_SHAPE
+    _, t, _, reads, _, phreds, _, _ = sample_sequences(nr, ln, error_rate=er,
+                                                       rng=np.random.default_rng([seed, 77, 0, k]))
+    return t, dict(dnaseqs=reads, phreds=phreds)
+
+
+class E2EClusters:
+    """The e2e field's one global list of clusters, n per rank.  At N > 1
+    each rank simulates its own block (untimed) and writes it to a staging
+    directory on the host (/dev/shm), and every rank maps all blocks, so
+    whichever rank the queue hands cluster k to reads it back (as each of the
+    reference's pmap workers reads its file, scripts/rifraf.jl:190):
+    `get(k)` -> rifraf keyword dict, `template(k)`."""
+
+    FIELDS = ("bases", "phreds", "lens", "tpl", "tlens")
+
+    def __init__(self, seed, n_per_rank, rank, world, dist=None):
+        self.n = n_per_rank * world
+        self.dir = None
+        lo = rank * n_per_rank
+        blk = [e2e_cluster(seed, k) for k in range(lo, lo + n_per_rank)]
+        if world == 1:
+            self._local = blk
+            return
+        import tempfile
+        base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+        self.dir = os.path.join(base, "rifraf_bench_e2e_%s_%s" % (os.environ.get("MASTER_ADDR", "x"),
+                                                                  os.environ.get("MASTER_PORT", "0")))
+        os.makedirs(self.dir, exist_ok=True)
+        arrs = {"bases": np.concatenate([r for _, kw in blk for r in kw["dnaseqs"]]).astype(np.uint8),
+                "phreds": np.concatenate([p for _, kw in blk for p in kw["phreds"]]).astype(np.int8),
+                "lens": np.array([len(kw["dnaseqs"]) for _, kw in blk] +
+                                 [len(r) for _, kw in blk for r in kw["dnaseqs"]], np.int64),
+                "tpl": np.concatenate([t for t, _ in blk]).astype(np.uint8),
+                "tlens": np.array([len(t) for t, _ in blk], np.int64)}
+        for f, a in arrs.items():
+            tmp = os.path.join(self.dir, f"b{rank}_{f}.tmp.npy")
+            np.save(tmp, a)
+            os.replace(tmp, os.path.join(self.dir, f"b{rank}_{f}.npy"))
+        dist.barrier()
+        self.blocks = []
+        for r in range(world):
+            m = {f: np.load(os.path.join(self.dir, f"b{r}_{f}.npy"), mmap_mode="r") for f in self.FIELDS}
+            nc = len(m["tlens"])
+            counts = np.asarray(m["lens"][:nc])
+            rl = np.asarray(m["lens"][nc:])
+            roff = np.concatenate([[0], np.cumsum(rl)])
+            coff = np.concatenate([[0], np.cumsum(counts)])
+            toff = np.concatenate([[0], np.cumsum(m["tlens"])])
+            self.blocks.append((m, roff, coff, toff))
+        self.per = n_per_rank
+
+    def get(self, k):
+        if self.dir is None:
+            return self._local[k][1]
+        m, roff, coff, toff = self.blocks[k // self.per]
+        c = k % self.per
+        reads = [np.array(m["bases"][roff[i]:roff[i + 1]]) for i in range(coff[c], coff[c + 1])]
+        phreds = [np.array(m["phreds"][roff[i]:roff[i + 1]]) for i in range(coff[c], coff[c + 1])]
+        return dict(dnaseqs=reads, phreds=phreds)
+
+    def template(self, k):
+        if self.dir is None:
+            return self._local[k][0]
+        m, _, _, toff = self.blocks[k // self.per]
+        c = k % self.per
+        return np.array(m["tpl"][toff[c]:toff[c + 1]])
+
+    def close(self, rank, dist=None):
+        """Drop the maps; after a barrier rank 0 removes the staging files."""
+        if self.dir is None:
+            return
+        self.blocks = None
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            import shutil
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def _digest(kw):
+    import hashlib
+    h = hashlib.sha256()
+    for r, p in zip(kw["dnaseqs"], kw["phreds"]):
+        h.update(np.asarray(r, np.uint8).tobytes())
+        h.update(np.asarray(p, np.int8).tobytes())
+        h.update(b"|")
+    return h.hexdigest()
+
+
+def dry_hand_out(args, rank, world, dist, n_max=8):
+    """--dry-run: the e2e field's cluster hand-out without the engine -- the
+    staged global list (at most n_max clusters per rank), one pass of the
+    process group's ClusterQueue, and on rank 0 the check that every cluster
+    was taken exactly once and read back identical to what one process
+    simulates for it."""
+    from rifraf_amd.batch import ClusterQueue
+    data = E2EClusters(args.seed, min(args.e2e_clusters, n_max), rank, world, dist)
+    q = ClusterQueue.for_process_group(data.n, max(1, min(args.e2e_wave, 2)))
+    got = {}
+    while True:
+        r = q.take()
+        if r is None:
+            break
+        for k in r:
+            got[k] = _digest(data.get(k))
+    if dist is not None:
+        dist.barrier()
+        allg = [None] * world
+        dist.all_gather_object(allg, got)
+    else:
+        allg = [got]
+    data.close(rank, dist)
+    if rank != 0:
+        return None
+    seen, once = {}, True
+    for g in allg:
+        for k, d in g.items():
+            once = once and k not in seen
+            seen[k] = d
+    ident = sorted(seen) == list(range(data.n)) and all(seen[k] == _digest(e2e_cluster(args.seed, k)[1])
+                                                         for k in range(data.n))
+    return {"clusters": data.n, "exactly_once": bool(once and sorted(seen) == list(range(data.n))),
+            "identical_to_one_process": bool(ident), "per_rank": [len(g) for g in allg]}
+
+
 def run_e2e(args, rank, world, gpu, dist, coll):
     """Whole rifraf() runs on the c4 cluster shape (SURVEY.md §8(d) config 4:
-    every read in each batch, quality scores on) through rifraf_batch on this
-    rank's GPU -- the native lockstep stage machine (rf_rifraf_batch) in one
-    process.  clusters_per_s = all ranks' clusters / the slowest rank's
-    wall time (host setup from reads included, read simulation excluded).
-    Two clusters are re-run through the Python stage machine (the reference
-    restatement) and must match exactly."""
-    from rifraf_amd.batch import rifraf_batch
+    every read in each batch, quality scores on) through rifraf_batch_queue:
+    one global list of clusters (--e2e-clusters per rank), handed out in
+    waves to whichever engine of whichever rank asks next (ClusterQueue on
+    the process group's store: the reference's pmap over files,
+    scripts/rifraf.jl:190), each wave through the native lockstep stage
+    machine (rf_rifraf_batch).  clusters_per_s = all clusters / the slowest
+    rank's wall time (host setup from reads included, read simulation
+    excluded).  Two of this rank's clusters are re-run through the Python
+    stage machine (the reference restatement) and must match exactly."""
+    from rifraf_amd.batch import ClusterQueue, rifraf_batch, rifraf_batch_queue
     from rifraf_amd.engine import Engine
     from rifraf_amd.model import RifrafParams
-    from rifraf_amd.sample import sample_sequences
-    n = args.e2e_clusters
-    clusters, templates = [], []
-    for k in range(n):
-        _, t, _, reads, _, phreds, _, _ = sample_sequences(
-            50, 1500, error_rate=0.01, rng=np.random.default_rng([args.seed, 77, rank, k]))
-        clusters.append(dict(dnaseqs=reads, phreds=phreds))
-        templates.append(t)
+    data = E2EClusters(args.seed, args.e2e_clusters, rank, world, dist)
     params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
     ne = max(1, args.e2e_engines)
     engs = [Engine(gpu) for _ in range(ne)]
+    warm = [data.get(k) for k in range(min(4, data.n))]
     for e in engs:
-        rifraf_batch(clusters[:4], params=params, engine=e)        # warm-up (kernels, pinned staging)
+        rifraf_batch(warm, params=params, engine=e)        # warm-up (kernels, pinned staging)
+    wave = max(1, args.e2e_wave)
+
+    def queued(excl):
+        """One full pass over the global list; (wall s, results, stats)."""
+        q = ClusterQueue.for_process_group(data.n, wave)
+        st = {}
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res = rifraf_batch_queue(data.get, q, params=params, engines=engs, init_exclusive=excl, stats=st)
+        return time.perf_counter() - t0, res, st
+
+    excl = bool(args.e2e_init_exclusive)
     # cold: the first full-size run also sizes each context's band arena; the
     # timed run is the steady state of a stream of waves (the arena is reused,
     # rf_release_bands) -- every stage of every cluster is recomputed
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    bopt = dict(engines=engs, wave=max(1, args.e2e_wave), init_exclusive=bool(args.e2e_init_exclusive))
-    rifraf_batch(clusters, params=params, **bopt)
-    cold = time.perf_counter() - t0
+    cold, _, _ = queued(excl)
     # steady state: five rounds of (unpinned run, run with this rank held to
     # 2 host cores -- its share at 8 ranks on the GPU box's 16; every thread
     # of the process pinned in place, no relaunch; the library's worker pools
     # follow the mask), medians of each (one run of either varies by ~10 %
-    # between rounds on one box, profiles/r05l_e2e_pinned.jsonl, r05al_bench.json)
-    pin = pin_rate = None
+    # between rounds on one box, profiles/r05l_e2e_pinned.jsonl, r05al_bench.json).
+    # Every rank decides to pin (or not) the same way, so all ranks make the
+    # same number of queue passes and barriers.
     allowed = sorted(os.sched_getaffinity(0))
-    if args.e2e_pin_cores > 0 and len(allowed) > args.e2e_pin_cores:
-        k = args.e2e_pin_cores
-        pin = allowed[(rank * k) % len(allowed):][:k] or allowed[:k]
-    pin_opt = dict(bopt, init_exclusive=bool(args.e2e_pin_exclusive) if ne > 1 and args.e2e_pin_exclusive >= 0
-                   else bopt["init_exclusive"])
-    runs, pin_runs, same_pin = [], [], True
+    k = args.e2e_pin_cores
+    can_pin = float(k > 0 and len(allowed) > k)
+    if dist is not None:
+        import torch
+        f = torch.tensor([can_pin], dtype=torch.float64, device=coll)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        can_pin = float(f.item())
+    pin = (allowed[(rank * k) % len(allowed):][:k] or allowed[:k]) if can_pin else None
+    pin_excl = bool(args.e2e_pin_exclusive) if ne > 1 and args.e2e_pin_exclusive >= 0 else excl
+    runs, pin_runs, stats, same_pin = [], [], [], True
     res = None
     for _ in range(5 if pin else 3):
-        if dist is not None:
-            dist.barrier()
-        t0 = time.perf_counter()
-        r_ = rifraf_batch(clusters, params=params, **bopt)
-        runs.append(time.perf_counter() - t0)
+        s_, r_, st = queued(excl)
+        runs.append(s_)
+        stats.append(st)
         res = res or r_
         if pin:
             saved = pin_threads(pin)
             try:
-                if dist is not None:
-                    dist.barrier()
-                t0 = time.perf_counter()
-                res_pin = rifraf_batch(clusters, params=params, **pin_opt)
-                pin_runs.append(time.perf_counter() - t0)
+                s_, res_pin, _ = queued(pin_excl)
+                pin_runs.append(s_)
             finally:
                 unpin_threads(saved)
-            same_pin = same_pin and all(np.array_equal(a.consensus, b.consensus) for a, b in zip(res, res_pin))
+            # the queue hands clusters out afresh: compare the ones this rank ran both times
+            same_pin = same_pin and all(np.array_equal(res[i].consensus, res_pin[i].consensus)
+                                        for i in set(res) & set(res_pin))
     elapsed = float(np.median(runs))
-    if pin:
-        pin_rate = (float(np.median(pin_runs)), same_pin)
-    ref = rifraf_batch(clusters[:2], params=params, engine=engs[0], native=False)
-    same = all(np.array_equal(a.consensus, b.consensus) and a.state.score == b.state.score and
-               qv_close(a, b) for a, b in zip(res[:2], ref))
+    mine = sorted(res)
+    chk = mine[:2]
+    ref = rifraf_batch([data.get(i) for i in chk], params=params, engine=engs[0], native=False)
+    same = all(np.array_equal(res[i].consensus, b.consensus) and res[i].state.score == b.state.score and
+               qv_close(res[i], b) for i, b in zip(chk, ref))
     for e in engs:
         e.close()
-    ok = sum(int(np.array_equal(r.consensus, t)) for r, t in zip(res, templates))
-    iters = sum(sum(r.state.stage_iterations) for r in res)
-    tot = [float(n), float(ok), float(iters), 1.0 if same else 0.0]
-    pin_s = pin_rate[0] if pin_rate else 0.0
+    ok = sum(int(np.array_equal(res[i].consensus, data.template(i))) for i in mine)
+    iters = sum(sum(res[i].state.stage_iterations) for i in mine)
+    med = stats[int(np.argsort(runs)[len(runs) // 2])]
+    tot = [float(len(mine)), float(ok), float(iters), 1.0 if same else 0.0]
+    pin_s = float(np.median(pin_runs)) if pin_runs else 0.0
+    per_rank = None
     if dist is not None:
         cold, _ = aggregate(cold, [0.0], coll)
         pin_s, _ = aggregate(pin_s, [0.0], coll)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"clusters": med.get("clusters"), "waves": med.get("waves"),
+                                          "busy_s": med.get("busy_s"), "barrier_wait_s": med.get("barrier_wait_s")})
         elapsed, tot = aggregate(elapsed, tot, coll)
-    return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": tot[0] / elapsed,
-            "clusters_per_s_per_gpu": tot[0] / elapsed / max(world, 1), "ranks": world,
-            "clusters": int(tot[0]), "seconds": elapsed,
-            "cold_clusters_per_s": tot[0] / cold,
-            "timing": "steady state: the median of five full runs over the clusters after the first ('cold', "
-                      "which also allocates the band arena), alternating with the pinned runs; host setup from "
+    data.close(rank, dist)
+    n_all = float(data.n)
+    return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": n_all / elapsed,
+            "clusters_per_s_per_gpu": n_all / elapsed / max(world, 1), "ranks": world,
+            "clusters": int(n_all), "clusters_run_once": int(tot[0]) == int(n_all), "seconds": elapsed,
+            "cold_clusters_per_s": n_all / cold,
+            "timing": "steady state: the median of five full passes over the clusters after the first ('cold', "
+                      "which also allocates the band arena), alternating with the pinned passes; host setup from "
                       "reads included, read simulation excluded",
             "processes_per_gpu": getattr(args, "processes_per_gpu", 1),
-            "engines_per_gpu": ne, "wave": bopt["wave"], "init_exclusive": bopt["init_exclusive"],
-            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass; waves of clusters taken "
-                      "from a shared queue by engines_per_gpu contexts (own HIP stream, own host thread) in one "
-                      "process, at most one of them in its native stage machine at a time when init_exclusive "
-                      "(scripts/e2e_pinned.py, profiles/r04l_e2e_pipeline.jsonl)",
+            "engines_per_gpu": ne, "wave": wave, "init_exclusive": excl,
+            "hand_out": "ClusterQueue (rifraf_amd/batch.py): one global list of clusters, waves handed to "
+                        "whichever engine of whichever rank asks next through the process group's store "
+                        "(scripts/rifraf.jl:190's pmap); per_rank: clusters / waves taken, seconds running them "
+                        "and waiting at the closing barrier, in the median unpinned pass",
+            "per_rank": per_rank if per_rank is not None else [{
+                "clusters": med.get("clusters"), "waves": med.get("waves"), "busy_s": med.get("busy_s"),
+                "barrier_wait_s": med.get("barrier_wait_s")}],
+            "driver": "rf_rifraf_batch (native lockstep INIT) + batched quality pass per wave; "
+                      "engines_per_gpu contexts (own HIP stream, own host thread) per process, at most one of "
+                      "them in its native stage machine at a time when init_exclusive",
             "params": "batch = all 50 reads, do_score (QVs), no reference",
             "consensus_equals_template": int(tot[1]), "stage_iterations": int(tot[2]),
             "consensus_misses_explained": "profiles/r04_e2e_misses.json: every miss converges at a consensus "
@@ -607,11 +770,11 @@ def run_e2e(args, rank, world, gpu, dist, coll):
             "same_as_python_stage_machine_note": "consensus and score bit-identical; QVs (device quality pass) "
                                                  "within 1e-12 relative + 1e-15 absolute",
             "runs_s": runs, "pinned_runs_s": pin_runs,
-            "pinned": None if pin_rate is None else {
-                "cores": len(pin), "clusters_per_s": tot[0] / pin_s, "ratio_to_unpinned": elapsed / pin_s,
-                "init_exclusive": pin_opt["init_exclusive"],
-                "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(pin_rate[1]),
-                "note": "the same steady-state run with every thread of the rank pinned to this many cores "
+            "pinned": None if not pin else {
+                "cores": len(pin), "clusters_per_s": n_all / pin_s, "ratio_to_unpinned": elapsed / pin_s,
+                "init_exclusive": pin_excl,
+                "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(same_pin),
+                "note": "the same steady-state pass with every thread of the rank pinned to this many cores "
                         "(a rank's share of the box's 16 at 8 ranks)"}}
 
 
@@ -807,6 +970,56 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
 
 
 C3_SEED = 3   # the c3 parity tests' cluster (tests/test_workloads.py::test_c3_*)
+GOLDEN_RUNS = os.path.join(REPO, "tests", "golden", "runs.npz")   # scripts/make_golden.py runs()
+C2_SEEDS = (1, 2, 3, 4, 5)
+C2_VARIANTS = {"default": dict(seed=1),
+               "throughput": dict(seed=1, batch_size=0, batch_fixed=False, do_score=True)}
+
+
+def golden_run(name, z=None):
+    """The CPU oracle engine's whole rifraf() run `name` ("c2_<seed>_<variant>",
+    "c3_throughput") from tests/golden/runs.npz (committed data, made by
+    scripts/make_golden.py; bench checks its runs against it)."""
+    z = np.load(GOLDEN_RUNS) if z is None else z
+    pre = name + "_"
+    return {k[len(pre):]: z[k] for k in z.files if k.startswith(pre)}
+
+
+def run_matches(res, rec, qv_rtol=1e-12, atol=1e-15):
+    """A rifraf() result against a golden_run record: consensus, every
+    stage's consensuses, score bits, stage iterations, penalty increases and
+    convergence exactly; QVs within qv_rtol (the native driver's device
+    quality pass uses the GPU's exp10; 0 = bit-exact)."""
+    st = res.consensus_stages
+    lens = [len(c) for x in st for c in x]
+    ok = (np.array_equal(np.asarray(res.consensus, np.uint8), rec["consensus"]) and
+          res.state.score == float(rec["score"]) and
+          list(res.state.stage_iterations) == rec["iters"].tolist() and
+          int(res.state.n_ref_indel_mults) == int(rec["mults"]) and
+          bool(res.state.converged) == bool(rec["converged"]) and
+          [len(x) for x in st] == rec["stage_counts"].tolist() and lens == rec["stage_lens"].tolist() and
+          np.array_equal(np.concatenate([np.asarray(c, np.uint8) for x in st for c in x] or
+                                        [np.zeros(0, np.uint8)]), rec["stages"]))
+    if not ok:
+        return False
+    if "sub" not in rec:
+        return res.error_probs is None
+    if res.error_probs is None:
+        return False
+    pairs = [(res.error_probs.sub, rec["sub"]), (res.error_probs.dele, rec["dele"]),
+             (res.error_probs.ins, rec["ins"]), (res.aln_error_probs, rec["aln"])]
+    if qv_rtol == 0:
+        return all(np.array_equal(a, b) for a, b in pairs)
+    return all(np.shape(a) == np.shape(b) and np.allclose(a, b, rtol=qv_rtol, atol=atol) for a, b in pairs)
+
+
+def c2_cluster(seed):
+    """configs[1]: sample_sequences(100, 1000; error_rate=0.01), no reference
+    (sample.jl:277-298)."""
+    from rifraf_amd.sample import sample_sequences
+    rng = np.random.default_rng(seed)
+    _, template, _, reads, _, phreds, _, _ = sample_sequences(100, 1000, error_rate=0.01, rng=rng)
+    return template, reads, phreds
 
 
 def c3_cluster(seed=C3_SEED):
@@ -910,7 +1123,8 @@ def run_c3(args, gpu):
     template, reads, phreds, ref = c3_cluster()
     params = model.RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True)
     kw = dict(dnaseqs=reads, phreds=phreds, reference=ref)
-    eng = Engine(gpu)
+    eng = Engine(gpu)          # the product default options (latency-mode DP for small calls)
+    dp_lat = eng.get_option("dp_lat")
     try:
         rifraf_batch([kw], params=params, engine=eng, native=True)        # warm-up (kernels, arena)
         t0 = time.perf_counter()
@@ -928,6 +1142,35 @@ def run_c3(args, gpu):
         eng.close()
     same = (np.array_equal(nat.consensus, py.consensus) and nat.state.score == py.state.score and
             nat.state.stage_iterations == py.state.stage_iterations and qv_close(nat, py))
+    gold = golden_run("c3_throughput")
+    stages, frame, tot = stage_split(timer)
+    return {"metric": "one rifraf() run of configs[2] (reference-informed, codon frame correction)",
+            "workload": "c3", "reads": len(reads), "template_len": len(template), "reference_len": len(ref),
+            "params": "batch = all 1000 reads, do_score (QVs), seed 1; reference with a one-base frameshift",
+            "native_seconds_per_run": native_s, "runs_per_s": 1.0 / native_s,
+            "python_stage_machine_seconds": py_s, "same_as_python_stage_machine": bool(same),
+            "dp_lat": dp_lat,
+            "same_as_oracle": {"native": bool(run_matches(nat, gold)),
+                               "python_stage_machine": bool(run_matches(py, gold, qv_rtol=0)),
+                               "fixture": "tests/golden/runs.npz c3_throughput (scripts/make_golden.py: the CPU "
+                                          "oracle engine's run of this cluster); consensus, every stage's "
+                                          "consensuses, score bits, iterations, penalty increases exact; QVs "
+                                          "bit-exact (Python stage machine) / within 1e-12 (native driver's "
+                                          "device quality pass)"},
+            "consensus_equals_template": bool(np.array_equal(nat.consensus, template)),
+            "stage_iterations": list(nat.state.stage_iterations),
+            "penalty_increases": int(nat.state.n_ref_indel_mults),
+            "kernel_ms_total": tot, "codon_share_of_kernel_ms": tot["codon_ms"] / max(
+                tot["dp_ms"] + tot["score_ms"] + tot["walk_ms"], 1e-9),
+            "per_stage": stages, "frame_iterations": frame,
+            "timing": "kernel ms: HIP events on the engine stream, summed per stage from the Python stage "
+                      "machine's run (score_ms includes codon_ms); native_seconds_per_run: wall time of the "
+                      "library's stage machine, host work included"}
+
+
+def stage_split(timer):
+    """Per-stage and per-FRAME-iteration kernel time and work of a
+    _StageTimer'd run, and their totals."""
     stages = {}
     for (st, it), r in timer.rec.items():
         a = stages.setdefault(st, {"iterations": 0})
@@ -941,20 +1184,70 @@ def run_c3(args, gpu):
              if st == "FRAME"]
     tot = {k: sum(r.get(k, 0) for r in timer.rec.values())
            for k in ("dp_ms", "score_ms", "codon_ms", "walk_ms", "dp_cells", "proposals", "codon_proposals")}
-    return {"metric": "one rifraf() run of configs[2] (reference-informed, codon frame correction)",
-            "workload": "c3", "reads": len(reads), "template_len": len(template), "reference_len": len(ref),
-            "params": "batch = all 1000 reads, do_score (QVs), seed 1; reference with a one-base frameshift",
-            "native_seconds_per_run": native_s, "runs_per_s": 1.0 / native_s,
-            "python_stage_machine_seconds": py_s, "same_as_python_stage_machine": bool(same),
-            "consensus_equals_template": bool(np.array_equal(nat.consensus, template)),
-            "stage_iterations": list(nat.state.stage_iterations),
-            "penalty_increases": int(nat.state.n_ref_indel_mults),
-            "kernel_ms_total": tot, "codon_share_of_kernel_ms": tot["codon_ms"] / max(
-                tot["dp_ms"] + tot["score_ms"] + tot["walk_ms"], 1e-9),
-            "per_stage": stages, "frame_iterations": frame,
-            "timing": "kernel ms: HIP events on the engine stream, summed per stage from the Python stage "
-                      "machine's run (score_ms includes codon_ms); native_seconds_per_run: wall time of the "
-                      "library's stage machine, host work included"}
+    return stages, frame, tot
+
+
+def run_c2(args, gpu):
+    """configs[1] end to end (rank 0): rifraf() of sample_sequences(100, 1000;
+    error_rate=0.01), no reference, seeds 1..5, with the default params and
+    the throughput settings (every read in every batch, QV pass on).  Each
+    run goes through the library's stage machine (rf_rifraf_batch, one
+    cluster) on an engine with the product default options -- its realigns
+    have at most 100 lean tasks, so the DP runs in latency mode (k_dpx) --
+    and is checked against the CPU oracle engine's run of the same cluster
+    (tests/golden/runs.npz).  Reports the median wall time per run per
+    variant, and per-stage kernel ms of seed 1 from the Python stage machine
+    on the same engine (which must give the same result)."""
+    import rifraf_amd.model as model
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.engine import Engine
+    z = np.load(GOLDEN_RUNS)
+    clusters = {seed: c2_cluster(seed) for seed in C2_SEEDS}
+    eng = Engine(gpu)
+    dp_lat = eng.get_option("dp_lat")
+    out = {"metric": "one rifraf() run of configs[1] (100 reads x 1 kb, no reference)", "workload": "c2",
+           "seeds": list(C2_SEEDS), "dp_lat": dp_lat}
+    try:
+        for var, kw in C2_VARIANTS.items():
+            params = model.RifrafParams(**kw)
+            t, reads, phreds = clusters[C2_SEEDS[0]]
+            rifraf_batch([dict(dnaseqs=reads, phreds=phreds)], params=params, engine=eng, native=True)  # warm-up
+            secs, match, tmpl = [], [], []
+            for seed in C2_SEEDS:
+                t, reads, phreds = clusters[seed]
+                t0 = time.perf_counter()
+                res = rifraf_batch([dict(dnaseqs=reads, phreds=phreds)], params=params, engine=eng,
+                                   native=True)[0]
+                secs.append(time.perf_counter() - t0)
+                match.append(bool(run_matches(res, golden_run(f"c2_{seed}_{var}", z))))
+                tmpl.append(bool(np.array_equal(res.consensus, t)))
+            t, reads, phreds = clusters[C2_SEEDS[0]]
+            timer = _StageTimer(eng)
+            model.ITERATION_HOOK = timer.hook
+            try:
+                t0 = time.perf_counter()
+                py = model.rifraf(reads, phreds, params=params, engine=timer)
+                py_s = time.perf_counter() - t0
+            finally:
+                model.ITERATION_HOOK = None
+            stages, _, tot = stage_split(timer)
+            out[var] = {"params": "RifrafParams(%s)" % ", ".join(f"{k}={v}" for k, v in kw.items()),
+                        "native_seconds_per_run": float(np.median(secs)), "runs_per_s": 1.0 / float(np.median(secs)),
+                        "native_seconds": secs, "same_as_oracle": match, "all_same_as_oracle": all(match),
+                        "consensus_equals_template": tmpl,
+                        "python_stage_machine_seconds_seed1": py_s,
+                        "python_stage_machine_same_as_oracle_seed1": bool(
+                            run_matches(py, golden_run(f"c2_{C2_SEEDS[0]}_{var}", z), qv_rtol=0)),
+                        "kernel_ms_total_seed1": tot, "per_stage_seed1": stages}
+    finally:
+        eng.close()
+    out["timing"] = ("native_seconds_per_run: median wall time of the library's stage machine over the seeds "
+                     "(host work included, after one warm-up run); kernel ms: HIP events on the engine stream, "
+                     "summed per stage from the Python stage machine's run of seed 1")
+    out["oracle_fixture"] = ("tests/golden/runs.npz (scripts/make_golden.py runs(): the CPU oracle engine); "
+                             "consensus, stage consensuses, score bits, iterations exact, QVs within 1e-12 "
+                             "(device quality pass)")
+    return out
 
 
 class _TimedEngine:

@@ -429,12 +429,15 @@ struct Driver {
             bw.push_back(R.bw);
             moff.push_back(moff.back() + R.len + (int64_t)C.cons.size());
         }
-        if (!filled)   // (filled: the scratch slot holds this fill already, realign_B)
+        if (!filled) {   // (filled: the scratch slot holds this fill already, realign_B)
+            for (int c : cs)
+                clu[c].sip_pre = false;   // any other write to the scratch slot ends the cached fill
             if (int e = timed(T_FWD, [&] {
                     return rf_realign(ctx, (int32_t)cs.size(), sl.data(), sq.data(), tp.data(), bw.data(),
                                       RF_FWD | (skew ? RF_SKEW : 0), nullptr);
                 }))
                 return e;
+        }
         std::vector<int8_t> moves((size_t)std::max<int64_t>(moff.back(), 1));
         if (int e = timed(T_BT, [&] {
                 return rf_backtrace(ctx, (int32_t)cs.size(), sl.data(), moves.data(), moff.data(), nm.data(), nullptr);
@@ -739,7 +742,8 @@ struct Driver {
             batched(to_frame, [&](const std::vector<int> &s) {
                 std::vector<int32_t> sl, sq, tp, bw, nerr(s.size());
                 for (int c : s) {
-                    const Clu &C = clu[c];
+                    Clu &C = clu[c];
+                    C.sip_pre = false;   // the scratch slot takes edit_distance's band
                     sl.push_back(C.scratch_slot);
                     sq.push_back(C.edit_seq);
                     tp.push_back(C.tpl);

@@ -790,37 +790,77 @@ class ClusterQueue:
     worker takes the next file) across the GPUs of a node.  The counter lives
     in the process group's key-value store (torch.distributed's TCPStore:
     `add` is atomic), so no data-path collective is involved.  Every rank
-    must create its queues in the same order (the key carries a generation
-    number).  Without a store (one process) the counter is local."""
+    must create its store-backed queues in the same order (the key carries a
+    generation number counted over store-backed queues only), or pass the
+    same explicit `key`; rank 0 publishes each queue's (key, n, wave) and
+    the other ranks check theirs against it, so ranks that disagree fail
+    loudly instead of each running every cluster.  Without a store (one
+    process) the counter is local."""
 
     _gen = 0
 
-    def __init__(self, n: int, wave: int, store=None, prefix: str = "rifraf_cluster_queue"):
-        ClusterQueue._gen += 1
+    def __init__(self, n: int, wave: int, store=None, prefix: str = "rifraf_cluster_queue", key=None,
+                 rank: int = 0, timeout_s: float = 300.0):
         self.n, self.wave = int(n), max(1, int(wave))
         self.store = store
-        self.key = f"{prefix}/{ClusterQueue._gen}"
+        self.rank = int(rank)
         self._local = 0
         self._lock = threading.Lock()
+        if store is None:
+            self.key = f"{prefix}/local" if key is None else str(key)
+            return
+        if key is None:
+            ClusterQueue._gen += 1
+            key = f"{prefix}/{ClusterQueue._gen}"
+        self.key = str(key)
+        desc = f"{self.key} n={self.n} wave={self.wave}"
+        if self.rank == 0:
+            store.set(self.key + "/desc", desc)
+        else:
+            import datetime
+            try:
+                store.wait([self.key + "/desc"], datetime.timedelta(seconds=timeout_s))
+                got = store.get(self.key + "/desc").decode()
+            except Exception as e:  # noqa: BLE001 -- reported as the queue mismatch it is
+                raise RuntimeError(f"ClusterQueue: rank {self.rank} found no queue {self.key} published by "
+                                   f"rank 0 ({e}); create queues in the same order on every rank or pass key=")
+            if got != desc:
+                raise RuntimeError(f"ClusterQueue: rank {self.rank} has '{desc}', rank 0 published '{got}'")
 
     @classmethod
-    def for_process_group(cls, n: int, wave: int):
+    def for_process_group(cls, n: int, wave: int, key=None):
         """A queue on the default process group's store (every rank calls
-        this in the same order), or a local one when no group is up."""
+        this in the same order, or with the same `key`), or a local one when
+        no group is up."""
         store = None
+        rank = 0
         try:
             import torch.distributed as dist
             if dist.is_available() and dist.is_initialized():
                 from torch.distributed import distributed_c10d
                 store = distributed_c10d._get_default_store()
+                rank = dist.get_rank()
         except Exception:  # noqa: BLE001 -- no process group: one process takes every wave
             store = None
-        return cls(n, wave, store)
+        return cls(n, wave, store, key=key, rank=rank)
+
+    def failed(self):
+        """The rank that reported a failure on this queue, or None."""
+        if self.store is None or not self.store.check([self.key + "/failed"]):
+            return None
+        return int(self.store.get(self.key + "/failed").decode())
+
+    def fail(self):
+        """Mark the queue failed (this rank raised): no rank takes more waves."""
+        if self.store is not None:
+            self.store.set(self.key + "/failed", str(self.rank))
 
     def take(self):
         """The next wave's cluster indices (a range), or None when the queue
-        is empty."""
+        is empty (or a rank has failed)."""
         if self.store is not None:
+            if self.failed() is not None:
+                return None
             hi = int(self.store.add(self.key, self.wave))
         else:
             with self._lock:
@@ -832,24 +872,80 @@ class ClusterQueue:
         return range(lo, min(hi, self.n))
 
 
-def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=None, **kw):
+def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=None, engines=None,
+                       init_exclusive: bool = False, on_wave=None, stats=None, **kw):
     """rifraf_batch over the waves this process takes from `queue` (a
     ClusterQueue shared by the ranks of a node): `get_cluster(i)` gives
     cluster i's keyword dict (e.g. read from its FASTQ file, as each `pmap`
     worker does).  Returns {cluster index: RifrafResult} for the clusters
     this rank ran; over all ranks every cluster runs exactly once, with the
-    result rifraf() gives it alone (clusters are independent).  With a
-    store-backed queue every rank waits at a barrier once the queue is empty:
-    rank 0 hosts the store, so it must not tear the group down while another
-    rank still takes waves."""
+    result rifraf() gives it alone (clusters are independent).
+
+    engines: several engines of this process (e.g. two contexts on one GPU),
+    one host thread each, every thread taking its own waves from the queue
+    (init_exclusive: at most one of them in its native stage machine at a
+    time, as in rifraf_batch).  `on_wave(r)` is called with each wave's
+    range after it ran; `stats` (a dict) receives waves / clusters taken,
+    the seconds spent running them and the seconds waited at the closing
+    barrier.  With a store-backed queue every rank reaches that one barrier
+    once the queue is empty, also when it failed (rank 0 hosts the store, so
+    it must not tear the group down while another rank still takes waves):
+    a rank that raises marks the queue failed so the others stop taking
+    waves, and after the barrier the error is raised on it and a
+    RuntimeError on every other rank."""
+    import time
+    from .model import RifrafParams
+    params = params or RifrafParams()
+    engs = list(engines) if engines else [engine]
     out = {}
-    while True:
-        r = queue.take()
-        if r is None:
-            break
-        res = rifraf_batch([get_cluster(i) for i in r], params=params, engine=engine, wave=len(r), **kw)
-        out.update(zip(r, res))
+    errs = []
+    lock = threading.Lock()
+    ilock = threading.Lock() if init_exclusive and len(engs) > 1 else None
+    st = {"waves": 0, "clusters": 0, "busy_s": 0.0}
+
+    def worker(e):
+        try:
+            while True:
+                r = queue.take()
+                if r is None:
+                    return
+                t0 = time.perf_counter()
+                part = [get_cluster(i) for i in r]
+                if ilock is not None and kw.get("native", None) is not False and \
+                        native_eligible(part, params) and hasattr(e, "rifraf_batch_native"):
+                    res = _wave_native(part, params, e, init_lock=ilock, device_qv=kw.get("device_qv", True))
+                else:
+                    res = rifraf_batch(part, params=params, engine=e, wave=len(r), **kw)
+                with lock:
+                    out.update(zip(r, res))
+                    st["waves"] += 1
+                    st["clusters"] += len(r)
+                    st["busy_s"] += time.perf_counter() - t0
+                if on_wave is not None:
+                    on_wave(r)
+        except BaseException as ex:  # noqa: BLE001 -- re-raised below, after the barrier
+            with lock:
+                errs.append(ex)
+            queue.fail()
+
+    if len(engs) == 1:
+        worker(engs[0])
+    else:
+        ts = [threading.Thread(target=worker, args=(e,), daemon=True) for e in engs]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    t0 = time.perf_counter()
     if queue.store is not None:
         import torch.distributed as dist
         dist.barrier()
+    st["barrier_wait_s"] = time.perf_counter() - t0
+    if stats is not None:
+        stats.update(st)
+    if errs:
+        raise errs[0]
+    bad = queue.failed()
+    if bad is not None:
+        raise RuntimeError(f"rifraf_batch_queue: rank {bad} failed; its waves did not complete")
     return out

@@ -111,6 +111,12 @@ class RifrafResult:                            # model.jl:216-225
     aln_error_probs: np.ndarray | None = None
 
 
+# realign()'s B call also fills single_indel_proposals' skewed reference
+# alignment in FRAME (one engine call); False: single_indel_proposals fills
+# it itself (the reference's order; tests compare the two)
+SIP_CACHE = True
+
+
 class _Run:
     """Engine bindings of one rifraf() call (ids per the module docstring)."""
 
@@ -133,6 +139,13 @@ class _Run:
     def set_ref(self, ref):
         self.sip_ready = False
         self.e.set_sequences(self.REF, [ref])
+
+    def scratch(self):
+        """The scratch slot, for any write to it other than realign()'s
+        skewed fill (edit_distance, has_single_indels): the cached fill is
+        gone once it is written."""
+        self.sip_ready = False
+        return self.SCRATCH
 
 
 def log(params, level, msg):
@@ -299,7 +312,7 @@ def realign(state: RifrafState, run: _Run, params: RifrafParams):   # :679-714
             flags.append(RF_BWD)
         # FRAME with seeded indels: single_indel_proposals' skewed fill of the
         # reference against this consensus (model.jl:538-562) in the same call
-        sip = state.stage == Stage.FRAME and params.seed_indels and len(state.reference) > 0
+        sip = SIP_CACHE and state.stage == Stage.FRAME and params.seed_indels and len(state.reference) > 0
         if sip:
             slots.append(run.SCRATCH)
             ids.append(run.REF)
@@ -388,7 +401,7 @@ def _align_ref_moves(state: RifrafState, run: _Run, skew: bool):
     ref = state.reference
     if not (skew and run.sip_ready):
         run.set_ref(ref)
-        run.e.realign([run.SCRATCH], [run.REF], 0, [ref.bandwidth], RF_FWD | (RF_SKEW if skew else 0))
+        run.e.realign([run.scratch()], [run.REF], 0, [ref.bandwidth], RF_FWD | (RF_SKEW if skew else 0))
     run.sip_ready = False
     moves, _ = run.e.backtrace([run.SCRATCH])
     return moves[0]
@@ -471,7 +484,8 @@ def handle_candidates(candidates, state: RifrafState, run: _Run, params: RifrafP
 
 def edit_distance_engine(t, s, run: _Run):                        # align.jl:253-260
     from .align import Scratch, edit_distance
-    return edit_distance(t, s, scratch=Scratch(run.e, run.SCRATCH, 1, run.SCRATCH))
+    slot = run.scratch()
+    return edit_distance(t, s, scratch=Scratch(run.e, slot, 1, slot))
 
 
 def finish_stage(state: RifrafState, run: _Run, params: RifrafParams):   # :937-995

@@ -11,6 +11,15 @@ reference's own known-answer tests:
   tests/golden/config2.json   whole rifraf() runs on config-2-shaped
                               clusters (default params): final consensus,
                               score and stage iterations
+  tests/golden/runs.npz       whole rifraf() runs at the BASELINE configs'
+                              own shapes, the ones bench.py times: configs[1]
+                              (sample_sequences(100, 1000; error_rate=0.01),
+                              seeds 1..5, default params and the throughput
+                              settings) and configs[2] (bench.c3_cluster(),
+                              throughput settings) -- consensus, score, stage
+                              iterations, penalty increases, every stage's
+                              consensuses and the QVs; bench's c2 / c3 fields
+                              check their native runs against these
 
 usage: python scripts/make_golden.py   (deterministic; rerun to refresh)"""
 import json
@@ -81,7 +90,53 @@ def config2():
               open(os.path.join(OUT, "config2.json"), "w"), indent=1)
 
 
+def run_record(res):
+    """A whole rifraf() result as flat arrays (see runs())."""
+    st = res.consensus_stages
+    rec = dict(consensus=np.asarray(res.consensus, np.uint8), score=np.float64(res.state.score),
+               iters=np.asarray(res.state.stage_iterations, np.int64),
+               mults=np.int64(res.state.n_ref_indel_mults), converged=np.bool_(res.state.converged),
+               stage_counts=np.asarray([len(x) for x in st], np.int64),
+               stage_lens=np.asarray([len(c) for x in st for c in x], np.int64),
+               stages=np.concatenate([np.asarray(c, np.uint8) for x in st for c in x] or [np.zeros(0, np.uint8)]))
+    if res.error_probs is not None:
+        rec.update(sub=res.error_probs.sub, dele=res.error_probs.dele, ins=res.error_probs.ins,
+                   aln=np.asarray(res.aln_error_probs))
+    return rec
+
+
+C2_VARIANTS = {"default": dict(seed=1),
+               "throughput": dict(seed=1, batch_size=0, batch_fixed=False, do_score=True)}
+
+
+def c2_cluster(seed):
+    """configs[1]: sample_sequences(100, 1000; error_rate=0.01) (sample.jl:277-298)."""
+    rng = np.random.default_rng(seed)
+    _, t, _, reads, _, phreds, _, _ = sample_sequences(100, 1000, error_rate=0.01, rng=rng)
+    return t, reads, phreds
+
+
+def runs():
+    sys.path.insert(0, REPO)
+    import bench
+    out = {}
+    for seed in range(1, 6):
+        t, reads, phreds = c2_cluster(seed)
+        for var, kw in C2_VARIANTS.items():
+            res = rifraf(reads, phreds, params=RifrafParams(**kw), engine=OracleEngine())
+            for k, v in run_record(res).items():
+                out[f"c2_{seed}_{var}_{k}"] = v
+    t, reads, phreds, ref = bench.c3_cluster()
+    res = rifraf(reads, phreds, reference=ref, params=RifrafParams(**C2_VARIANTS["throughput"]),
+                 engine=OracleEngine())
+    for k, v in run_record(res).items():
+        out[f"c3_throughput_{k}"] = v
+    out["generator"] = np.asarray("scripts/make_golden.py runs() (CPU oracle engine)")
+    np.savez_compressed(os.path.join(OUT, "runs.npz"), **out)
+
+
 if __name__ == "__main__":
-    pairs()
-    config2()
-    print("wrote", os.path.join(OUT, "pairs.npz"), os.path.join(OUT, "config2.json"))
+    what = sys.argv[1:] or ["pairs", "config2", "runs"]
+    for w in what:
+        {"pairs": pairs, "config2": config2, "runs": runs}[w]()
+        print("wrote", w)

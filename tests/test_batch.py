@@ -91,15 +91,17 @@ def test_batch_engine_shards_oracle(wave, excl):
 
 
 @pytest.mark.gpu
-def test_batch_matches_separate_runs_hip(engine):
+def test_batch_matches_separate_runs_hip(run_engine):
+    engine = run_engine
     _check(lambda: engine, qv_rtol=QV_RTOL)
 
 
 @pytest.mark.gpu
-def test_batch_hip_matches_oracle_runs(engine):
+def test_batch_hip_matches_oracle_runs(run_engine):
     """HIP-batched clusters (one launch per request kind) against separate
     rifraf() runs on the CPU oracle engine: same consensus at every
     iteration, same score, same QVs (error_probs, aln_error_probs)."""
+    engine = run_engine
     from oracle_engine import OracleEngine
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import rifraf
@@ -131,12 +133,13 @@ NATIVE_PARAMS = {
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pset", sorted(NATIVE_PARAMS))
-def test_native_batch_matches_hub(engine, pset):
+def test_native_batch_matches_hub(run_engine, pset):
     """rf_rifraf_batch (the library's lockstep stage machine) against the
     Python stage machine over the same engine: identical consensus at every
     iteration, score, iteration counts and convergence; QVs bit-identical
     with the host quality pass (device_qv=False) and within 1e-12 with the
     device one (the default)."""
+    engine = run_engine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams
@@ -151,9 +154,10 @@ def test_native_batch_matches_hub(engine, pset):
 
 
 @pytest.mark.gpu
-def test_native_batch_matches_oracle_runs(engine):
+def test_native_batch_matches_oracle_runs(run_engine):
     """Native batched clusters against separate rifraf() runs on the CPU
     oracle engine (reference-free clusters, quality scores on)."""
+    engine = run_engine
     from oracle_engine import OracleEngine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import rifraf_batch
@@ -235,11 +239,12 @@ REF_PARAMS = {
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pset", sorted(REF_PARAMS))
-def test_native_reference_batch_matches_hub(engine, pset):
+def test_native_reference_batch_matches_hub(run_engine, pset):
     """rf_rifraf_batch_ref: reference-guided clusters (FRAME, REFINE) in the
     library's stage machine against the Python stage machine on the same
     engine -- consensus per iteration and stage, score, stage iterations,
     convergence, QVs, penalty increases and the reference's error rate."""
+    engine = run_engine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import native_eligible, rifraf_batch
     from rifraf_amd.model import RifrafParams
@@ -265,9 +270,10 @@ def test_native_reference_batch_matches_hub(engine, pset):
 
 
 @pytest.mark.gpu
-def test_native_reference_batch_matches_oracle_runs(engine):
+def test_native_reference_batch_matches_oracle_runs(run_engine):
     """Native reference-guided clusters against separate rifraf() runs on the
     CPU oracle engine (throughput settings, QVs on)."""
+    engine = run_engine
     from oracle_engine import OracleEngine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import rifraf_batch
@@ -281,10 +287,11 @@ def test_native_reference_batch_matches_oracle_runs(engine):
 
 
 @pytest.mark.gpu
-def test_native_auto_with_empty_read(engine):
+def test_native_auto_with_empty_read(run_engine):
     """rifraf_batch's automatic driver choice (native=None) with an empty read
     in one cluster gives what the Python stage machine gives (native=False):
     the same results, or the same error."""
+    engine = run_engine
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams
     clusters = [dict(c) for c in _ref_free_clusters()[:3]]
@@ -337,10 +344,11 @@ def _doubling_clusters(seed=12):
 
 
 @pytest.mark.gpu
-def test_native_batch_band_doubling_vs_oracle(engine):
+def test_native_batch_band_doubling_vs_oracle(run_engine):
     """Native batched driver with band doubling into line-padded layouts (the
     c4 e2e shape's failure mode: A and B of one read filled by calls that
     differ in padding) against separate oracle-engine rifraf() runs, QVs on."""
+    engine = run_engine
     from oracle_engine import OracleEngine
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams, rifraf
@@ -355,9 +363,10 @@ def test_native_batch_band_doubling_vs_oracle(engine):
 
 
 @pytest.mark.gpu
-def test_native_batch_engines_one_gpu(engine):
+def test_native_batch_engines_one_gpu(run_engine):
     """Three contexts on one GPU, one host thread each (rifraf_batch(engines=)),
     equal the single-engine native run."""
+    engine = run_engine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.engine import Engine
@@ -379,13 +388,14 @@ def test_native_batch_engines_one_gpu(engine):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("marks_min", [128, 0])
-def test_aln_error_sums_device_equals_host(engine, opts, marks_min):
+def test_aln_error_sums_device_equals_host(run_engine, opts, marks_min):
     """alignment_error_probs's sums (model.jl:817-840) folded on the device
     (k_aln_sums, default; with marks_min 0 the per-read marks + per-column
     fold launches that large clusters use) and on host threads
     (RF_OPT_ALN_SUMS_HOST) are the same bits, through the native driver's
     host quality pass (device_qv=False); both equal the Python stage
     machine's."""
+    engine = run_engine
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams
     params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True, max_iters=20)

@@ -72,7 +72,7 @@ def test_bench_self_launches_ranks(world):
     line (rank 0) whose reduction covers every rank's shard (N = 8: the
     driver's scaling run on one node, rehearsed with gloo)."""
     p, lines = _bench(["--gpus", str(world), "--backend", "gloo", "--config", "c4", "--clusters", "2",
-                       "--no-cpu", "--dry-run"])
+                       "--e2e-clusters", "3", "--no-cpu", "--dry-run"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1
     # stdout carries the JSON line only (gloo's connection report goes to stderr)
@@ -90,6 +90,12 @@ def test_bench_self_launches_ranks(world):
                     for t, rs in bench.make_workload(2, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, rank))
                     for r in rs) for rank in range(world)]
     assert out["rank_cells_min_max"] == [min(per_rank), max(per_rank)]
+    # the e2e field's hand-out (pmap's dynamic queue, scripts/rifraf.jl:190): one
+    # global list staged by the ranks, every cluster taken exactly once over all
+    # ranks and read back identical to one process's simulation of it
+    h = out["e2e_hand_out"]
+    assert h["clusters"] == world * 3 and h["exactly_once"] and h["identical_to_one_process"]
+    assert sum(h["per_rank"]) == world * 3
 
 
 def test_bench_rejects_world_mismatch():

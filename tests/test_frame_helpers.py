@@ -6,8 +6,9 @@ engines, against the reference's own known answers:
   single_indel_proposals  model.jl:538-562    <- test/test_model.jl:175-189
 
 These run the codon-move DP (skew_matches for single_indel_proposals) and the
-backtrace on the engine: "oracle" is the CPU stand-in (CPU suite), "hip" the
-MI355X engine (gpu)."""
+backtrace on the engine: "oracle" is the CPU stand-in (CPU suite), "hip-lat" /
+"hip-tp" the MI355X engine (gpu) in its default DP mode and with the
+throughput classes."""
 import math
 
 import numpy as np
@@ -20,12 +21,19 @@ from rifraf_amd.proposals import Deletion
 from rifraf_amd.types import dna_str
 
 
-@pytest.fixture(params=["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
+@pytest.fixture(params=["oracle", pytest.param("hip-lat", marks=pytest.mark.gpu),
+                        pytest.param("hip-tp", marks=pytest.mark.gpu)])
 def eng(request):
+    """hip-lat: the engine's product default DP (latency mode for small
+    calls: k_dpx); hip-tp: the throughput classes (conftest.DP_MODES)."""
     if request.param == "oracle":
         from oracle_engine import OracleEngine
-        return OracleEngine()
-    return request.getfixturevalue("engine")
+        yield OracleEngine()
+        return
+    e = request.getfixturevalue("engine")
+    old = e.set_option("dp_lat", e.product_dp_lat if request.param == "hip-lat" else 0)
+    yield e
+    e.set_option("dp_lat", old)
 
 
 def _state(eng, consensus, rseq):

@@ -1,4 +1,4 @@
-"""Committed golden fixtures (tests/golden/pairs.npz, config2.json; made by
+"""Committed golden fixtures (tests/golden/pairs.npz, config2.json, runs.npz; made by
 scripts/make_golden.py from the KAT-pinned oracle).
 
 CPU: the oracle still reproduces them (guards the checker against drift).
@@ -76,7 +76,8 @@ def _check_config2(engine):
 
 
 @pytest.mark.gpu
-def test_engine_reproduces_pairs(engine):
+def test_engine_reproduces_pairs(run_engine):
+    engine = run_engine
     seqs = [g["seq"] for g in PAIRS]
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [g["template"] for g in PAIRS])
@@ -101,5 +102,46 @@ def test_engine_reproduces_pairs(engine):
 
 
 @pytest.mark.gpu
-def test_engine_reproduces_config2(engine):
+def test_engine_reproduces_config2(run_engine):
+    engine = run_engine
     _check_config2(engine)
+
+
+def _run_fixture():
+    import bench
+    return bench, np.load(bench.GOLDEN_RUNS)
+
+
+@pytest.mark.parametrize("variant", ["default", "throughput"])
+def test_oracle_engine_reproduces_runs(variant):
+    """tests/golden/runs.npz (bench's c2 / c3 fields check against it): the
+    oracle engine still gives configs[1]'s seed-1 runs bit for bit."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.model import RifrafParams, rifraf
+    bench, z = _run_fixture()
+    t, reads, phreds = bench.c2_cluster(1)
+    res = rifraf(reads, phreds, params=RifrafParams(**bench.C2_VARIANTS[variant]), engine=OracleEngine())
+    assert bench.run_matches(res, bench.golden_run(f"c2_1_{variant}", z), qv_rtol=0)
+    assert np.array_equal(res.consensus, t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["default", "throughput"])
+def test_engine_reproduces_runs(run_engine, variant):
+    """configs[1] (100 reads x 1 kb), seeds 1..5, through the library's stage
+    machine (rf_rifraf_batch: what bench's c2 field times) and, for seed 1,
+    the Python stage machine, against the oracle engine's committed runs:
+    consensus per stage, score bits, iterations exact; QVs bit-exact on the
+    host quality pass, within 1e-12 on the device one."""
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams, rifraf
+    bench, z = _run_fixture()
+    params = RifrafParams(**bench.C2_VARIANTS[variant])
+    for seed in bench.C2_SEEDS:
+        t, reads, phreds = bench.c2_cluster(seed)
+        rec = bench.golden_run(f"c2_{seed}_{variant}", z)
+        nat = rifraf_batch([dict(dnaseqs=reads, phreds=phreds)], params=params, engine=run_engine, native=True)[0]
+        assert bench.run_matches(nat, rec), f"seed {seed}"
+        if seed == 1:
+            py = rifraf(reads, phreds, params=params, engine=run_engine)
+            assert bench.run_matches(py, rec, qv_rtol=0)

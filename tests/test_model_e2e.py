@@ -25,12 +25,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 G1 = os.path.join(HERE, "golden", "config1")
 
 
-@pytest.fixture(params=["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
+@pytest.fixture(params=["oracle", pytest.param("hip-lat", marks=pytest.mark.gpu),
+                        pytest.param("hip-tp", marks=pytest.mark.gpu)])
 def eng(request):
+    """hip-lat: the engine's product default DP (latency mode for small
+    calls: k_dpx); hip-tp: the throughput classes (conftest.DP_MODES)."""
     if request.param == "oracle":
         from oracle_engine import OracleEngine
-        return OracleEngine()
-    return request.getfixturevalue("engine")
+        yield OracleEngine()
+        return
+    e = request.getfixturevalue("engine")
+    old = e.set_option("dp_lat", e.product_dp_lat if request.param == "hip-lat" else 0)
+    yield e
+    e.set_option("dp_lat", old)
 
 
 def config1_run(f, refid, engine):
@@ -189,7 +196,7 @@ def test_full_model(eng):                                            # test_mode
 
 
 @pytest.mark.gpu
-def test_gpu_matches_oracle_run(engine):
+def test_gpu_matches_oracle_run(run_engine, oracle_memo):
     """Identical consensus after every iteration and identical final score,
     HIP engine vs oracle engine, on clusters that exercise INIT, FRAME (codon
     reference scoring) and REFINE."""
@@ -200,11 +207,42 @@ def test_gpu_matches_oracle_run(engine):
             8, 150, ref_error_rate=0.05, ref_errors=ErrorModel(8.0, 0.0, 0.0, 1.0, 1.0), error_rate=0.02,
             rng=rng)
         params = RifrafParams(batch_size=0 if case % 2 else 20, seed=case)
-        a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
-        b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+        a = rifraf(reads, phreds, reference=ref, params=params, engine=run_engine)
+        b = oracle_memo(("gpu_matches_oracle_run", case),
+                        lambda: rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine()))
         assert a.state.score == b.state.score
         assert np.array_equal(a.consensus, b.consensus)
         for sa, sb in zip(a.consensus_stages, b.consensus_stages):
             assert len(sa) == len(sb)
             for x, y in zip(sa, sb):
                 assert np.array_equal(x, y)
+
+
+def test_frame_batch_growth_before_single_indel_proposals(eng, monkeypatch):
+    """check_score's batch growth (model.jl:1102-1111) realigns the grown
+    batch inside a FRAME iteration before single_indel_proposals
+    (model.jl:1145-1149): the skewed reference fill that realign()'s B call
+    leaves in the scratch slot must be the current one.  Same run as with
+    single_indel_proposals filling the scratch slot itself (SIP_CACHE off)."""
+    import rifraf_amd.model as model
+    rng = np.random.default_rng(2)
+    ref, _, _, reads, _, phreds, _, _ = sample_sequences(
+        30, 240, error_rate=0.03, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
+    ref = np.concatenate([ref[:100], ref[101:]]).astype(np.uint8)
+    params = RifrafParams(batch_size=5, batch_threshold=0.0, batch_fixed=False, seed=1)
+    grown = []
+    check = model.check_score
+
+    def spy(state, run, p, old, rng_):
+        b = state.batch_size
+        ok = check(state, run, p, old, rng_)
+        grown.append(state.stage == Stage.FRAME and ok and state.batch_size > b)
+        return ok
+
+    monkeypatch.setattr(model, "check_score", spy)
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=eng)
+    assert any(grown)
+    monkeypatch.setattr(model, "SIP_CACHE", False)
+    b = rifraf(reads, phreds, reference=ref, params=params, engine=eng)
+    assert a.state.score == b.state.score
+    assert [list(map(dna_str, x)) for x in a.consensus_stages] == [list(map(dna_str, x)) for x in b.consensus_stages]

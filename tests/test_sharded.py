@@ -319,6 +319,8 @@ def _w_queue(rank, world, n, wave):
     from oracle_engine import OracleEngine
     from rifraf_amd.batch import ClusterQueue, rifraf_batch_queue
     from rifraf_amd.model import RifrafParams
+    if rank == 1:
+        ClusterQueue(5, 1)   # a local queue on one rank only must not shift the store-backed keys
     q = ClusterQueue.for_process_group(n, wave)
     params = RifrafParams(max_iters=20)
 
@@ -359,3 +361,46 @@ def test_cluster_queue_across_ranks(world):
                           engine=OracleEngine())
     for i in range(n):
         assert seen[i] == np.asarray(single[i].consensus).tolist()
+
+
+def _w_queue_mismatch(rank, world):
+    """Ranks that disagree on a queue's shape fail loudly at creation."""
+    from rifraf_amd.batch import ClusterQueue
+    try:
+        ClusterQueue.for_process_group(10 if rank == 0 else 11, 2, key="mismatch")
+    except RuntimeError as e:
+        return str(e)
+    return "ok"
+
+
+def test_cluster_queue_mismatch_is_loud():
+    got = _spawn(_w_queue_mismatch, 3)
+    assert got[0] == "ok"
+    for r in (1, 2):
+        assert "rank 0 published" in got[r]
+
+
+def _w_queue_fail(rank, world, n, wave):
+    """Rank 1 raises inside its first wave: every rank still reaches the
+    barrier; rank 1 re-raises its own error, the others a RuntimeError."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import ClusterQueue, rifraf_batch_queue
+    from rifraf_amd.model import RifrafParams
+    q = ClusterQueue.for_process_group(n, wave)
+
+    def get(i):
+        if rank == 1:
+            raise ValueError(f"bad cluster {i}")
+        return _queue_cluster(i)
+    try:
+        rifraf_batch_queue(get, q, params=RifrafParams(max_iters=20), engine=OracleEngine())
+    except Exception as e:  # noqa: BLE001
+        return type(e).__name__, str(e)
+    return "ok", ""
+
+
+def test_cluster_queue_failure_reaches_every_rank():
+    got = _spawn(_w_queue_fail, 3, 40, 1)
+    assert got[1][0] == "ValueError"
+    for r in (0, 2):
+        assert got[r][0] == "RuntimeError" and "rank 1 failed" in got[r][1]

@@ -87,7 +87,8 @@ def test_every_tied_choice_gives_the_same_consensus():
 
 
 @pytest.mark.gpu
-def test_tied_candidates_hip(engine):
+def test_tied_candidates_hip(run_engine):
+    engine = run_engine
     seen, res = _run(engine)
     _check_ties(seen)
     assert np.asarray(res.consensus).tolist() == FIX["consensus"]
@@ -95,7 +96,8 @@ def test_tied_candidates_hip(engine):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("native", [True, False])
-def test_tied_candidates_batched(engine, native):
+def test_tied_candidates_batched(run_engine, native):
+    engine = run_engine
     _, res = _run(engine, native=native)
     assert np.asarray(res.consensus).tolist() == FIX["consensus"]
     assert np.asarray(res.consensus_stages[0][1]).tolist() == FIX["consensus"]

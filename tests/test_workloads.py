@@ -76,19 +76,19 @@ def _masked(got, ref, t):
 
 
 @pytest.mark.parametrize("variant", ["default", "throughput_qv"])
-def test_c2_run_matches_oracle(engine, variant):
+def test_c2_run_matches_oracle(run_engine, oracle_memo, variant):
     from oracle_engine import OracleEngine
     rng = np.random.default_rng(2)
     _, template, _, reads, _, phreds, _, _ = sample_sequences(100, 1000, error_rate=0.01, rng=rng)
     params = (RifrafParams(seed=1) if variant == "default" else
               RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True))
-    a = rifraf(reads, phreds, params=params, engine=engine)
-    b = rifraf(reads, phreds, params=params, engine=OracleEngine())
+    a = rifraf(reads, phreds, params=params, engine=run_engine)
+    b = oracle_memo(("c2", variant), lambda: rifraf(reads, phreds, params=params, engine=OracleEngine()))
     assert_same_run(a, b)
     assert a.state.converged and np.array_equal(a.consensus, template)
 
 
-def test_c3_frame_run_matches_oracle(engine):
+def test_c3_frame_run_matches_oracle(run_engine, oracle_memo):
     from oracle_engine import OracleEngine
     rng = np.random.default_rng(3)
     ref, template, _, reads, _, phreds, _, _ = sample_sequences(
@@ -96,14 +96,15 @@ def test_c3_frame_run_matches_oracle(engine):
     # a single-base frameshift in the reference: INIT -> FRAME with codon scoring
     ref = np.concatenate([ref[:1300], ref[1301:2000], [2], ref[2000:]]).astype(np.uint8)
     params = RifrafParams(seed=1)
-    a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
-    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=run_engine)
+    b = oracle_memo("c3_default", lambda: rifraf(reads, phreds, reference=ref, params=params,
+                                                 engine=OracleEngine()))
     assert_same_run(a, b)
     assert a.state.stage_iterations[1] >= 2          # FRAME ran (with a penalty increase)
     assert a.state.n_ref_indel_mults == b.state.n_ref_indel_mults >= 1
 
 
-def test_c3_throughput_frame_run_matches_oracle(engine):
+def test_c3_throughput_frame_run_matches_oracle(run_engine, oracle_memo):
     """Config 3 at the throughput settings (SURVEY §8(d) "Parity runs"):
     every one of the 1000 reads in every batch (batch_size 0, batch_fixed
     false, model.jl:569-573) through INIT, FRAME (frameshifted reference:
@@ -115,8 +116,10 @@ def test_c3_throughput_frame_run_matches_oracle(engine):
         1000, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
     ref = np.concatenate([ref[:1300], ref[1301:2000], [2], ref[2000:]]).astype(np.uint8)
     params = RifrafParams(seed=1, batch_size=0, batch_fixed=False, do_score=True)
+    engine = run_engine
     a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
-    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    b = oracle_memo("c3_throughput", lambda: rifraf(reads, phreds, reference=ref, params=params,
+                                                    engine=OracleEngine()))
     assert_same_run(a, b)
     assert a.state.batch_size == 1000
     assert a.state.stage_iterations[1] >= 2 and a.state.n_ref_indel_mults >= 1
@@ -132,7 +135,7 @@ def test_c3_throughput_frame_run_matches_oracle(engine):
     assert n.state.n_ref_indel_mults == b.state.n_ref_indel_mults
 
 
-def test_c3_qv_with_reference_matches_oracle(engine):
+def test_c3_qv_with_reference_matches_oracle(run_engine, oracle_memo):
     """QV pass scoring the reference's codon moves too (use_ref_for_qvs,
     model.jl:617-628, :737-791), 2.6 kb template, 40 reads."""
     from oracle_engine import OracleEngine
@@ -140,8 +143,9 @@ def test_c3_qv_with_reference_matches_oracle(engine):
     ref, _, _, reads, _, phreds, _, _ = sample_sequences(
         40, 2601, error_rate=0.01, ref_error_rate=0.1, ref_errors=ErrorModel(10, 0, 0, 1, 1), rng=rng)
     params = RifrafParams(seed=1, do_score=True, use_ref_for_qvs=True)
-    a = rifraf(reads, phreds, reference=ref, params=params, engine=engine)
-    b = rifraf(reads, phreds, reference=ref, params=params, engine=OracleEngine())
+    a = rifraf(reads, phreds, reference=ref, params=params, engine=run_engine)
+    b = oracle_memo("c3_qv_ref", lambda: rifraf(reads, phreds, reference=ref, params=params,
+                                                engine=OracleEngine()))
     assert_same_run(a, b)
 
 
@@ -155,7 +159,7 @@ def _c4_clusters(n, seed=77):
     return out
 
 
-def test_c4_throughput_runs_match_oracle(engine):
+def test_c4_throughput_runs_match_oracle(run_engine, oracle_memo):
     """SURVEY §8(d) config 4 at its throughput settings (batch = all 50
     reads, QV pass on), two clusters as whole rifraf() runs: the HIP engine
     through the Python stage machine, through rf_rifraf_batch (the native
@@ -164,16 +168,17 @@ def test_c4_throughput_runs_match_oracle(engine):
     from rifraf_amd.batch import rifraf_batch
     params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
     clusters = _c4_clusters(2)
-    nat = rifraf_batch([kw for _, kw in clusters], params=params, engine=engine, native=True)
-    for (t, kw), n in zip(clusters, nat):
-        a = rifraf(params=params, engine=engine, **kw)
-        b = rifraf(params=params, engine=OracleEngine(), **kw)
+    nat = rifraf_batch([kw for _, kw in clusters], params=params, engine=run_engine, native=True)
+    for c, ((t, kw), n) in enumerate(zip(clusters, nat)):
+        a = rifraf(params=params, engine=run_engine, **kw)
+        b = oracle_memo(("c4_run", c), lambda: rifraf(params=params, engine=OracleEngine(), **kw))
         assert_same_run(a, b)
         assert_same_run(n, b, qv_rtol=1e-12)    # device quality pass
         assert b.error_probs is not None
 
 
-def test_c4_clusters_dense_bitexact(engine):
+def test_c4_clusters_dense_bitexact(run_engine):
+    engine = run_engine
     import bench
     clusters = bench.make_workload(4, 50, 1500, 0.01, 9, seed=bench.shard_seed(2024, 0))
     reads = [r for _, rs in clusters for r in rs]
@@ -191,7 +196,8 @@ def test_c4_clusters_dense_bitexact(engine):
 
 
 @pytest.mark.parametrize("nreads", [64, 256])
-def test_c5_sample_band_doubling_and_scores(engine, nreads):
+def test_c5_sample_band_doubling_and_scores(run_engine, nreads):
+    engine = run_engine
     import bench
     from oracle_engine import OracleEngine
     t, reads = bench.make_read_shard(5000, 10000, 0.03, 9, 2024, 0, nreads)
