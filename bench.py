@@ -894,9 +894,6 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
                    "note": "each rank's own timed-region time before the closing barrier: the spread of the "
                            "static per-rank cluster shards (equal shapes, seeded per rank)"}
 
-    # attainable streaming-read bandwidth over the same band arena (diagnostic)
-    probe_ms = eng.probe_stream(band_bytes, 3)
-    probe_gbs = band_bytes / (probe_ms * 1e-3) / 1e9 if probe_ms > 0 else None
     ms_step = elapsed / args.steps * 1e3
     dp_ms = float(np.mean(dps))
     sc_ms = float(np.mean(scs))
@@ -941,7 +938,6 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
                                     "bytes": dp_bytes, "ms": dp_ms},
                            "k_score": {"achieved": sc_gbs, "frac": sc_gbs / HBM_PEAK_GBS,
                                        "bytes": score_bytes, "ms": sc_ms}},
-        "stream_read_gbs": probe_gbs,
         "setup_s": gen_s,
     }
     if rank == 0:
@@ -955,18 +951,32 @@ def run_clusters(args, rank, world, gpu, dist, torch, coll):
             import oracle  # test infrastructure: the parity check only
             ref = [oracle.cpu_pass(t, rs, nthreads=cpu_threads())[0] for t, rs in clusters[:2]]
         result["parity"] = parity_check(dense[:len(ref)], ref, [t for t, _ in clusters[:len(ref)]])
-    # attainable write bandwidth of the DP's store pattern on this box
-    # (diagnostic: nontemporal 16-B stores, 16-lane streams of 2.75 KB
-    # chunks; destroys the bands, so after the parity download).  The c4 DP
-    # time varies by ~12 % between boxes (8.3 / 9.3 ms) at equal read rates.
-    try:
-        eng.probe_write(4, band_bytes, 2816, 16384)
-        wms = eng.probe_write(4, band_bytes, 2816, 16384)
-        result["stream_write_gbs"] = band_bytes / (wms * 1e-3) / 1e9 if wms > 0 else None
-    except Exception:  # pragma: no cover - diagnostic only
-        result["stream_write_gbs"] = None
     eng.close()
+    result["stream_read_gbs"], result["stream_write_gbs"] = probe_bandwidth(gpu, band_bytes)
     return result
+
+
+def probe_bandwidth(gpu, nbytes):
+    """Attainable HBM bandwidth on this box (diagnostics, scripts/probe_bw.hip,
+    outside the engine): stream reads over a buffer the size of the step's
+    band arena, and the DP fill's store pattern (nontemporal 16-B stores,
+    16-lane streams of 2.75 KB chunks).  The c4 DP time varies by ~12 %
+    between boxes (8.3 / 9.3 ms) at equal read rates.  (None, None) when the
+    probe library is not built."""
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    try:
+        from probe_bw import Probe
+        p = Probe(gpu, nbytes)
+    except Exception:  # noqa: BLE001 -- diagnostic only
+        return None, None
+    try:
+        rd = p.read_gbs(3)
+        p.write_gbs(4, 2816, 16384)
+        return rd, p.write_gbs(4, 2816, 16384)
+    except Exception:  # noqa: BLE001 -- diagnostic only
+        return None, None
+    finally:
+        p.close()
 
 
 C3_SEED = 3   # the c3 parity tests' cluster (tests/test_workloads.py::test_c3_*)

@@ -425,19 +425,6 @@ int rf_slot_geometry(rf_ctx *ctx, int32_t slot, int32_t which,
 /* Copy a slot's band (H x ncols doubles, column-major) to the host. */
 int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out);
 
-/* Diagnostics: stream-read the first `bytes` of the band arena `reps` times
- * (16-B loads, grid-stride) and report the mean ms per pass -- the
- * attainable-read-bandwidth calibration for the scorer's roofline. */
-int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms);
-
-/* Diagnostics: write probes over the band arena (DESTROYS band contents).
- * mode 1 = sequential 16-B stores over `bytes`; mode 2 = the DP fill's store
- * pattern: `nstreams` 16-lane streams each writing its own region in
- * `chunk_bytes` pieces; modes 3 and 4 = modes 1 and 2 with nontemporal
- * stores (the DP fill's).  Reports ms for one pass. */
-int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes,
-                   int32_t nstreams, double *ms);
-
 /* Kernel timing of the last rf_realign / rf_score call (HIP events on the
  * context stream), milliseconds; used by bench.py's roofline. */
 int rf_last_timing(const rf_ctx *ctx, double *dp_ms, double *score_ms,

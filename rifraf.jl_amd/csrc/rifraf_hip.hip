@@ -682,11 +682,6 @@ __device__ __forceinline__ void dpr_step(const DPTask &T, int q, int k, bool cod
     }
 }
 
-#if defined(RIFRAF_DIAG) && defined(DPL_NO_LDS_OUT_DIAG)
-#define DPL_NO_LDS_OUT 1   // diagnostic builds only: lean steps skip their LDS band output
-#else
-#define DPL_NO_LDS_OUT 0
-#endif
 // Whole-row DPP rotate of an f64 (no "old" operand: every lane has a source).
 template <int CTRL>
 __device__ __forceinline__ double dpp_rot_f64(double x)
@@ -736,7 +731,7 @@ __device__ __forceinline__ void dpl_step(double (&v1)[NP], double (&v2)[NP], con
         // (round 3: the mask on the insert / delete inputs instead of the cell,
         // and the exchanged value entering the max last, were no faster)
         nv[r] = fmax(fmax(v2[r] + ms, x_ins + R.is), x_del + R.ds) + lb[r];
-        if (st[r] && !DPL_NO_LDS_OUT)
+        if (st[r])
             Rb[u0 + r * ostep] = nv[r];
     }
 #pragma unroll
@@ -1017,34 +1012,11 @@ __device__ __forceinline__ void dpr_body(const int blk, const DPTask *__restrict
                 const int ii = max(1, min(top_c + (kk >> 1), T.n));
                 return rev ? T.n - ii : ii - 1;
             };
-#if defined(RIFRAF_DIAG) && defined(DPL_NOEDGE_DIAG)
-            (void)codes;
-            auto code_load = [&](int kb) -> uint64_t { return (uint64_t)kb; };
-#else
             auto code_load = [&](int kb) -> uint64_t { return coded ? codes[edge_ks(kb)] : 0; };
-#endif
             auto edge_load = [&](int kb, uint64_t rec) {
                 EdgeRec e;
-#if defined(RIFRAF_DIAG) && defined(DPL_NOEDGE_DIAG)
-                // diagnostic builds only (wrong bands, timing): edge records made
-                // up in registers, no edge loads behind the band stores
-                (void)rec;
-                e.mt = -0.01 - 1e-6 * (kb & 1023);
-                e.mm = -2.0 - 1e-6 * q;
-                e.is = -1.5;
-                e.ds = -1.5;
-                e.sb = (kb + q) & 3;
-                e.col = (kb >> 1) & 3;
-                return e;
-#endif
                 const int kk = kb + 2 * min(q, DPL_B - 1);
-#if defined(RIFRAF_DIAG) && defined(DPL_TAB_DIAG)   // diagnostic builds only: one L2-resident table slice
-                const int ks = edge_ks(kb) & 255;
-                const double *tb = tabs;
-                const uint8_t *sbase = bases;
-#else
                 const int ks = edge_ks(kb);
-#endif
                 const int kd = rev ? ks : ks + 1;
                 if (coded) {
                     const double *l3 = lut + 4 * (int)(rec & 0xffff);
@@ -1178,10 +1150,9 @@ __device__ __forceinline__ void dpr_body(const int blk, const DPTask *__restrict
                     // the first and last blocks) is one 8-B store
                     const ptrdiff_t lo2 = (lo + 1) & ~(ptrdiff_t)1, hi2 = hi & ~(ptrdiff_t)1;
                     const int nu = (int)((hi2 - lo2) >> 1);
-                    // (flags 512: diagnostics, every flush goes to the sink)
-                    // padding tasks (T = {}: nu = 0) and the diagnostics sink write
-                    // slots [0, 16*FL) of the sink -- never index -1
-                    const bool task_real = tid < ntasks && !(T.flags & 512);
+                    // padding tasks (T = {}: nu = 0) write slots [0, 16*FL) of
+                    // the sink -- never index -1
+                    const bool task_real = tid < ntasks;
                     const bool real = task_real && nu > 0;
                     dvec2 *g = real ? (dvec2 *)(band + lo2) : (dvec2 *)sink;
                     const int u2 = ub + (int)(lo2 - g0);   // even
@@ -1523,12 +1494,7 @@ __device__ __forceinline__ double dpx_cell(const DPTask &T, bool trim, int d, in
         const double best = fmax(t, fmax(x_ins + isds.x, x_del + isds.y));
         if (CHECK)
             emask |= __ballot(best == -RF_INF) & actm;   // "new score is invalid" (active diagonals)
-#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 8)
-        (void)lbv;
-        return best;   // diagnostic builds only (wrong bands): one FP64 op less on the chain
-#else
         return best + lbv;
-#endif
     }
     const bool valid = d < T.H && jj >= 0 && jj <= T.m && ii >= 0 && ii <= T.n;
     const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;   // align.jl:74-76
@@ -1707,9 +1673,6 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     using I3 = std::integral_constant<int, 3>;
     using BT = std::integral_constant<bool, true>;
     using BF = std::integral_constant<bool, false>;
-#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
-    const long long dg_c0 = clock64(), dg_w0 = wall_clock64();   // diagnostic builds only
-#endif
     // byte offset of kappa row 4u (reverse: K - 1 - 4u), advanced once per
     // pair of periods (the per-step select and multiply off the loop)
     const int drow = rev ? -(int)rowb : (int)rowb;
@@ -1733,11 +1696,7 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             // the kappa - 1 neighbour by a wave rotate: lane 0 (63) receives the
             // value of diagonal 127 (0 at kappa - 1 into diagonal 127), and
             // diagonal 127 >= H is -Inf / masked (the host sends H <= 127 only)
-#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 2)
-            const double xn = v1;   // diagnostic builds only (wrong bands): no DPP on the chain
-#else
             const double xn = PAR ? dpp_rot_f64<TaskLanes<64>::ROT_R1>(v1) : dpp_rot_f64<TaskLanes<64>::ROT_L1>(v1);
-#endif
             // codon neighbours at kappa - 3: d - 3 / d + 3 = lanes q - 2 / q + 1
             // (even), q - 1 / q + 2 (odd); this step's were read one step ago,
             // the next step's (ring row kappa - 2, the other parity) now
@@ -1761,9 +1720,6 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             }
             const unsigned ro = rob + (unsigned)(S * drow);   // = rowb * (rev ? K - 1 - k : k)
             const unsigned vo = PAR ? vo1 : vo0;
-#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 1)
-            if (!FAST)   // diagnostic builds only (wrong bands): no interior band stores
-#endif
             if (STAGE && FAST) {
                 if (vo != DPX_NOSTORE)
                     s_out[(rev ? 3 - S : S) * T.P + (int)(vo >> 3)] = v;
@@ -1809,11 +1765,6 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
     if (u + 1 < npairs)
         pair(u + 1, B2, A0, B0, C00, C01, A1, B1, C10, C11);
     (void)ntasks;
-#if defined(RIFRAF_DIAG) && defined(DPX_DIAG) && (DPX_DIAG & 4)
-    if (q == 0 && blockIdx.x == 0)
-        printf("k_dpx<%d> K %d cycles %lld wall_ticks %lld cycles/step %.1f\n", (int)CODON, K, clock64() - dg_c0,
-               wall_clock64() - dg_w0, (double)(clock64() - dg_c0) / K);
-#endif
     if (eflag || emask)
         set_err(err, 1);  // "new score is invalid"
     if (fset && out_score)
@@ -2572,7 +2523,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                 }
             }
         };
-        bool held = (split_mode & 8) != 0;   // registers hold the unit (diagnostics: never load)
+        bool held = false;   // the registers hold the unit
         for (Unit u = unit_first(r0); u.r < r1;) {
             const ScoreRead R = reads[u.r];
             const LeanWin w = unit_win(R, u);
@@ -2599,8 +2550,8 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
                         lean_row(sT + 6 * e, i >= 1 ? ps[k] : 4, pm[k], px[k], pn[k], pd[k]);
                 }
                 wg_barrier();                        // unit ready
-                held = (split_mode & 8) != 0;
-                if (nx.r < r1 && !held) {
+                held = false;
+                if (nx.r < r1) {
                     const ScoreRead R2 = reads[nx.r];
                     const LeanWin w2 = unit_win(R2, nx);
                     if (unit_pf(R2, nx, w2)) {
@@ -2652,7 +2603,7 @@ k_score_ws(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ gr
         const ScoreRead R = reads[u.r];
         const LeanWin w = unit_win(R, u);
         wg_barrier();                                // unit ready
-        if (tid >= u.s0 && tid < u.s0 + u.L && a <= m && !(split_mode & 2))
+        if (tid >= u.s0 && tid < u.s0 + u.L && a <= m)
             lean_chain_any(R, w, a, m, smem, smem + w.win, smem + 2 * w.win, tI, tS, tD);
         wg_barrier();                                // chains of the unit done
         const Unit nx = unit_next(u);
@@ -2945,7 +2896,6 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
             }
         }
     };
-    const bool do_load = !(split_mode & 4);
     // a wave with no column (every a > m) writes nothing; any other wave has
     // rows in every read (each band column holds at least one row)
     if (!__any(active))
@@ -2962,7 +2912,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         const int c = g.c, dfirst = g.dfirst, dlast = g.dlast;
         const int dfmax = g.dfmax, dlmin = g.dlmin;
         const bool peel = g.peel;
-        if (active && !(split_mode & 2)) {
+        if (active) {
             const int lo = max(D, dfirst), hi = min(D + S - 1, dlast);
             const double a0v = sA[min(max(lo - D, 0), S) * LS + tid];   // unconditional read, then select
             double aprev = (lo <= hi && lo >= 1 && a - c + lo >= 1) ? a0v : -RF_INF;
@@ -3146,7 +3096,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         Pos ahead = cur;
         if (ahead.r < r1)
             adv(ahead);
-        if (do_load && ahead.r < r1)
+        if (ahead.r < r1)
             load_seg(X, ahead.g, ahead.D, ahead.D == first_of(ahead.g));
         chains(cur.g, D);
         if (D + S > cur.g.dhi)
@@ -3160,7 +3110,7 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         cur.D = first_of(cur.g);
     }
     SegSet X0;
-    if (r0 < r1 && do_load)
+    if (r0 < r1)
         load_seg(X0, cur.g, cur.D, true);
     while (cur.r < r1)
         step(X0, cur);
@@ -3182,28 +3132,6 @@ k_score_segl(const WorkItem *__restrict__ items, const ScoreGroup *__restrict__ 
         for (int k = 0; k < 5; ++k)
             dst[k] = qnan;
     }
-}
-
-// Read-bandwidth probe over the band arena (calibrates the HBM roofline of
-// the scorer on the same allocation): grid-stride 16-B loads, 8 in flight.
-__global__ void __launch_bounds__(256) k_probe_stream(const dvec2 *__restrict__ src, int64_t n16,
-                                                      double *__restrict__ sink)
-{
-    const int64_t stride = (int64_t)gridDim.x * 256 * 8;
-    double acc = 0.0;
-    for (int64_t base = (int64_t)blockIdx.x * 256 * 8 + threadIdx.x; base < n16; base += stride) {
-        dvec2 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t e = base + u * 256;
-            v[u] = e < n16 ? src[e] : dvec2{0.0, 0.0};
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            acc += v[u].x + v[u].y;
-    }
-    if (acc == 12345.678)   // never true for band data; keeps the loads alive
-        sink[0] = acc;
 }
 
 // ---------------------------------------------------------------------
@@ -3480,14 +3408,11 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 // the three others (the same strict-> order), and a codon move leaves the box
 // (|u| = 3), so the next box starts at the cell it reaches.
 // ---------------------------------------------------------------------
-// 1 (default, round 4): the box's walk ranked in parallel (pointer
-// doubling over the 63 cells' successors) instead of one readlane step per
-// move: backtrace 19.8 -> 8.0 ms, alignment proposals 36.9 -> 12.9 ms per
-// 512 e2e clusters, bit-exact (profiles/r04ab_btw_rank.txt); 0: the
-// sequential walk
-#ifndef BTW_RANK
-#define BTW_RANK 1
-#endif
+// The box's walk is ranked in parallel (pointer doubling over the 63
+// cells' successors) instead of one readlane step per move (round 4:
+// backtrace 19.8 -> 8.0 ms, alignment proposals 36.9 -> 12.9 ms per 512 e2e
+// clusters, bit-exact, profiles/r04ab_btw_rank.txt; the sequential walk is
+// in git history).
 // elements staged per kappa row (the walk's box needs 3 -- 5 with codon
 // moves -- around its diagonal): 8 holds twice the kappa rows of 16 in the
 // same LDS, so windows are re-staged half as often: with the ranked walk,
@@ -3674,7 +3599,6 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             pack = valid ? (mv | ((sb != tbb) ? 8 : 0) | (sb << 4)) : 0;
         }
-#if BTW_RANK
         // ---- walk the box by ranking its cells in parallel: J0 = each box
         // cell's successor lane (or the sink, lane 63: leaves the box, reaches
         // (0, 0), or no move), J_r = J0^(2^r) by pointer doubling; lane k then
@@ -3758,55 +3682,6 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                 failed = 1;
             }
         }
-#else
-        // ---- walk the box (uniform control flow, one readlane per move)
-        const int bi = ii, bj = jj;
-        while (ii > 0 || jj > 0) {
-            const int di = bi - ii, dj = bj - jj, u = di - dj;
-            if (di > BT_DMAX || u < -1 || u > 1)
-                break;
-            const int pk = __builtin_amdgcn_readlane(pack, di * 3 + u + 1);
-            const int mv = pk & 7;
-            if (mv == 0 || cnt >= n + m) {
-                if (lane == 0)
-                    set_err(err, 2);  // failed to find a move
-                failed = 1;
-                break;
-            }
-            const int sb = pk >> 4;
-            const bool mism = pk & 8;
-            if (lane == 0) {
-                out[n + m - 1 - cnt] = (int8_t)mv;
-                if (mk) {
-                    // the forward step of this move ends at (ii, jj) (moves_to_proposals)
-                    if (mv == 1 && mism)
-                        mk[(size_t)jj * 9 + sb] = 1;
-                    else if (mv == 2 && do_indels)
-                        mk[(size_t)jj * 9 + 5 + sb] = 1;
-                    else if (mv == 3 && do_indels)
-                        mk[(size_t)jj * 9 + 4] = 1;
-                }
-            }
-            ++cnt;
-            if (mv == 1) {
-                errs += mism;
-                --ii;
-                --jj;
-            } else if (mv == 2) {
-                errs += 1;
-                --ii;
-            } else if (mv == 3) {
-                errs += 1;
-                --jj;
-            } else if (mv == 4) {   // codon moves propose nothing (model.jl:469-476)
-                errs += 3;
-                ii -= 3;
-            } else {
-                errs += 3;
-                jj -= 3;
-            }
-        }
-#endif
     }
     if (lane == 0) {
         nmoves[T.idx] = cnt;
@@ -4437,10 +4312,6 @@ struct Opts {
                             // this many workgroups remain
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
-#ifdef RIFRAF_DIAG
-    int diag_dp_sink = 0;       // RIFRAF_DP_SINK: interior band stores -> sink (bands invalid)
-    int diag_lean_nocomp = 0;   // RIFRAF_LEAN_NOCOMP: lean scorer stages but skips chains
-#endif
 };
 
 }  // namespace
@@ -4773,10 +4644,6 @@ void load_env_opts(Opts &o)
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
     o.seg_wgs = env_int("RIFRAF_SEG_WGS", o.seg_wgs);
-#ifdef RIFRAF_DIAG
-    o.diag_dp_sink = env_int("RIFRAF_DP_SINK", 0);
-    o.diag_lean_nocomp = env_int("RIFRAF_LEAN_NOCOMP", 0);
-#endif
 }
 
 ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool all_finite)
@@ -4838,16 +4705,6 @@ void launch_scorer(rf_ctx *ctx, const ScorePick &pk, unsigned nitems, unsigned g
     const double *d_tabs = (const double *)ctx->tab_arena.d;
     const double *d_bands = (const double *)ctx->band_arena.d;
     int sm = split ? 1 : 0;
-#ifdef RIFRAF_DIAG
-    // RIFRAF_LEAN_NOCOMP=1 (diagnostic builds only): the lean scorer stages
-    // every window but skips the chains (measures its load pipeline alone)
-    if (ctx->opt.diag_lean_nocomp & 1)
-        sm |= 2;
-    if (ctx->opt.diag_lean_nocomp & 2)   // k_score_segl: skip the segment loads
-        sm |= 4;
-    if (ctx->opt.diag_lean_nocomp & 4)   // k_score_ws: loaders skip their global loads (chains alone)
-        sm |= 8;
-#endif
     dim3 grid(nitems, gy);
     if (pk.seg) {
         int rchunk = 1;
@@ -5787,12 +5644,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 t.ncdel = S.ncdel;
                 t.flags = (dir == 1 ? 1 : 0) | (dir == 0 && (jf[k] & RF_SKEW) ? 2 : 0) |
                           (dir == 0 && (jf[k] & RF_TRIM) ? 4 : 0) | (S.coded ? RF_TASK_CODED : 0);
-#ifdef RIFRAF_DIAG
-                // RIFRAF_DP_SINK=1 (diagnostic builds only): the blocked interior's
-                // band stores all go to one small sink buffer (bands are then invalid)
-                if (ctx->opt.diag_dp_sink)
-                    t.flags |= 512;
-#endif
                 // out_score: forward scores win when both directions run
                 t.out_idx = (dir == 0 || !(jf[k] & RF_FWD)) ? k : njobs + k;
                 t.klen = t.H + 2 * t.m;
@@ -6733,88 +6584,6 @@ int rf_download_band(rf_ctx *ctx, int32_t slot, int32_t which, double *out)
     for (int jj = 0; jj <= b.m; ++jj)
         for (int d = 0; d < b.H; ++d)
             out[(size_t)jj * b.H + d] = buf[(size_t)(d + 2 * jj) * P + (d >> 1)];
-    return 0;
-}
-
-// Write-bandwidth probes over the band arena (destroys its contents):
-// mode 1: grid-stride 16-B stores (sequential); mode 2: the DP fill's
-// pattern -- 16-lane streams (4 per wave), each writing its own contiguous
-// region in chunks of `chunk16` 16-B units.
-__global__ void __launch_bounds__(64) k_probe_write(dvec2 *__restrict__ dst, int64_t n16, int mode,
-                                                    int chunk16, int nstreams)
-{
-    const dvec2 v = {1.0, 2.0};
-    const bool nt = mode >= 3;   // 3, 4: modes 1, 2 with nontemporal stores
-    if (mode == 1 || mode == 3) {
-        const int64_t stride = (int64_t)gridDim.x * 64;
-        for (int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x; e < n16; e += stride) {
-            if (nt)
-                __builtin_nontemporal_store(v, dst + e);
-            else
-                dst[e] = v;
-        }
-        return;
-    }
-    const int sid = blockIdx.x * 4 + (threadIdx.x >> 4);
-    const int q = threadIdx.x & 15;
-    if (sid >= nstreams)
-        return;
-    const int64_t per = n16 / nstreams;
-    dvec2 *g = dst + (int64_t)sid * per;
-    for (int64_t c0 = 0; c0 + chunk16 <= per; c0 += chunk16) {
-        for (int e = q; e < chunk16; e += 16) {
-            if (nt)
-                __builtin_nontemporal_store(v, g + c0 + e);
-            else
-                g[c0 + e] = v;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-int rf_probe_write(rf_ctx *ctx, int32_t mode, int64_t bytes, int32_t chunk_bytes, int32_t nstreams,
-                   double *ms)
-{
-    if (!ctx || bytes < 0 || !ms || mode < 1 || mode > 4 || ((mode & 1) == 0 && (chunk_bytes < 16 || nstreams < 1)))
-        return fail(ctx, RF_ERR_ARG, "rf_probe_write: bad arguments");
-    (void)hipSetDevice(ctx->device);
-    bytes = std::min<int64_t>(bytes, ctx->band_arena.cap) & ~(int64_t)15;
-    const int64_t n16 = bytes / 16;
-    const unsigned blocks = (mode & 1) ? 256 * 32 : (unsigned)((nstreams + 3) / 4);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    hipLaunchKernelGGL(k_probe_write, dim3(blocks), dim3(64), 0, ctx->stream, (dvec2 *)ctx->band_arena.d, n16,
-                       mode, chunk_bytes / 16, nstreams);
-    HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    HIPCHK(ctx, stream_wait(ctx));
-    float t = 0;
-    (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
-    *ms = t;
-    return 0;
-}
-
-int rf_probe_stream(rf_ctx *ctx, int64_t bytes, int32_t reps, double *ms)
-{
-    if (!ctx || bytes < 0 || reps < 1 || !ms)
-        return fail(ctx, RF_ERR_ARG, "rf_probe_stream: bad arguments");
-    (void)hipSetDevice(ctx->device);
-    bytes = std::min<int64_t>(bytes, ctx->band_arena.cap) & ~(int64_t)15;
-    if (bytes == 0) {
-        *ms = 0;
-        return 0;
-    }
-    if (int e = ensure_buf(ctx, ctx->scratch[9], 64)) return e;
-    const unsigned blocks = 256 * 8;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL(k_probe_stream, dim3(blocks), dim3(256), 0, ctx->stream,
-                           (const dvec2 *)ctx->band_arena.d, bytes / 16, (double *)ctx->scratch[9].p);
-    HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    HIPCHK(ctx, stream_wait(ctx));
-    float t = 0;
-    (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
-    *ms = t / reps;
     return 0;
 }
 

@@ -64,8 +64,6 @@ _SIGNATURES = {
     "rf_slot_geometry": (c_int, [c_void_p, c_int32, c_int32, POINTER(c_int32), POINTER(c_int32),
                                  POINTER(c_int32), POINTER(c_int32)]),
     "rf_download_band": (c_int, [c_void_p, c_int32, c_int32, c_void_p]),
-    "rf_probe_stream": (c_int, [c_void_p, c_int64, c_int32, POINTER(c_double)]),
-    "rf_probe_write": (c_int, [c_void_p, c_int32, c_int64, c_int32, c_int32, POINTER(c_double)]),
     "rf_last_timing": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "rf_last_backtrace_ms": (c_int, [c_void_p, POINTER(c_double)]),
     "rf_last_codon_ms": (c_int, [c_void_p, POINTER(c_double)]),

@@ -245,6 +245,16 @@ def _stat(key, value):
         STATS[key] += value
 
 
+# diagnostics: a list to receive (thread name, phase, t0, t1) of every native
+# wave's phases (setup, upload, native, qv), or None
+TIMELINE = None
+
+
+def _span(phase, t0):
+    if TIMELINE is not None:
+        TIMELINE.append((threading.current_thread().name, phase, t0, time.perf_counter()))
+
+
 def native_eligible(clusters, params) -> bool:
     """Whether rf_rifraf_batch(_ref) (rifraf_batch.cpp) can run these
     clusters: INIT enabled and deterministic batches -- the fixed
@@ -545,6 +555,8 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
         engine.release_bands()
     engine.reserve(int(est_bytes * 1.1) + (64 << 20))
     _stat("setup_native_s", time.perf_counter() - t_setup)
+    _span("setup", t_setup)
+    t_up = time.perf_counter()
     if allb is None:
         allb = np.concatenate(all_s)
     # Phred-coded reads: 2 B per position to the device, tables built there
@@ -558,6 +570,8 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
         engine.set_sequences_concat(0, allb, soff, ft["match"], ft["mismatch"], ft["ins"], ft["del"])
     engine.set_templates(0, [st_.consensus for st_ in states])
     _stat("upload_s", time.perf_counter() - t_setup)
+    _span("upload", t_up)
+    t_up = time.perf_counter()
     read_seq = np.arange(len(all_s), dtype=np.int32)
     read_len = lens.astype(np.int32)
     est = tabs["est"] if coded is not None else np.array([s.est_n_errors for s in allseqs])
@@ -575,12 +589,15 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
                           int(params.batch_fixed), params.batch_size, params.batch_threshold)
     ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
+    _span("prep", t_up)
     with (init_lock if init_lock is not None else contextlib.nullcontext()):
         t0 = time.perf_counter()   # the stage machine's own time, not the wait for the lock
         res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
                                              read_off[:-1], np.arange(K, dtype=np.int32), np.concatenate(cons),
                                              cons_off, ref=ref)
         _stat("native_s", time.perf_counter() - t0)
+        _span("native", t0)
+    t_res = time.perf_counter()
     cb_errors = ref["cb_errors"] if ref is not None else {}
     if coded is not None:                  # CodedRifrafSequence: the shared arrays
         src = tabs["source"]
@@ -613,6 +630,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
             stages[sg - 1].append(DNASeq(c))
         results.append(RifrafResult(consensus=st_.consensus, params=params, state=st_,
                                     consensus_stages=stages))
+    _span("results", t_res)
     for e in errors:
         if e is not None:
             raise e
@@ -652,6 +670,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
                 results[k].aln_error_probs = aln[row:row + m]
                 row += m
             _stat("score_phase_s", time.perf_counter() - t0)
+            _span("qv", t0)
             return results
         dense = engine.score_dense(groups, rows=[len(st_.consensus) + 1 for st_ in states])
         ridx = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int64) for k, st_ in enumerate(states)])

@@ -462,19 +462,6 @@ class Engine:
         data = np.asfortranarray(buf.reshape(ncols, H).T)
         return BandedArray((nrows, ncols), bw, default=default, data=data)
 
-    def probe_stream(self, nbytes: int, reps: int = 5) -> float:
-        """Mean ms to stream-read nbytes of the band arena (roofline calibration)."""
-        ms = c_double()
-        self._check(self.lib.rf_probe_stream(self.ctx, int(nbytes), int(reps), byref(ms)))
-        return ms.value
-
-    def probe_write(self, mode: int, nbytes: int, chunk_bytes: int = 0, nstreams: int = 0) -> float:
-        """ms for one write pass over the band arena (destroys band contents)."""
-        ms = c_double()
-        self._check(self.lib.rf_probe_write(self.ctx, int(mode), int(nbytes), int(chunk_bytes),
-                                            int(nstreams), byref(ms)))
-        return ms.value
-
     def last_backtrace_ms(self) -> float:
         """Kernel ms of the last backtrace / alignment_proposals call."""
         v = c_double()
