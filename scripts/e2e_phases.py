@@ -6,7 +6,7 @@ rounds of (unpinned, pinned) passes, each pass's wall time and its phase
 timeline (batch.TIMELINE: setup, upload, prep, native, results, qv per
 engine thread).
 
-usage: e2e_phases.py [N] [E,W[,X[,B]] ...]   (engines, wave, init_exclusive, sync_block)"""
+usage: e2e_phases.py [N] [E/W[/X[/B]] ...]   (engines, wave, init_exclusive, sync_block)"""
 import json
 import os
 import sys
@@ -22,7 +22,7 @@ from rifraf_amd.engine import Engine  # noqa: E402
 from rifraf_amd.model import RifrafParams  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
-settings = [tuple(int(x) for x in a.split(",")) for a in sys.argv[2:]] or [(2, 256)]
+settings = [tuple(int(x) for x in a.replace("/", ",").split(",")) for a in sys.argv[2:]] or [(2, 256)]
 settings = [st + (0, 0)[len(st) - 2:] for st in settings]
 data = bench.E2EClusters(2024, n, 0, 1)
 params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
