@@ -107,7 +107,9 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    per-read marks + per-column fold launches      */
 #define RF_OPT_SYNC_BLOCK  23   /* 1: host waits for the engine's stream sleep on
                                    a blocking-sync event instead of spinning
-                                   (ranks held to a few host cores)             */
+                                   (ranks held to a few host cores); 2: auto,
+                                   sleep when the waiting thread may run on
+                                   fewer than 4 CPUs (its affinity mask)       */
 #define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H <= 127
                                    per call (codon / skew / trim) run as one
                                    latency-bound task per wave, k_dpx (default

@@ -4430,7 +4430,12 @@ int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 // thread) while its kernels run.
 hipError_t stream_wait(rf_ctx *ctx)
 {
-    if (!ctx->opt.sync_block || !ctx->ev_block)
+    bool block = ctx->opt.sync_block == 1;
+    if (ctx->opt.sync_block == 2) {   // auto: sleep when this thread may run on fewer than 4 CPUs
+        cpu_set_t cs;
+        block = sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) < 4;
+    }
+    if (!block || !ctx->ev_block)
         return hipStreamSynchronize(ctx->stream);
     const hipError_t e = hipEventRecord(ctx->ev_block, ctx->stream);
     return e != hipSuccess ? e : hipEventSynchronize(ctx->ev_block);

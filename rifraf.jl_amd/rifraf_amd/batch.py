@@ -407,7 +407,7 @@ def _native_refs(part, states, refs, params, engine, nseq, nslot):
             "cb_errors": errors}
 
 
-def _wave_native(part, params, engine, init_lock=None, device_qv=True):
+def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_lock=None):
     """One wave through the native stage machine (rf_rifraf_batch), then
     (do_score) the quality pass of every cluster with three batched engine
     calls; host setup is vectorised across the wave's reads.  init_lock
@@ -427,169 +427,177 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
     from .rifrafsequences import RifrafSequence
     from .types import DNASeq
 
-    K = len(part)
-    t_setup = time.perf_counter()
-    check_params(params.scores, np.zeros(0, np.uint8), params)
-    all_s, all_lp, nread = [], [], []
-    phred_in = all(kw.get("error_log_ps") is None for kw in part)
-    for kw in part:                                                 # rifraf(), model.jl:1276-1287
-        if phred_in:
-            all_lp += list(kw["phreds"])
-        else:
-            elp = kw.get("error_log_ps")
-            all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
-        # code arrays pass as they are (DNASeq would only re-wrap them)
-        all_s += [x if type(x) is np.ndarray and x.dtype == np.uint8 and x.flags.c_contiguous else DNASeq(x)
-                  for x in kw["dnaseqs"]]
-        nread.append(len(kw["dnaseqs"]))
-    cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
-    if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
-        raise RifrafError("phred score cannot be negative")
-    lens = np.fromiter(map(len, all_s), np.int64, len(all_s))
-    if (lens == 0).any() or len(all_lp) != len(all_s) or \
-            (lens != np.fromiter(map(len, all_lp), np.int64, len(all_lp))).any():
-        raise RifrafError("empty read or length mismatch")
-    soff = np.zeros(len(all_s) + 1, np.int64)
-    np.cumsum(lens, out=soff[1:])
-    # integer Phred scores: the codes go to the device and the host builds no
-    # tables (est_n_errors and the initial consensus's logsumexp10 in one C++
-    # pass; RifrafSequence.many_coded), else the concatenated host tables
-    coded = None
-    allb = None
-    if (phred_in and cat_lp is not None and cat_lp.dtype.kind in "iu" and len(cat_lp)
-            and int(cat_lp.max()) <= 127):
-        device = None
-        if hasattr(engine, "set_sequences_codes"):
-            # the reads go to the device first, and the per-read setup sums
-            # (est_n_errors, logsumexp10) come back from it (round 5: no
-            # per-position host pass; rf_set_sequences_codes_prep)
-            if hasattr(engine, "release_bands"):
-                engine.release_bands()
-            allb = np.concatenate(all_s)
+    # setup_lock (several engines): one engine at a time in the host setup,
+    # which is mostly Python (the GIL): the first engine's stage machine
+    # starts after one setup, not after all of them interleaved
+    held = setup_lock is not None and setup_lock.acquire()
+    try:
+        K = len(part)
+        t_setup = time.perf_counter()
+        check_params(params.scores, np.zeros(0, np.uint8), params)
+        all_s, all_lp, nread = [], [], []
+        phred_in = all(kw.get("error_log_ps") is None for kw in part)
+        for kw in part:                                                 # rifraf(), model.jl:1276-1287
+            if phred_in:
+                all_lp += list(kw["phreds"])
+            else:
+                elp = kw.get("error_log_ps")
+                all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
+            # code arrays pass as they are (DNASeq would only re-wrap them)
+            all_s += [x if type(x) is np.ndarray and x.dtype == np.uint8 and x.flags.c_contiguous else DNASeq(x)
+                      for x in kw["dnaseqs"]]
+            nread.append(len(kw["dnaseqs"]))
+        cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
+        if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
+            raise RifrafError("phred score cannot be negative")
+        lens = np.fromiter(map(len, all_s), np.int64, len(all_s))
+        if (lens == 0).any() or len(all_lp) != len(all_s) or \
+                (lens != np.fromiter(map(len, all_lp), np.int64, len(all_lp))).any():
+            raise RifrafError("empty read or length mismatch")
+        soff = np.zeros(len(all_s) + 1, np.int64)
+        np.cumsum(lens, out=soff[1:])
+        # integer Phred scores: the codes go to the device and the host builds no
+        # tables (est_n_errors and the initial consensus's logsumexp10 in one C++
+        # pass; RifrafSequence.many_coded), else the concatenated host tables
+        coded = None
+        allb = None
+        if (phred_in and cat_lp is not None and cat_lp.dtype.kind in "iu" and len(cat_lp)
+                and int(cat_lp.max()) <= 127):
+            device = None
+            if hasattr(engine, "set_sequences_codes"):
+                # the reads go to the device first, and the per-read setup sums
+                # (est_n_errors, logsumexp10) come back from it (round 5: no
+                # per-position host pass; rf_set_sequences_codes_prep)
+                if hasattr(engine, "release_bands"):
+                    engine.release_bands()
+                allb = np.concatenate(all_s)
 
-            def device(code, lp_t, match_t, p10, grid):
-                r = engine.set_sequences_codes(0, allb, soff, code, lp_t, match_t, params.scores, prep=(p10, grid))
-                return r if r is not False else None
-        coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8, copy=False), soff, params.bandwidth,
-                                          params.scores,
-                                          device=device)
-    if coded is not None:
-        allseqs, tabs, lse_all = coded
-    else:
-        # one division / ufunc pass over every read (elementwise: equal to per-read calls)
-        lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
-            [np.asarray(x, np.float64) for x in all_lp])
-        allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
-                                                   phreds=cat_lp.astype(np.int8) if phred_in else None)
-        lse_all = None
-    nread = np.array(nread, np.int32)
-    read_off = np.zeros(K + 1, np.int32)
-    np.cumsum(nread, out=read_off[1:])
-    # initial consensus where none is given: the read of max logsumexp10(match scores)
-    need = [k for k, kw in enumerate(part) if kw.get("consensus") is None or len(kw["consensus"]) == 0]
-    first = {}
-    if need:
-        ridx = np.concatenate([np.arange(read_off[k], read_off[k + 1]) for k in need])
-        if lse_all is None:
-            ms = [allseqs[r].match_scores for r in ridx]
-            moff = np.zeros(len(ms) + 1, np.int64)
-            np.cumsum([len(x) for x in ms], out=moff[1:])
-        if lse_all is not None:
-            lse = lse_all[ridx]
-        elif len(need) == K and phred_in:
-            lse = _logsumexp10_many(tabs["match"], moff, codes=tabs["code"], table=tabs["match_table"])
+                def device(code, lp_t, match_t, p10, grid):
+                    r = engine.set_sequences_codes(0, allb, soff, code, lp_t, match_t, params.scores, prep=(p10, grid))
+                    return r if r is not False else None
+            coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8, copy=False), soff, params.bandwidth,
+                                              params.scores,
+                                              device=device)
+        if coded is not None:
+            allseqs, tabs, lse_all = coded
         else:
-            lse = _logsumexp10_many(np.concatenate(ms), moff)
-        at = 0
-        for k in need:
-            sc = lse[at:at + nread[k]]
-            first[k] = allseqs[read_off[k] + int(np.argmax(sc))].seq.copy()
-            at += nread[k]
-    states = []
-    refs_in = [DNASeq(kw["reference"]) if kw.get("reference") is not None and len(kw["reference"]) > 0
-               else np.zeros(0, np.uint8) for kw in part]
-    maxlen = np.maximum.reduceat(lens, read_off[:-1]) if K > 0 else lens
-    for k, kw in enumerate(part):
-        cons = first[k] if k in first else DNASeq(kw["consensus"])
-        states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], refs_in[k], params,
-                                    maxlen=int(maxlen[k])))
-    # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
-    # The bands of every batch read in one arena reservation (growing it in
-    # steps would re-allocate and compact tens of GB several times): A and B
-    # at the initial bandwidth plus the doubled bandwidth's regions, which a
-    # band-doubling realign allocates above them (the arena bump-allocates; a
-    # reservation of 1.5x the initial bands grew, and compacted every band,
-    # in each c3 run: 1,999 regions, ~1.8 ms of a 45 ms run, r05am trace)
-    nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
-    # every read's A/B band (upper bound: padded rows), one vector pass; a
-    # cluster whose batch is smaller than its reads counts its largest bands
-    mcons = np.fromiter((len(st_.consensus) for st_ in states), np.int64, K)
-    mrd = np.repeat(mcons, nread)
-    dn = np.abs(lens - mrd)
-    band = np.zeros(len(lens), np.int64)
-    for bw_ in (params.bandwidth, 2 * params.bandwidth):
-        Hs = 2 * bw_ + dn + 1
-        band += (Hs + 2 * mrd) * band_stride(Hs, pad_h=1) * 8
-    est_bytes = 2 * int(band.sum())
-    for k in np.flatnonzero(nb < nread):
-        bk = band[read_off[k]:read_off[k + 1]]
-        est_bytes -= 2 * int(bk.sum() - np.sort(bk)[::-1][:nb[k]].sum())
-    for k, st_ in enumerate(states):
-        m = len(st_.consensus)
-        L = len(refs_in[k])
-        if L > 0:
-            # reference-guided cluster (_native_refs): the reference's A and B
-            # at the read bandwidth, and the scratch slot's forward band, which
-            # at FRAME entry holds edit_distance's band at bw = ceil(min / 2)
-            # (align.jl:253-260) -- it grows with the square of the length
-            for bw_ in (params.bandwidth, 2 * params.bandwidth):
-                Hr = 2 * bw_ + abs(L - m) + 1
-                est_bytes += 2 * (Hr + 2 * m) * band_stride(Hr, pad_h=1) * 8
-            bwe = -(-min(L, m) // 2)
-            He = 2 * bwe + abs(L - m) + 1
-            est_bytes += (He + 2 * m) * band_stride(He, pad_h=1) * 8
-    # a new wave rewrites every slot it uses: the previous wave's bands are
-    # dropped and the arena is reused (sized once for a steady stream of waves)
-    uploaded = coded is not None and tabs["uploaded"]
-    if hasattr(engine, "release_bands") and not uploaded:
-        engine.release_bands()
-    engine.reserve(int(est_bytes * 1.1) + (64 << 20))
-    _stat("setup_native_s", time.perf_counter() - t_setup)
-    _span("setup", t_setup)
-    t_up = time.perf_counter()
-    if allb is None:
-        allb = np.concatenate(all_s)
-    # Phred-coded reads: 2 B per position to the device, tables built there
-    # (rf_set_sequences_codes; the same bits; already done with the setup
-    # sums above when `uploaded`); else the host tables
-    if not uploaded and not (
-            phred_in and hasattr(engine, "set_sequences_codes") and
-            engine.set_sequences_codes(0, allb, soff, tabs["code"], tabs["lp_table"], tabs["match_table"],
-                                       params.scores)):
-        ft = tabs["source"].full() if coded is not None else tabs
-        engine.set_sequences_concat(0, allb, soff, ft["match"], ft["mismatch"], ft["ins"], ft["del"])
-    engine.set_templates(0, [st_.consensus for st_ in states])
-    _stat("upload_s", time.perf_counter() - t_setup)
-    _span("upload", t_up)
-    t_up = time.perf_counter()
-    read_seq = np.arange(len(all_s), dtype=np.int32)
-    read_len = lens.astype(np.int32)
-    est = tabs["est"] if coded is not None else np.array([s.est_n_errors for s in allseqs])
-    thr = cquantile_poisson_many(est, params.bandwidth_pvalue)
-    fixed_off = fixed = None
-    if params.batch_fixed:
-        fb = [np.argsort(est[read_off[k]:read_off[k + 1]], kind="stable")[:st_.batch_fixed_size]
-              for k, st_ in enumerate(states)]                      # resample!, model.jl:1045-1049
-        fixed_off = np.zeros(K + 1, np.int32)
-        np.cumsum([len(b) for b in fb], out=fixed_off[1:])
-        fixed = np.concatenate(fb).astype(np.int32)
-    cons = [st_.consensus for st_ in states]
-    cons_off = np.zeros(K + 1, np.int64)
-    np.cumsum([len(c) for c in cons], out=cons_off[1:])
-    bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
-                          int(params.batch_fixed), params.batch_size, params.batch_threshold)
-    ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
-    _span("prep", t_up)
+            # one division / ufunc pass over every read (elementwise: equal to per-read calls)
+            lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
+                [np.asarray(x, np.float64) for x in all_lp])
+            allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
+                                                       phreds=cat_lp.astype(np.int8) if phred_in else None)
+            lse_all = None
+        nread = np.array(nread, np.int32)
+        read_off = np.zeros(K + 1, np.int32)
+        np.cumsum(nread, out=read_off[1:])
+        # initial consensus where none is given: the read of max logsumexp10(match scores)
+        need = [k for k, kw in enumerate(part) if kw.get("consensus") is None or len(kw["consensus"]) == 0]
+        first = {}
+        if need:
+            ridx = np.concatenate([np.arange(read_off[k], read_off[k + 1]) for k in need])
+            if lse_all is None:
+                ms = [allseqs[r].match_scores for r in ridx]
+                moff = np.zeros(len(ms) + 1, np.int64)
+                np.cumsum([len(x) for x in ms], out=moff[1:])
+            if lse_all is not None:
+                lse = lse_all[ridx]
+            elif len(need) == K and phred_in:
+                lse = _logsumexp10_many(tabs["match"], moff, codes=tabs["code"], table=tabs["match_table"])
+            else:
+                lse = _logsumexp10_many(np.concatenate(ms), moff)
+            at = 0
+            for k in need:
+                sc = lse[at:at + nread[k]]
+                first[k] = allseqs[read_off[k] + int(np.argmax(sc))].seq.copy()
+                at += nread[k]
+        states = []
+        refs_in = [DNASeq(kw["reference"]) if kw.get("reference") is not None and len(kw["reference"]) > 0
+                   else np.zeros(0, np.uint8) for kw in part]
+        maxlen = np.maximum.reduceat(lens, read_off[:-1]) if K > 0 else lens
+        for k, kw in enumerate(part):
+            cons = first[k] if k in first else DNASeq(kw["consensus"])
+            states.append(initial_state(cons, allseqs[read_off[k]:read_off[k + 1]], refs_in[k], params,
+                                        maxlen=int(maxlen[k])))
+        # ids: cluster k's reads (and batch slots) are read_off[k] + local index; template k.
+        # The bands of every batch read in one arena reservation (growing it in
+        # steps would re-allocate and compact tens of GB several times): A and B
+        # at the initial bandwidth plus the doubled bandwidth's regions, which a
+        # band-doubling realign allocates above them (the arena bump-allocates; a
+        # reservation of 1.5x the initial bands grew, and compacted every band,
+        # in each c3 run: 1,999 regions, ~1.8 ms of a 45 ms run, r05am trace)
+        nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
+        # every read's A/B band (upper bound: padded rows), one vector pass; a
+        # cluster whose batch is smaller than its reads counts its largest bands
+        mcons = np.fromiter((len(st_.consensus) for st_ in states), np.int64, K)
+        mrd = np.repeat(mcons, nread)
+        dn = np.abs(lens - mrd)
+        band = np.zeros(len(lens), np.int64)
+        for bw_ in (params.bandwidth, 2 * params.bandwidth):
+            Hs = 2 * bw_ + dn + 1
+            band += (Hs + 2 * mrd) * band_stride(Hs, pad_h=1) * 8
+        est_bytes = 2 * int(band.sum())
+        for k in np.flatnonzero(nb < nread):
+            bk = band[read_off[k]:read_off[k + 1]]
+            est_bytes -= 2 * int(bk.sum() - np.sort(bk)[::-1][:nb[k]].sum())
+        for k, st_ in enumerate(states):
+            m = len(st_.consensus)
+            L = len(refs_in[k])
+            if L > 0:
+                # reference-guided cluster (_native_refs): the reference's A and B
+                # at the read bandwidth, and the scratch slot's forward band, which
+                # at FRAME entry holds edit_distance's band at bw = ceil(min / 2)
+                # (align.jl:253-260) -- it grows with the square of the length
+                for bw_ in (params.bandwidth, 2 * params.bandwidth):
+                    Hr = 2 * bw_ + abs(L - m) + 1
+                    est_bytes += 2 * (Hr + 2 * m) * band_stride(Hr, pad_h=1) * 8
+                bwe = -(-min(L, m) // 2)
+                He = 2 * bwe + abs(L - m) + 1
+                est_bytes += (He + 2 * m) * band_stride(He, pad_h=1) * 8
+        # a new wave rewrites every slot it uses: the previous wave's bands are
+        # dropped and the arena is reused (sized once for a steady stream of waves)
+        uploaded = coded is not None and tabs["uploaded"]
+        if hasattr(engine, "release_bands") and not uploaded:
+            engine.release_bands()
+        engine.reserve(int(est_bytes * 1.1) + (64 << 20))
+        _stat("setup_native_s", time.perf_counter() - t_setup)
+        _span("setup", t_setup)
+        t_up = time.perf_counter()
+        if allb is None:
+            allb = np.concatenate(all_s)
+        # Phred-coded reads: 2 B per position to the device, tables built there
+        # (rf_set_sequences_codes; the same bits; already done with the setup
+        # sums above when `uploaded`); else the host tables
+        if not uploaded and not (
+                phred_in and hasattr(engine, "set_sequences_codes") and
+                engine.set_sequences_codes(0, allb, soff, tabs["code"], tabs["lp_table"], tabs["match_table"],
+                                           params.scores)):
+            ft = tabs["source"].full() if coded is not None else tabs
+            engine.set_sequences_concat(0, allb, soff, ft["match"], ft["mismatch"], ft["ins"], ft["del"])
+        engine.set_templates(0, [st_.consensus for st_ in states])
+        _stat("upload_s", time.perf_counter() - t_setup)
+        _span("upload", t_up)
+        t_up = time.perf_counter()
+        read_seq = np.arange(len(all_s), dtype=np.int32)
+        read_len = lens.astype(np.int32)
+        est = tabs["est"] if coded is not None else np.array([s.est_n_errors for s in allseqs])
+        thr = cquantile_poisson_many(est, params.bandwidth_pvalue)
+        fixed_off = fixed = None
+        if params.batch_fixed:
+            fb = [np.argsort(est[read_off[k]:read_off[k + 1]], kind="stable")[:st_.batch_fixed_size]
+                  for k, st_ in enumerate(states)]                      # resample!, model.jl:1045-1049
+            fixed_off = np.zeros(K + 1, np.int32)
+            np.cumsum([len(b) for b in fb], out=fixed_off[1:])
+            fixed = np.concatenate(fb).astype(np.int32)
+        cons = [st_.consensus for st_ in states]
+        cons_off = np.zeros(K + 1, np.int64)
+        np.cumsum([len(c) for c in cons], out=cons_off[1:])
+        bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
+                              int(params.batch_fixed), params.batch_size, params.batch_threshold)
+        ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
+        _span("prep", t_up)
+    finally:
+        if held:
+            setup_lock.release()
     with (init_lock if init_lock is not None else contextlib.nullcontext()):
         t0 = time.perf_counter()   # the stage machine's own time, not the wait for the lock
         res, bw = engine.rifraf_batch_native(bp, read_off, read_seq, read_len, thr, fixed_off, fixed,
@@ -687,7 +695,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True):
 
 
 def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=None, engines=None,
-                 init_exclusive: bool = False, device_qv: bool = True):
+                 init_exclusive: bool = False, device_qv: bool = True, setup_exclusive: bool = True):
     """rifraf() over many independent clusters, batched on one engine.
 
     engines: several engines (contexts, each with its own HIP stream, e.g.
@@ -696,7 +704,9 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
     the next wave from a shared queue, so one engine's host work (table
     setup, quality pass) overlaps another's kernels.  init_exclusive: at most
     one engine runs its native stage machine at a time (the others meanwhile
-    do host work: a two-stage pipeline of waves).  Clusters are independent,
+    do host work: a two-stage pipeline of waves).  setup_exclusive: at most
+    one engine in a native wave's host setup at a time (mostly Python, so
+    interleaving two setups only delays both).  Clusters are independent,
     so the results equal one engine's.  device_qv (native driver): the
     quality pass's normalisations on the device (see _wave_native).
 
@@ -720,6 +730,7 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
         nxt = [0]
         qlock = threading.Lock()
         ilock = threading.Lock() if init_exclusive else None
+        slock = threading.Lock() if setup_exclusive else None
 
         def worker(i):
             while True:
@@ -730,9 +741,10 @@ def rifraf_batch(clusters, params=None, engine=None, wave: int = 1024, native=No
                     return
                 part = clusters[starts[w]:starts[w] + wv]
                 try:
-                    if ilock is not None and (native is None or native) and \
+                    if (ilock is not None or slock is not None) and (native is None or native) and \
                             native_eligible(part, params) and hasattr(engines[i], "rifraf_batch_native"):
-                        out[w] = _wave_native(part, params, engines[i], init_lock=ilock, device_qv=device_qv)
+                        out[w] = _wave_native(part, params, engines[i], init_lock=ilock, device_qv=device_qv,
+                                              setup_lock=slock)
                     else:
                         out[w] = rifraf_batch(part, params=params, engine=engines[i], wave=wv, native=native,
                                               device_qv=device_qv)
@@ -892,7 +904,8 @@ class ClusterQueue:
 
 
 def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=None, engines=None,
-                       init_exclusive: bool = False, on_wave=None, stats=None, **kw):
+                       init_exclusive: bool = False, setup_exclusive: bool = True, on_wave=None, stats=None,
+                       **kw):
     """rifraf_batch over the waves this process takes from `queue` (a
     ClusterQueue shared by the ranks of a node): `get_cluster(i)` gives
     cluster i's keyword dict (e.g. read from its FASTQ file, as each `pmap`
@@ -903,7 +916,8 @@ def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=Non
     engines: several engines of this process (e.g. two contexts on one GPU),
     one host thread each, every thread taking its own waves from the queue
     (init_exclusive: at most one of them in its native stage machine at a
-    time, as in rifraf_batch).  `on_wave(r)` is called with each wave's
+    time; setup_exclusive: at most one in a wave's host setup, as in
+    rifraf_batch).  `on_wave(r)` is called with each wave's
     range after it ran; `stats` (a dict) receives waves / clusters taken,
     the seconds spent running them and the seconds waited at the closing
     barrier.  With a store-backed queue every rank reaches that one barrier
@@ -920,6 +934,7 @@ def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=Non
     errs = []
     lock = threading.Lock()
     ilock = threading.Lock() if init_exclusive and len(engs) > 1 else None
+    slock = threading.Lock() if setup_exclusive and len(engs) > 1 else None
     st = {"waves": 0, "clusters": 0, "busy_s": 0.0}
 
     def worker(e):
@@ -930,9 +945,10 @@ def rifraf_batch_queue(get_cluster, queue: ClusterQueue, params=None, engine=Non
                     return
                 t0 = time.perf_counter()
                 part = [get_cluster(i) for i in r]
-                if ilock is not None and kw.get("native", None) is not False and \
+                if (ilock is not None or slock is not None) and kw.get("native", None) is not False and \
                         native_eligible(part, params) and hasattr(e, "rifraf_batch_native"):
-                    res = _wave_native(part, params, e, init_lock=ilock, device_qv=kw.get("device_qv", True))
+                    res = _wave_native(part, params, e, init_lock=ilock, device_qv=kw.get("device_qv", True),
+                                       setup_lock=slock)
                 else:
                     res = rifraf_batch(part, params=params, engine=e, wave=len(r), **kw)
                 with lock:
