@@ -245,14 +245,18 @@ def _stat(key, value):
         STATS[key] += value
 
 
-# diagnostics: a list to receive (thread name, phase, t0, t1) of every native
-# wave's phases (setup, upload, native, qv), or None
+# diagnostics: a list to receive (thread name, phase, t0, t1, thread CPU s) of
+# every native wave's phases (setup, upload, prep, native, results, qv), or None
 TIMELINE = None
+_TL = threading.local()
 
 
 def _span(phase, t0):
     if TIMELINE is not None:
-        TIMELINE.append((threading.current_thread().name, phase, t0, time.perf_counter()))
+        c = time.thread_time()
+        TIMELINE.append((threading.current_thread().name, phase, t0, time.perf_counter(),
+                         c - getattr(_TL, "cpu", c)))
+        _TL.cpu = c
 
 
 def native_eligible(clusters, params) -> bool:
@@ -430,6 +434,8 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
     # setup_lock (several engines): one engine at a time in the host setup,
     # which is mostly Python (the GIL): the first engine's stage machine
     # starts after one setup, not after all of them interleaved
+    if TIMELINE is not None:
+        _TL.cpu = time.thread_time()
     held = setup_lock is not None and setup_lock.acquire()
     try:
         K = len(part)

@@ -10,6 +10,7 @@ usage: e2e_phases.py [N] [E/W[/X[/B[/S]]] ...]
   (engines, wave, init_exclusive 0, sync_block 0 (2: auto), setup_exclusive 1)"""
 import json
 import os
+import resource
 import sys
 import time
 
@@ -37,15 +38,18 @@ pin = allowed[:2]
 def one(ne, wave, excl, sx):
     q = B.ClusterQueue(n, wave)
     B.TIMELINE = []
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     B.rifraf_batch_queue(data.get, q, params=params, engines=engs[:ne], init_exclusive=bool(excl),
                          setup_exclusive=bool(sx))
     wall = time.perf_counter() - t0
-    tl = [(th, ph, round(a - t0, 4), round(b - t0, 4)) for th, ph, a, b in B.TIMELINE]
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    tl = [(th, ph, round(a - t0, 4), round(b - t0, 4), round(c, 4)) for th, ph, a, b, c in B.TIMELINE]
     B.TIMELINE = None
-    phases = {}
-    for _, ph, a, b in tl:
+    phases = {"process_cpu_s": round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 4)}
+    for _, ph, a, b, c in tl:
         phases[ph] = round(phases.get(ph, 0.0) + b - a, 4)
+        phases[ph + "_cpu"] = round(phases.get(ph + "_cpu", 0.0) + c, 4)
     return wall, phases, tl
 
 
