@@ -4424,21 +4424,47 @@ int fail(rf_ctx *ctx, int code, const std::string &msg)
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 // The host's wait for the context's stream.  HIP's stream synchronize spins
-// on the completion signal; with RF_OPT_SYNC_BLOCK the thread sleeps on a
-// blocking-sync event instead, so a rank held to a 2-core share leaves the
-// core to its other host work (quality pass, table setup, another engine's
-// thread) while its kernels run.
+// on the completion signal; with RF_OPT_SYNC_BLOCK the thread yields its core
+// and then sleeps between polls of an event instead, so a rank held to a
+// 2-core share leaves the core to its other host work (quality pass, table
+// setup, another engine's thread) while its kernels run.  (Round 6: a
+// blocking-sync hipEventSynchronize kept the waiting thread on its core --
+// the native stage machine's thread CPU time equalled its wall time,
+// profiles/r06e_e2e_phases.out.)  2: auto, block when this thread may run on
+// fewer than 4 CPUs.
+bool host_blocks(const rf_ctx *ctx)
+{
+    if (ctx->opt.sync_block == 2) {
+        cpu_set_t cs;
+        return sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) < 4;
+    }
+    return ctx->opt.sync_block == 1;
+}
+
 hipError_t stream_wait(rf_ctx *ctx)
 {
-    bool block = ctx->opt.sync_block == 1;
-    if (ctx->opt.sync_block == 2) {   // auto: sleep when this thread may run on fewer than 4 CPUs
-        cpu_set_t cs;
-        block = sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) < 4;
-    }
-    if (!block || !ctx->ev_block)
+    if (!ctx->ev_block || !host_blocks(ctx))
         return hipStreamSynchronize(ctx->stream);
-    const hipError_t e = hipEventRecord(ctx->ev_block, ctx->stream);
-    return e != hipSuccess ? e : hipEventSynchronize(ctx->ev_block);
+    hipError_t e = hipEventRecord(ctx->ev_block, ctx->stream);
+    if (e != hipSuccess)
+        return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((e = hipEventQuery(ctx->ev_block)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+            sched_yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(30));
+    }
+    return e;
+}
+
+// before a device-to-host copy into host memory that may be pageable (HIP
+// then copies through a staging buffer and spins until the stream reaches
+// the copy): a blocking host waits for the stream first, so the copy is
+// short
+hipError_t pre_d2h(rf_ctx *ctx)
+{
+    return host_blocks(ctx) ? stream_wait(ctx) : hipSuccess;
 }
 
 int ensure_buf(rf_ctx *ctx, DevBuf &b, size_t bytes)
@@ -4593,6 +4619,7 @@ int check_err_landed(rf_ctx *ctx)
 int check_err(rf_ctx *ctx)
 {
     int h = 0;
+    HIPCHK(ctx, pre_d2h(ctx));
     HIPCHK(ctx, hipMemcpyAsync(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, stream_wait(ctx));
     if (h) {
@@ -5402,6 +5429,7 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
     }
     ++ctx->layout_gen;
     if (prep && nseq > 0) {
+        HIPCHK(ctx, pre_d2h(ctx));
         HIPCHK(ctx, hipMemcpyAsync(est, d_est, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipMemcpyAsync(tsum, d_tsum, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipMemcpyAsync(ucode, d_ucode, (size_t)nseq * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -6058,6 +6086,7 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
         if (int e = launch_backtraces(ctx, tasks, nullptr, 0))
             return e;
     std::vector<int32_t> cnt(2 * (size_t)nslots);
+    HIPCHK(ctx, pre_d2h(ctx));
     if (nslots > 0)
         HIPCHK(ctx, hipMemcpyAsync(cnt.data(), d_cnt, sizeof(int32_t) * 2 * nslots,
                                    hipMemcpyDeviceToHost, ctx->stream));
@@ -6119,6 +6148,7 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     if (int e = launch_backtraces(ctx, tasks, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0))
         return e;
     HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, pre_d2h(ctx));
     HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, stream_wait(ctx));
     note_bt_ms(ctx);
@@ -6354,6 +6384,7 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                            d_hr, d_dense, d_ref, d_href, d_out, ctx->d_err);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    HIPCHK(ctx, pre_d2h(ctx));
     if (nprops > 0)
         HIPCHK(ctx, hipMemcpyAsync(out_total, d_out, nprops * 8, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<double> split_host;
@@ -6532,8 +6563,10 @@ static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_of
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    if (out && P.dense_total > 0)
+    if (out && P.dense_total > 0) {
+        HIPCHK(ctx, pre_d2h(ctx));
         HIPCHK(ctx, hipMemcpyAsync(out, d_dense, sizeof(double) * P.dense_total, out_kind, ctx->stream));
+    }
     HIPCHK(ctx, stream_wait(ctx));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
@@ -6709,6 +6742,7 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
                                (const int64_t *)ctx->scratch[23].p, (const uint32_t *)ctx->scratch[24].p,
                                (const double *)D.lut.p, (const double *)D.errlut.p, (double *)ctx->scratch[19].p, nc);
         HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, pre_d2h(ctx));
         if (out)
             HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost,
                                        ctx->stream));
@@ -6719,6 +6753,7 @@ int rf_internal_aln_sums_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_o
                            (const int32_t *)ctx->scratch[4].p, (const double *)D.lut.p, (const double *)D.errlut.p,
                            (double *)ctx->scratch[19].p);
         HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, pre_d2h(ctx));
         if (out)
             HIPCHK(ctx, hipMemcpyAsync(out, ctx->scratch[19].p, (size_t)rows * 4 * 8, hipMemcpyDeviceToHost,
                                        ctx->stream));
@@ -6905,6 +6940,7 @@ extern "C" int rf_qv_probs(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
                        (const uint8_t *)ctx->bytes_arena.d, d_pos, d_ins, d_aln, d_gerr);
     HIPCHK(ctx, hipGetLastError());
     std::vector<int32_t> gerr(ngroups);
+    HIPCHK(ctx, pre_d2h(ctx));
     HIPCHK(ctx, hipMemcpyAsync(out_pos, d_pos, npos * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(out_ins, d_ins, nins * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(out_aln, d_aln, naln * 8, hipMemcpyDeviceToHost, ctx->stream));
