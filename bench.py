@@ -534,7 +534,9 @@ class E2EClusters:
     directory on the host (/dev/shm), and every rank maps all blocks, so
     whichever rank the queue hands cluster k to reads it back (as each of the
     reference's pmap workers reads its file, scripts/rifraf.jl:190):
-    `get(k)` -> rifraf keyword dict, `template(k)`."""
+    `get(k)` -> rifraf keyword dict with the reads and Phred scores as
+    PackedReads (one buffer + offsets, as FASTQ ingest hands them over),
+    `template(k)`."""
 
     FIELDS = ("bases", "phreds", "lens", "tpl", "tlens")
 
@@ -544,7 +546,9 @@ class E2EClusters:
         lo = rank * n_per_rank
         blk = [e2e_cluster(seed, k) for k in range(lo, lo + n_per_rank)]
         if world == 1:
-            self._local = blk
+            from rifraf_amd.types import PackedReads
+            self._local = [(t, dict(dnaseqs=PackedReads.from_list(kw["dnaseqs"], np.uint8),
+                                    phreds=PackedReads.from_list(kw["phreds"], np.int8))) for t, kw in blk]
             return
         import tempfile
         base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
@@ -577,11 +581,13 @@ class E2EClusters:
     def get(self, k):
         if self.dir is None:
             return self._local[k][1]
+        from rifraf_amd.types import PackedReads
         m, roff, coff, toff = self.blocks[k // self.per]
         c = k % self.per
-        reads = [np.array(m["bases"][roff[i]:roff[i + 1]]) for i in range(coff[c], coff[c + 1])]
-        phreds = [np.array(m["phreds"][roff[i]:roff[i + 1]]) for i in range(coff[c], coff[c + 1])]
-        return dict(dnaseqs=reads, phreds=phreds)
+        a, b = roff[coff[c]], roff[coff[c + 1]]
+        off = roff[coff[c]:coff[c + 1] + 1] - a
+        return dict(dnaseqs=PackedReads(np.array(m["bases"][a:b]), off),
+                    phreds=PackedReads(np.array(m["phreds"][a:b]), off))
 
     def template(self, k):
         if self.dir is None:

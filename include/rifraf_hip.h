@@ -105,11 +105,13 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_ALN_MARKS_MIN 22 /* rf_aln_error_sums on the device: groups of more
                                    than this many reads (default 128) use the
                                    per-read marks + per-column fold launches      */
-#define RF_OPT_SYNC_BLOCK  23   /* 1: host waits for the engine's stream sleep on
-                                   a blocking-sync event instead of spinning
-                                   (ranks held to a few host cores); 2: auto,
+#define RF_OPT_SYNC_BLOCK  23   /* 1: host waits for the engine's stream yield
+                                   the core, then sleep between event polls,
+                                   instead of spinning (ranks held to a few
+                                   host cores); 2: auto,
                                    sleep when the waiting thread may run on
-                                   fewer than 4 CPUs (its affinity mask)       */
+                                   fewer than 4 CPUs (its affinity mask; the
+                                   default)                                     */
 #define RF_OPT_DP_NL64     24   /* at most this many non-lean DP tasks of H <= 127
                                    per call (codon / skew / trim) run as one
                                    latency-bound task per wave, k_dpx (default

@@ -4304,7 +4304,8 @@ struct Opts {
     int dp_streams = 1;     // RF_OPT_DP_STREAMS: DP classes on concurrent streams
     int aln_sums_host = 0;  // RF_OPT_ALN_SUMS_HOST: 1 = rf_aln_error_sums folds the moves on the host
     int aln_marks_min = 128;   // RF_OPT_ALN_MARKS_MIN: device QV sums in two launches above this many reads per group
-    int sync_block = 0;     // RF_OPT_SYNC_BLOCK: host waits sleep on a blocking-sync event instead of spinning
+    int sync_block = 2;     // RF_OPT_SYNC_BLOCK: 1 host waits yield / sleep instead of spinning; 2 (default)
+                            // auto: when the waiting thread may run on fewer than 4 CPUs
     int dp_nl64 = 1024;     // RF_OPT_DP_NL64: at most this many non-lean H <= 127 tasks run in k_dpx
     int score_wgs = 2048;   // RF_OPT_SCORE_WGS: split-mode k_score_ws takes reads in chunks so that about
                             // this many workgroups remain

@@ -30,6 +30,7 @@ import numpy as np
 from .bandedarrays import band_stride
 from .engine import RifrafError
 from .proposals import to_arrays
+from .types import PackedReads
 
 
 class _Request:
@@ -294,7 +295,12 @@ def native_eligible(clusters, params) -> bool:
             quals = kw.get("phreds")
         if quals is None or len(quals) != n:
             return False
-        ls = list(map(len, kw["dnaseqs"]))
+        ds = kw["dnaseqs"]
+        if isinstance(ds, PackedReads) and isinstance(quals, PackedReads):
+            if not np.array_equal(ds.off, quals.off) or (ds.lens() == 0).any():
+                return False
+            continue
+        ls = list(map(len, ds))
         if 0 in ls or ls != list(map(len, quals)):
             return False
     return True
@@ -443,30 +449,49 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         check_params(params.scores, np.zeros(0, np.uint8), params)
         all_s, all_lp, nread = [], [], []
         phred_in = all(kw.get("error_log_ps") is None for kw in part)
-        for kw in part:                                                 # rifraf(), model.jl:1276-1287
-            if phred_in:
-                all_lp += list(kw["phreds"])
-            else:
-                elp = kw.get("error_log_ps")
-                all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
-            # code arrays pass as they are (DNASeq would only re-wrap them)
-            all_s += [x if type(x) is np.ndarray and x.dtype == np.uint8 and x.flags.c_contiguous else DNASeq(x)
-                      for x in kw["dnaseqs"]]
-            nread.append(len(kw["dnaseqs"]))
-        cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
+        # reads handed over packed (PackedReads: one buffer + offsets per
+        # cluster, e.g. FASTQ ingest or bench's e2e staging): one concatenation
+        # per cluster instead of one per read, and no per-read objects here
+        packed = phred_in and all(isinstance(kw["dnaseqs"], PackedReads) and isinstance(kw["phreds"], PackedReads)
+                                  and kw["dnaseqs"].buf.dtype == np.uint8 and kw["phreds"].buf.dtype.kind in "iu"
+                                  for kw in part)
+        allb = None
+        if packed:
+            for kw in part:
+                if not np.array_equal(kw["dnaseqs"].off, kw["phreds"].off):
+                    raise RifrafError("empty read or length mismatch")
+            nread = [len(kw["dnaseqs"]) for kw in part]
+            lens = np.concatenate([kw["dnaseqs"].lens() for kw in part]) if part else np.zeros(0, np.int64)
+            cat_lp = np.concatenate([kw["phreds"].buf for kw in part]) if part else None
+            allb = np.concatenate([kw["dnaseqs"].buf for kw in part]) if part else np.zeros(0, np.uint8)
+            all_s = None
+            if (lens == 0).any():
+                raise RifrafError("empty read or length mismatch")
+        else:
+            for kw in part:                                                 # rifraf(), model.jl:1276-1287
+                if phred_in:
+                    all_lp += list(kw["phreds"])
+                else:
+                    elp = kw.get("error_log_ps")
+                    all_lp += [phred_to_log_p(p) for p in kw["phreds"]] if elp is None else list(elp)
+                # code arrays pass as they are (DNASeq would only re-wrap them)
+                all_s += [x if type(x) is np.ndarray and x.dtype == np.uint8 and x.flags.c_contiguous else DNASeq(x)
+                          for x in kw["dnaseqs"]]
+                nread.append(len(kw["dnaseqs"]))
+            cat_lp = np.concatenate(all_lp) if (phred_in and all_lp) else None
+            lens = np.fromiter(map(len, all_s), np.int64, len(all_s))
+            if (lens == 0).any() or len(all_lp) != len(all_s) or \
+                    (lens != np.fromiter(map(len, all_lp), np.int64, len(all_lp))).any():
+                raise RifrafError("empty read or length mismatch")
         if cat_lp is not None and len(cat_lp) and int(cat_lp.min()) < 0:
             raise RifrafError("phred score cannot be negative")
-        lens = np.fromiter(map(len, all_s), np.int64, len(all_s))
-        if (lens == 0).any() or len(all_lp) != len(all_s) or \
-                (lens != np.fromiter(map(len, all_lp), np.int64, len(all_lp))).any():
-            raise RifrafError("empty read or length mismatch")
-        soff = np.zeros(len(all_s) + 1, np.int64)
+        nall = len(lens)
+        soff = np.zeros(nall + 1, np.int64)
         np.cumsum(lens, out=soff[1:])
         # integer Phred scores: the codes go to the device and the host builds no
         # tables (est_n_errors and the initial consensus's logsumexp10 in one C++
         # pass; RifrafSequence.many_coded), else the concatenated host tables
         coded = None
-        allb = None
         if (phred_in and cat_lp is not None and cat_lp.dtype.kind in "iu" and len(cat_lp)
                 and int(cat_lp.max()) <= 127):
             device = None
@@ -476,20 +501,22 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
                 # per-position host pass; rf_set_sequences_codes_prep)
                 if hasattr(engine, "release_bands"):
                     engine.release_bands()
-                allb = np.concatenate(all_s)
+                if allb is None:
+                    allb = np.concatenate(all_s)
 
                 def device(code, lp_t, match_t, p10, grid):
                     r = engine.set_sequences_codes(0, allb, soff, code, lp_t, match_t, params.scores, prep=(p10, grid))
                     return r if r is not False else None
             coded = RifrafSequence.many_coded(all_s, cat_lp.astype(np.int8, copy=False), soff, params.bandwidth,
-                                              params.scores,
-                                              device=device)
+                                              params.scores, device=device, bases=allb)
         if coded is not None:
             allseqs, tabs, lse_all = coded
         else:
             # one division / ufunc pass over every read (elementwise: equal to per-read calls)
             lp = phred_to_log_p(cat_lp) if phred_in else np.concatenate(
                 [np.asarray(x, np.float64) for x in all_lp])
+            if all_s is None:   # packed reads on the host-table path: per-read views
+                all_s = [allb[soff[k]:soff[k + 1]] for k in range(nall)]
             allseqs, tabs = RifrafSequence.many_concat(all_s, lp, soff, params.bandwidth, params.scores,
                                                        phreds=cat_lp.astype(np.int8) if phred_in else None)
             lse_all = None
@@ -583,7 +610,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         _stat("upload_s", time.perf_counter() - t_setup)
         _span("upload", t_up)
         t_up = time.perf_counter()
-        read_seq = np.arange(len(all_s), dtype=np.int32)
+        read_seq = np.arange(nall, dtype=np.int32)
         read_len = lens.astype(np.int32)
         est = tabs["est"] if coded is not None else np.array([s.est_n_errors for s in allseqs])
         thr = cquantile_poisson_many(est, params.bandwidth_pvalue)
@@ -599,7 +626,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         np.cumsum([len(c) for c in cons], out=cons_off[1:])
         bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
                               int(params.batch_fixed), params.batch_size, params.batch_threshold)
-        ref = _native_refs(part, states, refs_in, params, engine, len(all_s), int(read_off[-1]))
+        ref = _native_refs(part, states, refs_in, params, engine, nall, int(read_off[-1]))
         _span("prep", t_up)
     finally:
         if held:

@@ -236,7 +236,7 @@ class RifrafSequence:
             {"match": match, "mismatch": mism, "ins": ins, "del": dele, **extra}
 
     @classmethod
-    def many_coded(cls, seqs, phreds, off, bandwidth: int, scores: Scores, device=None):
+    def many_coded(cls, seqs, phreds, off, bandwidth: int, scores: Scores, device=None, bases=None):
         """The native driver's setup (batch._wave_native) from concatenated
         int8 Phred scores, without building host tables: est_n_errors (the
         same Julia-order sum as many_concat) and logsumexp10 of every
@@ -251,7 +251,9 @@ class RifrafSequence:
         gathers, adds and maxima as many_concat, so the same bits).  Returns
         (objects, tables-dict with the codes and per-code tables, lse), or
         None when the library is absent; tables-dict["uploaded"] says whether
-        `device` uploaded the reads."""
+        `device` uploaded the reads.  seqs None: the objects' sequences are
+        views of `bases` (the concatenated reads, cut at `off`), made on
+        first access."""
         try:
             from . import _lib
             lib = _lib.load()
@@ -283,6 +285,7 @@ class RifrafSequence:
                                      P(lse)) != 0:
                 raise ValueError("rf_host_code_prep: invalid segments (empty sequence?)")
         src = _CodeSource(code, off64, vals, tmatch, scores)
+        src.bases = bases
         # per-sequence est / bandwidth live in the source's arrays (the
         # objects read and write them through properties), so neither this
         # loop nor a caller's bulk bandwidth update touches every object
@@ -291,12 +294,20 @@ class RifrafSequence:
         src.bwf = np.zeros(K, bool)
         out = []
         new = object.__new__
-        for k, sq in enumerate(seqs):
-            r = new(CodedRifrafSequence)
-            r.seq = sq
-            r._src = src
-            r._k = k
-            out.append(r)
+        if seqs is None:
+            for k in range(K):
+                r = new(CodedRifrafSequence)
+                r._src = src
+                r._k = k
+                out.append(r)
+        else:
+            put = _SEQ_SLOT.__set__
+            for k, sq in enumerate(seqs):
+                r = new(CodedRifrafSequence)
+                put(r, sq)
+                r._src = src
+                r._k = k
+                out.append(r)
         tabs = {"code": code, "match_table": tmatch, "lp_table": vals, "source": src, "uploaded": dev is not None,
                 "est": np.asarray(est, np.float64)}
         return out, tabs, lse
@@ -322,6 +333,7 @@ class RifrafSequence:
 
 
 _EMPTY = np.empty(0)
+_SEQ_SLOT = RifrafSequence.__dict__["seq"]
 _TABLES = ("error_log_p", "match_scores", "mismatch_scores", "ins_scores", "del_scores")
 
 
@@ -386,6 +398,21 @@ class CodedRifrafSequence(RifrafSequence):
     __slots__ = ("_src", "_k")
     codon_ins_scores = _EMPTY     # reads have no codon tables
     codon_del_scores = _EMPTY
+
+    @property
+    def seq(self):
+        slot = RifrafSequence.__dict__["seq"]
+        try:
+            return slot.__get__(self)
+        except AttributeError:   # many_coded(seqs=None): a view of the shared bases
+            src = self._src
+            v = src.bases[int(src.off[self._k]):int(src.off[self._k + 1])]
+            slot.__set__(self, v)
+            return v
+
+    @seq.setter
+    def seq(self, v):
+        RifrafSequence.__dict__["seq"].__set__(self, v)
 
     @property
     def est_n_errors(self):

@@ -408,3 +408,25 @@ def test_aln_error_sums_device_equals_host(run_engine, opts, marks_min):
     for a, b, c in zip(dev, host, hub):
         np.testing.assert_array_equal(a.aln_error_probs, b.aln_error_probs)
         assert_same_run(summary(a), summary(c))
+
+
+@pytest.mark.gpu
+def test_native_batch_packed_reads(run_engine):
+    """The native driver's packed-input path (PackedReads clusters: one
+    buffer + offsets, what bench's e2e staging and FASTQ ingest hand over)
+    gives the same runs as the same reads as lists."""
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    from rifraf_amd.sample import sample_sequences
+    from rifraf_amd.types import PackedReads
+    rng = np.random.default_rng(8)
+    cl, pk = [], []
+    for n, L in [(12, 300), (7, 240), (20, 180)]:
+        _, _, _, reads, _, phreds, _, _ = sample_sequences(n, L, error_rate=0.02, rng=rng)
+        cl.append(dict(dnaseqs=reads, phreds=phreds))
+        pk.append(dict(dnaseqs=PackedReads.from_list(reads, np.uint8), phreds=PackedReads.from_list(phreds, np.int8)))
+    params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
+    a = rifraf_batch(cl, params=params, engine=run_engine, native=True)
+    b = rifraf_batch(pk, params=params, engine=run_engine, native=True)
+    for x, y in zip(a, b):
+        assert_same_run(summary(x), summary(y))

@@ -4,6 +4,7 @@ vectorised Poisson thresholds equal the per-sequence Python code bit for bit."""
 import math
 
 import numpy as np
+import pytest
 
 from rifraf_amd import ErrorModel, RifrafSequence, Scores
 from rifraf_amd.poisson import cquantile_poisson, cquantile_poisson_many
@@ -212,3 +213,39 @@ def test_many_coded_equals_constructor():
         assert full["match"][off[k]:off[k + 1]].tobytes() == e.match_scores.tobytes()
         assert full["del"][off[k] + k:off[k + 1] + k + 1].tobytes() == e.del_scores.tobytes()
         assert len(o) == len(e) and o.bandwidth == 9 and not o.bandwidth_fixed
+
+
+def test_packed_reads_sequence():
+    """PackedReads: one buffer + offsets behaving as a list of read views."""
+    from rifraf_amd.types import PackedReads
+    reads = [np.array([0, 1, 2], np.uint8), np.array([3], np.uint8), np.array([2, 2], np.uint8)]
+    p = PackedReads.from_list(reads, np.uint8)
+    assert len(p) == 3 and list(p.lens()) == [3, 1, 2]
+    assert all(np.array_equal(a, b) for a, b in zip(p, reads))
+    assert np.array_equal(p[-1], reads[-1]) and len(p[0:2]) == 2
+    with pytest.raises(IndexError):
+        p[3]
+    with pytest.raises(ValueError):
+        PackedReads(np.zeros(3, np.uint8), [0, 4])
+
+
+def test_packed_reads_python_stage_machine_oracle():
+    """Clusters given as PackedReads run the Python stage machine (the oracle
+    engine) exactly as the same reads given as lists."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams
+    from rifraf_amd.sample import sample_sequences
+    from rifraf_amd.types import PackedReads
+    rng = np.random.default_rng(5)
+    cl, pk = [], []
+    for _ in range(3):
+        _, _, _, reads, _, phreds, _, _ = sample_sequences(6, 60, error_rate=0.03, rng=rng)
+        cl.append(dict(dnaseqs=reads, phreds=phreds))
+        pk.append(dict(dnaseqs=PackedReads.from_list(reads, np.uint8), phreds=PackedReads.from_list(phreds, np.int8)))
+    params = RifrafParams(batch_size=0, batch_fixed=False, do_score=True)
+    a = rifraf_batch(cl, params=params, engine=OracleEngine())
+    b = rifraf_batch(pk, params=params, engine=OracleEngine())
+    for x, y in zip(a, b):
+        assert np.array_equal(x.consensus, y.consensus) and x.state.score == y.state.score
+        assert np.array_equal(x.aln_error_probs, y.aln_error_probs)
