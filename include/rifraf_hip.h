@@ -129,6 +129,10 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_SEG_WGS     28   /* split-mode k_score_segl: reads per workgroup
                                    chosen so that about this many workgroups
                                    remain (default 262144)                      */
+#define RF_OPT_DP_PFIT     29   /* 1 (default): a lean NP >= 2 DP class in one
+                                   launch takes the smallest stride class that
+                                   holds its widest task (fewer repeated flush
+                                   stores); 0: the class maximum                */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -4311,6 +4311,7 @@ struct Opts {
                             // this many workgroups remain
     int seg_wgs = 262144;   // RF_OPT_SEG_WGS: split-mode k_score_segl takes reads in chunks so that about
                             // this many workgroups remain
+    int dp_pfit = 1;        // RF_OPT_DP_PFIT: lean NP >= 2 class launched at its tasks' stride class
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
 };
@@ -4677,6 +4678,7 @@ void load_env_opts(Opts &o)
     o.dp_lat = env_int("RIFRAF_DP_LAT", o.dp_lat);
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
     o.seg_wgs = env_int("RIFRAF_SEG_WGS", o.seg_wgs);
+    o.dp_pfit = env_int("RIFRAF_DP_PFIT", o.dp_pfit);
 }
 
 ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool all_finite)
@@ -4887,6 +4889,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_DP_LAT: return &o.dp_lat;
     case RF_OPT_SCORE_WGS: return &o.score_wgs;
     case RF_OPT_SEG_WGS: return &o.seg_wgs;
+    case RF_OPT_DP_PFIT: return &o.dp_pfit;
     default: return nullptr;
     }
 }
@@ -5737,6 +5740,25 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 cr[a][0].swap(keep);
             }
         }
+        // A lean NP >= 2 class launched whole (no stride split) takes the
+        // smallest stride class that holds its widest task (RF_OPT_DP_PFIT,
+        // round 6): the blocked flush issues dpl_flush_stores(NP, PM) 16-B
+        // stores per lane and lanes past a block's end repeat its last pair,
+        // so at the class maximum PM = 33 the c4 NP = 2 class (P <= 19)
+        // rewrote 18 % of its bytes (0.7 GB per step, r05j PMC)
+        if (ctx->opt.dp_pfit)
+            for (int a = 1; a <= 3; ++a) {
+                if (cr[a][1].empty() || ((psplit >> a) & 1))
+                    continue;
+                int pmax = 0;
+                for (const DPTask &t : cr[a][1])
+                    pmax = std::max(pmax, t.P);
+                int pmi = 0;
+                while (pmi < 3 && pmax > dpr_pm(a, pmi))
+                    ++pmi;
+                cp[a][pmi].insert(cp[a][pmi].end(), cr[a][1].begin(), cr[a][1].end());
+                cr[a][1].clear();
+            }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
         std::vector<DPTask> &all = P.tasks;
         all.clear();

@@ -186,6 +186,40 @@ def test_dp_wide_task_classes_long_reads(engine, opts, dp_wide, lat):
         assert_band_equal(engine.download_band(k, RF_BAND_A), A_exp, len(seqs[k]) + 1, len(t) + 1, bws[k])
 
 
+@pytest.mark.parametrize("pfit", [1, 0])
+@pytest.mark.parametrize("pad", [64, 1])
+def test_dp_lean_class_stride_fit(engine, opts, pfit, pad):
+    """RF_OPT_DP_PFIT (round 6): a lean NP = 2 / 4 / 8 class launched whole
+    takes the smallest stride class holding its widest task (fewer flush
+    stores per lane) instead of the class maximum.  Calls whose tasks sit in
+    the narrowest stride class, the widest, and a mix, for every NP, with the
+    throughput classes (no latency mode, no 32/64-lane wide tasks); bands
+    and A[end,end] bit-exact, odd and line-padded strides."""
+    opts("dp_lat", 0)
+    opts("dp_wide", 0)
+    opts("dp_pfit", pfit)
+    opts("band_pad", pad)
+    rng = np.random.default_rng(606 + pfit)
+    t = random_seq(700, rng)
+    for Hs in ((33, 35, 37), (61, 63), (33, 50, 63), (65, 68, 71), (120, 127), (129, 135, 140), (250, 255)):
+        seqs, bws = [], []
+        for k, H in enumerate(Hs * 3):
+            delta = (k % 3) - 1
+            bw = (H - 1 - abs(delta)) // 2
+            r = make_read(t, rng, 0.03, bw)
+            s, lp = r.seq, r.error_log_p
+            want = len(t) + delta
+            if len(s) > want:
+                s, lp = s[:want], lp[:want]
+            else:
+                extra = random_seq(want - len(s), rng)
+                s = np.concatenate([s, extra])
+                lp = np.concatenate([lp, np.full(len(extra), -1.2)])
+            seqs.append(RifrafSequence(s, lp, bw, SEQ_SCORES))
+            bws.append(bw)
+        _check_bands(engine, t, seqs, bws)
+
+
 @pytest.mark.parametrize("lat", [0, 2048])
 @pytest.mark.parametrize("m,n,bw", [(3, 40, 9), (8, 8, 9), (1, 1, 1), (2, 30, 2), (40, 3, 9), (25, 60, 6)])
 def test_dp_short_and_skewed_shapes(engine, opts, m, n, bw, lat):
