@@ -3431,10 +3431,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
          const double *__restrict__ bands, int8_t *__restrict__ moves, int32_t *__restrict__ nmoves,
          int32_t *__restrict__ nerr, int *__restrict__ err, uint8_t *__restrict__ mask, int do_indels)
 {
-    // two A window buffers of BTW_A / 2 doubles (round 6): the walk reads one
-    // while the next window is copied into the other by LDS-DMA
-    constexpr int WB = BTW_A / 2;
-    __shared__ __attribute__((aligned(16))) double sAb[2][WB];
+    __shared__ double sA[BTW_A];
     __shared__ double sTm[BTW_T], sTx[BTW_T], sTi[BTW_T], sTd[BTW_T];
     __shared__ double sTci[BTW_T], sTcd[BTW_T];   // codon tables (codon alignments only)
     __shared__ uint8_t sS[BTW_T], sTt[BTW_T];
@@ -3448,7 +3445,7 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     const int c = max(m - n, 0) + T.bw;
     const int K = H + 2 * m;
     const int wd = min(P, BTW_WD);
-    const int W = WB / wd;                             // kappa rows per window (>= 128)
+    const int W = BTW_A / wd;                          // kappa rows per window (>= 256)
     const bool skew = T.flags & 2, trim = T.flags & 4;
     const bool cod = T.ncins > 0 || T.ncdel > 0;
     const int ext = cod ? 2 : 0;                       // codon predecessors: 2 more rows / diagonals
@@ -3463,27 +3460,6 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     int klo = -1, e0 = 0;                              // A window: rows [klo, klo + W), elements [e0, e0 + wd)
     int q0 = -1, r0 = -1;                              // table rows [q0, q0 + BTW_T), bases [r0, r0 + BTW_T)
     int failed = 0;
-    // The next A window (round 6).  The walk only moves to lower kappa, so the
-    // window a re-stage will need is predictable -- the rows ending where the
-    // box's reach leaves this window, at the same elements -- and is copied
-    // into the other buffer by LDS-DMA (4-B pieces, lane-linear: piece j is
-    // doubles [32 j, 32 j + 32) of the window, element t = row * wd + col)
-    // as soon as a window is in place; a re-stage whose rows or elements the
-    // prediction misses loads synchronously as before.  Rows of 8 elements
-    // only (P >= BTW_WD).
-    int cb = 0;
-    double *sA = sAb[0];
-    const bool dma = wd == BTW_WD;
-    int pklo = -1, pe0 = 0, pna = 0;
-    auto dma_window = [&](double *dst, int lo, int ee0, int na) {
-        const int tl = lane >> 1, hl = lane & 1;
-        for (int j = 0; 32 * j < na; ++j) {
-            const int t = min(32 * j + tl, na - 1);
-            const char *src = (const char *)(A + (size_t)(lo + t / BTW_WD) * P + ee0 + t % BTW_WD) + 4 * hl;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)(dst + 32 * j), 4, 0, 0);
-        }
-    };
     while ((ii > 0 || jj > 0) && !failed) {
         // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
@@ -3492,59 +3468,39 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         const int elo = max(d0 - 2 - ext, 0) >> 1, ehi = min(d0 + 2 + ext, H - 1) >> 1;
         if (klo < 0 || klo_need < klo || elo < e0 || ehi >= e0 + wd) {
             const int khi = min(kap0 - 1, K - 1);
-            const bool hit = pklo >= 0 && klo_need >= pklo && khi < pklo + pna / wd && elo >= pe0 && ehi < pe0 + wd;
-            // the prefetch has landed (or the buffer it writes is free again)
-            __builtin_amdgcn_s_waitcnt(0);
+            klo = max(0, khi - W + 1);
+            e0 = min(max((d0 >> 1) - wd / 2, 0), P - wd);
+            const int nrow = khi - klo + 1, na = nrow * wd;
             wave_sync();                               // every lane is done with the old window
-            if (hit) {
-                cb ^= 1;
-                sA = sAb[cb];
-                klo = pklo;
-                e0 = pe0;
-            } else {
-                klo = max(0, khi - W + 1);
-                e0 = min(max((d0 >> 1) - wd / 2, 0), P - wd);
-                const int nrow = khi - klo + 1, na = nrow * wd;
-                // element t = row * wd + col, t = lane + 64 u: incremental row / col
-                const int qr = 64 / wd, rr = 64 % wd;
-                int row = lane / wd, col = lane % wd;
-                for (int u0 = 0; u0 < WB / 64; u0 += 16) {
-                    double v[16];
-                    int rw = row, cl = col;
+            // element t = row * wd + col, t = lane + 64 u: incremental row / col
+            const int qr = 64 / wd, rr = 64 % wd;
+            int row = lane / wd, col = lane % wd;
+            for (int u0 = 0; u0 < BTW_A / 64; u0 += 16) {
+                double v[16];
+                int rw = row, cl = col;
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) {     // issue all loads of the chunk
-                        const int t = lane + 64 * (u0 + u);
-                        v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
-                        rw += qr;
-                        cl += rr;
-                        if (cl >= wd) {
-                            cl -= wd;
-                            ++rw;
-                        }
+                for (int u = 0; u < 16; ++u) {         // issue all loads of the chunk
+                    const int t = lane + 64 * (u0 + u);
+                    v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
+                    rw += qr;
+                    cl += rr;
+                    if (cl >= wd) {
+                        cl -= wd;
+                        ++rw;
                     }
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        const int t = lane + 64 * (u0 + u);
-                        if (t < na)
-                            sA[t] = v[u];
-                    }
-                    row = rw;
-                    col = cl;
-                    if (64 * (u0 + 16) >= na)        // lane 0 holds the chunk's lowest t
-                        break;
                 }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int t = lane + 64 * (u0 + u);
+                    if (t < na)
+                        sA[t] = v[u];
+                }
+                row = rw;
+                col = cl;
+                if (64 * (u0 + 16) >= na)            // lane 0 holds the chunk's lowest t
+                    break;
             }
             wave_sync();
-            // the next window: the rows a re-stage at the box's reach will take
-            // (kappa of the cell then <= klo + 2 BT_DMAX + 2 + ext)
-            pklo = -1;
-            if (dma && klo > 0) {
-                const int phi = min(klo + 2 * BT_DMAX + 1 + ext, K - 1);
-                pklo = max(0, phi - W + 1);
-                pe0 = e0;
-                pna = (phi - pklo + 1) * wd;
-                dma_window(sAb[cb ^ 1], pklo, pe0, pna);
-            }
         }
         const int qlo_need = max(ii - BT_DMAX - 1 - ext, 0), rlo_need = max(jj - BT_DMAX - 2, 0);
         if (q0 < 0 || qlo_need < q0 || rlo_need < r0 || ii > q0 + BTW_T - 1 || max(jj - 1, 0) > r0 + BTW_T - 1) {
