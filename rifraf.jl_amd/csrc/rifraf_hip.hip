@@ -1434,6 +1434,213 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------
+// k_dpm: very wide bands without codon moves across several CUs (round 6;
+// edit_distance's band, align.jl:253-260).  k_dpw runs such a band in one
+// workgroup: 16 waves and a barrier per anti-diagonal, issue-bound on one
+// CU (3.33 ms per configs[2] call).  Here the band is cut into slices of
+// DPM_OWN band-row pairs, one single-wave workgroup each (no barrier per
+// step), which meet only every DPM_B anti-diagonals:
+//   - the wave holds 64 * DPM_NPL consecutive pairs: its slice and DPM_B / 2
+//     pairs (DPM_B diagonals) of each neighbouring slice.  After a hand-off
+//     every pair holds exact values; in the next DPM_B steps a wrong value
+//     enters at the wave's outer edges (their outer neighbours are unknown)
+//     and spreads inward one diagonal per step, so it never reaches the
+//     slice before the next hand-off refreshes the halo pairs;
+//   - the kappa-1 values of neighbouring diagonals move between lanes by DPP
+//     (wave_shr / wave_shl), within a lane in registers;
+//   - row records and template bases come from LDS rings, filled 64 rows /
+//     columns at a time one chunk of 64 periods ahead;
+//   - the slice's cells go to the band write-through (sc1 stores); at the
+//     end of a block of DPM_B anti-diagonals the wave waits for its stores
+//     (vmcnt(0)) and lane 0 publishes the block number (sc1 flag store); a
+//     wave polls its neighbours' flags (sc1 loads, bounded: error 4 rather
+//     than a hang) and reloads its halo pairs' last two values from the band
+//     (sc1 loads) -- the hand-off recipe of MI355X_MICROARCH.md
+//     (inter-workgroup visibility);
+//   - slices run on one XCD (workgroups at blockIdx multiples of 8).
+// Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical.
+// ---------------------------------------------------------------------
+constexpr int DPM_NPL = 2;                        // pairs per lane
+constexpr int DPM_B = 64;                         // anti-diagonals per hand-off
+constexpr int DPM_OWN = 64 * DPM_NPL - DPM_B;     // pairs per slice
+constexpr int DPM_RING = 256;                     // staged rows / columns (4 blocks of 64)
+constexpr int DPM_SPIN = 1 << 22;                 // flag polls before error 4
+
+__host__ __device__ constexpr int dpm_slices(int H) { return ((H + 1) / 2 + DPM_OWN - 1) / DPM_OWN; }
+constexpr size_t DPM_MAX_SLICES = 2048;           // slices per launch (all resident at once)
+
+__device__ __forceinline__ void st_sc1(double *p, double v)
+{
+    __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ void __launch_bounds__(64)
+k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__restrict__ bases,
+      const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
+      int *__restrict__ err, int *__restrict__ flags)
+{
+    if (blockIdx.x & 7)
+        return;
+    const int w = blockIdx.x >> 3, task = w / G, g = w % G;
+    if (task >= ntasks)
+        return;
+    const DPTask T = tasks[task];
+    const int npairs = (T.H + 1) >> 1;
+    const int Gt = dpm_slices(T.H);
+    if (g >= Gt)
+        return;
+    int *flag = flags + (size_t)task * G;
+    const int q = threadIdx.x;
+    const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
+    const uint8_t *sbase = bases + T.sb;
+    const uint8_t *tbase = bases + T.tb;
+    const double *tb = tabs + T.tab;
+    double *band = bands + T.band;
+    const int K = T.klen, H = T.H;
+    const int own_lo = g * DPM_OWN, own_hi = min(own_lo + DPM_OWN, npairs);
+    const int pb = own_lo - DPM_B / 2;           // the pair of lane 0, r = 0
+    __shared__ dvec2 s_mtmm[DPM_RING], s_isds[DPM_RING];
+    __shared__ uint8_t s_sb[DPM_RING], s_col[DPM_RING];
+    // pair pp = pb + x at period P reads read rows x + P + par + rbase and
+    // template column P + 127 - x + cbase: ring entries (x + P + par) and
+    // (P + 127 - x), blocks of 64 entries
+    const int rbase = pb - T.c, cbase = -(pb + 64 * DPM_NPL - 1);
+    struct Blk {
+        RowRec r;
+        int col;
+    };
+    auto blk_load = [&](int b) {
+        Blk x;
+        x.r = load_row_flat(T, rev, sbase, tb, rbase + 64 * b + q, false);
+        if (skew)
+            x.r.mm *= 0.99;
+        x.col = load_col_flat(T, rev, tbase, cbase + 64 * b + q);
+        return x;
+    };
+    auto blk_put = [&](int b, const Blk &x) {
+        const int i = (64 * b + q) & (DPM_RING - 1);
+        s_mtmm[i] = dvec2{x.r.mt, x.r.mm};
+        s_isds[i] = dvec2{x.r.is, x.r.ds};
+        s_sb[i] = (uint8_t)x.r.sb;
+        s_col[i] = (uint8_t)x.col;
+    };
+    blk_put(0, blk_load(0));
+    blk_put(1, blk_load(1));
+    Blk pend = blk_load(2);
+    double vev[DPM_NPL], vod[DPM_NPL];
+#pragma unroll
+    for (int r = 0; r < DPM_NPL; ++r)
+        vev[r] = vod[r] = -RF_INF;
+    int eflag = 0;
+    auto step = [&](auto PARC, const int k) {
+        constexpr int par = decltype(PARC)::value;
+        const int P = k >> 1;
+        const size_t row = (size_t)(rev ? K - 1 - k : k) * T.P;
+        // the neighbouring pair's kappa - 1 value across the lane edge
+        const double nbL = par ? 0.0 : dpp_f64<TaskLanes<64>::FROM_L1>(vod[DPM_NPL - 1]);
+        const double nbR = par ? dpp_f64<TaskLanes<64>::FROM_R1>(vev[0]) : 0.0;
+        double nv[DPM_NPL];
+#pragma unroll
+        for (int r = 0; r < DPM_NPL; ++r) {
+            const int x = q * DPM_NPL + r, pp = pb + x;
+            const int d = 2 * pp + par;
+            const int jj = P - pp, ii = pp + P + par - T.c;
+            const int ri = (x + P + par) & (DPM_RING - 1), ci = (P + 127 - x) & (DPM_RING - 1);
+            const dvec2 mtmm = s_mtmm[ri], isds = s_isds[ri];
+            const int sb = s_sb[ri], tbb = s_col[ci];
+            const double a2 = par ? vod[r] : vev[r];
+            const double a1l = par ? vev[r] : (r > 0 ? vod[r > 0 ? r - 1 : 0] : nbL);
+            const double a1r = par ? (r < DPM_NPL - 1 ? vev[r < DPM_NPL - 1 ? r + 1 : 0] : nbR) : vod[r];
+            const bool on = d >= 0 && d < H && d <= k;
+            const bool own = pp >= own_lo && pp < own_hi;
+            double v = -RF_INF;
+            if (on && jj <= T.m && ii >= 0 && ii <= T.n) {
+                if (ii == 0 && jj == 0) {
+                    v = 0.0;
+                } else {
+                    const double ms = sb == tbb ? mtmm.x : mtmm.y;
+                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;
+                    // align.jl:77-104: the maximum of the candidates
+                    v = fmax(fmax(a2 + ms, a1l + is), a1r + isds.y);
+                    eflag |= (own && v == -RF_INF) ? 1 : 0;   // "new score is invalid"
+                }
+                if (own && ii == T.n && jj == T.m && out_score)
+                    out_score[T.out_idx] = v;
+            }
+            if (own && on)
+                st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
+            nv[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < DPM_NPL; ++r) {
+            if (par)
+                vod[r] = nv[r];
+            else
+                vev[r] = nv[r];
+        }
+    };
+    for (int k = 0; k < K; k += 2) {
+        if ((k & 127) == 0) {                    // chunk t = k / 128: rows / columns of block t + 2
+            const int t = k >> 7;
+            __builtin_amdgcn_s_waitcnt(0);
+            blk_put(t + 2, pend);
+            pend = blk_load(t + 3);
+            wave_sync();
+        }
+        step(std::integral_constant<int, 0>{}, k);
+        if (k + 1 < K)
+            step(std::integral_constant<int, 1>{}, k + 1);
+        const int kn = k + 2;                    // steps done
+        if (kn % DPM_B == 0 && kn < K) {
+            // ---- hand-off after block kn / DPM_B
+            const int b = kn / DPM_B;
+            __builtin_amdgcn_s_waitcnt(0);       // this wave's band stores are out (sc1)
+            if (q == 0)
+                __hip_atomic_store(flag + g, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = true;
+            for (int nbg = g - 1; nbg <= g + 1; nbg += 2) {
+                if (nbg < 0 || nbg >= Gt)
+                    continue;
+                int spins = 0;
+                while (__hip_atomic_load(flag + nbg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < b) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins >= DPM_SPIN) {
+                        ok = false;
+                        break;
+                    }
+                }
+            }
+            if (!ok) {
+                set_err(err, 4);   // a neighbouring slice never arrived
+                return;
+            }
+            // halo pairs: the last even (kn - 2) and odd (kn - 1) values from the band
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r) {
+                const int pp = pb + q * DPM_NPL + r;
+                if (pp >= own_lo && pp < own_hi)
+                    continue;
+                const int de = 2 * pp, dod = 2 * pp + 1, ke = kn - 2, ko = kn - 1;
+                vev[r] = (pp >= 0 && de < H && de <= ke)
+                             ? ld_sc1(band + (size_t)(rev ? K - 1 - ke : ke) * T.P + ((rev ? H - 1 - de : de) >> 1))
+                             : -RF_INF;
+                vod[r] = (pp >= 0 && dod < H && dod <= ko)
+                             ? ld_sc1(band + (size_t)(rev ? K - 1 - ko : ko) * T.P + ((rev ? H - 1 - dod : dod) >> 1))
+                             : -RF_INF;
+            }
+        }
+    }
+    if (eflag)
+        set_err(err, 1);
+}
+
+// ---------------------------------------------------------------------
 // k_dpx: latency-bound non-lean tasks (round 5).
 //
 // The reference's codon DP (align.jl:77-104 with codon moves; skew_matches
@@ -4311,6 +4518,7 @@ struct Opts {
                             // this many workgroups remain
     int seg_wgs = 262144;   // RF_OPT_SEG_WGS: split-mode k_score_segl takes reads in chunks so that about
                             // this many workgroups remain
+    int dp_mc = 1;          // RF_OPT_DP_MC: H > 2040 bands without codon moves in k_dpm (0: k_dpw / k_dp)
     int dp_pfit = 1;        // RF_OPT_DP_PFIT: lean NP >= 2 class launched at its tasks' stride class
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
@@ -4340,7 +4548,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[28];
+    DevBuf scratch[29];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -4372,6 +4580,8 @@ struct rf_ctx {
         size_t nl = 0;         // latency-mode lean tasks, one k_dpx<false, false> class (RF_OPT_DP_LAT)
         size_t nww = 0;        // very wide bands without codon moves (k_dpw)
         int hmaxw = 0;
+        size_t nwm = 0;        // very wide bands without codon moves across CUs (k_dpm, RF_OPT_DP_MC)
+        int gm = 0;            // their most slices
         size_t n64 = 0, ng = 0;
         int hmax64 = 0, hmaxg = 0;
         std::vector<DPTask> tasks;   // host copy of the uploaded descriptors
@@ -4404,6 +4614,7 @@ const char *numeric_message(int code)
     case 1: return "new score is invalid";
     case 2: return "failed to find a move";
     case 3: return "failed to compute a valid score";
+    case 4: return "internal error: a band slice's neighbour never arrived (k_dpm)";
     default: return "numeric error";
     }
 }
@@ -4679,6 +4890,7 @@ void load_env_opts(Opts &o)
     o.score_wgs = env_int("RIFRAF_SCORE_WGS", o.score_wgs);
     o.seg_wgs = env_int("RIFRAF_SEG_WGS", o.seg_wgs);
     o.dp_pfit = env_int("RIFRAF_DP_PFIT", o.dp_pfit);
+    o.dp_mc = env_int("RIFRAF_DP_MC", o.dp_mc);
 }
 
 ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool all_finite)
@@ -4890,6 +5102,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SCORE_WGS: return &o.score_wgs;
     case RF_OPT_SEG_WGS: return &o.seg_wgs;
     case RF_OPT_DP_PFIT: return &o.dp_pfit;
+    case RF_OPT_DP_MC: return &o.dp_mc;
     default: return nullptr;
     }
 }
@@ -5618,8 +5831,8 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cww;
-        int hmax64 = 0, hmaxg = 0, hmaxw = 0;
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cww, cwm;
+        int hmax64 = 0, hmaxg = 0, hmaxw = 0, gm = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
         // of the tasks -- measured: c4 DP -5..9 %; splitting the wide classes,
@@ -5718,6 +5931,9 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
+                } else if (S.ncins == 0 && S.ncdel == 0 && ctx->opt.dp_mc) {
+                    cwm.push_back(t);   // k_dpm: across CUs, no codon moves (edit_distance's band)
+                    gm = std::max(gm, dpm_slices(t.H));
                 } else if (S.ncins == 0 && S.ncdel == 0 && t.H <= DPW_MAXH) {
                     cww.push_back(t);   // k_dpw: staged rows, no codon moves (edit_distance's band)
                     hmaxw = std::max(hmaxw, t.H);
@@ -5759,6 +5975,21 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 cp[a][pmi].insert(cp[a][pmi].end(), cr[a][1].begin(), cr[a][1].end());
                 cr[a][1].clear();
             }
+        // k_dpm's slices spin on each other: every workgroup of a launch must
+        // be resident at once, so large sets of very wide bands take the
+        // one-workgroup kernels
+        if (cwm.size() * (size_t)gm > DPM_MAX_SLICES) {
+            for (const DPTask &t : cwm)
+                if (t.H <= DPW_MAXH) {
+                    cww.push_back(t);
+                    hmaxw = std::max(hmaxw, t.H);
+                } else {
+                    cg.push_back(t);
+                    hmaxg = std::max(hmaxg, t.H);
+                }
+            cwm.clear();
+            gm = 0;
+        }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
         std::vector<DPTask> &all = P.tasks;
         all.clear();
@@ -5785,6 +6016,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         all.insert(all.end(), c64.begin(), c64.end());
         all.insert(all.end(), cg.begin(), cg.end());
         all.insert(all.end(), cww.begin(), cww.end());
+        all.insert(all.end(), cwm.begin(), cwm.end());
         if (int e = upload(ctx, ctx->scratch[8], all))
             return e;
         P.valid = true;
@@ -5809,6 +6041,8 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         P.ng = cg.size();
         P.nww = cww.size();
         P.hmaxw = hmaxw;
+        P.nwm = cwm.size();
+        P.gm = gm;
         P.hmax64 = hmax64;
         P.hmaxg = hmaxg;
     }
@@ -5826,7 +6060,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
     // bands), so the smaller ones run on side streams concurrently with the
     // largest: the machine stays full through every launch's tail.
     struct Launch {
-        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>,
+        int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>, 11 = k_dpm,
                        // 10 = k_dpw, 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean),
                        // 35 = latency-mode lean,
                        // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
@@ -5868,8 +6102,12 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             launches.push_back({9, at, P.ng});
             at += P.ng;
         }
-        if (P.nww)
+        if (P.nww) {
             launches.push_back({10, at, P.nww});
+            at += P.nww;
+        }
+        if (P.nwm)
+            launches.push_back({11, at, P.nwm});
     }
     // (Round 5: the lean 16-lane classes as ONE launch -- a kernel choosing the
     // class body per block, dynamic LDS of the largest class -- was slower:
@@ -5884,13 +6122,17 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (int e = ensure_buf(ctx, ctx->scratch[10], P.ng * 4 * (size_t)(P.hmaxg + 6) * 8))
             return e;
     }
+    if (P.nwm) {
+        if (int e = ensure_buf(ctx, ctx->scratch[28], P.nwm * (size_t)P.gm * sizeof(int)))
+            return e;
+    }
     // The latency-bound classes (few long tasks: k_dpx, k_dp) go first, on
     // the main stream: the others run beside them on the side streams, which
     // may share hardware queues with each other (round 5: the reference's
     // codon DP waited behind a read class on a shared queue, c3).  Otherwise
     // the largest launch stays on the main stream.
     std::stable_partition(launches.begin(), launches.end(),
-                          [](const Launch &L) { return L.kind == 34 || (L.kind >= 8 && L.kind <= 10); });
+                          [](const Launch &L) { return L.kind == 34 || (L.kind >= 8 && L.kind <= 11); });
     size_t big = 0;
     const bool lat_first = !launches.empty() &&
                            (launches[0].kind == 34 || (launches[0].kind >= 8 && launches[0].kind <= 10));
@@ -5966,6 +6208,12 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             const int ld = P.hmax64 + 6;
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
+        } else if (L.kind == 11) {
+            // H > 2040 without codon moves across CUs (k_dpm): 8 workgroups per
+            // slice (one works: one XCD), hand-off flags zeroed first
+            HIPCHK(ctx, hipMemsetAsync(ctx->scratch[28].p, 0, (size_t)n * P.gm * sizeof(int), st));
+            hipLaunchKernelGGL(k_dpm, dim3((unsigned)(8 * n * P.gm)), dim3(64), 0, st, d_tasks + L.at, n, P.gm, d_bases,
+                               d_tabs, d_bands, d_out, ctx->d_err, (int *)ctx->scratch[28].p);
         } else if (L.kind == 10) {
             // H > 2040 without codon moves: staged rows (k_dpw), a three-row value ring
             const int ld = P.hmaxw + 4;

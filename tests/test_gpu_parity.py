@@ -345,15 +345,18 @@ def test_dpx_invalid_score_is_loud(engine):
         oracle.forward(t, r)
 
 
+@pytest.mark.parametrize("mc", [1, 0])
 @pytest.mark.parametrize("m,dn,flags", [(2601, 21, RF_SKEW), (3000, -40, 0), (3400, 180, RF_SKEW | RF_TRIM),
                                          (2300, 0, RF_TRIM)])
-def test_dpw_edit_distance_bands(engine, m, dn, flags):
+def test_dpw_edit_distance_bands(engine, opts, m, dn, flags, mc):
     """Round 5: very wide bands without codon moves (edit_distance,
     align.jl:253-260: bw = ceil(min(m, n) / 2), skew_matches) run in k_dpw
     (staged row / column rings, three-row value ring): configs[2]'s shape
     (2,622 x 2,601), H up to ~3,600 (the k_dpw limit), skew and trim,
     forward and (no flags) backward; bands, A[end,end], backtraces and error
-    counts bit-exact vs the oracle."""
+    counts bit-exact vs the oracle.  mc 1 (the default since round 6): the
+    same bands across CUs in k_dpm's slices (RF_OPT_DP_MC); 0: k_dpw."""
+    opts("dp_mc", mc)
     rng = np.random.default_rng(m + dn)
     t = random_seq(m, rng)
     s = make_read(t, rng, 0.1, 9).seq
@@ -379,9 +382,11 @@ def test_dpw_edit_distance_bands(engine, m, dn, flags):
         assert_band_equal(engine.download_band(0, RF_BAND_B), oracle.backward(t, r), len(s) + 1, m + 1, bw)
 
 
-def test_dp_huge_band_global_ring(engine):
-    """H > 2040 (edit_distance-sized bands) takes the one-task-per-block path
-    (k_dp<256, false, 256>: 256 lanes per anti-diagonal, the ring in LDS)."""
+@pytest.mark.parametrize("mc", [1, 0])
+def test_dp_huge_band_global_ring(engine, opts, mc):
+    """H > 2040 (edit_distance-sized bands): k_dpm's slices across CUs (mc
+    1), or one task per block (mc 0)."""
+    opts("dp_mc", mc)
     rng = np.random.default_rng(5)
     t = random_seq(2300, rng)
     s = make_read(t, rng, 0.02, 1100)
@@ -394,9 +399,12 @@ def test_dp_huge_band_global_ring(engine):
     assert_band_equal(engine.download_band(0, RF_BAND_B), B_exp, len(s) + 1, 2301, 1100)
 
 
-def test_dp_band_beyond_lds_ring(engine):
-    """H > DPW_LDS_H (5114): the same block-wide DP with its ring in global
-    memory (k_dp<256, true, 256>); forward and backward bands bit-exact."""
+@pytest.mark.parametrize("mc", [1, 0])
+def test_dp_band_beyond_lds_ring(engine, opts, mc):
+    """H > DPW_LDS_H (5114): k_dpm (mc 1, 81 slices) or the block-wide DP
+    with its ring in global memory (k_dp<256, true, 256>, mc 0); forward and
+    backward bands bit-exact."""
+    opts("dp_mc", mc)
     rng = np.random.default_rng(6)
     t = random_seq(5300, rng)
     s = make_read(t, rng, 0.02, 2600)
@@ -409,6 +417,26 @@ def test_dp_band_beyond_lds_ring(engine):
     assert_band_equal(engine.download_band(0, RF_BAND_A), A_exp, len(s) + 1, len(t) + 1, 2600)
     B_exp = oracle.backward(t, s)
     assert_band_equal(engine.download_band(0, RF_BAND_B), B_exp, len(s) + 1, len(t) + 1, 2600)
+
+
+def test_dpm_several_wide_bands_one_call(engine):
+    """Several very wide bands in one rf_realign (k_dpm: every band's slices
+    in one launch, bands of different slice counts, H just above the 2,040
+    edge and far above), forward and backward, and a narrow read beside
+    them; bands and A[end,end] bit-exact."""
+    rng = np.random.default_rng(66)
+    t = random_seq(2200, rng)
+    seqs, bws = [], []
+    for bw, dn in ((1020, 2), (1100, -30), (1300, 0), (1019, 1)):
+        s = make_read(t, rng, 0.05, bw).seq
+        want = len(t) + dn
+        s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
+        seqs.append(RifrafSequence(s, np.full(len(s), -1.3), bw, SEQ_SCORES))
+        bws.append(bw)
+    seqs.append(make_read(t, rng, 0.02, 9))
+    bws.append(9)
+    assert all(2 * b + abs(len(s) - len(t)) + 1 > 2040 for s, b in zip(seqs[:4], bws[:4]))
+    _check_bands(engine, t, seqs, bws)
 
 
 @pytest.mark.parametrize("mode", ["fused", "split"])
