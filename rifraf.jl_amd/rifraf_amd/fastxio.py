@@ -67,6 +67,15 @@ def read_fastq(filename):
     return [DNASeq(s) for _, s, _ in recs], [q for _, _, q in recs], [n for n, _, _ in recs]
 
 
+def read_fastq_packed(filename):
+    """read_fastq with the reads and Phred scores as PackedReads (one buffer
+    + offsets each): the form the batched native driver takes without a
+    per-read concatenation (batch._wave_native).  -> (seqs, phreds, names)."""
+    from .types import PackedReads
+    seqs, phreds, names = read_fastq(filename)
+    return PackedReads.from_list(seqs, np.uint8), PackedReads.from_list(phreds, np.int8), names
+
+
 def write_fastq(filename, seqs, phreds, names=None):
     if not names or len(names) != len(seqs):
         names = [f"seq_{i + 1}" for i in range(len(seqs))]

@@ -249,3 +249,16 @@ def test_packed_reads_python_stage_machine_oracle():
     for x, y in zip(a, b):
         assert np.array_equal(x.consensus, y.consensus) and x.state.score == y.state.score
         assert np.array_equal(x.aln_error_probs, y.aln_error_probs)
+
+
+def test_read_fastq_packed_matches_lists():
+    """read_fastq_packed: the same reads and Phred scores as read_fastq, as
+    PackedReads (config 1's golden input)."""
+    import os
+    from rifraf_amd.fastxio import read_fastq, read_fastq_packed
+    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config1", "input-reads-1.fastq")
+    s, p, n = read_fastq(f)
+    ps, pp, pn = read_fastq_packed(f)
+    assert n == pn and len(ps) == len(s)
+    assert all(np.array_equal(a, b) for a, b in zip(ps, s))
+    assert all(np.array_equal(a, b) for a, b in zip(pp, p))
