@@ -427,7 +427,7 @@ def test_dpm_several_wide_bands_one_call(engine):
     rng = np.random.default_rng(66)
     t = random_seq(2200, rng)
     seqs, bws = [], []
-    for bw, dn in ((1020, 2), (1100, -30), (1300, 0), (1019, 1)):
+    for bw, dn in ((1025, 2), (1100, -30), (1300, 0), (1021, 1)):
         s = make_read(t, rng, 0.05, bw).seq
         want = len(t) + dn
         s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
