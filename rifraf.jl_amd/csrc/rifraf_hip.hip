@@ -1534,55 +1534,84 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     blk_put(1, blk_load(1));
     Blk pend = blk_load(2);
     double vev[DPM_NPL], vod[DPM_NPL];
+    // a pair's row record for its even step is the record its odd step read
+    // one period earlier (read row pp + P - c either way): carried here
+    dvec2 rmt[DPM_NPL], ris[DPM_NPL];
+    int rsb[DPM_NPL];
 #pragma unroll
-    for (int r = 0; r < DPM_NPL; ++r)
+    for (int r = 0; r < DPM_NPL; ++r) {
         vev[r] = vod[r] = -RF_INF;
+        const int ri = (q * DPM_NPL + r) & (DPM_RING - 1);
+        rmt[r] = s_mtmm[ri];
+        ris[r] = s_isds[ri];
+        rsb[r] = s_sb[ri];
+    }
     int eflag = 0;
-    auto step = [&](auto PARC, const int k) {
-        constexpr int par = decltype(PARC)::value;
-        const int P = k >> 1;
-        const size_t row = (size_t)(rev ? K - 1 - k : k) * T.P;
-        // the neighbouring pair's kappa - 1 value across the lane edge
-        const double nbL = par ? 0.0 : dpp_f64<TaskLanes<64>::FROM_L1>(vod[DPM_NPL - 1]);
-        const double nbR = par ? dpp_f64<TaskLanes<64>::FROM_R1>(vev[0]) : 0.0;
-        double nv[DPM_NPL];
+    // one period P: the even step 2P and the odd step 2P + 1.  The LDS reads
+    // of both (the period's template bases, the odd step's row records) are
+    // issued first; the cells are branch-free selects, only the band stores
+    // and the final score are conditional.
+    auto period = [&](const int P, const bool odd_too) {
+        int tbb[DPM_NPL];
+        dvec2 omt[DPM_NPL], ois[DPM_NPL];
+        int osb[DPM_NPL];
 #pragma unroll
         for (int r = 0; r < DPM_NPL; ++r) {
-            const int x = q * DPM_NPL + r, pp = pb + x;
-            const int d = 2 * pp + par;
-            const int jj = P - pp, ii = pp + P + par - T.c;
-            const int ri = (x + P + par) & (DPM_RING - 1), ci = (P + 127 - x) & (DPM_RING - 1);
-            const dvec2 mtmm = s_mtmm[ri], isds = s_isds[ri];
-            const int sb = s_sb[ri], tbb = s_col[ci];
-            const double a2 = par ? vod[r] : vev[r];
-            const double a1l = par ? vev[r] : (r > 0 ? vod[r > 0 ? r - 1 : 0] : nbL);
-            const double a1r = par ? (r < DPM_NPL - 1 ? vev[r < DPM_NPL - 1 ? r + 1 : 0] : nbR) : vod[r];
-            const bool on = d >= 0 && d < H && d <= k;
-            const bool own = pp >= own_lo && pp < own_hi;
-            double v = -RF_INF;
-            if (on && jj <= T.m && ii >= 0 && ii <= T.n) {
-                if (ii == 0 && jj == 0) {
-                    v = 0.0;
-                } else {
-                    const double ms = sb == tbb ? mtmm.x : mtmm.y;
-                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds.x;
-                    // align.jl:77-104: the maximum of the candidates
-                    v = fmax(fmax(a2 + ms, a1l + is), a1r + isds.y);
-                    eflag |= (own && v == -RF_INF) ? 1 : 0;   // "new score is invalid"
-                }
-                if (own && ii == T.n && jj == T.m && out_score)
-                    out_score[T.out_idx] = v;
-            }
-            if (own && on)
-                st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
-            nv[r] = v;
+            const int x = q * DPM_NPL + r;
+            const int ri = (x + P + 1) & (DPM_RING - 1), ci = (P + 127 - x) & (DPM_RING - 1);
+            tbb[r] = s_col[ci];
+            omt[r] = s_mtmm[ri];
+            ois[r] = s_isds[ri];
+            osb[r] = s_sb[ri];
         }
+        auto cells = [&](auto PARC, const dvec2 (&mt)[DPM_NPL], const dvec2 (&is2)[DPM_NPL], const int (&sbr)[DPM_NPL]) {
+            constexpr int par = decltype(PARC)::value;
+            const int k = 2 * P + par;
+            const size_t row = (size_t)(rev ? K - 1 - k : k) * T.P;
+            // the neighbouring pair's kappa - 1 value across the lane edge
+            const double nbL = par ? 0.0 : dpp_f64<TaskLanes<64>::FROM_L1>(vod[DPM_NPL - 1]);
+            const double nbR = par ? dpp_f64<TaskLanes<64>::FROM_R1>(vev[0]) : 0.0;
+            double nv[DPM_NPL];
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r) {
+                const int pp = pb + q * DPM_NPL + r;
+                const int d = 2 * pp + par;
+                const int jj = P - pp, ii = pp + P + par - T.c;
+                const double a2 = par ? vod[r] : vev[r];
+                const double a1l = par ? vev[r] : (r > 0 ? vod[r > 0 ? r - 1 : 0] : nbL);
+                const double a1r = par ? (r < DPM_NPL - 1 ? vev[r < DPM_NPL - 1 ? r + 1 : 0] : nbR) : vod[r];
+                const bool on = d >= 0 && d < H && d <= k;
+                const bool own = pp >= own_lo && pp < own_hi;
+                const bool valid = on && jj <= T.m && ii >= 0 && ii <= T.n;
+                const bool origin = ii == 0 && jj == 0;
+                const double ms = sbr[r] == tbb[r] ? mt[r].x : mt[r].y;
+                const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : is2[r].x;
+                // align.jl:77-104: the maximum of the candidates
+                const double best = fmax(fmax(a2 + ms, a1l + is), a1r + is2[r].y);
+                const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
+                eflag |= (own && valid && !origin && best == -RF_INF) ? 1 : 0;   // "new score is invalid"
+                if (own && on)
+                    st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
+                if (own && valid && ii == T.n && jj == T.m && out_score)
+                    out_score[T.out_idx] = v;
+                nv[r] = v;
+            }
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r) {
+                if (par)
+                    vod[r] = nv[r];
+                else
+                    vev[r] = nv[r];
+            }
+        };
+        cells(std::integral_constant<int, 0>{}, rmt, ris, rsb);
+        if (odd_too)
+            cells(std::integral_constant<int, 1>{}, omt, ois, osb);
 #pragma unroll
         for (int r = 0; r < DPM_NPL; ++r) {
-            if (par)
-                vod[r] = nv[r];
-            else
-                vev[r] = nv[r];
+            rmt[r] = omt[r];
+            ris[r] = ois[r];
+            rsb[r] = osb[r];
         }
     };
     for (int k = 0; k < K; k += 2) {
@@ -1593,9 +1622,7 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
             pend = blk_load(t + 3);
             wave_sync();
         }
-        step(std::integral_constant<int, 0>{}, k);
-        if (k + 1 < K)
-            step(std::integral_constant<int, 1>{}, k + 1);
+        period(k >> 1, k + 1 < K);
         const int kn = k + 2;                    // steps done
         if (kn % DPM_B == 0 && kn < K) {
             // ---- hand-off after block kn / DPM_B
