@@ -1460,10 +1460,21 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 //   - slices run on one XCD (workgroups at blockIdx multiples of 8).
 // Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical.
 // ---------------------------------------------------------------------
-constexpr int DPM_NPL = 2;                        // pairs per lane
-constexpr int DPM_B = 64;                         // anti-diagonals per hand-off
+#ifndef DPM_NPL_
+#define DPM_NPL_ 2
+#endif
+#ifndef DPM_B_
+#define DPM_B_ 64
+#endif
+// band stores: 0 write-through (sc1) 8-B stores; 1 plain stores and an
+// agent-scope release before the hand-off flag
+#ifndef DPM_ST
+#define DPM_ST 0
+#endif
+constexpr int DPM_NPL = DPM_NPL_;                 // pairs per lane
+constexpr int DPM_B = DPM_B_;                     // anti-diagonals per hand-off
 constexpr int DPM_OWN = 64 * DPM_NPL - DPM_B;     // pairs per slice
-constexpr int DPM_RING = 256;                     // staged rows / columns (4 blocks of 64)
+constexpr int DPM_RING = 512;                     // staged rows / columns (8 blocks of 64)
 constexpr int DPM_SPIN = 1 << 22;                 // flag polls before error 4
 
 __host__ __device__ constexpr int dpm_slices(int H) { return ((H + 1) / 2 + DPM_OWN - 1) / DPM_OWN; }
@@ -1508,9 +1519,10 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     __shared__ dvec2 s_mtmm[DPM_RING], s_isds[DPM_RING];
     __shared__ uint8_t s_sb[DPM_RING], s_col[DPM_RING];
     // pair pp = pb + x at period P reads read rows x + P + par + rbase and
-    // template column P + 127 - x + cbase: ring entries (x + P + par) and
-    // (P + 127 - x), blocks of 64 entries
+    // template column P + 64 DPM_NPL - 1 - x + cbase: ring entries
+    // (x + P + par) and (P + 64 DPM_NPL - 1 - x), blocks of 64 entries
     const int rbase = pb - T.c, cbase = -(pb + 64 * DPM_NPL - 1);
+    static_assert(64 * (DPM_NPL + 2) <= DPM_RING, "ring holds the chunk's blocks and the next");
     struct Blk {
         RowRec r;
         int col;
@@ -1530,9 +1542,10 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
         s_sb[i] = (uint8_t)x.r.sb;
         s_col[i] = (uint8_t)x.col;
     };
-    blk_put(0, blk_load(0));
-    blk_put(1, blk_load(1));
-    Blk pend = blk_load(2);
+    // a chunk of 64 periods reads blocks t .. t + DPM_NPL of its ring
+    for (int b = 0; b < DPM_NPL; ++b)
+        blk_put(b, blk_load(b));
+    Blk pend = blk_load(DPM_NPL);
     double vev[DPM_NPL], vod[DPM_NPL];
     // a pair's row record for its even step is the record its odd step read
     // one period earlier (read row pp + P - c either way): carried here
@@ -1558,7 +1571,7 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
 #pragma unroll
         for (int r = 0; r < DPM_NPL; ++r) {
             const int x = q * DPM_NPL + r;
-            const int ri = (x + P + 1) & (DPM_RING - 1), ci = (P + 127 - x) & (DPM_RING - 1);
+            const int ri = (x + P + 1) & (DPM_RING - 1), ci = (P + 64 * DPM_NPL - 1 - x) & (DPM_RING - 1);
             tbb[r] = s_col[ci];
             omt[r] = s_mtmm[ri];
             ois[r] = s_isds[ri];
@@ -1590,8 +1603,12 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
                 const double best = fmax(fmax(a2 + ms, a1l + is), a1r + is2[r].y);
                 const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
                 eflag |= (own && valid && !origin && best == -RF_INF) ? 1 : 0;   // "new score is invalid"
-                if (own && on)
-                    st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
+                if (own && on) {
+                    if (DPM_ST == 0)
+                        st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
+                    else
+                        band[row + ((rev ? H - 1 - d : d) >> 1)] = v;
+                }
                 if (own && valid && ii == T.n && jj == T.m && out_score)
                     out_score[T.out_idx] = v;
                 nv[r] = v;
@@ -1615,11 +1632,11 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
         }
     };
     for (int k = 0; k < K; k += 2) {
-        if ((k & 127) == 0) {                    // chunk t = k / 128: rows / columns of block t + 2
+        if ((k & 127) == 0) {                    // chunk t = k / 128: rows / columns of block t + DPM_NPL
             const int t = k >> 7;
             __builtin_amdgcn_s_waitcnt(0);
-            blk_put(t + 2, pend);
-            pend = blk_load(t + 3);
+            blk_put(t + DPM_NPL, pend);
+            pend = blk_load(t + DPM_NPL + 1);
             wave_sync();
         }
         period(k >> 1, k + 1 < K);
@@ -1627,6 +1644,8 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
         if (kn % DPM_B == 0 && kn < K) {
             // ---- hand-off after block kn / DPM_B
             const int b = kn / DPM_B;
+            if (DPM_ST == 1)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __builtin_amdgcn_s_waitcnt(0);       // this wave's band stores are out (sc1)
             if (q == 0)
                 __hip_atomic_store(flag + g, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
