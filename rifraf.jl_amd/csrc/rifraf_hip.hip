@@ -1680,6 +1680,10 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
                              ? ld_sc1(band + (size_t)(rev ? K - 1 - ko : ko) * T.P + ((rev ? H - 1 - dod : dod) >> 1))
                              : -RF_INF;
             }
+            // wait here, where nothing else is in flight: a value register
+            // still pending from these loads at the loop head would make
+            // hipcc wait vmcnt(0) -- every band store -- once per period
+            __builtin_amdgcn_s_waitcnt(0);
         }
     }
     if (eflag)
