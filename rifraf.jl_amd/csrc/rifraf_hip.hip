@@ -76,6 +76,13 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 #define DP_STORE(p, v) (*(p) = (v))
 #endif
 
+// block-wide wide-band fills (k_dp<1024>, k_dpw) with their value ring in
+// LDS meet at an LDS-only barrier per anti-diagonal; 1: __syncthreads
+// (rounds 4-5, which also drained every band store in flight)
+#ifndef DPW_FULLBAR
+#define DPW_FULLBAR 0
+#endif
+
 __host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
 // Row stride of a band as allocated: H >= pad_h (> 0) gives rows of a whole
 // number of 128-B lines, so that the wide-band scorer's 32-diagonal segments
@@ -315,8 +322,12 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
                 r0[d] = v;
             }
         }
-        if (BLOCK_SYNC)
+        // an LDS ring needs an LDS-only barrier (round 6: __syncthreads also
+        // drained the step's band stores); the global ring needs the full one
+        if (BLOCK_SYNC && (GRING || DPW_FULLBAR))
             __syncthreads();
+        else if (BLOCK_SYNC)
+            lds_barrier();
         else
             wave_sync();
     }
@@ -1411,7 +1422,13 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             else
                 vev[it] = v;
         }
-        __syncthreads();
+        // the value ring is in LDS: a barrier that waits for LDS only
+        // (round 6; __syncthreads also drained every band store of the step,
+        // vmcnt(0), once per anti-diagonal)
+        if (DPW_FULLBAR)
+            __syncthreads();
+        else
+            lds_barrier();
     };
     for (int k = 0; k < K; k += 2) {
         if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
@@ -1423,7 +1440,10 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
                 col_put(bcol(t), l, ncol);
                 ncol = col_load(bcol(t + 1), l);
             }
-            __syncthreads();
+            if (DPW_FULLBAR)
+                __syncthreads();
+            else
+                lds_barrier();
         }
         step(std::integral_constant<int, 0>{}, k);
         if (k + 1 < K)
