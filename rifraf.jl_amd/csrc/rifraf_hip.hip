@@ -1469,16 +1469,24 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 //   - the kappa-1 values of neighbouring diagonals move between lanes by DPP
 //     (wave_shr / wave_shl), within a lane in registers;
 //   - row records and template bases come from LDS rings, filled 64 rows /
-//     columns at a time one chunk of 64 periods ahead;
-//   - the slice's cells go to the band write-through (sc1 stores); at the
-//     end of a block of DPM_B anti-diagonals the wave waits for its stores
-//     (vmcnt(0)) and lane 0 publishes the block number (sc1 flag store); a
-//     wave polls its neighbours' flags (sc1 loads, bounded: error 4 rather
-//     than a hang) and reloads its halo pairs' last two values from the band
-//     (sc1 loads) -- the hand-off recipe of MI355X_MICROARCH.md
-//     (inter-workgroup visibility);
+//     columns at a time one chunk of 64 periods ahead; the rings carry a
+//     mirrored tail, so a lane's ring index is its constant plus the
+//     period's scalar one (no wrap per read);
+//   - a cell is a fixed sequence of selects: its validity is a per-lane
+//     range of periods, its store a buffer store whose offset is per-lane
+//     (lanes outside the slice or the band get an offset past the band and
+//     the range check drops the store), and the origin and the final score
+//     are scalar-branch steps;
+//   - hand-off through the band itself: the host fills each band with an
+//     all-ones pattern (a NaN no sum produces) before the launch; the slice
+//     stores every in-band cell it owns at every step (write-through, sc1)
+//     and a wave takes its halo pairs' last two values by polling those
+//     cells (sc1 loads, 64-bit single-copy atomic) until none holds the
+//     pattern -- one round trip, no flag and no store drain (bounded:
+//     error 4 rather than a hang);
 //   - slices run on one XCD (workgroups at blockIdx multiples of 8).
-// Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical.
+// Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical;
+// cells left of the DP (jj < 0) are stored as -Inf, which k_dpw leaves out.
 // ---------------------------------------------------------------------
 #ifndef DPM_NPL_
 #define DPM_NPL_ 2
@@ -1486,35 +1494,39 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 #ifndef DPM_B_
 #define DPM_B_ 64
 #endif
-// band stores: 0 write-through (sc1) 8-B stores; 1 plain stores and an
-// agent-scope release before the hand-off flag
-#ifndef DPM_ST
-#define DPM_ST 0
-#endif
 constexpr int DPM_NPL = DPM_NPL_;                 // pairs per lane
 constexpr int DPM_B = DPM_B_;                     // anti-diagonals per hand-off
 constexpr int DPM_OWN = 64 * DPM_NPL - DPM_B;     // pairs per slice
 constexpr int DPM_RING = 512;                     // staged rows / columns (8 blocks of 64)
-constexpr int DPM_SPIN = 1 << 22;                 // flag polls before error 4
+constexpr int DPM_RINGX = DPM_RING + 64 * DPM_NPL;   // + the mirrored tail
+constexpr int DPM_SPIN = 1 << 22;                 // polls before error 4
+constexpr unsigned DPM_NOSTORE = 0x80000000u;     // past every band (K * P * 8 < 2^31)
+constexpr long long DPM_UNSET = -1;               // the fill pattern of a band not yet stored
+constexpr int DPM_SC1 = 16;                       // buffer-store cache policy: sc1 (write-through)
+static_assert(DPM_OWN > 0 && (DPM_B / 2) % DPM_NPL == 0 && 128 % DPM_B == 0, "slice geometry");
 
 __host__ __device__ constexpr int dpm_slices(int H) { return ((H + 1) / 2 + DPM_OWN - 1) / DPM_OWN; }
-constexpr size_t DPM_MAX_SLICES = 2048;           // slices per launch (all resident at once)
+// Slices of one band spin on each other, so they must be resident together:
+// a task has at most DPM_TASK_SLICES (one XCD holds ~7 of these 22-KB
+// workgroups per CU, 32 CUs); workgroups dispatch in order, so the tasks of
+// a launch become resident one after another and DPM_MAX_SLICES only bounds
+// the grid.
+constexpr int DPM_TASK_SLICES = 160;
+constexpr size_t DPM_MAX_SLICES = 2048;
 
-__device__ __forceinline__ void st_sc1(double *p, double v)
-{
-    __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ double ld_sc1(const double *p)
 {
     return __longlong_as_double(
         (long long)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+template <bool TRIM>
 __global__ void __launch_bounds__(64)
 k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__restrict__ bases,
       const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
-      int *__restrict__ err, int *__restrict__ flags)
+      int *__restrict__ err)
 {
     if (blockIdx.x & 7)
         return;
@@ -1526,9 +1538,8 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     const int Gt = dpm_slices(T.H);
     if (g >= Gt)
         return;
-    int *flag = flags + (size_t)task * G;
     const int q = threadIdx.x;
-    const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
+    const bool rev = T.flags & 1, skew = T.flags & 2, trim = TRIM && (T.flags & 4);
     const uint8_t *sbase = bases + T.sb;
     const uint8_t *tbase = bases + T.tb;
     const double *tb = tabs + T.tab;
@@ -1536,32 +1547,68 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     const int K = T.klen, H = T.H;
     const int own_lo = g * DPM_OWN, own_hi = min(own_lo + DPM_OWN, npairs);
     const int pb = own_lo - DPM_B / 2;           // the pair of lane 0, r = 0
-    __shared__ dvec2 s_mtmm[DPM_RING], s_isds[DPM_RING];
-    __shared__ uint8_t s_sb[DPM_RING], s_col[DPM_RING];
-    // pair pp = pb + x at period P reads read rows x + P + par + rbase and
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc(band, 0, (int)((int64_t)K * T.P * 8), 0x00020000);
+    __shared__ dvec2 s_rec[2 * DPM_RINGX];      // {mt, mm}, {is, ds} per read row
+    __shared__ uint8_t s_sb[DPM_RINGX], s_col[DPM_RINGX];
+    // pair pp = pb + x at period P reads read row x + P + par + rbase and
     // template column P + 64 DPM_NPL - 1 - x + cbase: ring entries
     // (x + P + par) and (P + 64 DPM_NPL - 1 - x), blocks of 64 entries
     const int rbase = pb - T.c, cbase = -(pb + 64 * DPM_NPL - 1);
     static_assert(64 * (DPM_NPL + 2) <= DPM_RING, "ring holds the chunk's blocks and the next");
+    // a block's loads are held raw until it is put in LDS a chunk later (a
+    // select right after them would make hipcc wait for them at once; k_dpx)
     struct Blk {
-        RowRec r;
+        RawRow r;
         int col;
+        bool colok;
     };
     auto blk_load = [&](int b) {
         Blk x;
-        x.r = load_row_flat(T, rev, sbase, tb, rbase + 64 * b + q, false);
-        if (skew)
-            x.r.mm *= 0.99;
-        x.col = load_col_flat(T, rev, tbase, cbase + 64 * b + q);
+        x.r = load_row_raw(T, rev, sbase, tb, rbase + 64 * b + q, false);
+        const int jj = cbase + 64 * b + q;
+        const int jc = min(max(jj, 1), max(T.m, 1));
+        x.col = tbase[rev ? max(T.m - jc, 0) : jc - 1];
+        x.colok = jj >= 1 && jj <= T.m;
         return x;
     };
     auto blk_put = [&](int b, const Blk &x) {
-        const int i = (64 * b + q) & (DPM_RING - 1);
-        s_mtmm[i] = dvec2{x.r.mt, x.r.mm};
-        s_isds[i] = dvec2{x.r.is, x.r.ds};
-        s_sb[i] = (uint8_t)x.r.sb;
-        s_col[i] = (uint8_t)x.col;
+        const RowRec rr = row_val(x.r);
+        const dvec2 m2{rr.mt, skew ? rr.mm * 0.99 : rr.mm}, i2{rr.is, rr.ds};
+        const int i = ((64 * b) & (DPM_RING - 1)) + q;
+        s_rec[2 * i] = m2;
+        s_rec[2 * i + 1] = i2;
+        s_sb[i] = (uint8_t)rr.sb;
+        s_col[i] = (uint8_t)(x.colok ? x.col : 4);
+        if (i < DPM_RINGX - DPM_RING) {          // the mirrored tail
+            s_rec[2 * (i + DPM_RING)] = m2;
+            s_rec[2 * (i + DPM_RING) + 1] = i2;
+            s_sb[i + DPM_RING] = (uint8_t)rr.sb;
+            s_col[i + DPM_RING] = (uint8_t)(x.colok ? x.col : 4);
+        }
     };
+    // per pair and parity: the periods at which the cell is in the DP
+    // (d <= k, jj <= m, 0 <= ii <= n: P in [lo, lo + span]), the store offset
+    int lo[2][DPM_NPL];
+    unsigned span[2][DPM_NPL], vo[2][DPM_NPL];
+    bool own[DPM_NPL];
+#pragma unroll
+    for (int r = 0; r < DPM_NPL; ++r) {
+        const int pp = pb + q * DPM_NPL + r;
+        own[r] = pp >= own_lo && pp < own_hi;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int d = 2 * pp + a;
+            const bool inb = pp >= 0 && d < H;
+            const int l = max(pp, T.c - pp - a), h = min(pp + T.m, T.n + T.c - pp - a);
+            const bool ok = inb && l <= h;
+            lo[a][r] = ok ? l : (1 << 30);
+            span[a][r] = ok ? (unsigned)(h - l) : 0u;
+            vo[a][r] = (inb && own[r]) ? 8u * (unsigned)((rev ? H - 1 - d : d) >> 1) : DPM_NOSTORE;
+        }
+    }
+    const int porg = T.c >> 1;                       // the origin (ii = jj = 0): pair c / 2, step c
+    const int kfin = T.n + T.m + T.c;                // the final cell (ii = n, jj = m)
     // a chunk of 64 periods reads blocks t .. t + DPM_NPL of its ring
     for (int b = 0; b < DPM_NPL; ++b)
         blk_put(b, blk_load(b));
@@ -1571,74 +1618,81 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     // one period earlier (read row pp + P - c either way): carried here
     dvec2 rmt[DPM_NPL], ris[DPM_NPL];
     int rsb[DPM_NPL];
+    uint64_t bad[DPM_NPL];                       // lanes with a valid cell of -Inf
 #pragma unroll
     for (int r = 0; r < DPM_NPL; ++r) {
         vev[r] = vod[r] = -RF_INF;
-        const int ri = (q * DPM_NPL + r) & (DPM_RING - 1);
-        rmt[r] = s_mtmm[ri];
-        ris[r] = s_isds[ri];
+        bad[r] = 0;
+        const int ri = q * DPM_NPL + r;
+        rmt[r] = s_rec[2 * ri];
+        ris[r] = s_rec[2 * ri + 1];
         rsb[r] = s_sb[ri];
     }
-    int eflag = 0;
-    // one period P: the even step 2P and the odd step 2P + 1.  The LDS reads
-    // of both (the period's template bases, the odd step's row records) are
-    // issued first; the cells are branch-free selects, only the band stores
-    // and the final score are conditional.
-    auto period = [&](const int P, const bool odd_too) {
+    // one period P: the even step 2P and the odd step 2P + 1 (band rows at
+    // byte offsets so and so + dso).  The LDS reads of both (the period's
+    // template bases, the odd step's row records) are issued first.  EDGE:
+    // the period holds the origin or the final cell.
+    auto period = [&](auto EDGEC, const int P, const bool odd_too, const unsigned so0, const unsigned dso) {
+        constexpr bool EDGE = decltype(EDGEC)::value;
+        const int s = P & (DPM_RING - 1);
+        const int ir = q * DPM_NPL + 1 + s, ic = s + 64 * DPM_NPL - 1 - q * DPM_NPL;
         int tbb[DPM_NPL];
         dvec2 omt[DPM_NPL], ois[DPM_NPL];
         int osb[DPM_NPL];
 #pragma unroll
         for (int r = 0; r < DPM_NPL; ++r) {
-            const int x = q * DPM_NPL + r;
-            const int ri = (x + P + 1) & (DPM_RING - 1), ci = (P + 64 * DPM_NPL - 1 - x) & (DPM_RING - 1);
-            tbb[r] = s_col[ci];
-            omt[r] = s_mtmm[ri];
-            ois[r] = s_isds[ri];
-            osb[r] = s_sb[ri];
+            tbb[r] = s_col[ic - r];
+            omt[r] = s_rec[2 * (ir + r)];
+            ois[r] = s_rec[2 * (ir + r) + 1];
+            osb[r] = s_sb[ir + r];
         }
         auto cells = [&](auto PARC, const dvec2 (&mt)[DPM_NPL], const dvec2 (&is2)[DPM_NPL], const int (&sbr)[DPM_NPL]) {
             constexpr int par = decltype(PARC)::value;
             const int k = 2 * P + par;
-            const size_t row = (size_t)(rev ? K - 1 - k : k) * T.P;
+            const unsigned so = par ? so0 + dso : so0;
             // the neighbouring pair's kappa - 1 value across the lane edge
-            const double nbL = par ? 0.0 : dpp_f64<TaskLanes<64>::FROM_L1>(vod[DPM_NPL - 1]);
-            const double nbR = par ? dpp_f64<TaskLanes<64>::FROM_R1>(vev[0]) : 0.0;
+            // (lanes 0 and 63 hold halo pairs or pairs outside the band: what
+            // they receive there is never a slice's value)
+            const double nbL = par ? 0.0 : dpp_rot_f64<TaskLanes<64>::FROM_L1>(vod[DPM_NPL - 1]);
+            const double nbR = par ? dpp_rot_f64<TaskLanes<64>::FROM_R1>(vev[0]) : 0.0;
             double nv[DPM_NPL];
+            bool val[DPM_NPL];
 #pragma unroll
             for (int r = 0; r < DPM_NPL; ++r) {
-                const int pp = pb + q * DPM_NPL + r;
-                const int d = 2 * pp + par;
-                const int jj = P - pp, ii = pp + P + par - T.c;
                 const double a2 = par ? vod[r] : vev[r];
                 const double a1l = par ? vev[r] : (r > 0 ? vod[r > 0 ? r - 1 : 0] : nbL);
                 const double a1r = par ? (r < DPM_NPL - 1 ? vev[r < DPM_NPL - 1 ? r + 1 : 0] : nbR) : vod[r];
-                const bool on = d >= 0 && d < H && d <= k;
-                const bool own = pp >= own_lo && pp < own_hi;
-                const bool valid = on && jj <= T.m && ii >= 0 && ii <= T.n;
-                const bool origin = ii == 0 && jj == 0;
                 const double ms = sbr[r] == tbb[r] ? mt[r].x : mt[r].y;
-                const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : is2[r].x;
+                double is = is2[r].x;
+                if (TRIM) {
+                    const int jj = P - (pb + q * DPM_NPL + r);
+                    is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : is;
+                }
                 // align.jl:77-104: the maximum of the candidates
                 const double best = fmax(fmax(a2 + ms, a1l + is), a1r + is2[r].y);
-                const double v = valid ? (origin ? 0.0 : best) : -RF_INF;
-                eflag |= (own && valid && !origin && best == -RF_INF) ? 1 : 0;   // "new score is invalid"
-                if (own && on) {
-                    if (DPM_ST == 0)
-                        st_sc1(band + row + ((rev ? H - 1 - d : d) >> 1), v);
-                    else
-                        band[row + ((rev ? H - 1 - d : d) >> 1)] = v;
-                }
-                if (own && valid && ii == T.n && jj == T.m && out_score)
-                    out_score[T.out_idx] = v;
-                nv[r] = v;
+                val[r] = (unsigned)(P - lo[par][r]) <= span[par][r];
+                nv[r] = val[r] ? best : -RF_INF;
+            }
+            if (EDGE && k == T.c) {
+#pragma unroll
+                for (int r = 0; r < DPM_NPL; ++r)
+                    nv[r] = (pb + q * DPM_NPL + r == porg && val[r]) ? 0.0 : nv[r];
             }
 #pragma unroll
             for (int r = 0; r < DPM_NPL; ++r) {
+                bad[r] |= __builtin_amdgcn_ballot_w64(val[r] && nv[r] == -RF_INF);   // "new score is invalid"
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, nv[r]), brs, vo[par][r], so,
+                                                      DPM_SC1);
                 if (par)
                     vod[r] = nv[r];
                 else
                     vev[r] = nv[r];
+            }
+            if (EDGE && k == kfin && out_score) {
+#pragma unroll
+                for (int r = 0; r < DPM_NPL; ++r)
+                    if (own[r] && val[r] && pb + q * DPM_NPL + r == P - T.m)
+                        out_score[T.out_idx] = nv[r];
             }
         };
         cells(std::integral_constant<int, 0>{}, rmt, ris, rsb);
@@ -1651,62 +1705,77 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
             rsb[r] = osb[r];
         }
     };
-    for (int k = 0; k < K; k += 2) {
+    const int pfin = kfin >> 1;
+    const unsigned dso = 8u * (unsigned)(rev ? -T.P : T.P);   // band row step in bytes
+    unsigned so = 8u * (unsigned)((rev ? K - 1 : 0) * T.P);
+    for (int k = 0; k < K; k += 2, so += 2 * dso) {
         if ((k & 127) == 0) {                    // chunk t = k / 128: rows / columns of block t + DPM_NPL
             const int t = k >> 7;
-            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_s_waitcnt(0);       // after a hand-off: nothing left in flight
             blk_put(t + DPM_NPL, pend);
             pend = blk_load(t + DPM_NPL + 1);
             wave_sync();
         }
-        period(k >> 1, k + 1 < K);
+        const int P = k >> 1;
+        if (P == porg || P == pfin)
+            period(std::true_type{}, P, k + 1 < K, so, dso);
+        else
+            period(std::false_type{}, P, k + 1 < K, so, dso);
         const int kn = k + 2;                    // steps done
         if (kn % DPM_B == 0 && kn < K) {
-            // ---- hand-off after block kn / DPM_B
-            const int b = kn / DPM_B;
-            if (DPM_ST == 1)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __builtin_amdgcn_s_waitcnt(0);       // this wave's band stores are out (sc1)
-            if (q == 0)
-                __hip_atomic_store(flag + g, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool ok = true;
-            for (int nbg = g - 1; nbg <= g + 1; nbg += 2) {
-                if (nbg < 0 || nbg >= Gt)
-                    continue;
-                int spins = 0;
-                while (__hip_atomic_load(flag + nbg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < b) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins >= DPM_SPIN) {
-                        ok = false;
-                        break;
-                    }
-                }
-            }
-            if (!ok) {
-                set_err(err, 4);   // a neighbouring slice never arrived
-                return;
-            }
-            // halo pairs: the last even (kn - 2) and odd (kn - 1) values from the band
+            // ---- hand-off: the halo pairs' values at steps kn - 2 (even
+            // diagonal) and kn - 1 (odd), polled from their owners' cells
+            const double *re = band + (size_t)(rev ? K - 1 - (kn - 2) : kn - 2) * T.P;
+            const double *ro = band + (size_t)(rev ? K - 1 - (kn - 1) : kn - 1) * T.P;
+            bool pe[DPM_NPL], po[DPM_NPL];
+            const double *ae[DPM_NPL], *ao[DPM_NPL];
 #pragma unroll
             for (int r = 0; r < DPM_NPL; ++r) {
-                const int pp = pb + q * DPM_NPL + r;
-                if (pp >= own_lo && pp < own_hi)
-                    continue;
-                const int de = 2 * pp, dod = 2 * pp + 1, ke = kn - 2, ko = kn - 1;
-                vev[r] = (pp >= 0 && de < H && de <= ke)
-                             ? ld_sc1(band + (size_t)(rev ? K - 1 - ke : ke) * T.P + ((rev ? H - 1 - de : de) >> 1))
-                             : -RF_INF;
-                vod[r] = (pp >= 0 && dod < H && dod <= ko)
-                             ? ld_sc1(band + (size_t)(rev ? K - 1 - ko : ko) * T.P + ((rev ? H - 1 - dod : dod) >> 1))
-                             : -RF_INF;
+                const int pp = pb + q * DPM_NPL + r, de = 2 * pp, dod = 2 * pp + 1;
+                pe[r] = !own[r] && pp >= 0 && de < H;
+                po[r] = !own[r] && pp >= 0 && dod < H;
+                ae[r] = re + (pe[r] ? (rev ? H - 1 - de : de) >> 1 : 0);
+                ao[r] = ro + (po[r] ? (rev ? H - 1 - dod : dod) >> 1 : 0);
             }
-            // wait here, where nothing else is in flight: a value register
-            // still pending from these loads at the loop head would make
-            // hipcc wait vmcnt(0) -- every band store -- once per period
+            double he[DPM_NPL], ho[DPM_NPL];
+            for (int spins = 0;; ++spins) {
+#pragma unroll
+                for (int r = 0; r < DPM_NPL; ++r) {
+                    he[r] = ld_sc1(ae[r]);
+                    ho[r] = ld_sc1(ao[r]);
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                int wait = 0;
+#pragma unroll
+                for (int r = 0; r < DPM_NPL; ++r)
+                    wait |= ((int)pe[r] & (int)(__double_as_longlong(he[r]) == DPM_UNSET)) |
+                            ((int)po[r] & (int)(__double_as_longlong(ho[r]) == DPM_UNSET));
+                if (__builtin_amdgcn_ballot_w64(wait != 0) == 0)
+                    break;
+                if (spins >= DPM_SPIN) {
+                    set_err(err, 4);   // a neighbouring slice never arrived
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r) {
+                if (own[r])
+                    continue;
+                vev[r] = pe[r] ? he[r] : -RF_INF;
+                vod[r] = po[r] ? ho[r] : -RF_INF;
+            }
+            // nothing of the hand-off left in flight: a register still
+            // pending at the loop head would make hipcc wait vmcnt(0) -- every
+            // band store -- once per period
             __builtin_amdgcn_s_waitcnt(0);
         }
     }
-    if (eflag)
+    bool e = false;
+#pragma unroll
+    for (int r = 0; r < DPM_NPL; ++r)
+        e = e || (own[r] && ((bad[r] >> q) & 1));
+    if (e)
         set_err(err, 1);
 }
 
@@ -1750,7 +1819,6 @@ struct DpxStage {
     bool colok;
 };
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned DPX_NOSTORE = 0x80000000u;   // buffer offset past any band: the store is dropped
 // a k_dpx task: H <= 127 (lanes hold diagonal pairs) and a band below 2 GiB
 // (32-bit buffer offsets, DPX_NOSTORE past it)
@@ -4618,7 +4686,7 @@ struct rf_ctx {
     // a plan validated at the current epoch with the same job / slot list
     // needs no per-slot validation again
     uint64_t state_epoch = 1;
-    DevBuf scratch[29];
+    DevBuf scratch[28];
     // pinned host staging for sequence uploads (pageable H2D copies of a few
     // MB took ~14 ms per cluster upload on the box: page locking per call)
     void *pinned = nullptr;
@@ -6001,7 +6069,8 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 else if (t.H <= 2040) {
                     c64.push_back(t);
                     hmax64 = std::max(hmax64, t.H);
-                } else if (S.ncins == 0 && S.ncdel == 0 && ctx->opt.dp_mc) {
+                } else if (S.ncins == 0 && S.ncdel == 0 && ctx->opt.dp_mc && dpm_slices(t.H) <= DPM_TASK_SLICES &&
+                           (int64_t)t.klen * t.P * 8 < ((int64_t)1 << 31)) {
                     cwm.push_back(t);   // k_dpm: across CUs, no codon moves (edit_distance's band)
                     gm = std::max(gm, dpm_slices(t.H));
                 } else if (S.ncins == 0 && S.ncdel == 0 && t.H <= DPW_MAXH) {
@@ -6045,9 +6114,9 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 cp[a][pmi].insert(cp[a][pmi].end(), cr[a][1].begin(), cr[a][1].end());
                 cr[a][1].clear();
             }
-        // k_dpm's slices spin on each other: every workgroup of a launch must
-        // be resident at once, so large sets of very wide bands take the
-        // one-workgroup kernels
+        // k_dpm's slices spin on each other (one task's slices resident
+        // together, DPM_TASK_SLICES); a very large set of very wide bands
+        // takes the one-workgroup kernels
         if (cwm.size() * (size_t)gm > DPM_MAX_SLICES) {
             for (const DPTask &t : cwm)
                 if (t.H <= DPW_MAXH) {
@@ -6192,10 +6261,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (int e = ensure_buf(ctx, ctx->scratch[10], P.ng * 4 * (size_t)(P.hmaxg + 6) * 8))
             return e;
     }
-    if (P.nwm) {
-        if (int e = ensure_buf(ctx, ctx->scratch[28], P.nwm * (size_t)P.gm * sizeof(int)))
-            return e;
-    }
     // The latency-bound classes (few long tasks: k_dpx, k_dp) go first, on
     // the main stream: the others run beside them on the side streams, which
     // may share hardware queues with each other (round 5: the reference's
@@ -6280,10 +6345,16 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
         } else if (L.kind == 11) {
             // H > 2040 without codon moves across CUs (k_dpm): 8 workgroups per
-            // slice (one works: one XCD), hand-off flags zeroed first
-            HIPCHK(ctx, hipMemsetAsync(ctx->scratch[28].p, 0, (size_t)n * P.gm * sizeof(int), st));
-            hipLaunchKernelGGL(k_dpm, dim3((unsigned)(8 * n * P.gm)), dim3(64), 0, st, d_tasks + L.at, n, P.gm, d_bases,
-                               d_tabs, d_bands, d_out, ctx->d_err, (int *)ctx->scratch[28].p);
+            // slice (one works: one XCD); each band filled with the not-yet-
+            // stored pattern first (the slices poll their halo cells for it)
+            bool trim = false;
+            for (int i = 0; i < n; ++i) {
+                const DPTask &t = P.tasks[L.at + i];
+                trim = trim || (t.flags & 4);
+                HIPCHK(ctx, hipMemsetAsync(d_bands + t.band, 0xFF, (size_t)t.klen * t.P * 8, st));
+            }
+            hipLaunchKernelGGL(trim ? k_dpm<true> : k_dpm<false>, dim3((unsigned)(8 * n * P.gm)), dim3(64), 0, st,
+                               d_tasks + L.at, n, P.gm, d_bases, d_tabs, d_bands, d_out, ctx->d_err);
         } else if (L.kind == 10) {
             // H > 2040 without codon moves: staged rows (k_dpw), a three-row value ring
             const int ld = P.hmaxw + 4;
