@@ -1609,31 +1609,71 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
     }
     const int porg = T.c >> 1;                       // the origin (ii = jj = 0): pair c / 2, step c
     const int kfin = T.n + T.m + T.c;                // the final cell (ii = n, jj = m)
-    // a chunk of 64 periods reads blocks t .. t + DPM_NPL of its ring
-    for (int b = 0; b < DPM_NPL; ++b)
-        blk_put(b, blk_load(b));
-    Blk pend = blk_load(DPM_NPL);
+    // the wave's compute phase [Pa, Pb]: every pair it holds (slice and halo)
+    // is outside the DP before Pa and after Pb, i.e. -Inf there -- those
+    // periods are stores of -Inf only (for configs[2]'s band, the ~2,600 of
+    // 7,826 anti-diagonals before the origin and after the final cell)
+    int la = 1 << 30, hb = -1;
+#pragma unroll
+    for (int r = 0; r < DPM_NPL; ++r)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+            if (lo[a][r] != (1 << 30)) {
+                la = min(la, lo[a][r]);
+                hb = max(hb, lo[a][r] + (int)span[a][r]);
+            }
+    for (int o = 32; o > 0; o >>= 1) {
+        la = min(la, __shfl_xor(la, o));
+        hb = max(hb, __shfl_xor(hb, o));
+    }
+    const int Pa = __builtin_amdgcn_readfirstlane(la), Pb = __builtin_amdgcn_readfirstlane(hb);
+    const int NPER = (K + 1) >> 1;                   // periods: steps 2P, 2P + 1 < K
+    const unsigned dso = 8u * (unsigned)(rev ? -T.P : T.P);   // band row step in bytes
+    const unsigned so_base = 8u * (unsigned)((rev ? K - 1 : 0) * T.P);
+    auto so_of = [&](int P) { return so_base + (unsigned)(2 * P) * dso; };
+    // a period outside the compute phase: -Inf in every in-band cell the slice owns
+    auto blank = [&](int P) {
+        const unsigned so0 = so_of(P);
+#pragma unroll
+        for (int r = 0; r < DPM_NPL; ++r) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, -RF_INF), brs, vo[0][r], so0, DPM_SC1);
+            if (2 * P + 1 < K)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, -RF_INF), brs, vo[1][r], so0 + dso,
+                                                      DPM_SC1);
+        }
+    };
     double vev[DPM_NPL], vod[DPM_NPL];
     // a pair's row record for its even step is the record its odd step read
     // one period earlier (read row pp + P - c either way): carried here
     dvec2 rmt[DPM_NPL], ris[DPM_NPL];
     int rsb[DPM_NPL];
     uint64_t bad[DPM_NPL];                       // lanes with a valid cell of -Inf
+    Blk pend;
+    if (Pa <= Pb) {
+        // chunk t0 of Pa: blocks t0 .. t0 + DPM_NPL in the ring, t0 + DPM_NPL + 1 loading
+        const int t0 = Pa >> 6;
+        for (int b = t0; b <= t0 + DPM_NPL; ++b)
+            blk_put(b, blk_load(b));
+        pend = blk_load(t0 + DPM_NPL + 1);
+        wave_sync();
+    }
 #pragma unroll
     for (int r = 0; r < DPM_NPL; ++r) {
         vev[r] = vod[r] = -RF_INF;
         bad[r] = 0;
-        const int ri = q * DPM_NPL + r;
+        const int ri = q * DPM_NPL + r + (Pa & (DPM_RING - 1));
         rmt[r] = s_rec[2 * ri];
         ris[r] = s_rec[2 * ri + 1];
         rsb[r] = s_sb[ri];
     }
-    // one period P: the even step 2P and the odd step 2P + 1 (band rows at
-    // byte offsets so and so + dso).  The LDS reads of both (the period's
-    // template bases, the odd step's row records) are issued first.  EDGE:
-    // the period holds the origin or the final cell.
-    auto period = [&](auto EDGEC, const int P, const bool odd_too, const unsigned so0, const unsigned dso) {
+    // one period P of the compute phase: the even step 2P and the odd step
+    // 2P + 1.  The LDS reads of both (the period's template bases, the odd
+    // step's row records) are issued first.  EDGE: the period may hold the
+    // origin, the final cell or no odd step (K odd).
+    auto period = [&](auto EDGEC, const int P) {
         constexpr bool EDGE = decltype(EDGEC)::value;
+        const bool odd_too = !EDGE || 2 * P + 1 < K;
+        const unsigned so0 = so_of(P);
         const int s = P & (DPM_RING - 1);
         const int ir = q * DPM_NPL + 1 + s, ic = s + 64 * DPM_NPL - 1 - q * DPM_NPL;
         int tbb[DPM_NPL];
@@ -1680,7 +1720,8 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
             }
 #pragma unroll
             for (int r = 0; r < DPM_NPL; ++r) {
-                bad[r] |= __builtin_amdgcn_ballot_w64(val[r] && nv[r] == -RF_INF);   // "new score is invalid"
+                // "new score is invalid"
+                bad[r] |= __builtin_amdgcn_ballot_w64(nv[r] == -RF_INF) & __builtin_amdgcn_ballot_w64(val[r]);
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, nv[r]), brs, vo[par][r], so,
                                                       DPM_SC1);
                 if (par)
@@ -1705,72 +1746,90 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
             rsb[r] = osb[r];
         }
     };
-    const int pfin = kfin >> 1;
-    const unsigned dso = 8u * (unsigned)(rev ? -T.P : T.P);   // band row step in bytes
-    unsigned so = 8u * (unsigned)((rev ? K - 1 : 0) * T.P);
-    for (int k = 0; k < K; k += 2, so += 2 * dso) {
-        if ((k & 127) == 0) {                    // chunk t = k / 128: rows / columns of block t + DPM_NPL
-            const int t = k >> 7;
+    // ---- hand-off after period P: the halo pairs' values at steps 2P (even
+    // diagonal) and 2P + 1 (odd), polled from their owners' cells where the
+    // cell is in the DP (an owner computes every such cell; -Inf elsewhere)
+    auto hand_off = [&](const int P) {
+        const unsigned so0 = so_of(P);
+        bool pe[DPM_NPL], po[DPM_NPL];
+        const double *ae[DPM_NPL], *ao[DPM_NPL];
+#pragma unroll
+        for (int r = 0; r < DPM_NPL; ++r) {
+            pe[r] = !own[r] && (unsigned)(P - lo[0][r]) <= span[0][r];
+            po[r] = !own[r] && (unsigned)(P - lo[1][r]) <= span[1][r];
+            const int pp = pb + q * DPM_NPL + r, de = 2 * pp, dod = 2 * pp + 1;
+            ae[r] = band + (pe[r] ? (so0 >> 3) + ((rev ? H - 1 - de : de) >> 1) : 0);
+            ao[r] = band + (po[r] ? ((so0 + dso) >> 3) + ((rev ? H - 1 - dod : dod) >> 1) : 0);
+        }
+        double he[DPM_NPL], ho[DPM_NPL];
+        for (int spins = 0;; ++spins) {
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r) {
+                he[r] = ld_sc1(ae[r]);
+                ho[r] = ld_sc1(ao[r]);
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            int wait = 0;
+#pragma unroll
+            for (int r = 0; r < DPM_NPL; ++r)
+                wait |= ((int)pe[r] & (int)(__double_as_longlong(he[r]) == DPM_UNSET)) |
+                        ((int)po[r] & (int)(__double_as_longlong(ho[r]) == DPM_UNSET));
+            if (__builtin_amdgcn_ballot_w64(wait != 0) == 0)
+                break;
+            if (spins >= DPM_SPIN)
+                return false;   // a neighbouring slice never arrived
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int r = 0; r < DPM_NPL; ++r) {
+            if (own[r])
+                continue;
+            vev[r] = pe[r] ? he[r] : -RF_INF;
+            vod[r] = po[r] ? ho[r] : -RF_INF;
+        }
+        // nothing of the hand-off left in flight: a register still pending at
+        // the loop head would make hipcc wait vmcnt(0) -- every band store --
+        // once per period
+        __builtin_amdgcn_s_waitcnt(0);
+        return true;
+    };
+    // chunk refill at P = 64 t (t > t0), the period, the hand-off every DPM_B steps
+    auto body = [&](auto EDGEC, const int P) {
+        if ((P & 63) == 0 && P != Pa) {          // chunk t: rows / columns of block t + DPM_NPL
+            const int t = P >> 6;
             __builtin_amdgcn_s_waitcnt(0);       // after a hand-off: nothing left in flight
             blk_put(t + DPM_NPL, pend);
             pend = blk_load(t + DPM_NPL + 1);
             wave_sync();
         }
-        const int P = k >> 1;
-        if (P == porg || P == pfin)
-            period(std::true_type{}, P, k + 1 < K, so, dso);
-        else
-            period(std::false_type{}, P, k + 1 < K, so, dso);
-        const int kn = k + 2;                    // steps done
-        if (kn % DPM_B == 0 && kn < K) {
-            // ---- hand-off: the halo pairs' values at steps kn - 2 (even
-            // diagonal) and kn - 1 (odd), polled from their owners' cells
-            const double *re = band + (size_t)(rev ? K - 1 - (kn - 2) : kn - 2) * T.P;
-            const double *ro = band + (size_t)(rev ? K - 1 - (kn - 1) : kn - 1) * T.P;
-            bool pe[DPM_NPL], po[DPM_NPL];
-            const double *ae[DPM_NPL], *ao[DPM_NPL];
-#pragma unroll
-            for (int r = 0; r < DPM_NPL; ++r) {
-                const int pp = pb + q * DPM_NPL + r, de = 2 * pp, dod = 2 * pp + 1;
-                pe[r] = !own[r] && pp >= 0 && de < H;
-                po[r] = !own[r] && pp >= 0 && dod < H;
-                ae[r] = re + (pe[r] ? (rev ? H - 1 - de : de) >> 1 : 0);
-                ao[r] = ro + (po[r] ? (rev ? H - 1 - dod : dod) >> 1 : 0);
-            }
-            double he[DPM_NPL], ho[DPM_NPL];
-            for (int spins = 0;; ++spins) {
-#pragma unroll
-                for (int r = 0; r < DPM_NPL; ++r) {
-                    he[r] = ld_sc1(ae[r]);
-                    ho[r] = ld_sc1(ao[r]);
-                }
-                __builtin_amdgcn_s_waitcnt(0);
-                int wait = 0;
-#pragma unroll
-                for (int r = 0; r < DPM_NPL; ++r)
-                    wait |= ((int)pe[r] & (int)(__double_as_longlong(he[r]) == DPM_UNSET)) |
-                            ((int)po[r] & (int)(__double_as_longlong(ho[r]) == DPM_UNSET));
-                if (__builtin_amdgcn_ballot_w64(wait != 0) == 0)
-                    break;
-                if (spins >= DPM_SPIN) {
-                    set_err(err, 4);   // a neighbouring slice never arrived
-                    return;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-#pragma unroll
-            for (int r = 0; r < DPM_NPL; ++r) {
-                if (own[r])
-                    continue;
-                vev[r] = pe[r] ? he[r] : -RF_INF;
-                vod[r] = po[r] ? ho[r] : -RF_INF;
-            }
-            // nothing of the hand-off left in flight: a register still
-            // pending at the loop head would make hipcc wait vmcnt(0) -- every
-            // band store -- once per period
-            __builtin_amdgcn_s_waitcnt(0);
+        period(EDGEC, P);
+        const int kn = 2 * P + 2;                // steps done
+        return !(kn % DPM_B == 0 && P < Pb) || hand_off(P);
+    };
+    // the compute phase first (its hand-offs pace the neighbours), in runs of
+    // plain periods between the special ones
+    const int psp[3] = {porg, kfin >> 1, (K & 1) ? NPER - 1 : INT_MAX};
+    bool ok = true;
+    for (int P = Pa; P <= Pb && ok;) {
+        int stop = Pb + 1;
+        for (int i = 0; i < 3; ++i)
+            if (psp[i] >= P && psp[i] < stop)
+                stop = psp[i];
+        for (; P < stop && ok; ++P)
+            ok = body(std::false_type{}, P);
+        if (P <= Pb && ok) {
+            ok = body(std::true_type{}, P);
+            ++P;
         }
     }
+    if (!ok) {
+        set_err(err, 4);
+        return;
+    }
+    for (int P = 0; P < min(Pa, NPER); ++P)
+        blank(P);
+    for (int P = max(Pb + 1, Pa <= Pb ? 0 : NPER); P < NPER; ++P)
+        blank(P);
     bool e = false;
 #pragma unroll
     for (int r = 0; r < DPM_NPL; ++r)
