@@ -1488,11 +1488,14 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 // Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical;
 // cells left of the DP (jj < 0) are stored as -Inf, which k_dpw leaves out.
 // ---------------------------------------------------------------------
+// geometry (profiles/r06p_exp_dpm.out, configs[2]'s band, ms per call):
+// 1 pair per lane, hand-off every 32 steps 0.745; every 16 0.822; 2 pairs
+// per lane, every 32 1.064, every 64 0.984 (k_dpw: 3.35)
 #ifndef DPM_NPL_
-#define DPM_NPL_ 2
+#define DPM_NPL_ 1
 #endif
 #ifndef DPM_B_
-#define DPM_B_ 64
+#define DPM_B_ 32
 #endif
 constexpr int DPM_NPL = DPM_NPL_;                 // pairs per lane
 constexpr int DPM_B = DPM_B_;                     // anti-diagonals per hand-off
