@@ -135,9 +135,8 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    stores); 0: the class maximum                */
 #define RF_OPT_DP_MC       30   /* 1 (default): bands of H > 2040 without codon
                                    moves (edit_distance's) filled across CUs in
-                                   slices that hand off every 64 anti-diagonals
-                                   (k_dpm); 0: one workgroup per band (k_dpw /
-                                   k_dp)                                        */
+                                   slices that hand off every 32 anti-diagonals
+                                   (k_dpm); 0: one workgroup per band (k_dp)    */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

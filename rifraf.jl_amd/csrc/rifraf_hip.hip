@@ -8,7 +8,8 @@
 //               src/align.jl:50-112 (update), :114-179, :196-202
 //   k_dpx       the same fill for a few long tasks (H <= 127), one
 //               latency-bound task per wave (the reference's codon DP)
-//   k_dpw / k_dp  very wide bands (edit_distance, align.jl:253-260)
+//   k_dpm / k_dp  very wide bands (edit_distance, align.jl:253-260): band
+//               slices across the CUs of an XCD / one block per band
 //   k_score_ws / k_score_segl / k_score
 //               dense per-position proposal scoring of every batch read,
 //               left-folded over the batch in batch order
@@ -74,13 +75,6 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 #define DP_STORE(p, v) __builtin_nontemporal_store((v), (p))
 #else
 #define DP_STORE(p, v) (*(p) = (v))
-#endif
-
-// block-wide wide-band fills (k_dp<1024>, k_dpw) with their value ring in
-// LDS meet at an LDS-only barrier per anti-diagonal; 1: __syncthreads
-// (rounds 4-5, which also drained every band store in flight)
-#ifndef DPW_FULLBAR
-#define DPW_FULLBAR 0
 #endif
 
 __host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
@@ -324,7 +318,7 @@ k_dp(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ b
         }
         // an LDS ring needs an LDS-only barrier (round 6: __syncthreads also
         // drained the step's band stores); the global ring needs the full one
-        if (BLOCK_SYNC && (GRING || DPW_FULLBAR))
+        if (BLOCK_SYNC && GRING)
             __syncthreads();
         else if (BLOCK_SYNC)
             lds_barrier();
@@ -1262,204 +1256,13 @@ k_dpr(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------
-// k_dpw: k_dp<DPW_NT> for very wide bands without codon moves (round 5;
-// edit_distance's band, align.jl:253-260: bw = ceil(min(m, n) / 2), H ~ m,
-// configs[2]: H = 2,624, one task per call).  k_dp's step loads each cell's
-// table entries and bases from global memory right before their use: a
-// dependent round trip per anti-diagonal, ~1 us per step (7.9 ms per call,
-// profiles/r05a_kernel_stats_c3.csv).  Here the row records {match, mismatch
-// (x 0.99 under skew), ins, del, base} and the template bases are staged in
-// LDS rings of DPW_RR rows / columns, 64 at a time one chunk (64 periods)
-// ahead: pair pp at period P reads row R = P + pp + par (read row R - c) and
-// column J = P - pp + JOFF (template column J - JOFF), both sliding windows.
-// Without codon moves the value ring needs only kappa-1 and kappa-2: three
-// rows.  Same candidates, FP64 sums, strict-'>' value and stored positions as
-// k_dp: bit-identical.
-// ---------------------------------------------------------------------
-constexpr int DPW_RR = 2048;   // staged rows / columns (32 blocks of 64)
-// widest band k_dpw takes: npairs + 128 staged rows, and a three-row value ring
-// beside the static rings in 160 KB of LDS
-constexpr int DPW_MAXH = 3600;
-
-template <int NT>
-__global__ void __launch_bounds__(NT)
-k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ bases,
-      const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
-      int *__restrict__ err, int ring_ld)
-{
-    constexpr int DPW_PPL = (DPW_MAXH / 2 + NT) / NT;   // band pairs per lane and step (at most)
-    extern __shared__ __attribute__((aligned(16))) double smem[];   // value ring: rows of ring_ld (2 used)
-    __shared__ dvec2 s_mtmm[DPW_RR], s_isds[DPW_RR];
-    __shared__ uint8_t s_sb[DPW_RR], s_col[DPW_RR];
-    const int q = threadIdx.x;
-    const DPTask T = tasks[blockIdx.x];   // one task per workgroup
-    (void)ntasks;
-    const bool rev = T.flags & 1, skew = T.flags & 2, trim = T.flags & 4;
-    const uint8_t *sbase = bases + T.sb;
-    const uint8_t *tbase = bases + T.tb;
-    const double *tb = tabs + T.tab;
-    double *band = bands + T.band;
-    const int K = T.klen, H = T.H;
-    const int npairs = (H + 1) >> 1;
-    const int JOFF = (npairs + 63) & ~63;
-    for (int e = q; e < 3 * ring_ld; e += NT)
-        smem[e] = -RF_INF;
-    // block b of rows: R in [64b, 64b + 64) -> read row R - c; of columns:
-    // J in [64b, 64b + 64) -> template column J - JOFF
-    struct Rec {
-        double mt, mm, is, ds;
-        int sb;
-    };
-    auto row_load = [&](int b, int l) {
-        const RowRec r = load_row_flat(T, rev, sbase, tb, 64 * b + l - T.c, false);
-        return Rec{r.mt, skew ? r.mm * 0.99 : r.mm, r.is, r.ds, r.sb};
-    };
-    auto row_put = [&](int b, int l, const Rec &x) {
-        const int i = (64 * b + l) & (DPW_RR - 1);
-        s_mtmm[i] = dvec2{x.mt, x.mm};
-        s_isds[i] = dvec2{x.is, x.ds};
-        s_sb[i] = (uint8_t)x.sb;
-    };
-    auto col_load = [&](int b, int l) { return load_col_flat(T, rev, tbase, 64 * b + l - JOFF); };
-    auto col_put = [&](int b, int l, int v) { s_col[(64 * b + l) & (DPW_RR - 1)] = (uint8_t)v; };
-    // newest blocks chunk t needs: rows up to 64t + 63 + npairs, columns up to 64t + 63 + JOFF
-    auto brow = [&](int t) { return (64 * t + 63 + npairs) >> 6; };
-    auto bcol = [&](int t) { return t + (JOFF >> 6); };
-    for (int e = q; e < 64 * (brow(0) + 1); e += NT)
-        row_put(e >> 6, e & 63, row_load(e >> 6, e & 63));
-    for (int e = q; e < 64 * (bcol(0) + 1); e += NT)
-        col_put(e >> 6, e & 63, col_load(e >> 6, e & 63));
-    // one chunk ahead: wave 0 holds the next row block, wave 1 the next column block
-    const int l = q & 63, wv = q >> 6;
-    Rec nrow{};
-    int ncol = 4;
-    if (wv == 0)
-        nrow = row_load(brow(1), l);
-    else if (wv == 1)
-        ncol = col_load(bcol(1), l);
-    __syncthreads();
-
-    int eflag = 0;
-    // the last value of each of this lane's diagonals (2pp: vev, 2pp + 1: vod)
-    double vev[DPW_PPL], vod[DPW_PPL];
-    // a pair's row record changes at odd steps (R = P + pp + 1) and its
-    // template column at even steps (J = P - pp + JOFF): each is read from
-    // LDS once and used by two consecutive anti-diagonals
-    dvec2 mtmm[DPW_PPL], isds[DPW_PPL];
-    int sb[DPW_PPL], tbb[DPW_PPL];
-#pragma unroll
-    for (int it = 0; it < DPW_PPL; ++it) {
-        const int pp = q + it * NT;
-        vev[it] = vod[it] = -RF_INF;
-        const int R = pp & (DPW_RR - 1);   // step 0's row
-        mtmm[it] = s_mtmm[R];
-        isds[it] = s_isds[R];
-        sb[it] = s_sb[R];
-        tbb[it] = 4;
-    }
-    auto step = [&](auto PARC, const int k) {
-        constexpr int par = decltype(PARC)::value;
-        const int P = k >> 1;
-        // the neighbour pair's kappa - 1 value from LDS (two rows: this step's
-        // and the last); the lane's own kappa - 1 and kappa - 2 values are in
-        // registers (round 5: one LDS value read per cell instead of three)
-        double *r0 = smem + par * ring_ld + 1;
-        const double *r1 = smem + (1 - par) * ring_ld + 1;
-        double *row = band + (size_t)(rev ? K - 1 - k : k) * T.P;
-        // DPW_PPL pairs per lane (H <= DPW_MAXH), straight-line: every pair's
-        // LDS reads at clamped indices first, then the cells (round 5: a loop
-        // with a break per pair waited for each pair's reads in turn)
-        double a2[DPW_PPL], a1l[DPW_PPL], a1r[DPW_PPL];
-        bool on[DPW_PPL];
-#pragma unroll
-        for (int it = 0; it < DPW_PPL; ++it) {
-            const int pp = q + it * NT;
-            const int d = 2 * pp + par;
-            on[it] = d < H && d <= k;
-            const int dc = min(d, H);   // ring rows hold H + 2 entries from -1
-            if (par) {
-                const int R = (P + pp + 1) & (DPW_RR - 1);
-                mtmm[it] = s_mtmm[R];
-                isds[it] = s_isds[R];
-                sb[it] = s_sb[R];
-            } else {
-                tbb[it] = s_col[(P - pp + JOFF) & (DPW_RR - 1)];
-            }
-            // (d, kappa - 2): this parity's last value; (d -/+ 1, kappa - 1):
-            // the other parity's (own pair) and the neighbour pair's (LDS)
-            const double nb = r1[par ? dc + 1 : dc - 1];
-            a2[it] = par ? vod[it] : vev[it];
-            a1l[it] = par ? vev[it] : nb;
-            a1r[it] = par ? nb : vod[it];
-        }
-#pragma unroll
-        for (int it = 0; it < DPW_PPL; ++it) {
-            if (!on[it])
-                continue;
-            const int pp = q + it * NT;
-            const int d = 2 * pp + par;
-            const int jj = P - pp;
-            const int ii = d + jj - T.c;
-            double v = -RF_INF;
-            if (jj <= T.m && ii >= 0 && ii <= T.n) {
-                if (ii == 0 && jj == 0) {
-                    v = 0.0;
-                } else {
-                    const double ms = sb[it] == tbb[it] ? mtmm[it].x : mtmm[it].y;
-                    const double is = (trim && (jj == 0 || jj == T.m)) ? 0.0 : isds[it].x;
-                    // align.jl:77-104: the maximum of the candidates
-                    double best = fmax(fmax(a2[it] + ms, a1l[it] + is), a1r[it] + isds[it].y);
-                    eflag |= best == -RF_INF ? 1 : 0;   // "new score is invalid"
-                    v = best;
-                }
-                if (ii == T.n && jj == T.m && out_score)
-                    out_score[T.out_idx] = v;
-            }
-            row[(rev ? H - 1 - d : d) >> 1] = v;
-            r0[d] = v;
-            if (par)
-                vod[it] = v;
-            else
-                vev[it] = v;
-        }
-        // the value ring is in LDS: a barrier that waits for LDS only
-        // (round 6; __syncthreads also drained every band store of the step,
-        // vmcnt(0), once per anti-diagonal)
-        if (DPW_FULLBAR)
-            __syncthreads();
-        else
-            lds_barrier();
-    };
-    for (int k = 0; k < K; k += 2) {
-        if (k > 0 && (k & 127) == 0) {   // chunk t = k / 128 starts
-            const int t = k >> 7;
-            if (wv == 0) {
-                row_put(brow(t), l, nrow);
-                nrow = row_load(brow(t + 1), l);
-            } else if (wv == 1) {
-                col_put(bcol(t), l, ncol);
-                ncol = col_load(bcol(t + 1), l);
-            }
-            if (DPW_FULLBAR)
-                __syncthreads();
-            else
-                lds_barrier();
-        }
-        step(std::integral_constant<int, 0>{}, k);
-        if (k + 1 < K)
-            step(std::integral_constant<int, 1>{}, k + 1);
-    }
-    if (eflag)
-        set_err(err, 1);
-}
-
-// ---------------------------------------------------------------------
 // k_dpm: very wide bands without codon moves across several CUs (round 6;
-// edit_distance's band, align.jl:253-260).  k_dpw runs such a band in one
-// workgroup: 16 waves and a barrier per anti-diagonal, issue-bound on one
-// CU (3.33 ms per configs[2] call).  Here the band is cut into slices of
-// DPM_OWN band-row pairs, one single-wave workgroup each (no barrier per
-// step), which meet only every DPM_B anti-diagonals:
+// edit_distance's band, align.jl:253-260: bw = ceil(min(m, n) / 2), H ~ m,
+// configs[2]: H = 2,624, one band per call).  Round 5 ran such a band in
+// one 1024-thread workgroup (k_dpw: a barrier per anti-diagonal, issue-bound
+// on one CU, 3.35 ms per call).  Here the band is cut into slices of DPM_OWN
+// band-row pairs, one single-wave workgroup each (no barrier per step),
+// which meet only every DPM_B anti-diagonals:
 //   - the wave holds 64 * DPM_NPL consecutive pairs: its slice and DPM_B / 2
 //     pairs (DPM_B diagonals) of each neighbouring slice.  After a hand-off
 //     every pair holds exact values; in the next DPM_B steps a wrong value
@@ -1475,18 +1278,22 @@ k_dpw(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
 //   - a cell is a fixed sequence of selects: its validity is a per-lane
 //     range of periods, its store a buffer store whose offset is per-lane
 //     (lanes outside the slice or the band get an offset past the band and
-//     the range check drops the store), and the origin and the final score
-//     are scalar-branch steps;
+//     the range check drops the store); the origin, the final cell and a
+//     last period without its odd step are separate (EDGE) periods;
+//   - a wave computes only its compute phase, the periods at which some
+//     pair it holds is in the DP; before and after, its cells are -Inf
+//     stores (configs[2]: 2,602 of the band's 7,826 anti-diagonals);
 //   - hand-off through the band itself: the host fills each band with an
 //     all-ones pattern (a NaN no sum produces) before the launch; the slice
-//     stores every in-band cell it owns at every step (write-through, sc1)
-//     and a wave takes its halo pairs' last two values by polling those
-//     cells (sc1 loads, 64-bit single-copy atomic) until none holds the
-//     pattern -- one round trip, no flag and no store drain (bounded:
-//     error 4 rather than a hang);
-//   - slices run on one XCD (workgroups at blockIdx multiples of 8).
-// Same candidates, FP64 sums and strict-'>' values as k_dpw: bit-identical;
-// cells left of the DP (jj < 0) are stored as -Inf, which k_dpw leaves out.
+//     stores every in-band cell it owns (write-through, sc1) and a wave
+//     takes its halo pairs' last two values where they are in the DP by
+//     polling those cells (sc1 loads, 64-bit single-copy atomic) until none
+//     holds the pattern -- one round trip, no flag and no store drain
+//     (bounded: error 4 rather than a hang);
+//   - a band's slices run on one XCD (workgroup i runs on XCD i % 8), the
+//     bands of a launch spread over the eight.
+// Same candidates, FP64 sums and strict-'>' values as k_dp: bit-identical;
+// cells left of the DP (jj < 0) are stored as -Inf, which k_dp leaves out.
 // ---------------------------------------------------------------------
 // geometry (profiles/r06p_exp_dpm.out, configs[2]'s band, ms per call):
 // 1 pair per lane, hand-off every 32 steps 0.745; every 16 0.822; 2 pairs
@@ -1509,13 +1316,12 @@ constexpr int DPM_SC1 = 16;                       // buffer-store cache policy: 
 static_assert(DPM_OWN > 0 && (DPM_B / 2) % DPM_NPL == 0 && 128 % DPM_B == 0, "slice geometry");
 
 __host__ __device__ constexpr int dpm_slices(int H) { return ((H + 1) / 2 + DPM_OWN - 1) / DPM_OWN; }
-// Slices of one band spin on each other, so they must be resident together:
-// a task has at most DPM_TASK_SLICES (one XCD holds ~7 of these 22-KB
-// workgroups per CU, 32 CUs); workgroups dispatch in order, so the tasks of
-// a launch become resident one after another and DPM_MAX_SLICES only bounds
-// the grid.
+// A band's slices spin on each other, so they must be resident together:
+// at most DPM_TASK_SLICES per band (an XCD holds 8 of these 20-KB workgroups
+// per CU, 32 CUs).  Workgroups dispatch in order, so the bands of one XCD
+// become resident one after another (each waits only for earlier bands,
+// which are whole); wider bands take k_dp.
 constexpr int DPM_TASK_SLICES = 160;
-constexpr size_t DPM_MAX_SLICES = 2048;
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -1531,9 +1337,9 @@ k_dpm(const DPTask *__restrict__ tasks, int ntasks, int G, const uint8_t *__rest
       const double *__restrict__ tabs, double *__restrict__ bands, double *__restrict__ out_score,
       int *__restrict__ err)
 {
-    if (blockIdx.x & 7)
-        return;
-    const int w = blockIdx.x >> 3, task = w / G, g = w % G;
+    // workgroup i runs on XCD i % 8: task t takes XCD t % 8, its slice g
+    // the workgroups 8 ((t / 8) G + g) + t % 8
+    const int row = blockIdx.x >> 3, task = (row / G) * 8 + (blockIdx.x & 7), g = row % G;
     if (task >= ntasks)
         return;
     const DPTask T = tasks[task];
@@ -4718,7 +4524,7 @@ struct Opts {
                             // this many workgroups remain
     int seg_wgs = 262144;   // RF_OPT_SEG_WGS: split-mode k_score_segl takes reads in chunks so that about
                             // this many workgroups remain
-    int dp_mc = 1;          // RF_OPT_DP_MC: H > 2040 bands without codon moves in k_dpm (0: k_dpw / k_dp)
+    int dp_mc = 1;          // RF_OPT_DP_MC: H > 2040 bands without codon moves in k_dpm (0: k_dp)
     int dp_pfit = 1;        // RF_OPT_DP_PFIT: lean NP >= 2 class launched at its tasks' stride class
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
@@ -4778,8 +4584,6 @@ struct rf_ctx {
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
         size_t nx = 0;         // latency-bound non-lean tasks, k_dpx (RF_OPT_DP_NL64)
         size_t nl = 0;         // latency-mode lean tasks, one k_dpx<false, false> class (RF_OPT_DP_LAT)
-        size_t nww = 0;        // very wide bands without codon moves (k_dpw)
-        int hmaxw = 0;
         size_t nwm = 0;        // very wide bands without codon moves across CUs (k_dpm, RF_OPT_DP_MC)
         int gm = 0;            // their most slices
         size_t n64 = 0, ng = 0;
@@ -5221,13 +5025,11 @@ int rf_create(int device, rf_ctx **out)
         (void)hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
     }
     // the lean scorer may use up to the whole 160 KiB LDS of a CU, and so may
-    // the very-wide-band DP's ring
+    // the block-wide DP's ring
     (void)hipFuncSetAttribute((const void *)k_score_ws<WS_NPF, 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_dp<DPW_NT, false, DPW_NT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_dpw<DPW_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024 - DPW_RR * 34);
     *out = ctx;
     return 0;
 }
@@ -6031,8 +5833,8 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cww, cwm;
-        int hmax64 = 0, hmaxg = 0, hmaxw = 0, gm = 0;
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cwm;
+        int hmax64 = 0, hmaxg = 0, gm = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
         // of the tasks -- measured: c4 DP -5..9 %; splitting the wide classes,
@@ -6135,9 +5937,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                            (int64_t)t.klen * t.P * 8 < ((int64_t)1 << 31)) {
                     cwm.push_back(t);   // k_dpm: across CUs, no codon moves (edit_distance's band)
                     gm = std::max(gm, dpm_slices(t.H));
-                } else if (S.ncins == 0 && S.ncdel == 0 && t.H <= DPW_MAXH) {
-                    cww.push_back(t);   // k_dpw: staged rows, no codon moves (edit_distance's band)
-                    hmaxw = std::max(hmaxw, t.H);
                 } else {
                     cg.push_back(t);
                     hmaxg = std::max(hmaxg, t.H);
@@ -6176,21 +5975,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 cp[a][pmi].insert(cp[a][pmi].end(), cr[a][1].begin(), cr[a][1].end());
                 cr[a][1].clear();
             }
-        // k_dpm's slices spin on each other (one task's slices resident
-        // together, DPM_TASK_SLICES); a very large set of very wide bands
-        // takes the one-workgroup kernels
-        if (cwm.size() * (size_t)gm > DPM_MAX_SLICES) {
-            for (const DPTask &t : cwm)
-                if (t.H <= DPW_MAXH) {
-                    cww.push_back(t);
-                    hmaxw = std::max(hmaxw, t.H);
-                } else {
-                    cg.push_back(t);
-                    hmaxg = std::max(hmaxg, t.H);
-                }
-            cwm.clear();
-            gm = 0;
-        }
         auto by_len = [](const DPTask &x, const DPTask &y) { return x.klen > y.klen; };
         std::vector<DPTask> &all = P.tasks;
         all.clear();
@@ -6216,7 +6000,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         std::stable_sort(cg.begin(), cg.end(), by_len);
         all.insert(all.end(), c64.begin(), c64.end());
         all.insert(all.end(), cg.begin(), cg.end());
-        all.insert(all.end(), cww.begin(), cww.end());
         all.insert(all.end(), cwm.begin(), cwm.end());
         if (int e = upload(ctx, ctx->scratch[8], all))
             return e;
@@ -6240,8 +6023,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         P.nl = cl.size();
         P.n64 = c64.size();
         P.ng = cg.size();
-        P.nww = cww.size();
-        P.hmaxw = hmaxw;
         P.nwm = cwm.size();
         P.gm = gm;
         P.hmax64 = hmax64;
@@ -6262,7 +6043,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
     // largest: the machine stays full through every launch's tail.
     struct Launch {
         int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>, 11 = k_dpm,
-                       // 10 = k_dpw, 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean),
+                       // 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean),
                        // 35 = latency-mode lean,
                        // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
@@ -6303,10 +6084,6 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             launches.push_back({9, at, P.ng});
             at += P.ng;
         }
-        if (P.nww) {
-            launches.push_back({10, at, P.nww});
-            at += P.nww;
-        }
         if (P.nwm)
             launches.push_back({11, at, P.nwm});
     }
@@ -6332,7 +6109,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                           [](const Launch &L) { return L.kind == 34 || (L.kind >= 8 && L.kind <= 11); });
     size_t big = 0;
     const bool lat_first = !launches.empty() &&
-                           (launches[0].kind == 34 || (launches[0].kind >= 8 && launches[0].kind <= 10));
+                           (launches[0].kind == 34 || (launches[0].kind >= 8 && launches[0].kind <= 11));
     for (size_t i = 1; i < launches.size() && !lat_first; ++i)
         if (launches[i].n > launches[big].n)
             big = i;
@@ -6406,22 +6183,18 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             hipLaunchKernelGGL((k_dp<64, false>), dim3(n), dim3(64), 4 * ld * 8, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, ld, nullptr);
         } else if (L.kind == 11) {
-            // H > 2040 without codon moves across CUs (k_dpm): 8 workgroups per
-            // slice (one works: one XCD); each band filled with the not-yet-
-            // stored pattern first (the slices poll their halo cells for it)
+            // H > 2040 without codon moves across CUs (k_dpm): one workgroup per
+            // slice, a band's slices on one XCD; each band filled with the
+            // not-yet-stored pattern first (the slices poll their halo cells)
             bool trim = false;
             for (int i = 0; i < n; ++i) {
                 const DPTask &t = P.tasks[L.at + i];
                 trim = trim || (t.flags & 4);
                 HIPCHK(ctx, hipMemsetAsync(d_bands + t.band, 0xFF, (size_t)t.klen * t.P * 8, st));
             }
-            hipLaunchKernelGGL(trim ? k_dpm<true> : k_dpm<false>, dim3((unsigned)(8 * n * P.gm)), dim3(64), 0, st,
+            hipLaunchKernelGGL(trim ? k_dpm<true> : k_dpm<false>, dim3((unsigned)(8 * ((n + 7) / 8) * P.gm)), dim3(64),
+                               0, st,
                                d_tasks + L.at, n, P.gm, d_bases, d_tabs, d_bands, d_out, ctx->d_err);
-        } else if (L.kind == 10) {
-            // H > 2040 without codon moves: staged rows (k_dpw), a three-row value ring
-            const int ld = P.hmaxw + 4;
-            hipLaunchKernelGGL(k_dpw<DPW_NT>, dim3(n), dim3(DPW_NT), 3 * ld * 8, st, d_tasks + L.at, n, d_bases, d_tabs,
-                               d_bands, d_out, ctx->d_err, ld);
         } else {
             // H > 2040: one task per DPW_NT-thread block, the ring in LDS when it fits
             const int ld = P.hmaxg + 6;

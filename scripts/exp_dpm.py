@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """edit_distance's band at configs[2]'s shape (2,622 x 2,601, skew, bw =
 ceil(min / 2): H = 2,623) filled alone: per-call ms (HIP events) of
-rf_realign with RF_OPT_DP_MC 1 (k_dpm) and 0 (k_dpw), for the library named
+rf_realign with RF_OPT_DP_MC 1 (k_dpm) and 0 (k_dp; k_dpw before round 6), for the library named
 by RIFRAF_HIP_LIB.  With library names as arguments it runs itself once per
 library (child processes) and prints one JSON line each.
 usage: exp_dpm.py [lib.so ...]"""

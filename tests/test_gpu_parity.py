@@ -348,14 +348,13 @@ def test_dpx_invalid_score_is_loud(engine):
 @pytest.mark.parametrize("mc", [1, 0])
 @pytest.mark.parametrize("m,dn,flags", [(2601, 21, RF_SKEW), (3000, -40, 0), (3400, 180, RF_SKEW | RF_TRIM),
                                          (2300, 0, RF_TRIM)])
-def test_dpw_edit_distance_bands(engine, opts, m, dn, flags, mc):
-    """Round 5: very wide bands without codon moves (edit_distance,
-    align.jl:253-260: bw = ceil(min(m, n) / 2), skew_matches) run in k_dpw
-    (staged row / column rings, three-row value ring): configs[2]'s shape
-    (2,622 x 2,601), H up to ~3,600 (the k_dpw limit), skew and trim,
-    forward and (no flags) backward; bands, A[end,end], backtraces and error
-    counts bit-exact vs the oracle.  mc 1 (the default since round 6): the
-    same bands across CUs in k_dpm's slices (RF_OPT_DP_MC); 0: k_dpw."""
+def test_dpm_edit_distance_bands(engine, opts, m, dn, flags, mc):
+    """Very wide bands without codon moves (edit_distance, align.jl:253-260:
+    bw = ceil(min(m, n) / 2), skew_matches): configs[2]'s shape (2,622 x
+    2,601) and wider, skew and trim, forward and (no flags) backward; bands,
+    A[end,end], backtraces and error counts bit-exact vs the oracle.  mc 1
+    (the default since round 6): k_dpm's slices across CUs (RF_OPT_DP_MC);
+    0: one block per band (k_dp)."""
     opts("dp_mc", mc)
     rng = np.random.default_rng(m + dn)
     t = random_seq(m, rng)
@@ -436,6 +435,25 @@ def test_dpm_several_wide_bands_one_call(engine):
     seqs.append(make_read(t, rng, 0.02, 9))
     bws.append(9)
     assert all(2 * b + abs(len(s) - len(t)) + 1 > 2040 for s, b in zip(seqs[:4], bws[:4]))
+    _check_bands(engine, t, seqs, bws)
+
+
+def test_dpm_bands_sharing_an_xcd(engine):
+    """Eleven very wide bands in one call: k_dpm puts band t on XCD t % 8, so
+    bands 8-10 queue behind bands 0-2 on their XCDs (workgroups dispatch in
+    order; a band's slices wait only for earlier, whole bands).  Bands of
+    different slice counts; forward and backward bit-exact."""
+    rng = np.random.default_rng(67)
+    t = random_seq(2100, rng)
+    seqs, bws = [], []
+    for i in range(11):
+        bw = 1021 + 37 * i
+        s = make_read(t, rng, 0.04, bw).seq
+        want = len(t) + (i % 5) - 2
+        s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
+        seqs.append(RifrafSequence(s, np.full(len(s), -1.1), bw, SEQ_SCORES))
+        bws.append(bw)
+    assert all(2 * b + abs(len(s) - len(t)) + 1 > 2040 for s, b in zip(seqs, bws))
     _check_bands(engine, t, seqs, bws)
 
 
