@@ -3816,8 +3816,11 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         // cell's successor lane (or the sink, lane 63: leaves the box, reaches
         // (0, 0), or no move), J_r = J0^(2^r) by pointer doubling; lane k then
         // finds the k-th cell of the walk from lane 1 (the current cell) by
-        // the binary digits of k, and emits the k-th move.  The same moves,
-        // marks, error counts and failure points as the sequential walk below.
+        // the binary digits of k, and emits the k-th move.  Round r applies
+        // J_r to the lane's cell and squares J_r with two independent
+        // permutes (round 6: 6 dependent permute rounds instead of 11).  The
+        // same moves, marks, error counts and failure points as the
+        // sequential walk (git history).
         {
             constexpr int SINK = 63;
             const int mv0 = pack & 7;
@@ -3831,15 +3834,12 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             int J = (blane && inbox && (ti > 0 || tj > 0)) ? ndi * 3 + nu + 1 : SINK;
             if (lane == SINK)
                 J = SINK;
-            int Jr[6];
-            Jr[0] = J;
-#pragma unroll
-            for (int r = 1; r < 6; ++r)
-                Jr[r] = __builtin_amdgcn_ds_bpermute(Jr[r - 1] << 2, Jr[r - 1]);
             int cell = 1;   // lane k: the k-th cell of the walk
 #pragma unroll
             for (int r = 0; r < 6; ++r) {
-                const int nx = __builtin_amdgcn_ds_bpermute(cell << 2, Jr[r]);
+                const int nx = __builtin_amdgcn_ds_bpermute(cell << 2, J);
+                if (r < 5)
+                    J = __builtin_amdgcn_ds_bpermute(J << 2, J);
                 cell = ((lane >> r) & 1) ? nx : cell;
             }
             // cells reached; a cell with no move (mv 0) ends the walk in failure
@@ -3871,10 +3871,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                         mk[(size_t)cj * 9 + 4] = 1;
                 }
             }
-            int e = emit ? (mvk == 1 ? (mism ? 1 : 0) : (mvk <= 3 ? 1 : 3)) : 0;
-            for (int off = 32; off >= 1; off >>= 1)
-                e += __shfl_xor(e, off);
-            errs += e;
+            // count_errors: 1 per mismatch or indel, 3 per codon move
+            errs += __popcll(__ballot(emit && (mvk >= 2 || mism))) + 2 * __popcll(__ballot(emit && mvk >= 4));
             if (nmv > 0) {
                 // the cell after the last move
                 int ni = ci, nj = cj;
