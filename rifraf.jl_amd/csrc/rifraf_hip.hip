@@ -3634,6 +3634,10 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 #ifndef BTW_WD_ELEMS
 #define BTW_WD_ELEMS 8
 #endif
+// window loads in flight per lane (one memory round trip per chunk)
+#ifndef BTW_CHUNK
+#define BTW_CHUNK 16
+#endif
 constexpr int BTW_WD = BTW_WD_ELEMS;   // staged elements per kappa row when P > BTW_WD (>= 6: codon boxes)
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
@@ -3688,11 +3692,11 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             // element t = row * wd + col, t = lane + 64 u: incremental row / col
             const int qr = 64 / wd, rr = 64 % wd;
             int row = lane / wd, col = lane % wd;
-            for (int u0 = 0; u0 < BTW_A / 64; u0 += 16) {
-                double v[16];
+            for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
+                double v[BTW_CHUNK];
                 int rw = row, cl = col;
 #pragma unroll
-                for (int u = 0; u < 16; ++u) {         // issue all loads of the chunk
+                for (int u = 0; u < BTW_CHUNK; ++u) {  // issue all loads of the chunk
                     const int t = lane + 64 * (u0 + u);
                     v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
                     rw += qr;
@@ -3703,14 +3707,14 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 16; ++u) {
+                for (int u = 0; u < BTW_CHUNK; ++u) {
                     const int t = lane + 64 * (u0 + u);
                     if (t < na)
                         sA[t] = v[u];
                 }
                 row = rw;
                 col = cl;
-                if (64 * (u0 + 16) >= na)            // lane 0 holds the chunk's lowest t
+                if (64 * (u0 + BTW_CHUNK) >= na)     // lane 0 holds the chunk's lowest t
                     break;
             }
             wave_sync();
@@ -3761,37 +3765,38 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             }
             wave_sync();
         }
-        // ---- box: the move of cell (ci, cj), packed mv | mismatch << 3 | read base << 4
+        // ---- box: the move of cell (ci, cj), packed mv | mismatch << 3 | read base << 4.
+        // Branch-free: every LDS read is issued at a selected (valid) index and
+        // masked after, so the box is one LDS round trip (round 6; the guarded
+        // reads were exec-mask branches and three dependent round trips).
         int pack = 0;
         {
             const int ci = ii - bdi, cj = jj - bdj;
-            const bool valid = blane && bdj >= 0 && ci >= 0 && cj >= 0 && (ci > 0 || cj > 0) &&
-                               ci - cj + c >= 0 && ci - cj + c < H;
-            auto inb = [&](int i2, int j2) {
-                if (i2 < 0 || j2 < 0)
-                    return false;
-                const int d = i2 - j2 + c;
-                return d >= 0 && d < H;
-            };
-            const bool in1 = valid && inb(ci - 1, cj - 1), in2 = valid && inb(ci - 1, cj),
-                       in3 = valid && inb(ci, cj - 1);
-            auto aix = [&](bool in, int i2, int j2) {
-                const int d = i2 - j2 + c;
-                return in ? (d + 2 * j2 - klo) * wd + (d >> 1) - e0 : 0;
-            };
-            const double a1 = sA[aix(in1, ci - 1, cj - 1)], a2 = sA[aix(in2, ci - 1, cj)],
-                         a3 = sA[aix(in3, ci, cj - 1)];
-            const int ks = valid ? max(ci - 1, 0) - q0 : 0;
-            const int kd = valid ? ci - q0 : 0;
-            const int sb = (valid && ci >= 1) ? sS[ci - 1 - q0] : 4;
-            const int tbb = (valid && cj >= 1) ? sTt[cj - 1 - r0] : 4;
-            double ms = (sb == tbb) ? sTm[ks] : sTx[ks];
-            double is = sTi[ks];
-            const double ds = sTd[kd];
-            if (skew && sb != tbb)
-                ms *= 0.99;
-            if (trim && (cj == 0 || cj == m))
-                is = 0.0;
+            const int dc = ci - cj + c, kap = ci + cj + c;   // the cell's diagonal and kappa
+            const bool valid = blane & (bdj >= 0) & (ci >= 0) & (cj >= 0) & ((ci | cj) != 0) &
+                               ((unsigned)dc < (unsigned)H);
+            // predecessors in the band: (ci-1, cj-1) diagonal dc, (ci-1, cj) dc-1, (ci, cj-1) dc+1
+            const bool in1 = valid & (ci >= 1) & (cj >= 1), in2 = valid & (ci >= 1) & (dc >= 1),
+                       in3 = valid & (cj >= 1) & (dc + 1 < H);
+            // indices masked to 0 off the band (an and, not a select: hipcc
+            // turns selects of computed indices into exec-mask branches)
+            const int row1 = (kap - 2 - klo) * wd - e0, row2 = row1 + wd;
+            const int a1i = (row1 + (dc >> 1)) & -(int)in1;
+            const int a2i = (row2 + ((dc - 1) >> 1)) & -(int)in2;
+            const int a3i = (row2 + ((dc + 1) >> 1)) & -(int)in3;
+            const double a1 = sA[a1i], a2 = sA[a2i], a3 = sA[a3i];
+            const int ks = (max(ci - 1, 0) - q0) & -(int)valid;
+            const int kd = (ci - q0) & -(int)valid;
+            const bool hs = valid & (ci >= 1), ht = valid & (cj >= 1);
+            const int sbr = sS[(ci - 1 - q0) & -(int)hs], tbr = sTt[(cj - 1 - r0) & -(int)ht];
+            const double tm = sTm[ks], tx = sTx[ks], ti = sTi[ks], ds = sTd[kd];
+            // every read issued before the selects (else hipcc sinks a load
+            // into a branch of its own or after another's wait)
+            asm volatile("" ::"v"(tm), "v"(tx), "v"(ti), "v"(ds), "v"(a1), "v"(a2), "v"(a3), "v"(sbr), "v"(tbr));
+            const int sb = hs ? sbr : 4, tbb = ht ? tbr : 4;
+            const bool mis = sb != tbb;
+            const double ms = mis ? (skew ? tx * 0.99 : tx) : tm;
+            const double is = (trim & ((cj == 0) | (cj == m))) ? 0.0 : ti;
             double best = -RF_INF, x;
             int mv = 0;
             x = a1 + ms;
@@ -3802,15 +3807,17 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             if (in3 && x > best) { best = x; mv = 3; }
             if (cod) {
                 // TRACE_CODON_INSERT from (ci - 3, cj), TRACE_CODON_DELETE from (ci, cj - 3)
-                const bool in4 = valid && T.ncins > 0 && ci >= 3 && inb(ci - 3, cj);
-                const bool in5 = valid && T.ncdel > 0 && cj >= 3 && inb(ci, cj - 3);
-                const double a4 = sA[aix(in4, ci - 3, cj)], a5 = sA[aix(in5, ci, cj - 3)];
-                x = a4 + sTci[in4 ? ci - 3 - q0 : 0];
+                const bool in4 = valid & (T.ncins > 0) & (ci >= 3) & (dc >= 3);
+                const bool in5 = valid & (T.ncdel > 0) & (cj >= 3) & (dc + 3 < H);
+                const int row3 = row1 - wd;
+                const double a4 = sA[(row3 + ((dc - 3) >> 1)) & -(int)in4];
+                const double a5 = sA[(row3 + ((dc + 3) >> 1)) & -(int)in5];
+                x = a4 + sTci[(ci - 3 - q0) & -(int)in4];
                 if (in4 && x > best) { best = x; mv = 4; }
-                x = a5 + sTcd[valid ? ci - q0 : 0];
+                x = a5 + sTcd[kd];
                 if (in5 && x > best) { best = x; mv = 5; }
             }
-            pack = valid ? (mv | ((sb != tbb) ? 8 : 0) | (sb << 4)) : 0;
+            pack = valid ? (mv | (mis ? 8 : 0) | (sb << 4)) : 0;
         }
         // ---- walk the box by ranking its cells in parallel: J0 = each box
         // cell's successor lane (or the sink, lane 63: leaves the box, reaches
@@ -3825,10 +3832,8 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             constexpr int SINK = 63;
             const int mv0 = pack & 7;
             const int bu = lane % 3 - 1;
-            int ndi = bdi, nu = bu;
-            if (mv0 == 1) { ndi = bdi + 1; }
-            else if (mv0 == 2) { ndi = bdi + 1; nu = bu + 1; }
-            else if (mv0 == 3) { nu = bu - 1; }
+            const int ndi = bdi + (int)((mv0 == 1) | (mv0 == 2));
+            const int nu = bu + (int)(mv0 == 2) - (int)(mv0 == 3);
             const bool inbox = (mv0 >= 1 && mv0 <= 3) && ndi <= BT_DMAX && nu >= -1 && nu <= 1;
             const int ti = ii - ndi, tj = jj - (ndi - nu);
             int J = (blane && inbox && (ti > 0 || tj > 0)) ? ndi * 3 + nu + 1 : SINK;
