@@ -707,7 +707,7 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         f = torch.tensor([can_pin], dtype=torch.float64, device=coll)
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         can_pin = float(f.item())
-    pin = (allowed[(rank * k) % len(allowed):][:k] or allowed[:k]) if can_pin else None
+    pin = idle_cpus(allowed, k, dist) if can_pin else None
     pin_excl = bool(args.e2e_pin_exclusive) if ne > 1 and args.e2e_pin_exclusive >= 0 else excl
     runs, pin_runs, stats, same_pin = [], [], [], True
     res = None
@@ -777,11 +777,13 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                                                  "within 1e-12 relative + 1e-15 absolute",
             "runs_s": runs, "pinned_runs_s": pin_runs,
             "pinned": None if not pin else {
-                "cores": len(pin), "clusters_per_s": n_all / pin_s, "ratio_to_unpinned": elapsed / pin_s,
+                "cores": len(pin), "cpus": [int(c) for c in pin], "clusters_per_s": n_all / pin_s,
+                "ratio_to_unpinned": elapsed / pin_s,
                 "init_exclusive": pin_excl,
                 "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(same_pin),
                 "note": "the same steady-state pass with every thread of the rank pinned to this many cores "
-                        "(a rank's share of the box's 16 at 8 ranks)"}}
+                        "(a rank's share of the box's 16 at 8 ranks): the idlest of its allowed cpus, disjoint "
+                        "across ranks (bench.idle_cpus)"}}
 
 
 def qv_close(a, b, rtol=1e-12, atol=1e-15):
@@ -794,6 +796,52 @@ def qv_close(a, b, rtol=1e-12, atol=1e-15):
     pairs = [(getattr(a.error_probs, f), getattr(b.error_probs, f)) for f in ("sub", "dele", "ins")]
     pairs.append((a.aln_error_probs, b.aln_error_probs))
     return all(np.shape(x) == np.shape(y) and np.allclose(x, y, rtol=rtol, atol=atol) for x, y in pairs)
+
+
+def cpu_busy(cpus, dt=0.3):
+    """Busy fraction of each cpu over `dt` seconds (/proc/stat)."""
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    name, *v = line.split()
+                    v = [int(x) for x in v]
+                    out[int(name[3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+        return out
+    a = snap()
+    time.sleep(dt)
+    b = snap()
+    busy = {}
+    for c in cpus:
+        if c in a and c in b and b[c][0] > a[c][0]:
+            busy[c] = 1.0 - (b[c][1] - a[c][1]) / (b[c][0] - a[c][0])
+        else:
+            busy[c] = 1.0
+    return busy
+
+
+def idle_cpus(allowed, k, dist=None):
+    """The k idlest of the rank's allowed cpus (the GPU box's host is shared:
+    its first cpus carry other work, r06v's pinned passes on cpus 0-1 ran
+    0.17 - 0.32 s); with a process group, ranks take disjoint sets in rank
+    order from the gathered measurements."""
+    try:
+        busy = cpu_busy(allowed)
+    except OSError:
+        busy = {c: 0.0 for c in allowed}
+    order = sorted(allowed, key=lambda c: (busy[c], c))
+    if dist is None:
+        return order[:k]
+    lists = [None] * dist.get_world_size()
+    dist.all_gather_object(lists, order)
+    taken, mine = set(), None
+    for r, lst in enumerate(lists):
+        pick = [c for c in lst if c not in taken][:k] or lst[:k]
+        taken.update(pick)
+        if r == dist.get_rank():
+            mine = pick
+    return mine
 
 
 def pin_threads(cpus):

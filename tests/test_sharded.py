@@ -404,3 +404,31 @@ def test_cluster_queue_failure_reaches_every_rank():
     assert got[1][0] == "ValueError"
     for r in (0, 2):
         assert got[r][0] == "RuntimeError" and "rank 1 failed" in got[r][1]
+
+
+# ----------------------------------------------------------------------
+def _idle_cpus_rank(rank, world):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    allowed = sorted(os.sched_getaffinity(0))
+    return bench.idle_cpus(allowed, 2, dist), allowed
+
+
+def test_bench_pins_ranks_to_disjoint_idle_cpus():
+    """bench's pinned e2e passes: each rank takes the 2 idlest of its allowed
+    cpus, disjoint across ranks (world 3, gloo); one process takes 2 of its
+    allowed cpus."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    allowed = sorted(os.sched_getaffinity(0))
+    one = bench.idle_cpus(allowed, 2)
+    assert len(set(one)) == min(2, len(allowed)) and set(one) <= set(allowed)
+    got = _spawn(_idle_cpus_rank, 3)
+    picks = [got[r][0] for r in range(3)]
+    if len(allowed) >= 6:
+        assert len(set().union(*map(set, picks))) == 6
+    for r in range(3):
+        assert set(picks[r]) <= set(got[r][1]) and len(picks[r]) == 2
