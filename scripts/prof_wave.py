@@ -31,7 +31,7 @@ t0 = time.perf_counter()
 pr.runcall(B.rifraf_batch, cl, params=params, engine=e, wave=n)
 wall = time.perf_counter() - t0
 print(f"wall {wall:.4f} s for {n} clusters")
-for th, ph, a, b in B.TIMELINE:
+for th, ph, a, b, *_ in B.TIMELINE:
     print(f"  {ph:8s} {b - a:.4f}")
 for key in ("tottime", "cumulative"):
     s = io.StringIO()
