@@ -1318,10 +1318,13 @@ static_assert(DPM_OWN > 0 && (DPM_B / 2) % DPM_NPL == 0 && 128 % DPM_B == 0, "sl
 __host__ __device__ constexpr int dpm_slices(int H) { return ((H + 1) / 2 + DPM_OWN - 1) / DPM_OWN; }
 // A band's slices spin on each other, so they must be resident together:
 // at most DPM_TASK_SLICES per band (an XCD holds 8 of these 20-KB workgroups
-// per CU, 32 CUs).  Workgroups dispatch in order, so the bands of one XCD
-// become resident one after another (each waits only for earlier bands,
-// which are whole); wider bands take k_dp.
+// per CU, 32 CUs: 256).  Workgroups of one launch dispatch in order, so the
+// bands of one XCD become resident one after another (each waits only for
+// earlier bands, which are whole); wider bands take k_dp.  Launches from
+// other streams (a second engine) interleave with it, so one launch keeps
+// to DPM_XCD_SLICES per XCD (more bands: further launches on its stream).
 constexpr int DPM_TASK_SLICES = 160;
+constexpr int DPM_XCD_SLICES = 64;
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -6189,15 +6192,23 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             // H > 2040 without codon moves across CUs (k_dpm): one workgroup per
             // slice, a band's slices on one XCD; each band filled with the
             // not-yet-stored pattern first (the slices poll their halo cells)
-            bool trim = false;
-            for (int i = 0; i < n; ++i) {
-                const DPTask &t = P.tasks[L.at + i];
-                trim = trim || (t.flags & 4);
-                HIPCHK(ctx, hipMemsetAsync(d_bands + t.band, 0xFF, (size_t)t.klen * t.P * 8, st));
+            // At most DPM_XCD_SLICES slices per XCD per launch, launches in
+            // sequence on this stream: a launch's bands become resident in
+            // order, but two launches from different streams interleave, so
+            // each keeps to a share of an XCD (four such launches fit at once)
+            const int per = 8 * std::max(1, DPM_XCD_SLICES / P.gm);
+            for (int c0 = 0; c0 < n; c0 += per) {
+                const int nc = std::min(per, n - c0);
+                bool trim = false;
+                for (int i = c0; i < c0 + nc; ++i) {
+                    const DPTask &t = P.tasks[L.at + i];
+                    trim = trim || (t.flags & 4);
+                    HIPCHK(ctx, hipMemsetAsync(d_bands + t.band, 0xFF, (size_t)t.klen * t.P * 8, st));
+                }
+                hipLaunchKernelGGL(trim ? k_dpm<true> : k_dpm<false>, dim3((unsigned)(8 * ((nc + 7) / 8) * P.gm)),
+                                   dim3(64), 0, st, d_tasks + L.at + c0, nc, P.gm, d_bases, d_tabs, d_bands, d_out,
+                                   ctx->d_err);
             }
-            hipLaunchKernelGGL(trim ? k_dpm<true> : k_dpm<false>, dim3((unsigned)(8 * ((n + 7) / 8) * P.gm)), dim3(64),
-                               0, st,
-                               d_tasks + L.at, n, P.gm, d_bases, d_tabs, d_bands, d_out, ctx->d_err);
         } else {
             // H > 2040: one task per DPW_NT-thread block, the ring in LDS when it fits
             const int ld = P.hmaxg + 6;

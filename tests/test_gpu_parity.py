@@ -439,21 +439,23 @@ def test_dpm_several_wide_bands_one_call(engine):
 
 
 def test_dpm_bands_sharing_an_xcd(engine):
-    """Eleven very wide bands in one call: k_dpm puts band t on XCD t % 8, so
-    bands 8-10 queue behind bands 0-2 on their XCDs (workgroups dispatch in
-    order; a band's slices wait only for earlier, whole bands).  Bands of
-    different slice counts; forward and backward bit-exact."""
+    """Seventeen very wide bands of 32 slices in one call: k_dpm puts band t
+    on XCD t % 8 and takes 64 slices per XCD per launch, so bands 8-15 queue
+    behind bands 0-7 on their XCDs inside the first launch (workgroups
+    dispatch in order; a band's slices wait only for earlier, whole bands)
+    and band 16 runs in a second launch; forward and backward bit-exact."""
     rng = np.random.default_rng(67)
     t = random_seq(2100, rng)
     seqs, bws = [], []
-    for i in range(11):
-        bw = 1021 + 37 * i
+    for i in range(17):
+        bw = 1021
         s = make_read(t, rng, 0.04, bw).seq
         want = len(t) + (i % 5) - 2
         s = s[:want] if len(s) > want else np.concatenate([s, random_seq(want - len(s), rng)])
         seqs.append(RifrafSequence(s, np.full(len(s), -1.1), bw, SEQ_SCORES))
         bws.append(bw)
-    assert all(2 * b + abs(len(s) - len(t)) + 1 > 2040 for s, b in zip(seqs, bws))
+    Hs = [2 * b + abs(len(s) - len(t)) + 1 for s, b in zip(seqs, bws)]
+    assert all(2040 < H <= 2047 for H in Hs)   # 32 slices each
     _check_bands(engine, t, seqs, bws)
 
 
