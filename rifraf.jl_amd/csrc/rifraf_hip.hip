@@ -3664,10 +3664,10 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     const int n = T.n, m = T.m, H = T.H, P = T.P;
     const int c = max(m - n, 0) + T.bw;
     const int K = H + 2 * m;
-    const int wd = min(P, BTW_WD);
-    const int W = BTW_A / wd;                          // kappa rows per window (>= 256)
     const bool skew = T.flags & 2, trim = T.flags & 4;
     const bool cod = T.ncins > 0 || T.ncdel > 0;
+    const int wd = min(P, cod ? max(BTW_WD, 6) : BTW_WD);   // codon boxes need 5 elements around the walk
+    const int W = BTW_A / wd;                          // kappa rows per window (>= 256)
     const int ext = cod ? 2 : 0;                       // codon predecessors: 2 more rows / diagonals
     const double *t_cins = tb + 4 * (size_t)n + 1;     // cins[ii - 3], ncins = n - 2 entries
     const double *t_cdel = t_cins + T.ncins;           // cdel[ii], ncdel = n + 1 entries
@@ -3867,32 +3867,23 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             const int ci = ii - cdi, cj = jj - (cdi - cdu);
             const int ksb = pk >> 4;
             const bool mism = pk & 8;
-            if (emit) {
+            // the forward step of this move ends at (ci, cj) (moves_to_proposals):
+            // a mismatch marks (cj, read base), an insertion (cj, 5 + base), a
+            // deletion (cj, 4) -- one store, its slot selected (no branches)
+            const bool mark = emit && mk && ((mvk == 1 && mism) || (do_indels && (mvk == 2 || mvk == 3)));
+            const int slot9 = cj * 9 + (mvk == 1 ? ksb : (mvk == 2 ? 5 + ksb : 4));
+            if (emit)
                 out[n + m - 1 - (cnt + lane)] = (int8_t)mvk;
-                if (mk) {
-                    // the forward step of this move ends at (ci, cj) (moves_to_proposals)
-                    if (mvk == 1 && mism)
-                        mk[(size_t)cj * 9 + ksb] = 1;
-                    else if (mvk == 2 && do_indels)
-                        mk[(size_t)cj * 9 + 5 + ksb] = 1;
-                    else if (mvk == 3 && do_indels)
-                        mk[(size_t)cj * 9 + 4] = 1;
-                }
-            }
+            if (mark)
+                mk[(size_t)slot9] = 1;
             // count_errors: 1 per mismatch or indel, 3 per codon move
             errs += __popcll(__ballot(emit && (mvk >= 2 || mism))) + 2 * __popcll(__ballot(emit && mvk >= 4));
             if (nmv > 0) {
                 // the cell after the last move
-                int ni = ci, nj = cj;
-                switch (mvk) {
-                case 1: ni -= 1; nj -= 1; break;
-                case 2: ni -= 1; break;
-                case 3: nj -= 1; break;
-                case 4: ni -= 3; break;
-                default: nj -= 3; break;
-                }
-                ii = __builtin_amdgcn_readlane(ni, nmv - 1);
-                jj = __builtin_amdgcn_readlane(nj, nmv - 1);
+                const int di = (mvk == 1 || mvk == 2) ? 1 : (mvk == 4 ? 3 : 0);
+                const int dj = (mvk == 1 || mvk == 3) ? 1 : (mvk == 5 ? 3 : 0);
+                ii = __builtin_amdgcn_readlane(ci - di, nmv - 1);
+                jj = __builtin_amdgcn_readlane(cj - dj, nmv - 1);
             }
             cnt += nmv;
             if (fail_now) {
