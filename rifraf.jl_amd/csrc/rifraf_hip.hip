@@ -1327,6 +1327,7 @@ constexpr int DPM_TASK_SLICES = 160;
 constexpr int DPM_XCD_SLICES = 64;
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double ld_sc1(const double *p)
 {
@@ -1683,6 +1684,9 @@ constexpr int DPX_W = 72;       // doubles per LDS band row: 2 pad | 64 lanes | 
 #ifndef DPX_STAGE
 #define DPX_STAGE 1   // interior rows staged in LDS, four per contiguous flush
 #endif
+#ifndef DPX_FL16
+#define DPX_FL16 1    // the flush in 16-B stores when the run is 16-B aligned
+#endif
 constexpr int DPX_RING = 256;   // staged rows / columns: 4 blocks of 64
 struct DpxStage {
     RawRow r;
@@ -1953,13 +1957,31 @@ k_dpx(const DPTask *__restrict__ tasks, int ntasks, const uint8_t *__restrict__ 
             step(BT{}, I1{}, I3{}, 2 * u + 1, b, col1);
             if (STAGE) {
                 // rows 4u .. 4u + 3 (reverse: K - 4 - 4u .. K - 1 - 4u) are one
-                // run of 4P doubles: 8-B stores of consecutive lanes
+                // run of 4P doubles.  A 16-B aligned run (forward always; reverse
+                // when K is even) goes out as 16-B stores of consecutive lanes,
+                // a fixed DPX_FL16 per lane (4P <= 260 doubles: 130 pairs),
+                // lanes past the run at an offset past the band; else 8-B
+                // stores in a loop (round 6: the loop issued ~30 instructions
+                // per pair of periods)
                 wave_sync();
                 const unsigned base = rev ? rob - 3u * rowb : rob;
                 const int n = 4 * T.P;
-                for (int t = q; t < n; t += 64)
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, s_out[t]), brs,
-                                                          base + 8u * (unsigned)t, 0, 0);
+                if (DPX_FL16 && (base & 15u) == 0) {
+                    const dvec2 *s2 = reinterpret_cast<const dvec2 *>(s_out);
+                    const int n2 = n >> 1;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const int t = q + 64 * j;
+                        const dvec2 v = s2[min(t, n2 - 1)];
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), brs,
+                                                               t < n2 ? base + 16u * (unsigned)t : DPX_NOSTORE, 0,
+                                                               0);
+                    }
+                } else {
+                    for (int t = q; t < n; t += 64)
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, s_out[t]), brs,
+                                                              base + 8u * (unsigned)t, 0, 0);
+                }
                 wave_sync();
             }
         } else {
