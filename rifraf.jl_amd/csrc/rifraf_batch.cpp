@@ -100,6 +100,10 @@ struct Clu {
     // the scratch slot already holds single_indel_proposals' skewed fill of
     // the reference against this consensus (filled beside the B realign)
     bool sip_pre = false;
+    // the reference slot's A band is the forward fill of this consensus at
+    // the reference's bandwidth (smart_forward in FRAME): has_single_indels'
+    // align_moves (model.jl:532-536) is the same fill, so its walk reads it
+    bool ref_a_ok = false;
 };
 
 struct Driver {
@@ -264,10 +268,12 @@ struct Driver {
             Read &R = reads[jobs[j].ridx];
             R.bw = jobs[j].bw;
             R.fixed = true;
-            if (jobs[j].k >= 0)
+            if (jobs[j].k >= 0) {
                 C.slot_scores[jobs[j].k] = score[j];
-            else
+            } else {
                 C.ref_score = score[j];
+                C.ref_a_ok = true;
+            }
         }
         return 0;
     }
@@ -416,14 +422,14 @@ struct Driver {
     // (rows) against the consensus in the cluster's scratch slot with the
     // reference's bandwidth, then the backtrace moves
     int ref_moves(const std::vector<int> &cs, bool skew, std::vector<std::vector<int8_t>> &mv,
-                  bool filled = false)
+                  bool filled = false, bool ref_slot = false)
     {
         std::vector<int32_t> sl, sq, tp, bw, nm(cs.size());
         std::vector<int64_t> moff{0};
         for (int c : cs) {
             const Clu &C = clu[c];
             const Read &R = reads[C.ref_read];
-            sl.push_back(C.scratch_slot);
+            sl.push_back(ref_slot ? C.ref_slot : C.scratch_slot);
             sq.push_back(R.seq);
             tp.push_back(C.tpl);
             bw.push_back(R.bw);
@@ -450,18 +456,37 @@ struct Driver {
     }
 
     // has_single_indels (model.jl:532-536) of clusters `cs` -> flags
+    // (round 6: a cluster whose reference A band is current -- FRAME, the
+    // consensus and reference unchanged since smart_forward -- walks that
+    // band instead of refilling the scratch slot: the same fill, so the same
+    // moves, one latency-bound codon fill less per FRAME iteration)
     void has_single_indels(std::vector<int> &cs, std::vector<uint8_t> &flag)
     {
         flag.assign(clu.size(), 0);
-        batched(cs, [&](const std::vector<int> &s) {
-            std::vector<std::vector<int8_t>> mv;
-            if (int e = ref_moves(s, false, mv))
-                return e;
-            for (size_t i = 0; i < s.size(); ++i)
-                for (int8_t m : mv[i])
-                    flag[s[i]] |= (m == 2 || m == 3);   // TRACE_INSERT / TRACE_DELETE
-            return 0;
-        });
+        std::vector<int> fill, cur;
+        for (int c : cs)
+            (clu[c].ref_a_ok ? cur : fill).push_back(c);
+        for (int pass = 0; pass < 2; ++pass)
+            batched(pass ? cur : fill, [&](const std::vector<int> &s) {
+                std::vector<std::vector<int8_t>> mv;
+                if (int e = ref_moves(s, false, mv, pass == 1, pass == 1))
+                    return e;
+                for (size_t i = 0; i < s.size(); ++i)
+                    for (int8_t m : mv[i])
+                        flag[s[i]] |= (m == 2 || m == 3);   // TRACE_INSERT / TRACE_DELETE
+                return 0;
+            });
+        // the clusters left (batched drops a failing one), in the callers' order
+        std::vector<uint8_t> left(clu.size(), 0);
+        for (int c : fill)
+            left[c] = 1;
+        for (int c : cur)
+            left[c] = 1;
+        std::vector<int> kept;
+        for (int c : cs)
+            if (left[c])
+                kept.push_back(c);
+        cs.swap(kept);
     }
 
     // single_indel_proposals (model.jl:538-562) -> clu[c].seeds; clusters whose
@@ -662,6 +687,8 @@ struct Driver {
     // a cluster whose upload fails keeps its error.
     void set_consensus(std::vector<int> &cs)
     {
+        for (int c : cs)
+            clu[c].ref_a_ok = false;
         batched(cs, [&](const std::vector<int> &s) { return upload_templates(s); });
     }
 
@@ -771,6 +798,7 @@ struct Driver {
                 rate *= RP.ref_error_mult;
                 rate = std::min(std::max(rate, 1e-10), 0.5);
                 double thr = 0.0;
+                C.ref_a_ok = false;   // a new reference
                 // the caller builds the reference with log p = log10(rate) and
                 // uploads it (rifrafsequences.jl constructor), returns its threshold
                 if (cb(cb_user, c, 0, rate, &thr) != 0) {
@@ -807,6 +835,7 @@ struct Driver {
                         continue;
                     }
                     double thr = 0.0;
+                    C.ref_a_ok = false;   // new indel scores
                     // the caller rescales the reference's indel scores and re-uploads it
                     if (cb(cb_user, c, 1, (double)C.n_ref_indel_mults, &thr) != 0)
                         fail_cluster(c, "reference callback failed (penalty increase)");
