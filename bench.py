@@ -777,7 +777,8 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                                                  "within 1e-12 relative + 1e-15 absolute",
             "runs_s": runs, "pinned_runs_s": pin_runs,
             "pinned": None if not pin else {
-                "cores": len(pin), "cpus": [int(c) for c in pin], "clusters_per_s": n_all / pin_s,
+                "cores": len(pin), "cpus": [int(c) for c in pin], "cpu_nodes": [cpu_node(c) for c in pin],
+                "home_node": home_node(), "clusters_per_s": n_all / pin_s,
                 "ratio_to_unpinned": elapsed / pin_s,
                 "init_exclusive": pin_excl,
                 "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(same_pin),
@@ -821,16 +822,55 @@ def cpu_busy(cpus, dt=0.3):
     return busy
 
 
+def cpu_node(c):
+    """NUMA node of cpu c (sysfs), or -1."""
+    try:
+        for name in os.listdir(f"/sys/devices/system/cpu/cpu{c}"):
+            if name.startswith("node") and name[4:].isdigit():
+                return int(name[4:])
+    except OSError:
+        pass
+    return -1
+
+
+def home_node():
+    """NUMA node holding most of this process's resident pages
+    (/proc/self/numa_maps), else that of the cpu its main thread last ran
+    on, or -1."""
+    pages = {}
+    try:
+        with open("/proc/self/numa_maps") as f:
+            for line in f:
+                for tok in line.split():
+                    if tok[0] == "N" and "=" in tok and tok[1:tok.index("=")].isdigit():
+                        n = int(tok[1:tok.index("=")])
+                        pages[n] = pages.get(n, 0) + int(tok[tok.index("=") + 1:])
+    except (OSError, ValueError):
+        pages = {}
+    if pages:
+        return max(pages, key=pages.get)
+    try:
+        with open("/proc/self/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return cpu_node(int(fields[36]))   # field 39: processor
+    except (OSError, ValueError, IndexError):
+        return -1
+
+
 def idle_cpus(allowed, k, dist=None):
-    """The k idlest of the rank's allowed cpus (the GPU box's host is shared:
-    its first cpus carry other work, r06v's pinned passes on cpus 0-1 ran
-    0.17 - 0.32 s); with a process group, ranks take disjoint sets in rank
-    order from the gathered measurements."""
+    """The k idlest of the rank's allowed cpus on its home NUMA node (the GPU
+    box's host is shared: its first cpus carry other work, r06v's pinned
+    passes on cpus 0-1 ran 0.17 - 0.32 s; and cpus of another node left the
+    first pinned passes of r06w / r07f at 0.25 - 0.41 s against 0.18 - 0.20 s
+    for the later ones, its host buffers being remote until they migrate);
+    with a process group, ranks take disjoint sets in rank order from the
+    gathered measurements."""
     try:
         busy = cpu_busy(allowed)
     except OSError:
         busy = {c: 0.0 for c in allowed}
-    order = sorted(allowed, key=lambda c: (busy[c], c))
+    home = home_node()
+    order = sorted(allowed, key=lambda c: (home >= 0 and cpu_node(c) != home, busy[c], c))
     if dist is None:
         return order[:k]
     lists = [None] * dist.get_world_size()
