@@ -3714,33 +3714,51 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             e0 = min(max((d0 >> 1) - wd / 2, 0), P - wd);
             const int nrow = khi - klo + 1, na = nrow * wd;
             wave_sync();                               // every lane is done with the old window
-            // element t = row * wd + col, t = lane + 64 u: incremental row / col
-            const int qr = 64 / wd, rr = 64 % wd;
-            int row = lane / wd, col = lane % wd;
-            for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
-                double v[BTW_CHUNK];
-                int rw = row, cl = col;
+            if (wd == 8 && na == BTW_A) {
+                // a whole window of 8-element rows (the common case): lane =
+                // 8 rows x 8 columns per u, so each load is the previous one's
+                // address plus 8 rows and each LDS slot an immediate offset
+                // (round 6: the generic loop spent ~10 instructions per element)
+                const double *src = A + (size_t)(klo + (lane >> 3)) * P + e0 + (lane & 7);
+                const size_t step = (size_t)8 * P;
+                for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
+                    double v[BTW_CHUNK];
 #pragma unroll
-                for (int u = 0; u < BTW_CHUNK; ++u) {  // issue all loads of the chunk
-                    const int t = lane + 64 * (u0 + u);
-                    v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
-                    rw += qr;
-                    cl += rr;
-                    if (cl >= wd) {
-                        cl -= wd;
-                        ++rw;
+                    for (int u = 0; u < BTW_CHUNK; ++u)
+                        v[u] = src[(size_t)(u0 + u) * step];
+#pragma unroll
+                    for (int u = 0; u < BTW_CHUNK; ++u)
+                        sA[lane + 64 * (u0 + u)] = v[u];
+                }
+            } else {
+                // element t = row * wd + col, t = lane + 64 u: incremental row / col
+                const int qr = 64 / wd, rr = 64 % wd;
+                int row = lane / wd, col = lane % wd;
+                for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
+                    double v[BTW_CHUNK];
+                    int rw = row, cl = col;
+#pragma unroll
+                    for (int u = 0; u < BTW_CHUNK; ++u) {   // issue all loads of the chunk
+                        const int t = lane + 64 * (u0 + u);
+                        v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
+                        rw += qr;
+                        cl += rr;
+                        if (cl >= wd) {
+                            cl -= wd;
+                            ++rw;
+                        }
                     }
-                }
 #pragma unroll
-                for (int u = 0; u < BTW_CHUNK; ++u) {
-                    const int t = lane + 64 * (u0 + u);
-                    if (t < na)
-                        sA[t] = v[u];
+                    for (int u = 0; u < BTW_CHUNK; ++u) {
+                        const int t = lane + 64 * (u0 + u);
+                        if (t < na)
+                            sA[t] = v[u];
+                    }
+                    row = rw;
+                    col = cl;
+                    if (64 * (u0 + BTW_CHUNK) >= na)      // lane 0 holds the chunk's lowest t
+                        break;
                 }
-                row = rw;
-                col = cl;
-                if (64 * (u0 + BTW_CHUNK) >= na)     // lane 0 holds the chunk's lowest t
-                    break;
             }
             wave_sync();
         }
