@@ -92,8 +92,7 @@ const char *rf_last_error(const rf_ctx *ctx);
 #define RF_OPT_DP_NP8      11   /* 0: H 128..255 bands in k_dp<64> instead of k_dpr<8> */
 #define RF_OPT_DP_NP8_LEAN 12   /* 0: k_dpr<8> general steps only                      */
 #define RF_OPT_DP_STREAMS  13   /* 0: DP classes serialised on the context stream      */
-#define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 16 or 32 KB; 0 (default)
-                                   auto: 32 for launches of at most 64 walks    */
+#define RF_OPT_BT_WIN_KB   15   /* k_bt_win A-window LDS: 16 (default) or 32 KB        */
 #define RF_OPT_STAGE_KB    16   /* rf_set_sequences host staging chunk, KB of tables   */
 #define RF_OPT_BAND_PAD    17   /* an rf_realign call whose widest band has H >= value
                                     lays out all its bands with kappa rows of whole

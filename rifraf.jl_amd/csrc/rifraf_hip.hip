@@ -3666,7 +3666,6 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 constexpr int BTW_WD = BTW_WD_ELEMS;   // staged elements per kappa row when P > BTW_WD (>= 6: codon boxes)
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
 constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
-constexpr int BTW_FEW = 64;    // RF_OPT_BT_WIN_KB auto: launches of at most this many walks take 32 KB
 
 template <int BTW_A>   // doubles of the A window (4096: 32 KB, 2048: 16 KB)
 __global__ void __launch_bounds__(64)
@@ -4547,8 +4546,7 @@ struct Opts {
                                      // bit 1: H 64..127 in 32 lanes)
     int band_pad_h = 64;    // RF_OPT_BAND_PAD: a realign call whose widest band has H >= this gets
                             // 128-B-line rows for all its bands (0: never, 1: always)
-    int bt_win_kb = 0;      // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS; 0 auto: 32 for
-                            // launches of at most BTW_FEW walks, 16 otherwise)
+    int bt_win_kb = 16;     // RF_OPT_BT_WIN_KB: k_bt_win A window (16 or 32 KB of LDS)
     int stage_kb = 262144;  // RF_OPT_STAGE_KB: rf_set_sequences staging chunk (KB of tables)
     int dp_psplit = -1;     // RF_OPT_DP_PSPLIT: lean stride-class split mask (-1 auto)
     int dp_np8 = 1;         // RF_OPT_DP_NP8: H 128..255 in k_dpr<8> (0: k_dp<64>)
@@ -6303,11 +6301,7 @@ static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d
     if (!win.empty()) {
         if (int e = upload(ctx, ctx->scratch[16], win))
             return e;
-        // a launch of few walks (the reference's, edit_distance's) is one
-        // latency-bound wave each: the 32-KB window halves its re-stages; many
-        // walks keep the 16-KB window (occupancy; round 4)
-        const int kb = ctx->opt.bt_win_kb ? ctx->opt.bt_win_kb : (win.size() <= (size_t)BTW_FEW ? 32 : 16);
-        auto kern = kb == 16 ? k_bt_win<2048> : k_bt_win<4096>;
+        auto kern = ctx->opt.bt_win_kb == 16 ? k_bt_win<2048> : k_bt_win<4096>;
         hipLaunchKernelGGL(kern, dim3((unsigned)win.size()), dim3(64), 0, ctx->stream,
                            (const BTTask *)ctx->scratch[16].p, (const uint8_t *)ctx->bytes_arena.d,
                            (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d,
