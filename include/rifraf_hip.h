@@ -137,6 +137,9 @@ const char *rf_last_error(const rf_ctx *ctx);
                                    moves (edit_distance's) filled across CUs in
                                    slices that hand off every 32 anti-diagonals
                                    (k_dpm); 0: one workgroup per band (k_dp)    */
+#define RF_OPT_BT_NW       31   /* 4 (default): a backtrace launch of at most 64
+                                   walks runs each on 4 waves (k_bt_win<4096, 4>,
+                                   a 252-cell box); 1: one wave per walk        */
 /* Keys 3, 5-8, 14 and 20 selected scorer variants measured slower and removed
    in round 3 (k_score_lean, the 128-lane k_score_ws, k_score_seg /
    k_score_segc, 16-diagonal k_score_segl, the unspecialised k_score_w2);

@@ -3623,7 +3623,7 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 // The walk is sequential, so the wave parallelises it across a "box" of the
 // cells it can reach next: from the current cell (ii0, jj0) lane l computes
 // the move of cell (ii0 - di, jj0 - dj), di = l / 3, dj = di - (l % 3 - 1),
-// i.e. the 3 band diagonals around the walk's diagonal for BT_DMAX + 1 steps
+// i.e. the 3 band diagonals around the walk's diagonal for 21 steps
 // (63 cells).  Each move is the first strictly-best candidate over the
 // stored A values (align.jl:77-104, the same FP64 sums as the forward fill),
 // so it equals the trace band's move.  The walk then follows the box with
@@ -3665,20 +3665,39 @@ __global__ void k_gather(int64_t nprops, const int32_t *__restrict__ pgroup,
 #endif
 constexpr int BTW_WD = BTW_WD_ELEMS;   // staged elements per kappa row when P > BTW_WD (>= 6: codon boxes)
 constexpr int BTW_T = 256;     // staged table rows / template bases per window
-constexpr int BT_DMAX = 20;    // box depth: cells di = 0 .. BT_DMAX (3 diagonals)
 
-template <int BTW_A>   // doubles of the A window (4096: 32 KB, 2048: 16 KB)
-__global__ void __launch_bounds__(64)
+// NW > 1 (round 6): a launch of few walks (the reference's, edit_distance's:
+// one latency-bound walk each) gives each walk NW waves and a box of
+// 3 x (21 NW) cells; the rank's successor tables go through LDS with a block
+// barrier per round (8 rounds for 252 cells) and the results are broadcast
+// through LDS.  A box then carries ~4x the moves for ~2x the round latency.
+constexpr int BTW_FEW = 64;    // launches of at most this many walks take NW = 4
+
+template <int BTW_A, int NW = 1>   // doubles of the A window (4096: 32 KB, 2048: 16 KB); waves per walk
+__global__ void __launch_bounds__(64 * NW)
 k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, const double *__restrict__ tabs,
          const double *__restrict__ bands, int8_t *__restrict__ moves, int32_t *__restrict__ nmoves,
          int32_t *__restrict__ nerr, int *__restrict__ err, uint8_t *__restrict__ mask, int do_indels)
 {
+    constexpr int NT = 64 * NW;                         // threads: box cells + the sink
+    constexpr int BD = 21 * NW - 1;                     // box depth: cells di = 0 .. BD (3 diagonals)
+    constexpr int TT = NW == 1 ? BTW_T : 2 * BTW_T;     // staged table rows / template bases
+    constexpr int RB = NW == 1 ? 6 : (NW == 2 ? 7 : 8); // doubling rounds: log2(NT)
+    static_assert(NW == 1 || NW == 2 || NW == 4, "1, 2 or 4 waves per walk");
+    constexpr int NX = NW > 1 ? NT : 1;                 // LDS rank arrays (NW > 1 only)
     __shared__ double sA[BTW_A];
-    __shared__ double sTm[BTW_T], sTx[BTW_T], sTi[BTW_T], sTd[BTW_T];
-    __shared__ double sTci[BTW_T], sTcd[BTW_T];   // codon tables (codon alignments only)
-    __shared__ uint8_t sS[BTW_T], sTt[BTW_T];
+    __shared__ double sTm[TT], sTx[TT], sTi[TT], sTd[TT];
+    __shared__ double sTci[TT], sTcd[TT];   // codon tables (codon alignments only)
+    __shared__ uint8_t sS[TT], sTt[TT];
+    __shared__ int sJ[2][NX], sPk[NX], sMv[NX], sNi[NX], sNj[NX], sCnt[NW];
     const BTTask T = tasks[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    auto bsync = [&]() {
+        if constexpr (NW == 1)
+            wave_sync();
+        else
+            __syncthreads();
+    };
     const double *A = bands + T.A;
     const uint8_t *s = bases + T.sb;
     const uint8_t *tt = bases + T.tb;
@@ -3695,9 +3714,9 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
     const double *t_cdel = t_cins + T.ncins;           // cdel[ii], ncdel = n + 1 entries
     int8_t *out = moves + T.out;
     uint8_t *mk = mask ? mask + T.mask : nullptr;
-    // this lane's box cell offsets
-    const int bdi = lane / 3, bdj = bdi - (lane % 3 - 1);
-    const bool blane = lane < 3 * (BT_DMAX + 1);
+    // this thread's box cell offsets
+    const int bdi = tid / 3, bdj = bdi - (tid % 3 - 1);
+    const bool blane = tid < 3 * (BD + 1);
     int ii = n, jj = m, cnt = 0, errs = 0;
     int klo = -1, e0 = 0;                              // A window: rows [klo, klo + W), elements [e0, e0 + wd)
     int q0 = -1, r0 = -1;                              // table rows [q0, q0 + BTW_T), bases [r0, r0 + BTW_T)
@@ -3706,40 +3725,41 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         // ---- windows for the box at (ii, jj)
         const int kap0 = ii + jj + c;                  // kappa of the current cell
         const int d0 = ii - jj + c;
-        const int klo_need = max(kap0 - 2 * BT_DMAX - 3 - ext, 0);
+        const int klo_need = max(kap0 - 2 * BD - 3 - ext, 0);
         const int elo = max(d0 - 2 - ext, 0) >> 1, ehi = min(d0 + 2 + ext, H - 1) >> 1;
         if (klo < 0 || klo_need < klo || elo < e0 || ehi >= e0 + wd) {
             const int khi = min(kap0 - 1, K - 1);
             klo = max(0, khi - W + 1);
             e0 = min(max((d0 >> 1) - wd / 2, 0), P - wd);
             const int nrow = khi - klo + 1, na = nrow * wd;
-            wave_sync();                               // every lane is done with the old window
+            bsync();                                   // every thread is done with the old window
             if (wd == 8 && na == BTW_A) {
-                // a whole window of 8-element rows (the common case): lane =
-                // 8 rows x 8 columns per u, so each load is the previous one's
-                // address plus 8 rows and each LDS slot an immediate offset
-                // (round 6: the generic loop spent ~10 instructions per element)
-                const double *src = A + (size_t)(klo + (lane >> 3)) * P + e0 + (lane & 7);
-                const size_t step = (size_t)8 * P;
-                for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
+                // a whole window of 8-element rows (the common case): thread =
+                // NT / 8 rows x 8 columns per u, so each load is the previous
+                // one's address plus NT / 8 rows and each LDS slot an immediate
+                // offset (round 6: the generic loop spent ~10 instructions per
+                // element)
+                const double *src = A + (size_t)(klo + (tid >> 3)) * P + e0 + (tid & 7);
+                const size_t step = (size_t)(NT / 8) * P;
+                for (int u0 = 0; u0 < BTW_A / NT; u0 += BTW_CHUNK) {
                     double v[BTW_CHUNK];
 #pragma unroll
                     for (int u = 0; u < BTW_CHUNK; ++u)
                         v[u] = src[(size_t)(u0 + u) * step];
 #pragma unroll
                     for (int u = 0; u < BTW_CHUNK; ++u)
-                        sA[lane + 64 * (u0 + u)] = v[u];
+                        sA[tid + NT * (u0 + u)] = v[u];
                 }
             } else {
-                // element t = row * wd + col, t = lane + 64 u: incremental row / col
-                const int qr = 64 / wd, rr = 64 % wd;
-                int row = lane / wd, col = lane % wd;
-                for (int u0 = 0; u0 < BTW_A / 64; u0 += BTW_CHUNK) {
+                // element t = row * wd + col, t = tid + NT u: incremental row / col
+                const int qr = NT / wd, rr = NT % wd;
+                int row = tid / wd, col = tid % wd;
+                for (int u0 = 0; u0 < BTW_A / NT; u0 += BTW_CHUNK) {
                     double v[BTW_CHUNK];
                     int rw = row, cl = col;
 #pragma unroll
                     for (int u = 0; u < BTW_CHUNK; ++u) {   // issue all loads of the chunk
-                        const int t = lane + 64 * (u0 + u);
+                        const int t = tid + NT * (u0 + u);
                         v[u] = t < na ? A[(size_t)(klo + rw) * P + e0 + cl] : 0.0;
                         rw += qr;
                         cl += rr;
@@ -3750,29 +3770,29 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                     }
 #pragma unroll
                     for (int u = 0; u < BTW_CHUNK; ++u) {
-                        const int t = lane + 64 * (u0 + u);
+                        const int t = tid + NT * (u0 + u);
                         if (t < na)
                             sA[t] = v[u];
                     }
                     row = rw;
                     col = cl;
-                    if (64 * (u0 + BTW_CHUNK) >= na)      // lane 0 holds the chunk's lowest t
+                    if (NT * (u0 + BTW_CHUNK) >= na)      // thread 0 holds the chunk's lowest t
                         break;
                 }
             }
-            wave_sync();
+            bsync();
         }
-        const int qlo_need = max(ii - BT_DMAX - 1 - ext, 0), rlo_need = max(jj - BT_DMAX - 2, 0);
-        if (q0 < 0 || qlo_need < q0 || rlo_need < r0 || ii > q0 + BTW_T - 1 || max(jj - 1, 0) > r0 + BTW_T - 1) {
-            q0 = max(0, ii - BTW_T + 1);               // del index ii .. ; ks = ii - 1 ..
-            r0 = max(0, max(jj - 1, 0) - BTW_T + 1);
-            wave_sync();
-            constexpr int NU = BTW_T / 64;
+        const int qlo_need = max(ii - BD - 1 - ext, 0), rlo_need = max(jj - BD - 2, 0);
+        if (q0 < 0 || qlo_need < q0 || rlo_need < r0 || ii > q0 + TT - 1 || max(jj - 1, 0) > r0 + TT - 1) {
+            q0 = max(0, ii - TT + 1);                  // del index ii .. ; ks = ii - 1 ..
+            r0 = max(0, max(jj - 1, 0) - TT + 1);
+            bsync();
+            constexpr int NU = TT / NT;
             double vm[NU], vx[NU], vi[NU], vd[NU];
             int vs[NU], vt[NU];
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const int q = q0 + lane + 64 * u;
+                const int q = q0 + tid + NT * u;
                 const int ks = min(q, n - 1);
                 const int qd = min(q, n);
                 vm[u] = tb[ks];
@@ -3780,12 +3800,12 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
                 vi[u] = tb[2 * (size_t)n + ks];
                 vd[u] = tb[3 * (size_t)n + qd];
                 vs[u] = q < n ? s[q] : 4;
-                const int r = r0 + lane + 64 * u;
+                const int r = r0 + tid + NT * u;
                 vt[u] = r < m ? tt[r] : 4;
             }
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const int e = lane + 64 * u;
+                const int e = tid + NT * u;
                 sTm[e] = vm[u];
                 sTx[e] = vx[u];
                 sTi[e] = vi[u];
@@ -3796,17 +3816,17 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             if (cod) {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    const int q = q0 + lane + 64 * u;
+                    const int q = q0 + tid + NT * u;
                     vm[u] = T.ncins > 0 ? t_cins[min(q, T.ncins - 1)] : 0.0;
                     vx[u] = T.ncdel > 0 ? t_cdel[min(q, T.ncdel - 1)] : 0.0;
                 }
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    sTci[lane + 64 * u] = vm[u];
-                    sTcd[lane + 64 * u] = vx[u];
+                    sTci[tid + NT * u] = vm[u];
+                    sTcd[tid + NT * u] = vx[u];
                 }
             }
-            wave_sync();
+            bsync();
         }
         // ---- box: the move of cell (ci, cj), packed mv | mismatch << 3 | read base << 4.
         // Branch-free: every LDS read is issued at a selected (valid) index and
@@ -3872,39 +3892,78 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
         // same moves, marks, error counts and failure points as the
         // sequential walk (git history).
         {
-            constexpr int SINK = 63;
+            constexpr int SINK = NT - 1;
             const int mv0 = pack & 7;
-            const int bu = lane % 3 - 1;
+            const int bu = tid % 3 - 1;
             const int ndi = bdi + (int)((mv0 == 1) | (mv0 == 2));
             const int nu = bu + (int)(mv0 == 2) - (int)(mv0 == 3);
-            const bool inbox = (mv0 >= 1 && mv0 <= 3) && ndi <= BT_DMAX && nu >= -1 && nu <= 1;
+            const bool inbox = (mv0 >= 1 && mv0 <= 3) && ndi <= BD && nu >= -1 && nu <= 1;
             const int ti = ii - ndi, tj = jj - (ndi - nu);
             int J = (blane && inbox && (ti > 0 || tj > 0)) ? ndi * 3 + nu + 1 : SINK;
-            if (lane == SINK)
+            if (tid == SINK)
                 J = SINK;
-            int cell = 1;   // lane k: the k-th cell of the walk
+            int cell = 1;   // thread k: the k-th cell of the walk
+            int pk;
+            if constexpr (NW == 1) {
 #pragma unroll
-            for (int r = 0; r < 6; ++r) {
-                const int nx = __builtin_amdgcn_ds_bpermute(cell << 2, J);
-                if (r < 5)
-                    J = __builtin_amdgcn_ds_bpermute(J << 2, J);
-                cell = ((lane >> r) & 1) ? nx : cell;
+                for (int r = 0; r < RB; ++r) {
+                    const int nx = __builtin_amdgcn_ds_bpermute(cell << 2, J);
+                    if (r < RB - 1)
+                        J = __builtin_amdgcn_ds_bpermute(J << 2, J);
+                    cell = ((lane >> r) & 1) ? nx : cell;
+                }
+                pk = __builtin_amdgcn_ds_bpermute(cell << 2, pack);
+            } else {
+                // the same rounds through LDS (two tables, a block barrier each)
+                sPk[tid] = pack;
+                sJ[0][tid] = J;
+                bsync();
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int nx = sJ[r & 1][cell];
+                    if (r < RB - 1) {
+                        J = sJ[r & 1][J];
+                        sJ[(r + 1) & 1][tid] = J;
+                    }
+                    cell = ((tid >> r) & 1) ? nx : cell;
+                    bsync();
+                }
+                pk = sPk[cell];
             }
             // cells reached; a cell with no move (mv 0) ends the walk in failure
-            const int pk = __builtin_amdgcn_ds_bpermute(cell << 2, pack);
             const bool visited = cell != SINK;
-            const int nvis = __popcll(__ballot(visited));
             const int mvk = pk & 7;
-            const bool nomove_last = __builtin_amdgcn_readlane(mvk, max(nvis - 1, 0)) == 0;
+            const int cdi = cell / 3, cdu = cell % 3 - 1;
+            const int ci = ii - cdi, cj = jj - (cdi - cdu);
+            // the cell after this move
+            const int di = (mvk == 1 || mvk == 2) ? 1 : (mvk == 4 ? 3 : 0);
+            const int dj = (mvk == 1 || mvk == 3) ? 1 : (mvk == 5 ? 3 : 0);
+            int nvis;
+            bool nomove_last;
+            if constexpr (NW == 1) {
+                nvis = __popcll(__ballot(visited));
+                nomove_last = __builtin_amdgcn_readlane(mvk, max(nvis - 1, 0)) == 0;
+            } else {
+                const int cw = __popcll(__ballot(visited));
+                if (lane == 0)
+                    sCnt[wv] = cw;
+                sMv[tid] = mvk;
+                sNi[tid] = ci - di;
+                sNj[tid] = cj - dj;
+                bsync();
+                nvis = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    nvis += sCnt[w];
+                nomove_last = sMv[max(nvis - 1, 0)] == 0;
+            }
             int nmv = nomove_last ? nvis - 1 : nvis;
             bool fail_now = nomove_last;
             if (cnt + nmv > n + m) {   // the sequential walk's cnt >= n + m check
                 nmv = n + m - cnt;
                 fail_now = true;
             }
-            const bool emit = lane < nmv;
-            const int cdi = cell / 3, cdu = cell % 3 - 1;
-            const int ci = ii - cdi, cj = jj - (cdi - cdu);
+            const bool emit = tid < nmv;
             const int ksb = pk >> 4;
             const bool mism = pk & 8;
             // the forward step of this move ends at (ci, cj) (moves_to_proposals):
@@ -3913,27 +3972,40 @@ k_bt_win(const BTTask *__restrict__ tasks, const uint8_t *__restrict__ bases, co
             const bool mark = emit && mk && ((mvk == 1 && mism) || (do_indels && (mvk == 2 || mvk == 3)));
             const int slot9 = cj * 9 + (mvk == 1 ? ksb : (mvk == 2 ? 5 + ksb : 4));
             if (emit)
-                out[n + m - 1 - (cnt + lane)] = (int8_t)mvk;
+                out[n + m - 1 - (cnt + tid)] = (int8_t)mvk;
             if (mark)
                 mk[(size_t)slot9] = 1;
-            // count_errors: 1 per mismatch or indel, 3 per codon move
+            // count_errors: 1 per mismatch or indel, 3 per codon move (this
+            // wave's threads; the waves' sums are added at the end)
             errs += __popcll(__ballot(emit && (mvk >= 2 || mism))) + 2 * __popcll(__ballot(emit && mvk >= 4));
             if (nmv > 0) {
-                // the cell after the last move
-                const int di = (mvk == 1 || mvk == 2) ? 1 : (mvk == 4 ? 3 : 0);
-                const int dj = (mvk == 1 || mvk == 3) ? 1 : (mvk == 5 ? 3 : 0);
-                ii = __builtin_amdgcn_readlane(ci - di, nmv - 1);
-                jj = __builtin_amdgcn_readlane(cj - dj, nmv - 1);
+                if constexpr (NW == 1) {
+                    ii = __builtin_amdgcn_readlane(ci - di, nmv - 1);
+                    jj = __builtin_amdgcn_readlane(cj - dj, nmv - 1);
+                } else {
+                    ii = sNi[nmv - 1];
+                    jj = sNj[nmv - 1];
+                }
             }
             cnt += nmv;
             if (fail_now) {
-                if (lane == 0)
+                if (tid == 0)
                     set_err(err, 2);  // failed to find a move
                 failed = 1;
             }
         }
     }
-    if (lane == 0) {
+    if constexpr (NW > 1) {
+        bsync();
+        if (lane == 0)
+            sCnt[wv] = errs;
+        bsync();
+        errs = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            errs += sCnt[w];
+    }
+    if (tid == 0) {
         nmoves[T.idx] = cnt;
         nerr[T.idx] = errs;
     }
@@ -4562,6 +4634,7 @@ struct Opts {
     int seg_wgs = 262144;   // RF_OPT_SEG_WGS: split-mode k_score_segl takes reads in chunks so that about
                             // this many workgroups remain
     int dp_mc = 1;          // RF_OPT_DP_MC: H > 2040 bands without codon moves in k_dpm (0: k_dp)
+    int bt_nw = 4;          // RF_OPT_BT_NW: waves per walk in launches of at most BTW_FEW walks (4 or 1)
     int dp_pfit = 1;        // RF_OPT_DP_PFIT: lean NP >= 2 class launched at its tasks' stride class
     int dp_lat = 2048;      // RF_OPT_DP_LAT: a call with at most this many lean H <= 127 tasks runs them all as
                             // one k_dpx launch (latency mode: the launch cannot fill the GPU)
@@ -4932,6 +5005,7 @@ void load_env_opts(Opts &o)
     o.seg_wgs = env_int("RIFRAF_SEG_WGS", o.seg_wgs);
     o.dp_pfit = env_int("RIFRAF_DP_PFIT", o.dp_pfit);
     o.dp_mc = env_int("RIFRAF_DP_MC", o.dp_mc);
+    o.bt_nw = env_int("RIFRAF_BT_NW", o.bt_nw);
 }
 
 ScorePick pick_scorer(const Opts &o, const std::vector<ScoreRead> &reads, bool all_finite)
@@ -5142,6 +5216,7 @@ static int *opt_slot(rf_ctx *ctx, int32_t key)
     case RF_OPT_SEG_WGS: return &o.seg_wgs;
     case RF_OPT_DP_PFIT: return &o.dp_pfit;
     case RF_OPT_DP_MC: return &o.dp_mc;
+    case RF_OPT_BT_NW: return &o.bt_nw;
     default: return nullptr;
     }
 }
@@ -6301,8 +6376,11 @@ static int launch_backtraces(rf_ctx *ctx, std::vector<BTTask> &tasks, uint8_t *d
     if (!win.empty()) {
         if (int e = upload(ctx, ctx->scratch[16], win))
             return e;
-        auto kern = ctx->opt.bt_win_kb == 16 ? k_bt_win<2048> : k_bt_win<4096>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)win.size()), dim3(64), 0, ctx->stream,
+        // a launch of few walks (the reference's, edit_distance's: one
+        // latency-bound walk each) runs each walk on 4 waves (NW = 4)
+        const bool few = win.size() <= (size_t)BTW_FEW && ctx->opt.bt_nw != 1;
+        auto kern = few ? k_bt_win<4096, 4> : ctx->opt.bt_win_kb == 16 ? k_bt_win<2048> : k_bt_win<4096>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)win.size()), dim3(few ? 256 : 64), 0, ctx->stream,
                            (const BTTask *)ctx->scratch[16].p, (const uint8_t *)ctx->bytes_arena.d,
                            (const double *)ctx->tab_arena.d, (const double *)ctx->band_arena.d,
                            (int8_t *)ctx->scratch[3].p, d_cnt, d_cnt + nslots, ctx->d_err, d_mask, do_indels);

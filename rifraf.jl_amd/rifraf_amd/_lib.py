@@ -76,7 +76,7 @@ OPTIONS = {"score_mode": 1, "score_kernel": 2, "lean_lds_kb": 4, "dp_psplit": 10
            "dp_np8": 11, "dp_np8_lean": 12, "dp_streams": 13, "bt_win_kb": 15, "stage_kb": 16,
            "band_pad": 17, "dp_wide": 18, "aln_sums_host": 19,
            "aln_marks_min": 22, "sync_block": 23, "dp_nl64": 24, "dp_lat": 26,
-           "score_wgs": 27, "seg_wgs": 28, "dp_pfit": 29, "dp_mc": 30}
+           "score_wgs": 27, "seg_wgs": 28, "dp_pfit": 29, "dp_mc": 30, "bt_nw": 31}
 # symbolic values of the enum-like options
 OPTION_VALUES = {"score_mode": {"auto": 0, "fused": 1, "split": 2},
                  "score_kernel": {"auto": 0, "general": 1, "seg": 2, "ws": 3}}

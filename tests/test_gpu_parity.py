@@ -966,14 +966,16 @@ def test_alignment_proposals_device(engine, do_indels):
         np.testing.assert_array_equal(masks[c], exp, err_msg=f"cluster {c}")
 
 
+@pytest.mark.parametrize("nw", [4, 1])
 @pytest.mark.parametrize("win_kb,pad", [(32, 64), (16, 64), (16, 1)])
 @pytest.mark.parametrize("L,bw,skew", [(700, 9, 0), (400, 40, 30), (300, 120, -40), (260, 9, 60), (90, 3, 0)])
-def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
-    """k_bt_win (wave per read, LDS windows of kappa rows, re-staged as the
-    walk leaves them) against the oracle's backtrace and count_errors, and the
-    fused proposal marking against the host moves_to_proposals union, on long
-    reads (many windows), wide bands (small windows: P up to 129) and reads
-    longer / shorter than the template."""
+def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad, nw):
+    """k_bt_win (LDS windows of kappa rows, re-staged as the walk leaves
+    them) against the oracle's backtrace and count_errors, and the fused
+    proposal marking against the host moves_to_proposals union, on long reads
+    (many windows), wide bands (small windows: P up to 129) and reads longer /
+    shorter than the template; a walk on 4 waves (RF_OPT_BT_NW, the default
+    for launches of few walks) and on one."""
     from rifraf_amd.align import moves_to_proposals_np
     rng = np.random.default_rng(L + bw)
     t = random_seq(L, rng)
@@ -994,6 +996,7 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
     opts("bt_win_kb", win_kb)
+    opts("bt_nw", nw)
     got, nerr = engine.backtrace(np.arange(n))
     exp_mask = np.zeros((L + 1, 9), np.uint8)
     for k, s in enumerate(seqs):
@@ -1006,8 +1009,9 @@ def test_backtrace_windowed(engine, opts, L, bw, skew, win_kb, pad):
     np.testing.assert_array_equal(engine.alignment_proposals([np.arange(n)], True)[0], exp_mask)
 
 
+@pytest.mark.parametrize("nw", [4, 1])
 @pytest.mark.parametrize("L,bw,codon", [(90, 9, True), (400, 70, True), (700, 150, False), (520, 140, True)])
-def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
+def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon, nw):
     """Round 4: k_bt_win also walks codon alignments (reference-style tables:
     TRACE_CODON_INSERT / _DELETE leave the box, the windows cover the +-3
     predecessors) and bands of any height (H = 301 .. 281 here, above the old
@@ -1033,6 +1037,7 @@ def test_backtrace_windowed_codon_and_wide(engine, opts, L, bw, codon):
     engine.set_sequences(0, seqs)
     engine.set_templates(0, [t])
     engine.realign(np.arange(n), np.arange(n), 0, [bw] * n, RF_FWD | RF_BWD)
+    opts("bt_nw", nw)
     got, nerr = engine.backtrace(np.arange(n))
     exp_mask = np.zeros((L + 1, 9), np.uint8)
     ncod = 0
