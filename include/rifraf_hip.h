@@ -287,15 +287,19 @@ int rf_score_dense_dev(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off,
  * clusters: the INIT stage of every cluster runs in lockstep on this context
  * with one batched engine call per step kind (rifraf_batch.cpp); each
  * cluster ends exactly as a separate rifraf() call would (consensus, score,
- * iteration count).  Scope: no reference, deterministic batches
- * (batch_fixed, or batch_size >= #reads); the caller (rifraf_amd.batch)
- * uploads the reads and initial consensus first and supplies the host
- * values that need the Python mirror's transcendental functions.
+ * iteration count).  The caller (rifraf_amd.batch) uploads the reads and
+ * initial consensus first and supplies the host values that need the Python
+ * mirror's transcendental functions.
  *   read_off[c]..read_off[c+1]: cluster c's reads; read_seq / read_len per
  *     read: its sequence id and length; threshold per read:
  *     cquantile(Poisson(est_n_errors), bandwidth_pvalue) (model.jl:661)
  *   fixed_off / fixed: the fixed batch per cluster (local read indices in
  *     batch order, sortperm of est_n_errors; required if batch_fixed)
+ *   random batches (resample!, model.jl:1038-1066: batch_size below the read
+ *     count without batch_fixed, or in REFINE) are drawn here from
+ *     params->est_n_errors (per read) and params->seed (per cluster), with
+ *     rifraf_amd/resampling.py's RNG and draw; both NULL: such a cluster is
+ *     rejected (RF_ERR_ARG)
  *   slot_base[c]: first of the cluster's batch slots; tpl_id[c]: its template
  *   cons / cons_off: the initial consensus per cluster (already uploaded)
  * Outputs per cluster: final score, INIT iterations, status (0 = reached
@@ -310,6 +314,10 @@ typedef struct rf_batch_params {
     int32_t batch_fixed;
     int32_t batch_size;              /* params.batch_size (<= 1: every read) */
     double batch_threshold;
+    double batch_randomness;         /* initial state.batch_randomness (model.jl:592) */
+    double batch_mult;               /* its decay per iteration (model.jl:1234-1238) */
+    const double *est_n_errors;      /* per read, or NULL: resample!'s weights */
+    const uint64_t *seed;            /* per cluster, or NULL: the random batches' RNG */
 } rf_batch_params;
 int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *params,
                     const int32_t *read_off, const int32_t *read_seq, const int32_t *read_len,
@@ -333,9 +341,7 @@ int rf_rifraf_batch(rf_ctx *ctx, int32_t nclusters, const rf_batch_params *param
  *   event 1 (penalty increase), value = n_ref_indel_mults: rescale the
  *     reference's indel scores by ref_indel_mult^n (model.jl:978-985) and
  *     upload it again.
- * cb returns 0, or nonzero to fail the cluster.  Scope as rf_rifraf_batch,
- * plus: a cluster with a reference and do_refine needs batch_size >= #reads
- * (REFINE resamples at random otherwise). */
+ * cb returns 0, or nonzero to fail the cluster.  Scope as rf_rifraf_batch. */
 typedef struct rf_batch_ref_params {
     int32_t do_frame, do_refine, seed_indels, indel_correction_only;
     int32_t max_ref_indel_mults, pad;

@@ -13,11 +13,11 @@
 // one host thread per cluster; this driver removes that interpreter cost
 // (SURVEY.md §8(f) row 1).
 //
-// Scope: clusters without a reference (the INIT stage converges when no
-// candidate improves the score, model.jl:937-948) whose batches are
-// deterministic -- the fixed lowest-error batch (batch_fixed) or every read.
-// Random resampling (StatsBase.sample) and the reference-guided FRAME stage
-// stay in the Python stage machine.  Host inputs that need transcendental
+// Scope: every stage but SCORE (rf_rifraf_batch_ref adds FRAME and REFINE
+// for clusters with a reference), fixed, full or random batches.  Random
+// batches (resample!, model.jl:1038-1066) use rifraf_amd/resampling.py's
+// RNG and draw (BatchRng, wsample_norep below), so both stage machines draw
+// the same reads from the same seed.  Host inputs that need transcendental
 // functions (the per-read Poisson thresholds of smart_forward_moves!, the
 // fixed batch order) are computed by the caller with the Python mirror's own
 // code, so no host libm result here can differ from the Python path's.
@@ -31,7 +31,9 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <utility>
 #include <mutex>
+#include <queue>
 #include <string>
 #include <thread>
 #include <vector>
@@ -60,6 +62,128 @@ struct Cand {
     Prop p;
     double score;
 };
+
+// xoshiro256++ seeded by splitmix64; rand() = the top 53 bits
+// (rifraf_amd/resampling.py BatchRng)
+struct BatchRng {
+    uint64_t s[4] = {0, 0, 0, 0};
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    void seed(uint64_t x)
+    {
+        for (int i = 0; i < 4; ++i) {
+            x += 0x9E3779B97F4A7C15ull;
+            uint64_t z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            s[i] = z ^ (z >> 31);
+        }
+    }
+    uint64_t next()
+    {
+        const uint64_t r = rotl(s[0] + s[3], 23) + s[0];
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    double rand() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+// resample!'s random batch (model.jl:1051-1054; resampling.py random_batch):
+// weights 1 - err ./ sum(err), reweight (:1017-1036), then StatsBase 0.31's
+// A-ExpJ draw without replacement (efraimidis_aexpj_wsample_norep!: keys
+// w / Exp(1), exponential jumps, a min-heap of (key, index)); the batch is
+// the n items by descending (key, index).  Sums run in index order; each
+// product is its own statement (no contraction into an FMA); log1p / exp /
+// log are the libm calls CPython's math module makes.  Returns false (the
+// message in `err`) when fewer than n weights are > 0 or one is negative.
+static bool random_batch(BatchRng &rng, const double *est, int n, int k, double randomness,
+                         std::vector<int32_t> &out, std::string &err)
+{
+    double se = 0.0;
+    for (int i = 0; i < n; ++i)
+        se += est[i];
+    std::vector<double> w(n), e(n);
+    for (int i = 0; i < n; ++i)
+        w[i] = 1.0 - est[i] / se;
+    double sw = 0.0;
+    for (int i = 0; i < n; ++i)
+        sw += w[i];
+    for (int i = 0; i < n; ++i)
+        w[i] = w[i] / sw;
+    double weight = 0.0;
+    if (randomness > 0.5) {
+        weight = (randomness - 0.5) * 2.0;
+        for (int i = 0; i < n; ++i)
+            e[i] = 1.0 / n;
+    } else if (randomness < 0.5) {
+        weight = 1.0 - randomness * 2.0;
+        // reverse(sortperm(w))[1:k]: a stable ascending order, read from its end
+        std::vector<int32_t> ord(n);
+        for (int i = 0; i < n; ++i)
+            ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return w[a] < w[b]; });
+        std::fill(e.begin(), e.end(), 0.0);
+        for (int i = 0; i < k; ++i)
+            e[ord[n - 1 - i]] = 1.0 / k;
+    } else {
+        e = w;
+    }
+    const double keep = 1.0 - weight;
+    for (int i = 0; i < n; ++i) {
+        const double a = weight * e[i];
+        const double b = keep * w[i];
+        w[i] = a + b;
+    }
+    auto randexp = [&rng] { return -std::log1p(-rng.rand()); };
+    using Key = std::pair<double, int32_t>;
+    std::priority_queue<Key, std::vector<Key>, std::greater<Key>> pq;   // min-heap of (key, index)
+    int s = 0;
+    for (; s < n && (int)pq.size() < k; ++s) {
+        if (w[s] < 0) {
+            err = "Negative weight found in weight vector at index " + std::to_string(s + 1);
+            return false;
+        }
+        if (w[s] > 0)
+            pq.push({w[s] / randexp(), s});
+    }
+    if ((int)pq.size() < k) {
+        err = "wv must have at least " + std::to_string(k) + " strictly positive entries (got " +
+              std::to_string(pq.size()) + ")";
+        return false;
+    }
+    double threshold = pq.top().first;
+    double x = threshold * randexp();
+    for (int i = s; i < n; ++i) {
+        const double wi = w[i];
+        if (wi < 0) {
+            err = "Negative weight found in weight vector at index " + std::to_string(i + 1);
+            return false;
+        }
+        if (!(wi > 0))
+            continue;
+        x -= wi;
+        if (!(x <= 0))
+            continue;
+        const double t = std::exp(-wi / threshold);
+        const double m = rng.rand() * (1.0 - t);
+        const double key = -wi / std::log(t + m);
+        pq.pop();
+        pq.push({key, i});
+        threshold = pq.top().first;
+        x = threshold * randexp();
+    }
+    out.resize(k);
+    for (int d = k - 1; d >= 0; --d) {   // ascending pops fill the batch from its end
+        out[d] = pq.top().second;
+        pq.pop();
+    }
+    return true;
+}
 
 struct Read {
     int32_t seq = 0, len = 0, bw = 0;
@@ -104,6 +228,8 @@ struct Clu {
     // the reference's bandwidth (smart_forward in FRAME): has_single_indels'
     // align_moves (model.jl:532-536) is the same fill, so its walk reads it
     bool ref_a_ok = false;
+    double batch_randomness = 0.9;              // state.batch_randomness (model.jl:177)
+    BatchRng rng;                               // resample!'s random batches
 };
 
 struct Driver {
@@ -171,13 +297,18 @@ struct Driver {
         cs.swap(ok);
     }
 
-    // ---------------- resample! (model.jl:1038-1066), deterministic cases
+    // ---------------- resample! (model.jl:1038-1066)
     void resample(Clu &C, int c)
     {
         if (P.batch_fixed && (C.stage == ST_INIT || C.stage == ST_FRAME)) {
             C.batch.assign(fixed.begin() + fixed_off[c], fixed.begin() + fixed_off[c + 1]);
+        } else if (C.batch_size < C.nreads) {
+            std::string err;
+            if (!random_batch(C.rng, P.est_n_errors + C.r0, C.nreads, C.batch_size, C.batch_randomness, C.batch,
+                              err))
+                fail_cluster(c, err);
+            C.realign_As = true;
         } else {
-            // batch_size >= #reads (the caller guarantees it): every read
             C.batch.resize(C.nreads);
             for (int k = 0; k < C.nreads; ++k)
                 C.batch[k] = k;
@@ -333,6 +464,8 @@ struct Driver {
         std::vector<int> a, b;
         for (int c : cs) {
             Clu &C = clu[c];
+            if (C.failed)
+                continue;
             while (C.n_slots < (int)C.batch.size()) {   // grow As / Bs (fresh A[end,end] = 0.0)
                 C.slot_scores.push_back(0.0);
                 ++C.n_slots;
@@ -914,9 +1047,16 @@ struct Driver {
             handle_candidates(hc, cands);
             finish_stage(fin);
             std::vector<int> nl;
-            for (int c : act)
-                if (!clu[c].failed && !clu[c].converged && !clu[c].done)
-                    nl.push_back(c);
+            for (int c : act) {
+                Clu &C = clu[c];
+                if (C.failed || C.converged || C.done)
+                    continue;
+                // update batch randomness (model.jl:1217-1226)
+                if ((!P.batch_fixed || (C.stage == ST_REFINE && C.stage_iters[ST_REFINE - 1] > 1)) &&
+                    C.batch_size < C.nreads)
+                    C.batch_randomness *= P.batch_mult;
+                nl.push_back(c);
+            }
             live.swap(nl);
         }
     }
@@ -1013,13 +1153,17 @@ extern "C" int rf_rifraf_batch_ref(rf_ctx *ctx, int32_t nclusters, const rf_batc
         // outside the native driver's scope (the caller checks first)
         const bool ref_ok = !C.has_ref || (refs[c].ref_len > 0 && refs[c].edit_seq >= 0 && refs[c].ref_slot >= 0 &&
                                            refs[c].scratch_slot >= 0);
-        const bool refine_random = C.has_ref && D.RP.do_refine && bs < C.nreads;   // REFINE resamples
+        C.batch_randomness = params->batch_randomness;
+        if (params->seed)
+            C.rng.seed(params->seed[c]);
+        // random batches: below the read count without batch_fixed, or in REFINE
+        const bool random = bs < C.nreads && (!params->batch_fixed || (C.has_ref && D.RP.do_refine));
         const char *why = C.nreads < 1 ? "no reads"
                           : C.cons.empty() ? "empty consensus"
-                          : (!params->batch_fixed && bs < C.nreads) ? "a random batch smaller than the read count"
+                          : (random && (!params->est_n_errors || !params->seed))
+                              ? "a random batch without est_n_errors and seed"
                           : (params->batch_fixed && fixed_off[c + 1] - fixed_off[c] < 1) ? "an empty fixed batch"
                           : !ref_ok ? "an incomplete reference record"
-                          : refine_random ? "a REFINE stage with a random batch"
                           : nullptr;
         if (why)
             return rf_internal_fail(ctx, RF_ERR_ARG,

@@ -87,7 +87,8 @@ class BatchParams(ctypes.Structure):
     """rf_batch_params (include/rifraf_hip.h)."""
     _fields_ = [("max_iters", c_int32), ("min_dist", c_int32), ("bandwidth", c_int32),
                 ("do_alignment_proposals", c_int32), ("batch_fixed", c_int32), ("batch_size", c_int32),
-                ("batch_threshold", c_double)]
+                ("batch_threshold", c_double), ("batch_randomness", c_double), ("batch_mult", c_double),
+                ("est_n_errors", c_void_p), ("seed", c_void_p)]
 
 
 class BatchRefParams(ctypes.Structure):

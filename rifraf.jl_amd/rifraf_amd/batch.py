@@ -30,6 +30,7 @@ import numpy as np
 from .bandedarrays import band_stride
 from .engine import RifrafError
 from .proposals import to_arrays
+from .resampling import cluster_seeds
 from .types import PackedReads
 
 
@@ -262,24 +263,19 @@ def _span(phase, t0):
 
 def native_eligible(clusters, params) -> bool:
     """Whether rf_rifraf_batch(_ref) (rifraf_batch.cpp) can run these
-    clusters: INIT enabled and deterministic batches -- the fixed
-    lowest-error batch or every read (random resampling stays in the Python
-    stage machine).  Clusters with a reference run INIT -> FRAME -> REFINE
-    natively when REFINE (which resamples at random below the read count)
-    sees every read, and the quality pass does not use the reference."""
+    clusters: INIT enabled, fixed, full or random batches (the native driver
+    draws random ones with resampling.py's RNG and draw).  Clusters with a
+    reference run INIT -> FRAME -> REFINE natively when the quality pass does
+    not use the reference."""
     if not params.do_init:
         return False
     for kw in clusters:
         n = len(kw["dnaseqs"])
         if n < 1:
             return False
-        if not params.batch_fixed and 1 < params.batch_size < n:
-            return False
         ref = kw.get("reference")
         if ref is not None and len(ref) > 0:
             if params.do_score and params.use_ref_for_qvs:
-                return False
-            if params.do_refine and 1 < params.batch_size < n:
                 return False
             try:
                 from .model import check_params
@@ -558,7 +554,12 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         # band-doubling realign allocates above them (the arena bump-allocates; a
         # reservation of 1.5x the initial bands grew, and compacted every band,
         # in each c3 run: 1,999 regions, ~1.8 ms of a 45 ms run, r05am trace)
-        nb = np.array([st_.batch_fixed_size if params.batch_fixed else len(st_.sequences) for st_ in states])
+        # batch slots per cluster: the fixed batch and / or the random or full
+        # one (a reference-guided cluster's REFINE follows a fixed INIT / FRAME;
+        # a batch that check_score grows later grows the arena)
+        nb = np.array([max(st_.batch_fixed_size if params.batch_fixed else 0,
+                           st_.batch_size if not params.batch_fixed or (len(refs_in[k]) > 0 and params.do_refine)
+                           else 0) for k, st_ in enumerate(states)])
         # every read's A/B band (upper bound: padded rows), one vector pass; a
         # cluster whose batch is smaller than its reads counts its largest bands
         mcons = np.fromiter((len(st_.consensus) for st_ in states), np.int64, K)
@@ -624,8 +625,15 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         cons = [st_.consensus for st_ in states]
         cons_off = np.zeros(K + 1, np.int64)
         np.cumsum([len(c) for c in cons], out=cons_off[1:])
+        # random batches (resample!): every read's est_n_errors and a seed per
+        # cluster for the driver's RNG (resampling.py); kept alive in `keep`
+        est_c = np.ascontiguousarray(est, np.float64)
+        seeds = cluster_seeds(params.seed, K)
+        keep = (est_c, seeds)
         bp = _lib.BatchParams(params.max_iters, params.min_dist, params.bandwidth, int(params.do_alignment_proposals),
-                              int(params.batch_fixed), params.batch_size, params.batch_threshold)
+                              int(params.batch_fixed), params.batch_size, params.batch_threshold,
+                              states[0].batch_randomness if K else 0.9, params.batch_mult,
+                              est_c.ctypes.data, seeds.ctypes.data)
         ref = _native_refs(part, states, refs_in, params, engine, nall, int(read_off[-1]))
         _span("prep", t_up)
     finally:
@@ -638,6 +646,7 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
                                              cons_off, ref=ref)
         _stat("native_s", time.perf_counter() - t0)
         _span("native", t0)
+    del keep
     t_res = time.perf_counter()
     cb_errors = ref["cb_errors"] if ref is not None else {}
     if coded is not None:                  # CodedRifrafSequence: the shared arrays

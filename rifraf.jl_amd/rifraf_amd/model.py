@@ -28,6 +28,7 @@ from .errormodel import ErrorModel, Scores, phred_to_log_p
 from .poisson import cquantile_poisson
 from .proposals import (DEL, INS, SUB, Deletion, Insertion, Proposal, ScoredProposal, Substitution,
                         apply_proposals, choose_candidates, to_arrays)
+from .resampling import BatchRng, error_weights, reweight, wsample_norep
 from .rifrafsequences import RifrafSequence
 from .types import BASES, CODON_LENGTH, DNASeq, dna_str
 
@@ -217,8 +218,10 @@ def initial_state(consensus, sequences, reference, params: RifrafParams, maxlen=
         if len(reference) > 0 else RifrafSequence()
     return RifrafState(consensus=DNASeq(consensus), ref_scores=params.ref_scores, reference=refseq,
                        batch_fixed_size=batch_fixed_size, batch_size=batch_size,
-                       base_batch_size=batch_size, sequences=sequences, maxlen=maxlen,
-                       batch_randomness=params.batch_randomness)
+                       base_batch_size=batch_size, sequences=sequences, maxlen=maxlen)
+    # batch_randomness keeps RifrafState's default 0.9 (model.jl:177): the
+    # reference's initial_state (:604-614) does not pass params.batch_randomness,
+    # which check_params validates (:887) and nothing else reads
 
 
 def use_ref(ref: RifrafSequence, stage: Stage, use_ref_for_qvs: bool) -> bool:   # :617-628
@@ -530,36 +533,19 @@ def finish_stage(state: RifrafState, run: _Run, params: RifrafParams):   # :937-
         raise RifrafError(f"  invalid stage: {state.stage}")
 
 
-def reweight(wv, n, randomness):                                   # :1017-1036
-    if randomness < 0.0 or randomness > 1.0:
-        raise RifrafError("randomness must be between 0.0 and 1.0")
-    wv = np.asarray(wv, np.float64)
-    wv = wv / wv.sum()
-    indices = np.argsort(wv, kind="stable")[::-1][:n]
-    endpoint = wv
-    weight = 0.0
-    if randomness > 0.5:
-        weight = (randomness - 0.5) * 2.0
-        endpoint = np.full(len(wv), 1.0 / len(wv))
-    elif randomness < 0.5:
-        weight = 1.0 - randomness * 2.0
-        endpoint = np.zeros(len(wv))
-        endpoint[indices] = 1.0 / n
-    return weight * endpoint + (1.0 - weight) * wv
-
-
-def resample(state: RifrafState, params: RifrafParams, rng: np.random.Generator):   # :1038-1066
+def resample(state: RifrafState, params: RifrafParams, rng: BatchRng):   # :1038-1066
     err_weights = np.array([s.est_n_errors for s in state.sequences])
     if state.stage in (Stage.INIT, Stage.FRAME) and params.batch_fixed:
         state.batch_seqs = np.argsort(err_weights, kind="stable")[:state.batch_fixed_size].tolist()
         log(params, 2, "    kept fixed batch")
         return
-    wv = reweight(1.0 - err_weights / err_weights.sum(), state.batch_size, state.batch_randomness)
     n = state.batch_size
+    wv = reweight(error_weights(err_weights), n, state.batch_randomness)
     if n < len(state.sequences):
-        # StatsBase.sample(data, Weights, n, replace=false): weighted sampling
-        # without replacement (RNG stream not reproducible: parity unpinned)
-        state.batch_seqs = rng.choice(len(state.sequences), size=n, replace=False, p=wv / wv.sum()).tolist()
+        # StatsBase.sample(data, Weights, n, replace=false): the draw and the
+        # RNG of resampling.py, which the native driver shares (the batch
+        # Julia's RNG stream would draw is parity-unpinned)
+        state.batch_seqs = wsample_norep(rng, wv, n)
         state.realign_As = True
         log(params, 2, f"    sampled {n} new sequences")
     else:
@@ -910,7 +896,7 @@ def rifraf(dnaseqs, phreds=None, *, error_log_ps=None, consensus=None, reference
     check_params(params.scores, reference, params)
     sequences = [RifrafSequence(s, p, params.bandwidth, params.scores) for s, p in zip(dnaseqs, error_log_ps)]
     state = initial_state(consensus, sequences, reference, params)
-    rng = np.random.default_rng(params.seed)
+    rng = BatchRng(params.seed)
     if engine is None:
         from .align import default_engine
         engine = default_engine()

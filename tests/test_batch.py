@@ -128,7 +128,17 @@ NATIVE_PARAMS = {
     "default": dict(max_iters=60),                                          # fixed batch of 5
     "all_reads_qv": dict(batch_size=0, batch_fixed=False, do_score=True),
     "fixed3_noaln": dict(batch_fixed_size=3, do_alignment_proposals=False, do_score=True, max_iters=4),
+    # random batches (resample!, model.jl:1051-1054): drawn by the native
+    # driver with resampling.py's RNG; the second grows its batch on every
+    # score drop (check_score, model.jl:1092-1101) and resamples there too
+    "random_batch": dict(batch_size=5, batch_fixed=False, seed=7, do_score=True, max_iters=40),
+    "random_grow": dict(batch_size=3, batch_fixed=False, batch_threshold=0.0, seed=3, max_iters=30),
 }
+
+
+def _same_batches(a, b):
+    """The final batch (the reads of the last random draw, in draw order)."""
+    assert [int(i) for i in a.state.batch_seqs] == [int(i) for i in b.state.batch_seqs]
 
 
 @pytest.mark.gpu
@@ -151,28 +161,38 @@ def test_native_batch_matches_hub(run_engine, pset):
     for a, b, c in zip(nat, hub, dqv):
         assert_same_run(summary(a), summary(b))
         assert_same_run(summary(c), summary(b), qv_rtol=QV_RTOL)
+        _same_batches(a, b)
+    if pset == "random_batch":      # drawn below the read count
+        assert sum(len(r.state.batch_seqs) < len(k["dnaseqs"]) for r, k in zip(nat, clusters)) >= 4
+    if pset == "random_grow":       # grown past the initial 3
+        assert any(len(r.state.batch_seqs) > 3 for r in nat)
 
 
 @pytest.mark.gpu
-def test_native_batch_matches_oracle_runs(run_engine):
+@pytest.mark.parametrize("random", [False, True])
+def test_native_batch_matches_oracle_runs(run_engine, random):
     """Native batched clusters against separate rifraf() runs on the CPU
-    oracle engine (reference-free clusters, quality scores on)."""
+    oracle engine (reference-free clusters, quality scores on; random:
+    batches of 4 drawn at random every iteration)."""
     engine = run_engine
     from oracle_engine import OracleEngine
     from rifraf_amd import ErrorModel, Scores
     from rifraf_amd.batch import rifraf_batch
     from rifraf_amd.model import RifrafParams, rifraf
-    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), do_score=True, max_iters=60)
+    extra = dict(batch_size=4, batch_fixed=False, seed=19) if random else {}
+    params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), do_score=True, max_iters=60, **extra)
     clusters = _ref_free_clusters(seed=5)[:5]
-    ref = [summary(rifraf(params=params, engine=OracleEngine(), **kw)) for kw in clusters]
+    ref = [rifraf(params=params, engine=OracleEngine(), **kw) for kw in clusters]
     got = rifraf_batch(clusters, params=params, engine=engine, native=True)
     for r, g in zip(ref, got):
-        assert_same_run(summary(g), r, qv_rtol=QV_RTOL)
+        assert_same_run(summary(g), summary(r), qv_rtol=QV_RTOL)
+        _same_batches(g, r)
 
 
 def test_native_scope():
-    """Clusters with a reference, random resampling or an engine without the
-    native driver take the Python stage machine."""
+    """What takes the Python stage machine: an engine without the native
+    driver, INIT disabled, reference QVs, bad reference scores, empty reads or
+    mismatched quality vectors.  Random batches run natively."""
     from oracle_engine import OracleEngine
     from rifraf_amd.batch import native_eligible, rifraf_batch
     from rifraf_amd.engine import RifrafError
@@ -180,13 +200,12 @@ def test_native_scope():
     clusters = _ref_free_clusters()
     assert native_eligible(clusters, RifrafParams())
     assert native_eligible(clusters, RifrafParams(batch_size=0, batch_fixed=False))
-    assert not native_eligible(clusters, RifrafParams(batch_size=4, batch_fixed=False))
-    # references: native when REFINE (random resampling below the read
-    # count) sees every read and the QV pass does not score the reference
+    assert native_eligible(clusters, RifrafParams(batch_size=4, batch_fixed=False))
+    # references: native unless the QV pass scores the reference
     ref_clusters = _ref_clusters()
     assert native_eligible(ref_clusters, RifrafParams(batch_size=0, batch_fixed=False))
     assert native_eligible(ref_clusters, RifrafParams(batch_size=0))
-    assert not native_eligible(ref_clusters, RifrafParams(batch_size=5))
+    assert native_eligible(ref_clusters, RifrafParams(batch_size=5))
     assert native_eligible(ref_clusters, RifrafParams(batch_size=5, do_refine=False))
     assert not native_eligible(ref_clusters, RifrafParams(batch_size=0, do_score=True, use_ref_for_qvs=True))
     from rifraf_amd import ErrorModel, Scores
@@ -234,6 +253,8 @@ REF_PARAMS = {
     "unseeded_subs": dict(batch_size=0, batch_fixed=False, seed_indels=False, indel_correction_only=False,
                           max_ref_indel_mults=1, do_alignment_proposals=False, max_iters=30),
     "no_refine": dict(batch_size=6, do_refine=False, ref_error_mult=2.0, do_score=True),
+    # the default fixed INIT / FRAME batch, then REFINE's random batches of 6
+    "random_refine": dict(batch_size=6, seed=11, do_score=True),
 }
 
 
@@ -262,11 +283,15 @@ def test_native_reference_batch_matches_hub(run_engine, pset):
         assert a.state.ref_error_rate == b.state.ref_error_rate or (
             np.isinf(a.state.ref_error_rate) and np.isinf(b.state.ref_error_rate))
         assert a.state.reference.bandwidth == b.state.reference.bandwidth
+        _same_batches(a, b)
         frames += a.state.stage_iterations[1] > 0
     assert frames >= 3
     if pset == "throughput_qv":   # the whole FRAME path: penalty increases, then REFINE
         assert any(r.state.n_ref_indel_mults >= 1 for r in nat)
         assert any(r.state.stage_iterations[2] > 0 for r in nat)
+    if pset == "random_refine":   # random REFINE batches below the read count
+        assert any(r.state.stage_iterations[2] > 0 and len(r.state.batch_seqs) < len(k["dnaseqs"])
+                   for r, k in zip(nat, clusters))
 
 
 @pytest.mark.gpu
