@@ -1106,6 +1106,8 @@ def run_matches(res, rec, qv_rtol=1e-12, atol=1e-15):
                                         [np.zeros(0, np.uint8)]), rec["stages"]))
     if not ok:
         return False
+    if "batch" in rec and [int(i) for i in res.state.batch_seqs] != rec["batch"].tolist():
+        return False     # a random batch (resampling.py): the final draw
     if "sub" not in rec:
         return res.error_probs is None
     if res.error_probs is None:
@@ -1212,6 +1214,9 @@ class _StageTimer:
         return out
 
 
+C3_DEFAULT = dict(seed=1, do_score=True)   # scripts/make_golden.py C3_DEFAULT
+
+
 def run_c3(args, gpu):
     """configs[2] end to end (rank 0): one rifraf() run of the 1000-read
     2.6 kb cluster with its frameshifted reference at the throughput settings
@@ -1239,6 +1244,15 @@ def run_c3(args, gpu):
             nat = rifraf_batch([kw], params=params, engine=eng, native=True)[0]
             runs.append(time.perf_counter() - t0)
         native_s = float(np.median(runs))
+        # the default batches: fixed 5 in INIT / FRAME, REFINE's random 20
+        # (drawn in the native driver, resampling.py's RNG), QVs on
+        dparams = model.RifrafParams(**C3_DEFAULT)
+        rifraf_batch([kw], params=dparams, engine=eng, native=True)
+        druns = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            dnat = rifraf_batch([kw], params=dparams, engine=eng, native=True)[0]
+            druns.append(time.perf_counter() - t0)
         timer = _StageTimer(eng)
         model.ITERATION_HOOK = timer.hook
         try:
@@ -1267,6 +1281,14 @@ def run_c3(args, gpu):
                                           "bit-exact (Python stage machine) / within 1e-12 (native driver's "
                                           "device quality pass)"},
             "consensus_equals_template": bool(np.array_equal(nat.consensus, template)),
+            "default": {"params": "RifrafParams(%s)" % ", ".join(f"{k}={v}" for k, v in C3_DEFAULT.items()),
+                        "batches": "fixed 5 lowest-error reads in INIT / FRAME, then REFINE's random batches of "
+                                   "20 drawn by the native driver (rifraf_amd/resampling.py's RNG and draw)",
+                        "native_seconds_per_run": float(np.median(druns)), "native_seconds": druns,
+                        "stage_iterations": list(dnat.state.stage_iterations),
+                        "same_as_oracle": bool(run_matches(dnat, golden_run("c3_default"))),
+                        "fixture": "tests/golden/runs.npz c3_default (the CPU oracle engine's rifraf(); the final "
+                                   "random batch included)"},
             "stage_iterations": list(nat.state.stage_iterations),
             "penalty_increases": int(nat.state.n_ref_indel_mults),
             "kernel_ms_total": tot, "codon_share_of_kernel_ms": tot["codon_ms"] / max(

@@ -131,12 +131,39 @@ def runs():
                  engine=OracleEngine())
     for k, v in run_record(res).items():
         out[f"c3_throughput_{k}"] = v
+    out.update(c3_default_record())
     out["generator"] = np.asarray("scripts/make_golden.py runs() (CPU oracle engine)")
     np.savez_compressed(os.path.join(OUT, "runs.npz"), **out)
+
+
+C3_DEFAULT = dict(seed=1, do_score=True)
+
+
+def c3_default_record():
+    """configs[2] with the default batches: the fixed 5 lowest-error reads in
+    INIT / FRAME, then REFINE's random batches of 20 (resampling.py's RNG,
+    seed 1), QVs on."""
+    sys.path.insert(0, REPO)
+    import bench
+    t, reads, phreds, ref = bench.c3_cluster()
+    res = rifraf(reads, phreds, reference=ref, params=RifrafParams(**C3_DEFAULT), engine=OracleEngine())
+    rec = {f"c3_default_{k}": v for k, v in run_record(res).items()}
+    rec["c3_default_batch"] = np.asarray(res.state.batch_seqs, np.int64)
+    return rec
+
+
+def runs_c3_default():
+    """Add (or replace) the c3_default record of runs.npz, keeping the rest."""
+    path = os.path.join(OUT, "runs.npz")
+    with np.load(path) as z:
+        out = {k: z[k] for k in z.files}
+    out = {k: v for k, v in out.items() if not k.startswith("c3_default_")}
+    out.update(c3_default_record())
+    np.savez_compressed(path, **out)
 
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["pairs", "config2", "runs"]
     for w in what:
-        {"pairs": pairs, "config2": config2, "runs": runs}[w]()
+        {"pairs": pairs, "config2": config2, "runs": runs, "runs_c3_default": runs_c3_default}[w]()
         print("wrote", w)

@@ -125,6 +125,37 @@ def test_oracle_engine_reproduces_runs(variant):
     assert np.array_equal(res.consensus, t)
 
 
+def test_oracle_engine_reproduces_c3_default_run():
+    """runs.npz's c3_default (bench's c3.default field): configs[2] with the
+    default batches -- REFINE draws random batches of 20 (resampling.py) --
+    on the oracle engine, final batch included."""
+    from oracle_engine import OracleEngine
+    from rifraf_amd.model import RifrafParams, rifraf
+    bench, z = _run_fixture()
+    t, reads, phreds, ref = bench.c3_cluster()
+    res = rifraf(reads, phreds, reference=ref, params=RifrafParams(**bench.C3_DEFAULT), engine=OracleEngine())
+    rec = bench.golden_run("c3_default", z)
+    assert bench.run_matches(res, rec, qv_rtol=0)
+    assert res.state.stage_iterations[2] >= 1 and len(rec["batch"]) == 20
+
+
+@pytest.mark.gpu
+def test_engine_reproduces_c3_default_run(run_engine):
+    """The same run through the library's stage machine (its own random
+    draws) and the Python stage machine on the HIP engine."""
+    from rifraf_amd.batch import rifraf_batch
+    from rifraf_amd.model import RifrafParams, rifraf
+    bench, z = _run_fixture()
+    t, reads, phreds, ref = bench.c3_cluster()
+    params = RifrafParams(**bench.C3_DEFAULT)
+    rec = bench.golden_run("c3_default", z)
+    nat = rifraf_batch([dict(dnaseqs=reads, phreds=phreds, reference=ref)], params=params, engine=run_engine,
+                       native=True)[0]
+    assert bench.run_matches(nat, rec)
+    py = rifraf(reads, phreds, reference=ref, params=params, engine=run_engine)
+    assert bench.run_matches(py, rec, qv_rtol=0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["default", "throughput"])
 def test_engine_reproduces_runs(run_engine, variant):

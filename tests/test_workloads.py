@@ -102,6 +102,13 @@ def test_c3_frame_run_matches_oracle(run_engine, oracle_memo):
     assert_same_run(a, b)
     assert a.state.stage_iterations[1] >= 2          # FRAME ran (with a penalty increase)
     assert a.state.n_ref_indel_mults == b.state.n_ref_indel_mults >= 1
+    # the library's stage machine: REFINE's random batches of 20 drawn there
+    from rifraf_amd.batch import rifraf_batch
+    n = rifraf_batch([dict(dnaseqs=reads, phreds=phreds, reference=ref)], params=params, engine=run_engine,
+                     native=True)[0]
+    assert_same_run(n, b)
+    assert [int(i) for i in n.state.batch_seqs] == [int(i) for i in b.state.batch_seqs]
+    assert len(b.state.batch_seqs) < len(reads)
 
 
 def test_c3_throughput_frame_run_matches_oracle(run_engine, oracle_memo):
