@@ -77,10 +77,7 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 #define DP_STORE(p, v) (*(p) = (v))
 #endif
 
-#ifndef RIFRAF_BAND_ODD
-#define RIFRAF_BAND_ODD 1
-#endif
-__host__ __device__ inline int band_P(int H) { return RIFRAF_BAND_ODD ? (((H + 1) >> 1) | 1) : ((H + 1) >> 1); }
+__host__ __device__ inline int band_P(int H) { return ((H + 1) >> 1) | 1; }
 // Row stride of a band as allocated: H >= pad_h (> 0) gives rows of a whole
 // number of 128-B lines, so that the wide-band scorer's 32-diagonal segments
 // read exactly one line per kappa row (k_score_segl); else the odd stride.
@@ -793,13 +790,11 @@ __host__ __device__ constexpr int dpl_flush_stores(int np, int pm, int lpt = 16)
 }
 // stride classes of the lean DP launches: k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
 // takes the lean tasks of NP class npi with P <= dpr_pm (the largest is the
-// class maximum 16 * NP | 1); NP = 1 has one class per stride P = 10 .. 17
-// (DPR_P1_CLASSES, PFIX: exactly that stride)
-constexpr int DPR_P1_MIN = 10, DPR_P1_CLASSES = 8;
+// class maximum 16 * NP | 1)
 __host__ __device__ constexpr int dpr_pm(int npi, int pmi)
 {
-    // NP = 1: P = 10 .. 17 (H <= 31); NP = 2: 17..33; NP = 4: 33..65; NP = 8: 65..129
-    return npi == 0 ? DPR_P1_MIN + pmi : npi == 1 ? 19 + 4 * pmi + (pmi == 3 ? 2 : 0) : (((16 << npi) * (pmi + 5)) / 8) | 1;
+    // NP = 1: P <= 17 (H <= 31); NP = 2: 17..33; NP = 4: 33..65; NP = 8: 65..129
+    return npi == 0 ? 11 + 2 * pmi : npi == 1 ? 19 + 4 * pmi + (pmi == 3 ? 2 : 0) : (((16 << npi) * (pmi + 5)) / 8) | 1;
 }
 extern __shared__ __attribute__((aligned(16))) char dpl_smem[];
 
@@ -4695,7 +4690,7 @@ struct rf_ctx {
         uint64_t val_epoch = 0;   // state_epoch at which the job list was last validated
         std::vector<int32_t> slot, seq, tpl, bw, flags;   // flags: per job (rf_realign_jobs)
         size_t nr[4][2] = {};   // k_dpr<1,2,4,8> x {general, lean}
-        size_t nrp[4][DPR_P1_CLASSES] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
+        size_t nrp[4][4] = {};  // lean k_dpr<NP, true, PM> split by band row stride (dpr_pm)
         size_t nw[2] = {};     // lean wide-task classes (RF_OPT_DP_WIDE)
         size_t nx = 0;         // latency-bound non-lean tasks, k_dpx (RF_OPT_DP_NL64)
         size_t nl = 0;         // latency-mode lean tasks, one k_dpx<false, false> class (RF_OPT_DP_LAT)
@@ -5950,7 +5945,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         if (moved)
             ++ctx->layout_gen;
         // band offsets are only final after every allocation (arena growth moves them)
-        std::vector<DPTask> cr[4][2], c64, cg, cp[4][DPR_P1_CLASSES], cw[2], cwm;
+        std::vector<DPTask> cr[4][2], c64, cg, cp[4][4], cw[2], cwm;
         int hmax64 = 0, hmaxg = 0, gm = 0;
         // RF_OPT_DP_PSPLIT: bit npi set = split lean class NP = 1 << npi by stride
         // (default: NP = 1 only, and only when that class holds at least half
@@ -6032,11 +6027,11 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                 } else if (lean && wide >= 0 && ((ctx->opt.dp_wide >> wide) & 1)) {
                     cw[wide].push_back(t);
                 } else if (lean && ((psplit >> npi) & 1) && np8 &&
-                           !(npi == 0 && (t.P < DPR_P1_MIN || t.P >= DPR_P1_MIN + DPR_P1_CLASSES))) {
-                    // NP = 1 stride classes take exactly P = 10 .. 17 (PFIX
+                           !(npi == 0 && DPR_PFIX && (t.P < dpr_pm(0, 0) || t.P > dpr_pm(0, 3) || !(t.P & 1)))) {
+                    // NP = 1 stride classes take exactly P = 11, 13, 15, 17 (PFIX
                     // kernels); other strides stay in the generic lean class
-                    int pmi = npi == 0 ? t.P - DPR_P1_MIN : 0;
-                    while (npi > 0 && pmi < 3 && t.P > dpr_pm(npi, pmi))
+                    int pmi = 0;
+                    while (pmi < 3 && t.P > dpr_pm(npi, pmi))
                         ++pmi;
                     cp[npi][pmi].push_back(t);
                 } else if (t.H <= 31)
@@ -6132,7 +6127,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             for (int b = 0; b < 2; ++b)
                 P.nr[a][b] = cr[a][b].size();
         for (int a = 0; a < 4; ++a)
-            for (int b = 0; b < DPR_P1_CLASSES; ++b)
+            for (int b = 0; b < 4; ++b)
                 P.nrp[a][b] = cp[a][b].size();
         for (int a = 0; a < 2; ++a)
             P.nw[a] = cw[a].size();
@@ -6162,8 +6157,7 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
         int kind;      // 0..7 = k_dpr<1<<(kind>>1), kind&1>, 8 = k_dp<64,false>, 9 = k_dp<DPW_NT,..>, 11 = k_dpm,
                        // 32 / 33 = lean wide tasks, 34 = k_dpx (few non-lean),
                        // 35 = latency-mode lean,
-                       // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)> (npi >= 1),
-                       // 40 + pmi = k_dpr<1, true, dpr_pm(0, pmi), 16, PFIX>
+                       // 16 + 4 * npi + pmi = k_dpr<1 << npi, true, dpr_pm(npi, pmi)>
         size_t at, n;
     };
     std::vector<Launch> launches;
@@ -6176,9 +6170,9 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
                     at += P.nr[a][b];
                 }
         for (int a = 0; a < 4; ++a)
-            for (int b = 0; b < (a == 0 ? DPR_P1_CLASSES : 4); ++b)
+            for (int b = 0; b < 4; ++b)
                 if (P.nrp[a][b]) {
-                    launches.push_back({a == 0 ? 40 + b : 16 + 4 * a + b, at, P.nrp[a][b]});
+                    launches.push_back({16 + 4 * a + b, at, P.nrp[a][b]});
                     at += P.nrp[a][b];
                 }
         for (int a = 0; a < 2; ++a)
@@ -6267,20 +6261,17 @@ static int realign_impl(rf_ctx *ctx, int32_t njobs, const int32_t *slot, const i
             const size_t lds = (L.kind & 1) ? 4 * (size_t)dpl_task_bytes(np) : 0;
             hipLaunchKernelGGL(kr[L.kind], dim3((n + 3) / 4), dim3(64), lds, st, d_tasks + L.at, n, d_bases,
                                d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
-        } else if ((L.kind >= 20 && L.kind < 32) || (L.kind >= 40 && L.kind < 40 + DPR_P1_CLASSES)) {
+        } else if (L.kind >= 16 && L.kind < 32) {
             using KFn = void (*)(const DPTask *, int, const uint8_t *, const double *, double *, double *, int *,
                                  double *, const double *);
 #define KP(a, b) k_dpr<1 << (a), true, dpr_pm(a, b), 16, (a) == 0 && DPR_PFIX>
-            const KFn kp[12] = {KP(1, 0), KP(1, 1), KP(1, 2), KP(1, 3), KP(2, 0), KP(2, 1),
-                                KP(2, 2), KP(2, 3), KP(3, 0), KP(3, 1), KP(3, 2), KP(3, 3)};
-            const KFn kp1[DPR_P1_CLASSES] = {KP(0, 0), KP(0, 1), KP(0, 2), KP(0, 3),
-                                             KP(0, 4), KP(0, 5), KP(0, 6), KP(0, 7)};
+            const KFn kp[16] = {KP(0, 0), KP(0, 1), KP(0, 2), KP(0, 3), KP(1, 0), KP(1, 1), KP(1, 2), KP(1, 3),
+                                KP(2, 0), KP(2, 1), KP(2, 2), KP(2, 3), KP(3, 0), KP(3, 1), KP(3, 2), KP(3, 3)};
 #undef KP
-            const bool one = L.kind >= 40;
-            const int c = one ? L.kind - 40 : L.kind - 20, npi = one ? 0 : 1 + (c >> 2), pmi = one ? c : c & 3;
-            hipLaunchKernelGGL(one ? kp1[c] : kp[c], dim3((n + 3) / 4), dim3(64),
-                               4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)), st, d_tasks + L.at, n, d_bases,
-                               d_tabs, d_bands, d_out, ctx->d_err, (double *)ctx->scratch[7].p, d_lut);
+            const int c = L.kind - 16, npi = c >> 2, pmi = c & 3;
+            hipLaunchKernelGGL(kp[c], dim3((n + 3) / 4), dim3(64), 4 * (size_t)dpl_task_bytes(1 << npi, dpr_pm(npi, pmi)),
+                               st, d_tasks + L.at, n, d_bases, d_tabs, d_bands, d_out, ctx->d_err,
+                               (double *)ctx->scratch[7].p, d_lut);
         } else if (L.kind == 34) {
             // few non-lean tasks (H <= 127): one latency-bound task per wave (k_dpx)
             hipLaunchKernelGGL((k_dpx<true, true>), dim3(n), dim3(128), 0, st, d_tasks + L.at, n, d_bases, d_tabs,

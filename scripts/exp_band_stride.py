@@ -1,7 +1,8 @@
 #!/usr/bin/env python
-"""Band row stride A/B at the c4 shape: for each library named (built with
-RIFRAF_BAND_ODD = 1 / 0: kappa rows of ceil(H/2) | 1 or ceil(H/2)
-doubles), the DP fill alone (realign FWD|BWD, HIP-event ms, 3 x 5 calls)
+"""Band row stride A/B at the c4 shape (round 6, profiles/r08d): for each
+library named (built at commit db2b22a with RIFRAF_BAND_ODD = 1 / 0: kappa
+rows of ceil(H/2) | 1 or ceil(H/2) doubles; the even layout and its NP = 1
+stride classes were not kept), the DP fill alone (realign FWD|BWD, HIP-event ms, 3 x 5 calls)
 and, for the first 64 reads, the scores and the downloaded A / B bands
 (column-major, layout independent) hashed, so both layouts must agree.
 usage: exp_band_stride.py nclusters lib.so [lib.so ...]"""
