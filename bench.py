@@ -456,14 +456,16 @@ def main():
         result = run_clusters(args, rank, world, gpu, dist, torch, coll)
         if args.config == "c4" and args.e2e_clusters > 0:
             result["e2e"] = run_e2e(args, rank, world, gpu, dist, coll)
+        # the rank-0 legs below report a failure in their own field (the
+        # other ranks are already on their way to the next collective)
         if args.config == "c4" and not args.no_c2 and rank == 0:
             # configs[1] beside the headline line: whole runs of the 1 kb
             # cluster, latency mode, checked against the oracle's runs
-            result["c2"] = run_c2(args, gpu)
+            result["c2"] = rank0_leg(run_c2, args, gpu)
         if args.config == "c4" and not args.no_c3 and rank == 0:
             # configs[2] beside the headline line: the reference-informed path
             # (FRAME, codon moves) end to end, rank 0 only (one cluster)
-            result["c3"] = run_c3(args, gpu)
+            result["c3"] = rank0_leg(run_c3, args, gpu)
         if args.config == "c4" and not args.no_secondary:
             # configs[4] beside the headline line: driver-measured 10 kb reads
             # with band doubling, read-sharded over the same ranks
@@ -1078,6 +1080,16 @@ GOLDEN_RUNS = os.path.join(REPO, "tests", "golden", "runs.npz")   # scripts/make
 C2_SEEDS = (1, 2, 3, 4, 5)
 C2_VARIANTS = {"default": dict(seed=1),
                "throughput": dict(seed=1, batch_size=0, batch_fixed=False, do_score=True)}
+
+
+def rank0_leg(fn, *a):
+    """A rank-0-only field of the bench line: its result, or the error it
+    raised (type, message, traceback tail) so that the line still prints."""
+    import traceback
+    try:
+        return fn(*a)
+    except Exception as e:  # noqa: BLE001 -- reported in the field, not hidden
+        return {"error": f"{type(e).__name__}: {e}", "traceback": traceback.format_exc()[-2000:]}
 
 
 def golden_run(name, z=None):
