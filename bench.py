@@ -711,14 +711,20 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         can_pin = float(f.item())
     pin = idle_cpus(allowed, k, dist) if can_pin else None
     pin_excl = bool(args.e2e_pin_exclusive) if ne > 1 and args.e2e_pin_exclusive >= 0 else excl
-    runs, pin_runs, stats, same_pin = [], [], [], True
+    runs, pin_runs, stats, same_pin, pin_sets = [], [], [], True, []
     res = None
-    for _ in range(5 if pin else 3):
+    for p_ in range(5 if pin else 3):
         s_, r_, st = queued(excl)
         runs.append(s_)
         stats.append(st)
         res = res or r_
         if pin:
+            # the idlest cpus at this pass (the shared host's load moves
+            # between passes: r08h's first three pinned passes ran 0.43 - 0.46 s
+            # on cpus picked once, the last two 0.19 - 0.23 s)
+            if p_ > 0:
+                pin = idle_cpus(allowed, k, dist)
+            pin_sets.append([int(c) for c in pin])
             saved = pin_threads(pin)
             try:
                 s_, res_pin, _ = queued(pin_excl)
@@ -751,8 +757,13 @@ def run_e2e(args, rank, world, gpu, dist, coll):
         elapsed, tot = aggregate(elapsed, tot, coll)
     data.close(rank, dist)
     n_all = float(data.n)
+    best, pin_best = float(min(runs)), (float(min(pin_runs)) if pin_runs else 0.0)
+    if dist is not None:
+        best, _ = aggregate(best, [0.0], coll)
+        pin_best, _ = aggregate(pin_best, [0.0], coll)
     return {"metric": "whole rifraf() runs per second (c4 cluster shape)", "clusters_per_s": n_all / elapsed,
             "clusters_per_s_per_gpu": n_all / elapsed / max(world, 1), "ranks": world,
+            "clusters_per_s_best": n_all / best,
             "clusters": int(n_all), "clusters_run_once": int(tot[0]) == int(n_all), "seconds": elapsed,
             "cold_clusters_per_s": n_all / cold,
             "timing": "steady state: the median of five full passes over the clusters after the first ('cold', "
@@ -782,6 +793,11 @@ def run_e2e(args, rank, world, gpu, dist, coll):
                 "cores": len(pin), "cpus": [int(c) for c in pin], "cpu_nodes": [cpu_node(c) for c in pin],
                 "home_node": home_node(), "clusters_per_s": n_all / pin_s,
                 "ratio_to_unpinned": elapsed / pin_s,
+                "cpus_per_pass": pin_sets,
+                "clusters_per_s_best": n_all / pin_best if pin_best > 0 else None,
+                "ratio_best": best / pin_best if pin_best > 0 else None,
+                "best_note": "the fastest of the five passes of each kind (medians above): the shared host's "
+                             "other load reaches either kind of pass",
                 "init_exclusive": pin_excl,
                 "host_cpus_unpinned": len(os.sched_getaffinity(0)), "same_consensus": bool(same_pin),
                 "note": "the same steady-state pass with every thread of the rank pinned to this many cores "
