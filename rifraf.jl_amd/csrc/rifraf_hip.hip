@@ -4673,6 +4673,10 @@ struct rf_ctx {
     // the error flag): one D2H + one synchronize per call
     void *hout = nullptr;
     size_t hout_bytes = 0;
+    // pinned ring for the per-call descriptor uploads (upload()): the runtime
+    // stages a pageable H2D copy through a blit of its own
+    void *up = nullptr;
+    size_t up_bytes = 0, up_off = 0;
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
@@ -4808,14 +4812,38 @@ int ensure_buf(rf_ctx *ctx, DevBuf &b, size_t bytes)
     return 0;
 }
 
+#ifndef RF_UP_RING
+#define RF_UP_RING (32 << 20)   // bytes of the pinned upload ring (0: pageable copies)
+#endif
 template <class T>
 int upload(rf_ctx *ctx, DevBuf &b, const std::vector<T> &v)
 {
-    if (int e = ensure_buf(ctx, b, std::max<size_t>(v.size() * sizeof(T), 16)))
+    const size_t bytes = v.size() * sizeof(T);
+    if (int e = ensure_buf(ctx, b, std::max<size_t>(bytes, 16)))
         return e;
-    if (!v.empty())
-        HIPCHK(ctx, hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
-                                   ctx->stream));
+    if (!bytes)
+        return 0;
+    if (RF_UP_RING > 0 && bytes <= (size_t)RF_UP_RING / 4) {
+        if (!ctx->up) {
+            if (hipHostMalloc(&ctx->up, RF_UP_RING, hipHostMallocDefault) != hipSuccess)
+                return fail(ctx, RF_ERR_HIP, "pinned upload ring allocation failed");
+            ctx->up_bytes = RF_UP_RING;
+            ctx->up_off = 0;
+        }
+        const size_t need = (bytes + 255) & ~(size_t)255;
+        if (ctx->up_off + need > ctx->up_bytes) {
+            // every copy out of the ring is on this stream: once it drains,
+            // the ring is free again
+            HIPCHK(ctx, stream_wait(ctx));
+            ctx->up_off = 0;
+        }
+        char *h = (char *)ctx->up + ctx->up_off;
+        std::memcpy(h, v.data(), bytes);
+        ctx->up_off += need;
+        HIPCHK(ctx, hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return 0;
+    }
+    HIPCHK(ctx, hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
     return 0;
 }
 
@@ -5167,6 +5195,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipHostFree(ctx->pinned);
     if (ctx->hout)
         (void)hipHostFree(ctx->hout);
+    if (ctx->up)
+        (void)hipHostFree(ctx->up);
     if (ctx->d_err)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
