@@ -4677,6 +4677,10 @@ struct rf_ctx {
     // stages a pageable H2D copy through a blit of its own
     void *up = nullptr;
     size_t up_bytes = 0, up_off = 0;
+    // pinned landing zone for the other calls' downloads (ensure_hdn): the
+    // error flag at 0, results from 16
+    void *hdn = nullptr;
+    size_t hdn_bytes = 0;
     DevBuf grow_segs;   // compaction descriptors (arena_grow may run inside other uploads)
     int *d_err = nullptr;
     double dp_ms = 0, score_ms = 0, gather_ms = 0, bt_ms = 0;
@@ -4971,18 +4975,55 @@ int check_err_landed(rf_ctx *ctx)
     return 0;
 }
 
-int check_err(rf_ctx *ctx)
+// Downloads of a call land in ctx->hdn (pinned: a pageable D2H copy is
+// staged by the runtime through a blit and a wait of its own): the error
+// flag at offset 0 (land_err), results from HDN_RES; the call queues them
+// behind its kernels, waits once, then copies the results out.
+constexpr size_t HDN_RES = 16;
+int ensure_hdn(rf_ctx *ctx, size_t bytes)
 {
-    int h = 0;
-    HIPCHK(ctx, pre_d2h(ctx));
-    HIPCHK(ctx, hipMemcpyAsync(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, stream_wait(ctx));
+    const size_t want = HDN_RES + bytes;
+    if (ctx->hdn_bytes >= want)
+        return 0;
+    if (ctx->hdn) {
+        HIPCHK(ctx, stream_wait(ctx));
+        (void)hipHostFree(ctx->hdn);
+    }
+    ctx->hdn = nullptr;
+    ctx->hdn_bytes = 0;
+    const size_t sz = std::max<size_t>(want + want / 4, 1 << 20);
+    if (hipHostMalloc(&ctx->hdn, sz, hipHostMallocDefault) != hipSuccess)
+        return fail(ctx, RF_ERR_HIP, "pinned download buffer allocation failed");
+    ctx->hdn_bytes = sz;
+    return 0;
+}
+
+// queue the error flag's copy into ctx->hdn (after ensure_hdn)
+hipError_t land_err(rf_ctx *ctx)
+{
+    return hipMemcpyAsync(ctx->hdn, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+}
+
+// after the stream wait: the landed error flag
+int check_err_hdn(rf_ctx *ctx)
+{
+    const int h = *(const int *)ctx->hdn;
     if (h) {
         int z = 0;
         HIPCHK(ctx, hipMemcpy(ctx->d_err, &z, sizeof(int), hipMemcpyHostToDevice));
         return fail(ctx, RF_ERR_NUMERIC, numeric_message(h));
     }
     return 0;
+}
+
+int check_err(rf_ctx *ctx)
+{
+    if (int e = ensure_hdn(ctx, 0))
+        return e;
+    HIPCHK(ctx, pre_d2h(ctx));
+    HIPCHK(ctx, land_err(ctx));
+    HIPCHK(ctx, stream_wait(ctx));
+    return check_err_hdn(ctx);
 }
 
 int band_rows(int n, int m, int bw) { return 2 * bw + std::abs(n - m) + 1; }
@@ -5197,6 +5238,8 @@ int rf_destroy(rf_ctx *ctx)
         (void)hipHostFree(ctx->hout);
     if (ctx->up)
         (void)hipHostFree(ctx->up);
+    if (ctx->hdn)
+        (void)hipHostFree(ctx->hdn);
     if (ctx->d_err)
         (void)hipFree(ctx->d_err);
     for (auto &e : ctx->ev)
@@ -6485,22 +6528,23 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
     if (nslots > 0)
         if (int e = launch_backtraces(ctx, tasks, nullptr, 0))
             return e;
-    std::vector<int32_t> cnt(2 * (size_t)nslots);
+    // counts, then the moves, land in ctx->hdn with the error flag: one wait
+    const size_t cb = (sizeof(int32_t) * 2 * (size_t)nslots + 15) & ~(size_t)15;
+    if (int e = ensure_hdn(ctx, cb + (moves ? (size_t)total : 0)))
+        return e;
+    const int32_t *cnt = (const int32_t *)((char *)ctx->hdn + HDN_RES);
+    const int8_t *all = (const int8_t *)((char *)ctx->hdn + HDN_RES + cb);
     HIPCHK(ctx, pre_d2h(ctx));
     if (nslots > 0)
-        HIPCHK(ctx, hipMemcpyAsync(cnt.data(), d_cnt, sizeof(int32_t) * 2 * nslots,
-                                   hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<int8_t> all;
-    if (moves) {
-        all.resize(total);
-        if (total > 0)
-            HIPCHK(ctx, hipMemcpyAsync(all.data(), ctx->scratch[3].p, total, hipMemcpyDeviceToHost,
-                                       ctx->stream));
-    }
+        HIPCHK(ctx, hipMemcpyAsync((void *)cnt, d_cnt, sizeof(int32_t) * 2 * nslots, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    if (moves && total > 0)
+        HIPCHK(ctx, hipMemcpyAsync((void *)all, ctx->scratch[3].p, total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, land_err(ctx));
     HIPCHK(ctx, stream_wait(ctx));
     if (nslots > 0)
         note_bt_ms(ctx);
-    if (int e = check_err(ctx))
+    if (int e = check_err_hdn(ctx))
         return e;
     for (int32_t k = 0; k < nslots; ++k) {
         if (nmoves)
@@ -6508,7 +6552,7 @@ int rf_backtrace(rf_ctx *ctx, int32_t nslots, const int32_t *slot, int8_t *moves
         if (nerrors)
             nerrors[k] = cnt[nslots + k];
         if (moves)   // the walk leaves the moves at the end of the read's n+m slot
-            std::memcpy(moves + moves_off[k], all.data() + offs[k] + tasks[k].n + tasks[k].m - cnt[k], cnt[k]);
+            std::memcpy(moves + moves_off[k], all + offs[k] + tasks[k].n + tasks[k].m - cnt[k], cnt[k]);
     }
     return 0;
 }
@@ -6548,11 +6592,18 @@ int rf_alignment_proposals(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off
     if (int e = launch_backtraces(ctx, tasks, (uint8_t *)ctx->scratch[2].p, do_indels ? 1 : 0))
         return e;
     HIPCHK(ctx, hipGetLastError());
+    if (int e = ensure_hdn(ctx, mask_total))
+        return e;
     HIPCHK(ctx, pre_d2h(ctx));
-    HIPCHK(ctx, hipMemcpyAsync(out_mask, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync((char *)ctx->hdn + HDN_RES, ctx->scratch[2].p, mask_total, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIPCHK(ctx, land_err(ctx));
     HIPCHK(ctx, stream_wait(ctx));
     note_bt_ms(ctx);
-    return check_err(ctx);
+    if (int e = check_err_hdn(ctx))
+        return e;
+    std::memcpy(out_mask, (char *)ctx->hdn + HDN_RES, mask_total);
+    return 0;
 }
 
 int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,
@@ -6784,9 +6835,15 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
                            d_hr, d_dense, d_ref, d_href, d_out, ctx->d_err);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    // the totals land in ctx->hdn with the error flag (per-read columns, a
+    // test / sharding path, stay pageable)
+    if (int e = ensure_hdn(ctx, (size_t)std::max<int64_t>(nprops, 0) * 8))
+        return e;
     HIPCHK(ctx, pre_d2h(ctx));
     if (nprops > 0)
-        HIPCHK(ctx, hipMemcpyAsync(out_total, d_out, nprops * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->hdn + HDN_RES, d_out, nprops * 8, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    HIPCHK(ctx, land_err(ctx));
     std::vector<double> split_host;
     if (out_per_seq && split_total > 0) {
         split_host.resize(split_total);
@@ -6825,7 +6882,11 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
             }
         }
     }
-    return check_err(ctx);
+    if (int e = check_err_hdn(ctx))
+        return e;
+    if (nprops > 0)
+        std::memcpy(out_total, (char *)ctx->hdn + HDN_RES, nprops * 8);
+    return 0;
 }
 
 static int score_dense_impl(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_t *slots,

@@ -1,14 +1,17 @@
 #!/bin/bash
-# Pinned upload ring A/B (round 6, profiles/r08j_up_ring_ab.txt): parity of the
-# product library, then configs[2] native runs with the ring (librifraf_hip)
-# and with pageable copies (librifraf_noring: scripts/build_variant.sh noring
-# -DRF_UP_RING=0), two alternations.
+# Host-transfer A/B on configs[2] (round 6): parity of the product library,
+# then native c3 runs (scripts/c3_repeat.py, median of 9) for each library
+# named, two alternations.  r08j: the pinned upload ring (librifraf_hip vs
+# librifraf_noring, built with -DRF_UP_RING=0); r08k: pinned download landing
+# (librifraf_hip vs librifraf_base, the previous commit).
+# usage: scripts/exp_up_ring.sh TAG lib [lib ...]
 set -o pipefail
-mkdir -p gpurun_out/r08j
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_batch.py tests/test_model_e2e.py > gpurun_out/r08j/par.log 2>&1 || { tail -20 gpurun_out/r08j/par.log; exit 1; }
-tail -1 gpurun_out/r08j/par.log
+TAG=$1; shift
+mkdir -p gpurun_out/$TAG
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_batch.py tests/test_model_e2e.py > gpurun_out/$TAG/par.log 2>&1 || { tail -20 gpurun_out/$TAG/par.log; exit 1; }
+tail -1 gpurun_out/$TAG/par.log
 for rep in 1 2; do
-  for lib in hip noring; do
+  for lib in "$@"; do
     echo -n "$lib $rep "
     RIFRAF_HIP_LIB=$PWD/rifraf.jl_amd/librifraf_$lib.so timeout -k 10 200 python scripts/c3_repeat.py 9 || exit 1
   done
