@@ -4819,6 +4819,31 @@ int ensure_buf(rf_ctx *ctx, DevBuf &b, size_t bytes)
 #ifndef RF_UP_RING
 #define RF_UP_RING (32 << 20)   // bytes of the pinned upload ring (0: pageable copies)
 #endif
+// `bytes` of the pinned upload ring for one H2D copy on the context's stream
+// (*h = nullptr: too large for the ring, copy from pageable memory)
+int ring_take(rf_ctx *ctx, size_t bytes, char **h)
+{
+    *h = nullptr;
+    if (RF_UP_RING <= 0 || bytes > (size_t)RF_UP_RING / 4)
+        return 0;
+    if (!ctx->up) {
+        if (hipHostMalloc(&ctx->up, RF_UP_RING, hipHostMallocDefault) != hipSuccess)
+            return fail(ctx, RF_ERR_HIP, "pinned upload ring allocation failed");
+        ctx->up_bytes = RF_UP_RING;
+        ctx->up_off = 0;
+    }
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (ctx->up_off + need > ctx->up_bytes) {
+        // every copy out of the ring is on this stream: once it drains, the
+        // ring is free again
+        HIPCHK(ctx, stream_wait(ctx));
+        ctx->up_off = 0;
+    }
+    *h = (char *)ctx->up + ctx->up_off;
+    ctx->up_off += need;
+    return 0;
+}
+
 template <class T>
 int upload(rf_ctx *ctx, DevBuf &b, const std::vector<T> &v)
 {
@@ -4827,27 +4852,13 @@ int upload(rf_ctx *ctx, DevBuf &b, const std::vector<T> &v)
         return e;
     if (!bytes)
         return 0;
-    if (RF_UP_RING > 0 && bytes <= (size_t)RF_UP_RING / 4) {
-        if (!ctx->up) {
-            if (hipHostMalloc(&ctx->up, RF_UP_RING, hipHostMallocDefault) != hipSuccess)
-                return fail(ctx, RF_ERR_HIP, "pinned upload ring allocation failed");
-            ctx->up_bytes = RF_UP_RING;
-            ctx->up_off = 0;
-        }
-        const size_t need = (bytes + 255) & ~(size_t)255;
-        if (ctx->up_off + need > ctx->up_bytes) {
-            // every copy out of the ring is on this stream: once it drains,
-            // the ring is free again
-            HIPCHK(ctx, stream_wait(ctx));
-            ctx->up_off = 0;
-        }
-        char *h = (char *)ctx->up + ctx->up_off;
+    char *h;
+    if (int e = ring_take(ctx, bytes, &h))
+        return e;
+    if (h)
         std::memcpy(h, v.data(), bytes);
-        ctx->up_off += need;
-        HIPCHK(ctx, hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, ctx->stream));
-        return 0;
-    }
-    HIPCHK(ctx, hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(b.p, h ? (const void *)h : (const void *)v.data(), bytes, hipMemcpyHostToDevice,
+                               ctx->stream));
     return 0;
 }
 
@@ -6784,17 +6795,33 @@ int rf_score(rf_ctx *ctx, int32_t ngroups, const int32_t *slot_off, const int32_
     int32_t *d_hr = (int32_t *)pb;      pb += align_up(ngroups * 4, 256);
     int32_t *d_href = (int32_t *)pb;    pb += align_up(ngroups * 4, 256);
     int64_t *d_gstart = (int64_t *)pb;
+    // the seven arrays in their device layout: one copy out of the ring
+    const size_t pused = (size_t)((char *)(d_gstart + ngroups + 1) - (char *)ctx->scratch[4].p);
+    char *h;
+    if (int e = ring_take(ctx, pused, &h))
+        return e;
+    auto put = [&](void *d, const void *src, size_t n) -> hipError_t {
+        if (!n)
+            return hipSuccess;
+        if (h) {
+            std::memcpy(h + ((char *)d - (char *)ctx->scratch[4].p), src, n);
+            return hipSuccess;
+        }
+        return hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, ctx->stream);
+    };
     if (nprops > 0) {
-        HIPCHK(ctx, hipMemcpyAsync(d_pgroup, pgroup.data(), nprops * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(d_pos, pos + prop_off[0], nprops * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(d_kind, kind + prop_off[0], nprops, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(d_base, base + prop_off[0], nprops, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, put(d_pgroup, pgroup.data(), nprops * 4));
+        HIPCHK(ctx, put(d_pos, pos + prop_off[0], nprops * 4));
+        HIPCHK(ctx, put(d_kind, kind + prop_off[0], nprops));
+        HIPCHK(ctx, put(d_base, base + prop_off[0], nprops));
     }
     if (ngroups > 0) {
-        HIPCHK(ctx, hipMemcpyAsync(d_hr, has_reads.data(), ngroups * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(d_href, has_ref.data(), ngroups * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(d_gstart, gstart.data(), (ngroups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, put(d_hr, has_reads.data(), ngroups * 4));
+        HIPCHK(ctx, put(d_href, has_ref.data(), ngroups * 4));
+        HIPCHK(ctx, put(d_gstart, gstart.data(), (ngroups + 1) * 8));
     }
+    if (h && (nprops > 0 || ngroups > 0))
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[4].p, h, pused, hipMemcpyHostToDevice, ctx->stream));
     // work buffers: dense totals, split partials, codon scratch + outputs, final totals
     const size_t wbytes = align_up(std::max<int64_t>(dense_total, 1) * 8, 256) +
                           (split ? align_up(std::max<int64_t>(split_total, 1) * 8, 256) : 0) +
