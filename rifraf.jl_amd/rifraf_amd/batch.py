@@ -238,7 +238,7 @@ class _Hub:
 
 
 STATS = {"launches": 0, "engine_s": 0.0, "native_s": 0.0, "score_phase_s": 0.0, "setup_native_s": 0.0,
-         "upload_s": 0.0}
+         "upload_s": 0.0, "qv_refill_skipped": 0}
 _STATS_LOCK = threading.Lock()   # waves of several engines update STATS from their own threads
 
 
@@ -689,20 +689,34 @@ def _wave_native(part, params, engine, init_lock=None, device_qv=True, setup_loc
         # realign_rescore (every batch read is bandwidth_fixed: one fill each),
         # estimate_probs over the dense totals, alignment_error_probs's sums
         groups = [read_off[k] + np.arange(len(st_.batch_seqs), dtype=np.int32) for k, st_ in enumerate(states)]
-        sq = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int32) for k, st_ in enumerate(states)])
-        tp = np.concatenate([np.full(len(g), k, np.int32) for k, g in enumerate(groups)])
-        bws = np.abs(np.asarray(bw, np.int64))[sq].astype(np.int32)   # = the reads' .bandwidth set above
-        engine.set_templates(0, [st_.consensus for st_ in states])
-        sc = engine.realign(np.concatenate(groups), sq, tp, bws, RF_FWD | RF_BWD)
-        at = 0
-        for st_ in states:
-            n = len(st_.batch_seqs)
-            st_.slot_scores = [float(v) for v in sc[at:at + n]]
-            total = st_.slot_scores[0]                              # rescore!, model.jl:630-635
-            for v in st_.slot_scores[1:st_.n_slots]:
-                total += v
-            st_.score = total
-            at += n
+        # The bands already hold that fill when every cluster converged
+        # without changing its consensus in its last iteration and its batch
+        # was every read from the start (the slots never changed reads, and
+        # every consensus change was followed by an A and B fill): the device
+        # templates are the final consensi and the native final score is the
+        # same left fold of the same A[end, end] values, so the fill is
+        # skipped.  Otherwise (a cluster stopped at max_iters, fixed or random
+        # batches) every cluster is refilled as the reference does.
+        current = not params.batch_fixed and all(
+            (params.batch_size <= 1 or params.batch_size >= int(nread[k])) and r["status"] == 1 and
+            len(r["stages"]) > 0 and np.array_equal(np.asarray(r["stages"][-1]), np.asarray(r["consensus"]))
+            for k, r in enumerate(res))
+        _stat("qv_refill_skipped", 1 if current else 0)
+        if not current:
+            sq = np.concatenate([read_off[k] + np.asarray(st_.batch_seqs, np.int32) for k, st_ in enumerate(states)])
+            tp = np.concatenate([np.full(len(g), k, np.int32) for k, g in enumerate(groups)])
+            bws = np.abs(np.asarray(bw, np.int64))[sq].astype(np.int32)   # = the reads' .bandwidth set above
+            engine.set_templates(0, [st_.consensus for st_ in states])
+            sc = engine.realign(np.concatenate(groups), sq, tp, bws, RF_FWD | RF_BWD)
+            at = 0
+            for st_ in states:
+                n = len(st_.batch_seqs)
+                st_.slot_scores = [float(v) for v in sc[at:at + n]]
+                total = st_.slot_scores[0]                              # rescore!, model.jl:630-635
+                for v in st_.slot_scores[1:st_.n_slots]:
+                    total += v
+                st_.score = total
+                at += n
         tl = [len(st_.consensus) for st_ in states]
         qv = None
         if device_qv and coded is not None and hasattr(engine, "qv_probs") and min(tl) > 0:

@@ -155,9 +155,13 @@ def test_native_batch_matches_hub(run_engine, pset):
     from rifraf_amd.model import RifrafParams
     params = RifrafParams(scores=Scores.from_errors(ErrorModel(1, 2, 2)), **NATIVE_PARAMS[pset])
     clusters = _ref_free_clusters()
+    from rifraf_amd import batch as B
     hub = rifraf_batch(clusters, params=params, engine=engine, native=False)
+    skipped = B.STATS["qv_refill_skipped"]
     nat = rifraf_batch(clusters, params=params, engine=engine, native=True, device_qv=False)
     dqv = rifraf_batch(clusters, params=params, engine=engine, native=True)
+    if pset == "all_reads_qv":   # every cluster converged: the QV pass reuses the final bands
+        assert B.STATS["qv_refill_skipped"] == skipped + 2
     for a, b, c in zip(nat, hub, dqv):
         assert_same_run(summary(a), summary(b))
         assert_same_run(summary(c), summary(b), qv_rtol=QV_RTOL)
