@@ -5762,11 +5762,22 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
     const size_t prep_tab = 512 * 8, prep_grid = 65536 * 8, prep_out = (size_t)std::max(nseq, 1) * 20;
     if (prep) {
         if (int e = ensure_buf(ctx, ctx->scratch[27], prep_tab + prep_grid + prep_out)) return e;
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[27].p, p10_t, 256 * 8, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + 256 * 8, match_t, 256 * 8, hipMemcpyHostToDevice,
-                                   ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + prep_tab, grid, prep_grid, hipMemcpyHostToDevice,
-                                   ctx->stream));
+        // the two tables and the grid as one copy out of the pinned ring
+        char *h;
+        if (int e = ring_take(ctx, prep_tab + prep_grid, &h)) return e;
+        if (h) {
+            std::memcpy(h, p10_t, 256 * 8);
+            std::memcpy(h + 256 * 8, match_t, 256 * 8);
+            std::memcpy(h + prep_tab, grid, prep_grid);
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[27].p, h, prep_tab + prep_grid, hipMemcpyHostToDevice,
+                                       ctx->stream));
+        } else {
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scratch[27].p, p10_t, 256 * 8, hipMemcpyHostToDevice, ctx->stream));
+            HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + 256 * 8, match_t, 256 * 8,
+                                       hipMemcpyHostToDevice, ctx->stream));
+            HIPCHK(ctx, hipMemcpyAsync((char *)ctx->scratch[27].p + prep_tab, grid, prep_grid,
+                                       hipMemcpyHostToDevice, ctx->stream));
+        }
     }
     double *d_est = (double *)((char *)ctx->scratch[27].p + prep_tab + prep_grid);
     double *d_tsum = d_est + std::max(nseq, 1);
@@ -5844,11 +5855,18 @@ static int set_sequences_codes_impl(rf_ctx *ctx, int32_t first, int32_t nseq, co
     }
     ++ctx->layout_gen;
     if (prep && nseq > 0) {
+        // est | tsum | ucode are contiguous on the device: one copy into the
+        // pinned landing zone
+        const size_t ob = (size_t)std::max(nseq, 1) * 20;
+        if (int e = ensure_hdn(ctx, ob)) return e;
+        char *hl = (char *)ctx->hdn + HDN_RES;
         HIPCHK(ctx, pre_d2h(ctx));
-        HIPCHK(ctx, hipMemcpyAsync(est, d_est, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(tsum, d_tsum, (size_t)nseq * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipMemcpyAsync(ucode, d_ucode, (size_t)nseq * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(hl, d_est, ob, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, stream_wait(ctx));
+        const size_t ns = (size_t)std::max(nseq, 1);
+        std::memcpy(est, hl, (size_t)nseq * 8);
+        std::memcpy(tsum, hl + ns * 8, (size_t)nseq * 8);
+        std::memcpy(ucode, hl + ns * 16, (size_t)nseq * 4);
     }
     return 0;
 }
